@@ -1,0 +1,165 @@
+"""Script executor: parse → validate/translate → rewrite → instruction generation →
+execute (reference: api/ScriptExecutorUtils.java, api/mlcontext/ScriptExecutor.java,
+api/DMLScript.java:execute).
+
+Used by the MLContext, JMLC, CLI and bench front ends."""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..conf import DMLConfig, get_default_config
+from ..parser.dml_parser import parse_dml
+from ..compiler.translator import Translator
+from ..compiler.lops import compile_program
+from ..compiler.hops import explain_dag
+from ..compiler.blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
+from ..runtime.instructions import make_impl
+from ..runtime.program import ExecutionContext, exec_blocks
+from ..runtime.data import FrameBlock, ListObject
+from ..ops.backend import backend, place, maybe_bf16
+from ..utils.stats import Statistics
+
+
+def parse(source, pydml=False, filename=""):
+    if pydml:
+        from ..parser.pydml_parser import parse_pydml
+        return parse_pydml(source, filename=filename)
+    return parse_dml(source, filename=filename)
+
+
+class CompiledScript:
+    def __init__(self, cp, config, inputs, outputs, t_parse, t_compile):
+        self.cp = cp
+        self.config = config
+        self.inputs = inputs
+        self.outputs = outputs
+        self.t_parse = t_parse
+        self.t_compile = t_compile
+
+
+def compile_script(source, args=None, inputs=(), outputs=(), config=None, pydml=False, filename="",
+                   base_dir=None):
+    config = config or get_default_config()
+    t0 = time.perf_counter()
+    prog = parse(source, pydml=pydml, filename=filename)
+    t1 = time.perf_counter()
+    tr = Translator(args or {}, config, base_dir=base_dir or (os.path.dirname(filename) if filename else None))
+    cp = tr.compile(prog, inputs=inputs, outputs=outputs)
+    compile_program(cp, make_impl, config)
+    t2 = time.perf_counter()
+    return CompiledScript(cp, config, set(inputs), list(outputs), t1 - t0, t2 - t1)
+
+
+def convert_input(v, dist=None, config=None):
+    """Python/numpy/torch/pandas objects → DML runtime values."""
+    if isinstance(v, (bool, int, float, str)):
+        return v
+    if isinstance(v, np.generic):
+        return v.item()
+    if isinstance(v, (FrameBlock, ListObject)):
+        return v
+    from ..parallel import dist as D
+    if isinstance(v, D.DistMatrix):
+        return v
+    try:
+        import pandas as pd
+        if isinstance(v, pd.DataFrame):
+            if all(np.issubdtype(t, np.number) for t in v.dtypes):
+                v = v.to_numpy(dtype=np.float64)
+            else:
+                return FrameBlock([v[c].tolist() for c in v.columns],
+                                  ["DOUBLE" if np.issubdtype(t, np.number) else "STRING" for t in v.dtypes],
+                                  [str(c) for c in v.columns])
+        elif isinstance(v, pd.Series):
+            v = v.to_numpy(dtype=np.float64).reshape(-1, 1)
+    except ImportError:
+        pass
+    if hasattr(v, "toarray") and not isinstance(v, np.ndarray):   # scipy sparse
+        v = v.toarray()
+    if isinstance(v, (list, tuple)):
+        v = np.asarray(v, dtype=np.float64)
+    if isinstance(v, np.ndarray):
+        if v.ndim == 1:
+            v = v.reshape(-1, 1)
+        t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64))
+    elif isinstance(v, torch.Tensor):
+        t = v
+        if t.dim() == 1:
+            t = t.reshape(-1, 1)
+    else:
+        raise TypeError(f"unsupported input type {type(v).__name__}")
+    if dist is not None and config is not None and t.shape[0] >= config.dist_min_rows:
+        return D.scatter_rows_from_global(dist, t)
+    if t.dtype == torch.bfloat16:
+        return t.to(backend.device)
+    return maybe_bf16(place(t))
+
+
+def execute(cs: CompiledScript, inputs=None, out=None, stats=None, dist=None):
+    config = cs.config
+    backend.configure(config)
+    if dist is None:
+        from ..parallel import dist as D
+        dist = D.get_context()
+    ctx = ExecutionContext(cs.cp, config, stats=stats, out=out, dist=dist)
+    for k, v in (inputs or {}).items():
+        ctx.vars[k] = convert_input(v, dist, config)
+    if config.explain:
+        ctx.print(explain(cs.cp, config.explain))
+    t0 = time.perf_counter()
+    try:
+        exec_blocks(ctx, cs.cp.blocks)
+    finally:
+        if stats is not None:
+            stats.t_exec += time.perf_counter() - t0
+            stats.t_parse += cs.t_parse
+            stats.t_compile += cs.t_compile
+    return {k: ctx.vars.get(k) for k in cs.outputs}, ctx
+
+
+def run(source, args=None, inputs=None, outputs=(), config=None, pydml=False, filename="", out=None,
+        stats=None):
+    inputs = inputs or {}
+    cs = compile_script(source, args, inputs=inputs.keys(), outputs=outputs, config=config, pydml=pydml,
+                        filename=filename)
+    res, _ = execute(cs, inputs, out=out, stats=stats)
+    return res
+
+
+# ----------------------------------------------------------------------------
+def explain(cp, level="hops"):
+    lines = ["# EXPLAIN (" + level + "):"]
+
+    def blocks(bl, ind):
+        for b in bl:
+            if isinstance(b, BasicBlock):
+                lines.append(f"{ind}GENERIC (lines {b.pos.line if b.pos else '?'}) [live_out={sorted(b.live_out or [])}]")
+                if level.startswith("runtime"):
+                    for ins in b.instrs or []:
+                        lines.append(f"{ind}  {ins.opcode} {list(ins.ins)} -> {ins.out}")
+                else:
+                    roots = list(b.roots) + [h for k, h in b.env_out.items()]
+                    lines.append(explain_dag(roots, ind + "  "))
+            elif isinstance(b, IfBlock):
+                lines.append(f"{ind}IF")
+                blocks(b.then_blocks, ind + "  ")
+                lines.append(f"{ind}ELSE")
+                blocks(b.else_blocks, ind + "  ")
+            elif isinstance(b, WhileBlock):
+                lines.append(f"{ind}WHILE")
+                blocks(b.body, ind + "  ")
+            elif isinstance(b, ForBlock):
+                lines.append(f"{ind}{'PARFOR' if b.parfor else 'FOR'} {b.var}")
+                blocks(b.body, ind + "  ")
+
+    for key, fb in cp.functions.items():
+        if fb.body is not None:
+            lines.append(f"FUNCTION {key[0]}::{key[1]}")
+            blocks(fb.body, "  ")
+    lines.append("MAIN PROGRAM")
+    blocks(cp.blocks, "  ")
+    return "\n".join(lines)

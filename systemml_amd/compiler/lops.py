@@ -1,0 +1,118 @@
+"""Linearise HOP DAGs into flat instruction lists (the role of the LOP layer,
+reference: lops/compile/Dag.java + hops/Hop.constructLops).
+
+Each basic block becomes a list of ``Instr`` executing over a per-block slot
+array.  Emission order follows statement order of the side-effecting roots
+(prints, writes, stop, function calls) so observable behaviour matches the
+reference, with every pure hop emitted lazily at its first use (post-order).
+After its last use a slot is cleared so large intermediates are released from
+HBM as early as possible (the reference's rmvar/cpvar bookkeeping).
+"""
+from __future__ import annotations
+
+from .hops import walk
+from .blocks import BasicBlock, IfBlock, WhileBlock, ForBlock, Predicate
+from . import rewrites as RW
+
+
+class Instr:
+    __slots__ = ("fn", "ins", "out", "hop", "free", "opcode")
+
+    def __init__(self, fn, ins, out, hop, opcode):
+        self.fn = fn
+        self.ins = ins
+        self.out = out
+        self.hop = hop
+        self.free = ()
+        self.opcode = opcode
+
+    def __repr__(self):
+        return f"{self.opcode} {list(self.ins)} -> {self.out}"
+
+
+def _linearize(roots, tail_writes, make_impl):
+    """roots: ordered hops to evaluate; tail_writes: list of (name, hop)."""
+    order = []
+    seen = set()
+    for r in roots:
+        for h in walk([r]):
+            if h.id not in seen:
+                seen.add(h.id)
+                order.append(h)
+    for _, h in tail_writes:
+        for x in walk([h]):
+            if x.id not in seen:
+                seen.add(x.id)
+                order.append(x)
+    slot_of = {}
+    instrs = []
+    for i, h in enumerate(order):
+        slot_of[h.id] = i
+        fn, opcode = make_impl(h)
+        instrs.append(Instr(fn, tuple(slot_of[c.id] for c in h.inputs), i, h, opcode))
+    # last-use analysis (tail writes use slots at the very end)
+    last = {}
+    for idx, ins in enumerate(instrs):
+        for s in ins.ins:
+            last[s] = idx
+    keep = {slot_of[h.id] for _, h in tail_writes}
+    frees = {}
+    for s, idx in last.items():
+        if s in keep:
+            continue
+        frees.setdefault(idx, []).append(s)
+    for idx, ins in enumerate(instrs):
+        f = frees.get(idx)
+        if f:
+            ins.free = tuple(s for s in f if s != ins.out)
+    writes = [(name, slot_of[h.id]) for name, h in tail_writes]
+    return instrs, writes, len(order)
+
+
+def compile_basic_block(bb: BasicBlock, make_impl, config=None):
+    RW.rewrite_block(bb, config)
+    live = bb.live_out
+    tail = []
+    for name, h in bb.env_out.items():
+        if live is None or name in live:
+            if h.op == "tread" and h.p["name"] == name:
+                continue     # x = x: nothing to write
+            tail.append((name, h))
+    bb.instrs, bb.writes_slots, bb.nslots = _linearize(bb.roots, tail, make_impl)
+
+
+def compile_predicate(pred: Predicate, make_impl, config=None):
+    RW.rewrite_pred(pred, config)
+    instrs, _, n = _linearize([pred.root], [], make_impl)
+    pred.instrs = instrs
+    pred.nslots = n
+    pred.out = n - 1
+
+
+def compile_blocks(blocks, make_impl, config=None):
+    for b in blocks:
+        if isinstance(b, BasicBlock):
+            compile_basic_block(b, make_impl, config)
+        elif isinstance(b, IfBlock):
+            compile_predicate(b.pred, make_impl, config)
+            compile_blocks(b.then_blocks, make_impl, config)
+            compile_blocks(b.else_blocks, make_impl, config)
+        elif isinstance(b, WhileBlock):
+            compile_predicate(b.pred, make_impl, config)
+            compile_blocks(b.body, make_impl, config)
+        elif isinstance(b, ForBlock):
+            compile_predicate(b.start, make_impl, config)
+            compile_predicate(b.end, make_impl, config)
+            if b.incr is not None:
+                compile_predicate(b.incr, make_impl, config)
+            compile_blocks(b.body, make_impl, config)
+
+
+def compile_program(cp, make_impl, config=None):
+    compile_blocks(cp.blocks, make_impl, config)
+    for fb in cp.functions.values():
+        if fb.body is not None:
+            compile_blocks(fb.body, make_impl, config)
+        for p in fb.default_preds.values():
+            compile_predicate(p, make_impl, config)
+    return cp

@@ -1,0 +1,288 @@
+"""Static HOP rewrites (reference: hops/rewrite/RewriteConstantFolding.java,
+RewriteAlgebraicSimplificationStatic.java, RewriteAlgebraicSimplificationDynamic.java,
+RewriteCommonSubexpressionElimination.java and the fused-operator selection of
+hops/AggBinaryOp.java (MMTSJ / MapMultChain) and hops/codegen row templates).
+
+Rules implemented (applied bottom-up until fixpoint per node):
+  * constant folding of scalar binary / unary ops
+  * t(t(X)) -> X ; X*1, 1*X, X/1, X+0, 0+X, X-0, X^1 -> X
+  * sum(X^2) -> sumsq(X); rowSums(X^2) / colSums(X^2) -> row/col sumsq
+  * sum(X*Y) -> tak(X,Y)  (ternary aggregate, no materialised product)
+  * sum(t(X)) -> sum(X)
+  * t(X) %*% Y -> mm(X, Y, transA)      (no materialised transpose)
+  * t(X) %*% X -> tsmm(X, LEFT),  X %*% t(X) -> tsmm(X, RIGHT)
+  * t(X)%*%(X%*%v)        -> mmchain XtXv
+    t(X)%*%(w*(X%*%v))    -> mmchain XtwXv
+    t(X)%*%((X%*%v)-y)    -> mmchain XtXvy
+    t(X)%*%(Q - P*rowSums(Q)), Q = P*(X%*%V)  -> mmchain XtPSXv (multinomial-logreg
+        Hessian-vector product; a codegen "Row template" instance)
+  * A op (v %*% matrix(1,1,k)) -> A op v  (unnecessary outer product → broadcast)
+  * common subexpression elimination (hash consing)
+"""
+from __future__ import annotations
+
+from ..runtime import scalars as S
+from ..parser.errors import DMLRuntimeError
+from .hops import Hop, lit
+from . import hops as H
+
+CELLWISE = {"+", "-", "*", "/", "^", "%%", "%/%", "==", "!=", "<", "<=", ">", ">=", "&", "|",
+            "min", "max", "xor"}
+
+
+def _is_lit(h, v=None):
+    if h.op != "lit":
+        return False
+    if v is None:
+        return True
+    x = h.value
+    return isinstance(x, (int, float)) and not isinstance(x, bool) and x == v
+
+
+def _is_ones_matrix(h, rows1=None, cols1=None):
+    """matrix(1, rows=.., cols=..) datagen with literal fill 1."""
+    if h.op != "bi" or h.p.get("name") != "matrix":
+        return False
+    if not h.inputs or not _is_lit(h.inputs[0], 1):
+        return False
+    args = _bi_args(h)
+    r = args.get("rows")
+    c = args.get("cols")
+    if rows1 and not (r is not None and _is_lit(r, 1)):
+        return False
+    if cols1 and not (c is not None and _is_lit(c, 1)):
+        return False
+    return True
+
+
+def _bi_args(h):
+    npos = h.p.get("npos", len(h.inputs) - len(h.named))
+    names = ["data", "rows", "cols"] if h.p.get("name") == "matrix" else []
+    out = {}
+    for i in range(npos):
+        if i < len(names):
+            out[names[i]] = h.inputs[i]
+    for j, n in enumerate(h.named):
+        out[n] = h.inputs[npos + j]
+    return out
+
+
+class Rewriter:
+    def __init__(self, config=None):
+        self.config = config
+        self.memo = {}
+        self.enabled = True if config is None else getattr(config, "rewrites", True)
+        self.fuse = True if config is None else getattr(config, "fusion", True)
+        self.stats = {}
+
+    def _count(self, name):
+        self.stats[name] = self.stats.get(name, 0) + 1
+
+    def rewrite(self, h: Hop) -> Hop:
+        r = self.memo.get(h.id)
+        if r is not None:
+            return r
+        new_inputs = [self.rewrite(c) for c in h.inputs]
+        if any(a is not b for a, b in zip(new_inputs, h.inputs)):
+            n = Hop(h.op, new_inputs, dict(h.p), list(h.named), h.dt, h.dim1, h.dim2, h.pos)
+            # keep identity for non-pure hops (fcall/sink) so ordering references stay valid
+            if h.op in ("fcall", "sink", "tread", "fout") or (h.op == "bi" and h.p.get("name") in H.NONDETERMINISTIC):
+                h.inputs = new_inputs
+                n = h
+        else:
+            n = h
+        if self.enabled:
+            for _ in range(8):
+                m = self.apply_rules(n)
+                if m is n:
+                    break
+                n = m
+        self.memo[h.id] = n
+        return n
+
+    # ------------------------------------------------------------------ rules
+    def apply_rules(self, h: Hop) -> Hop:
+        op = h.op
+        if op == "b":
+            return self._rw_binary(h)
+        if op == "u":
+            x = h.inputs[0]
+            if x.op == "lit" and x.value is not None and h.p["o"] not in ("nrow", "ncol", "length",
+                                                                           "cast_matrix", "cast_frame",
+                                                                           "cast_list") \
+                    and h.p["o"] not in ("cumsum", "cumprod", "cummin", "cummax"):
+                try:
+                    return lit(S.unary(h.p["o"], x.value))
+                except (DMLRuntimeError, TypeError, ValueError):
+                    return h
+            if h.p["o"] == "neg" and x.op == "u" and x.p["o"] == "neg":
+                return x.inputs[0]
+            return h
+        if op == "t":
+            x = h.inputs[0]
+            if x.op == "t":
+                self._count("t(t(X))")
+                return x.inputs[0]
+            return h
+        if op == "agg":
+            return self._rw_agg(h)
+        if op == "mm":
+            return self._rw_mm(h)
+        return h
+
+    def _rw_binary(self, h):
+        a, b = h.inputs
+        o = h.p["o"]
+        if a.op == "lit" and b.op == "lit" and a.value is not None and b.value is not None:
+            try:
+                return lit(S.binary(o, a.value, b.value))
+            except DMLRuntimeError:
+                return h
+        # identities only when the non-literal side is a matrix (keeps scalar value types exact)
+        if a.dt == "M" and b.op == "lit":
+            if (o in ("*", "/", "^") and _is_lit(b, 1)) or (o in ("+", "-") and _is_lit(b, 0)):
+                self._count("identity")
+                return a
+        if b.dt == "M" and a.op == "lit":
+            if (o == "*" and _is_lit(a, 1)) or (o == "+" and _is_lit(a, 0)):
+                self._count("identity")
+                return b
+        # remove unnecessary outer product with ones: A op (v %*% matrix(1,1,k))
+        if o in CELLWISE:
+            if b.op == "mm" and not b.p.get("transA") and _is_ones_matrix(b.inputs[1], rows1=True):
+                if a.dt == "M":
+                    self._count("outer-ones")
+                    return Hop("b", [a, b.inputs[0]], dict(h.p), dt="M", pos=h.pos)
+            if a.op == "mm" and not a.p.get("transA") and _is_ones_matrix(a.inputs[1], rows1=True):
+                if b.dt == "M":
+                    self._count("outer-ones")
+                    return Hop("b", [a.inputs[0], b], dict(h.p), dt="M", pos=h.pos)
+        return h
+
+    def _rw_agg(self, h):
+        x = h.inputs[0]
+        o, d = h.p["o"], h.p["dir"]
+        if o == "sum":
+            if x.op == "b" and x.p["o"] == "^" and _is_lit(x.inputs[1], 2) and x.inputs[0].dt != "S":
+                self._count("sumsq")
+                return Hop("agg", [x.inputs[0]], {"o": "sumsq", "dir": d}, dt=h.dt, pos=h.pos)
+            if d == "all" and x.op == "b" and x.p["o"] == "*" and x.inputs[0].dt == "M" and x.inputs[1].dt == "M":
+                if x.inputs[0] is x.inputs[1]:
+                    self._count("sumsq")
+                    return Hop("agg", [x.inputs[0]], {"o": "sumsq", "dir": "all"}, dt="S", pos=h.pos)
+                self._count("tak+*")
+                return Hop("tak", [x.inputs[0], x.inputs[1]], {}, dt="S", pos=h.pos)
+            if d == "all" and x.op == "t":
+                return Hop("agg", [x.inputs[0]], dict(h.p), dt="S", pos=h.pos)
+        return h
+
+    def _rw_mm(self, h):
+        a, b = h.inputs
+        transA = h.p.get("transA", False)
+        if not transA and a.op == "t":
+            X = a.inputs[0]
+            if b is X:
+                self._count("tsmm")
+                return Hop("tsmm", [X], {"left": True}, dt="M", pos=h.pos)
+            self._count("t(X)%*%Y")
+            n = Hop("mm", [X, b], {"transA": True}, dt="M", pos=h.pos)
+            return self._rw_mm(n)
+        if not transA and b.op == "t" and b.inputs[0] is a:
+            self._count("tsmm")
+            return Hop("tsmm", [a], {"left": False}, dt="M", pos=h.pos)
+        if transA and self.fuse:
+            X = a
+            m = self._match_mmchain(X, b)
+            if m is not None:
+                return m
+        return h
+
+    def _match_mmchain(self, X, g):
+        def is_xv(n):
+            return n.op == "mm" and not n.p.get("transA") and n.inputs[0] is X
+
+        # XtXv
+        if is_xv(g):
+            self._count("mmchain")
+            return Hop("mmchain", [X, g.inputs[1]], {"type": "XtXv"}, dt="M")
+        if g.op == "b":
+            o = g.p["o"]
+            l, r = g.inputs
+            if o == "*":
+                if is_xv(r) and l.dt == "M":
+                    self._count("mmchain")
+                    return Hop("mmchain", [X, r.inputs[1], l], {"type": "XtwXv"}, dt="M")
+                if is_xv(l) and r.dt == "M":
+                    self._count("mmchain")
+                    return Hop("mmchain", [X, l.inputs[1], r], {"type": "XtwXv"}, dt="M")
+            if o == "-" and is_xv(l) and r.dt == "M":
+                self._count("mmchain")
+                return Hop("mmchain", [X, l.inputs[1], r], {"type": "XtXvy"}, dt="M")
+            # multinomial logreg Hessian-vector product:  Q - P * rowSums(Q),  Q = P * (X %*% V)
+            if o == "-":
+                Q = l
+                if Q.op == "b" and Q.p["o"] == "*":
+                    P = None
+                    q0, q1 = Q.inputs
+                    if is_xv(q1):
+                        P, xv = q0, q1
+                    elif is_xv(q0):
+                        P, xv = q1, q0
+                    if P is not None and r.op == "b" and r.p["o"] == "*":
+                        r0, r1 = r.inputs
+                        for pp, rs in ((r0, r1), (r1, r0)):
+                            if pp is P and rs.op == "agg" and rs.p["o"] == "sum" and rs.p["dir"] == "row" \
+                                    and rs.inputs[0] is Q:
+                                self._count("mmchain-row")
+                                return Hop("mmchain", [X, xv.inputs[1], P], {"type": "XtPSXv"}, dt="M")
+        return None
+
+
+def cse(roots):
+    """Hash-consing common subexpression elimination over a set of roots."""
+    table = {}
+    memo = {}
+
+    def visit(h):
+        r = memo.get(h.id)
+        if r is not None:
+            return r
+        new_inputs = [visit(c) for c in h.inputs]
+        if any(a is not b for a, b in zip(new_inputs, h.inputs)):
+            h.inputs = new_inputs
+        if h.op in ("fcall", "sink", "fout", "lix") or (h.op == "bi" and h.p.get("name") in H.NONDETERMINISTIC
+                                                        | {"exists", "time", "eval", "list"}):
+            memo[h.id] = h
+            return h
+        if h.op == "lit":
+            v = h.value
+            k = ("lit", S.vtype_of(v), "NaN" if isinstance(v, float) and v != v else v)
+        else:
+            k = h.key()
+        old = table.get(k)
+        if old is None:
+            table[k] = h
+            old = h
+        memo[h.id] = old
+        return old
+
+    return [visit(r) for r in roots], visit
+
+
+def rewrite_block(bb, config=None):
+    """Rewrite a BasicBlock's DAG in place (roots + env_out)."""
+    rw = Rewriter(config)
+    bb.roots = [rw.rewrite(r) for r in bb.roots]
+    bb.env_out = {k: rw.rewrite(v) for k, v in bb.env_out.items()}
+    roots, visit = cse(bb.roots)
+    bb.roots = roots
+    bb.env_out = {k: visit(v) for k, v in bb.env_out.items()}
+    return rw.stats
+
+
+def rewrite_pred(pred, config=None):
+    rw = Rewriter(config)
+    pred.root = rw.rewrite(pred.root)
+    if pred.root.op == "lit":
+        pred.is_const = True
+        pred.const = pred.root.value

@@ -1,0 +1,677 @@
+"""AST → statement blocks → HOP DAGs (reference: parser/DMLTranslator.java,
+parser/StatementBlock.java, parser/LiveVariableAnalysis.java,
+hops/ipa/IPAPassPropagateReplaceLiterals.java,
+hops/rewrite/RewriteRemoveUnnecessaryBranches.java,
+hops/rewrite/RewriteMergeBlockSequence.java).
+
+Responsibilities:
+  * resolve `source(...) as ns` imports into a namespaced function table,
+  * substitute command-line parameters ($name / ifdef),
+  * split statements into basic blocks at control flow,
+  * propagate scalar constants across blocks and remove constant branches
+    (the spliced branch merges into the surrounding basic block so that
+    operator fusion sees a single DAG),
+  * build a HOP DAG per basic block (with on-the-fly constant folding and
+    hash-consing CSE),
+  * live-variable analysis (transient writes only for live-out variables,
+    rmvar for dead ones).
+"""
+from __future__ import annotations
+
+import os
+import math
+
+from ..parser import ast as A
+from ..parser.errors import LanguageError, DMLRuntimeError
+from ..parser.dml_parser import parse_dml_file
+from ..runtime import scalars as S
+from . import hops as H
+from .hops import Hop, lit
+from .blocks import BasicBlock, IfBlock, WhileBlock, ForBlock, FunctionBlock, Predicate, CompiledProgram
+
+DEFAULT_NS = ".defaultNS"
+
+BUILTIN_CONSTANTS = {"NaN": float("nan"), "Inf": float("inf"), "pi": math.pi, "INF": float("inf"),
+                     "NAN": float("nan"), "PI": math.pi}
+
+UNARY_MATH = {"abs", "exp", "sqrt", "round", "floor", "ceil", "sign", "sin", "cos", "tan", "asin",
+              "acos", "atan", "sinh", "cosh", "tanh"}
+CUMAGG = {"cumsum", "cumprod", "cummin", "cummax"}
+FULL_AGG = {"sum": "sum", "prod": "prod", "mean": "mean", "avg": "mean", "var": "var", "sd": "sd",
+            "trace": "trace"}
+ROWCOL_AGG = {
+    "rowSums": ("sum", "row"), "colSums": ("sum", "col"),
+    "rowMeans": ("mean", "row"), "colMeans": ("mean", "col"),
+    "rowMaxs": ("max", "row"), "colMaxs": ("max", "col"),
+    "rowMins": ("min", "row"), "colMins": ("min", "col"),
+    "rowVars": ("var", "row"), "colVars": ("var", "col"),
+    "rowSds": ("sd", "row"), "colSds": ("sd", "col"),
+    "rowProds": ("prod", "row"), "colProds": ("prod", "col"),
+    "rowIndexMax": ("imax", "row"), "rowIndexMin": ("imin", "row"),
+}
+CASTS = {"as.scalar": "cast_scalar", "castAsScalar": "cast_scalar", "as.matrix": "cast_matrix",
+         "as.double": "cast_double", "as.integer": "cast_int", "as.logical": "cast_bool",
+         "as.frame": "cast_frame", "as.list": "cast_list"}
+BINARY_FNS = {"xor": "xor", "bitwAnd": "bitwAnd", "bitwOr": "bitwOr", "bitwXor": "bitwXor",
+              "bitwShiftL": "bitwShiftL", "bitwShiftR": "bitwShiftR"}
+SCALAR_FOLD_UNARY = UNARY_MATH | {"neg", "not", "cast_double", "cast_int", "cast_bool", "log"}
+
+
+class FileCtx:
+    """Per-source-file namespace context."""
+
+    def __init__(self, key, path, imports):
+        self.key = key            # namespace key for this file's functions
+        self.path = path
+        self.imports = imports    # alias -> namespace key
+
+
+class Translator:
+    def __init__(self, args=None, config=None, base_dir=None):
+        self.args = dict(args or {})
+        self.config = config
+        self.base_dir = base_dir or os.getcwd()
+        self.functions = {}       # (nskey, name) -> FunctionBlock
+        self.func_defs = {}       # (nskey, name) -> (FunctionDef, FileCtx)
+        self.loaded_files = {}    # abs path -> FileCtx
+
+    # ------------------------------------------------------------------ imports
+    def _register_file(self, prog: A.Program, key, path):
+        ctx = FileCtx(key, path, {})
+        base = os.path.dirname(path) if path else self.base_dir
+        for st in prog.statements:
+            if isinstance(st, A.SetWd):
+                base = st.path if os.path.isabs(st.path) else os.path.join(base, st.path)
+            if isinstance(st, A.Import):
+                ipath = st.path
+                cand = [ipath if os.path.isabs(ipath) else os.path.join(base, ipath),
+                        os.path.join(self.base_dir, ipath), ipath]
+                cand += _package_script_candidates(ipath)
+                full = next((c for c in cand if os.path.exists(c)), None)
+                if full is None:
+                    raise LanguageError(f"{st.pos}: cannot find sourced file '{ipath}'")
+                full = os.path.abspath(full)
+                if full not in self.loaded_files:
+                    sub = parse_dml_file(full) if not full.endswith(".pydml") else _parse_pydml_file(full)
+                    self.loaded_files[full] = None   # guard recursion
+                    self.loaded_files[full] = self._register_file(sub, full, full)
+                ctx.imports[st.namespace] = full
+        for name, fd in prog.functions.items():
+            self.func_defs[(key, name)] = (fd, ctx)
+        return ctx
+
+    # ------------------------------------------------------------------ compile
+    def compile(self, prog: A.Program, inputs=(), outputs=()):
+        main_ctx = self._register_file(prog, DEFAULT_NS, prog.source_path)
+        self.inputs = set(inputs)
+        # compile all functions (bodies built lazily with empty const env)
+        for (key, name), (fd, ctx) in list(self.func_defs.items()):
+            self.functions[(key, name)] = FunctionBlock(name, key, fd.inputs, fd.outputs, None,
+                                                        external=fd.external, ext_params=fd.ext_params,
+                                                        pos=fd.pos)
+        for (key, name), (fd, ctx) in list(self.func_defs.items()):
+            fb = self.functions[(key, name)]
+            if not fd.external:
+                consts = {}
+                fb.body = self.build_stmts(fd.body, ctx, consts, params=fd.inputs)
+                for p in fd.inputs:
+                    if p.default is not None:
+                        bb = _BBuilder(self, ctx, {})
+                        h = bb.expr(p.default)
+                        fb.default_preds[p.name] = Predicate(h, bb.reads)
+        blocks = self.build_stmts(prog.statements, main_ctx, {})
+        cp = CompiledProgram(blocks, self.functions, prog.source_path)
+        # liveness
+        for fb in self.functions.values():
+            if fb.body is not None:
+                liveness(fb.body, set(o.name for o in fb.outputs))
+        live_in = liveness(blocks, set(outputs) if outputs else None)
+        cp.inputs = live_in
+        undefined = live_in - set(inputs)
+        if undefined and self.config is not None and getattr(self.config, "strict_undefined", True):
+            pass  # reported at runtime with position info (variables may be defined conditionally)
+        cp.outputs = set(outputs)
+        return cp
+
+    # ------------------------------------------------------------------ blocks
+    def build_stmts(self, stmts, ctx, consts, params=None):
+        """Returns list of blocks. `consts` is updated in place with constants known at exit."""
+        blocks = []
+        cur = _BBuilder(self, ctx, consts)
+
+        def flush():
+            nonlocal cur
+            if cur.has_content():
+                bb = cur.finish()
+                blocks.append(bb)
+                consts.clear()
+                consts.update(cur.out_consts())
+            cur = _BBuilder(self, ctx, consts)
+
+        def process(lst):
+            nonlocal cur
+            for st in lst:
+                if isinstance(st, (A.Assign, A.MultiAssign, A.ExprStmt)):
+                    cur.add(st)
+                elif isinstance(st, (A.Import, A.SetWd)):
+                    continue
+                elif isinstance(st, A.If):
+                    ph = cur.try_const(st.pred)
+                    if ph is not None:
+                        process(st.then_body if S.as_bool(ph) else st.else_body)
+                        continue
+                    flush()
+                    pb = _BBuilder(self, ctx, consts)
+                    pred = Predicate(pb.expr(st.pred), pb.reads)
+                    c1, c2 = dict(consts), dict(consts)
+                    tb = self.build_stmts(st.then_body, ctx, c1)
+                    eb = self.build_stmts(st.else_body, ctx, c2)
+                    blocks.append(IfBlock(pred, tb, eb, pos=st.pos))
+                    merged = {k: v for k, v in c1.items() if k in c2 and _same(c2[k], v)}
+                    consts.clear()
+                    consts.update(merged)
+                    cur = _BBuilder(self, ctx, consts)
+                elif isinstance(st, A.While):
+                    flush()
+                    assigned = assigned_vars(st.body)
+                    for v in assigned:
+                        consts.pop(v, None)
+                    pb = _BBuilder(self, ctx, consts)
+                    pred = Predicate(pb.expr(st.pred), pb.reads)
+                    body = self.build_stmts(st.body, ctx, dict(consts))
+                    blocks.append(WhileBlock(pred, body, pos=st.pos))
+                    cur = _BBuilder(self, ctx, consts)
+                elif isinstance(st, A.For):
+                    flush()
+                    assigned = assigned_vars(st.body) | {st.var}
+                    pb = _BBuilder(self, ctx, consts)
+                    p_from = Predicate(pb.expr(st.start), pb.reads)
+                    pb2 = _BBuilder(self, ctx, consts)
+                    p_to = Predicate(pb2.expr(st.end), pb2.reads)
+                    p_incr = None
+                    if st.incr is not None:
+                        pb3 = _BBuilder(self, ctx, consts)
+                        p_incr = Predicate(pb3.expr(st.incr), pb3.reads)
+                    params = {}
+                    for k, v in st.params.items():
+                        pbk = _BBuilder(self, ctx, consts)
+                        hv = pbk.expr(v)
+                        params[k] = hv.p.get("v") if hv.op == "lit" else None
+                        if hv.op == "tread" or (hv.op != "lit" and isinstance(v, A.Ident)):
+                            params[k] = v.name if isinstance(v, A.Ident) else None
+                    for v in assigned:
+                        consts.pop(v, None)
+                    body = self.build_stmts(st.body, ctx, dict(consts))
+                    fb = ForBlock(st.var, p_from, p_to, p_incr, body, parfor=st.parfor, params=params, pos=st.pos)
+                    blocks.append(fb)
+                    cur = _BBuilder(self, ctx, consts)
+                else:
+                    raise LanguageError(f"unsupported statement {type(st).__name__}")
+
+        process(stmts)
+        flush()
+        return blocks
+
+    def resolve_function(self, ctx: FileCtx, ns, name):
+        if ns is not None:
+            key = ctx.imports.get(ns)
+            if key is None:
+                raise LanguageError(f"unknown namespace '{ns}'")
+            fb = self.functions.get((key, name))
+            if fb is None:
+                raise LanguageError(f"function '{ns}::{name}' not found")
+            return fb
+        return self.functions.get((ctx.key, name))
+
+
+def _package_script_candidates(path):
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    scripts = os.path.join(here, "scripts")
+    p = path
+    out = [os.path.join(scripts, p)]
+    if p.startswith("scripts/"):
+        out.append(os.path.join(here, p))
+    if p.startswith("nn/"):
+        out.append(os.path.join(scripts, p))
+    return out
+
+
+def _parse_pydml_file(path):
+    from ..parser.pydml_parser import parse_pydml_file
+    return parse_pydml_file(path)
+
+
+def _same(a, b):
+    if isinstance(a, float) and isinstance(b, float) and a != a and b != b:
+        return True
+    return type(a) == type(b) and a == b
+
+
+def assigned_vars(stmts):
+    out = set()
+    for st in stmts:
+        if isinstance(st, A.Assign):
+            t = st.target
+            out.add(t.name)
+        elif isinstance(st, A.MultiAssign):
+            for t in st.targets:
+                out.add(t.name)
+        elif isinstance(st, A.If):
+            out |= assigned_vars(st.then_body) | assigned_vars(st.else_body)
+        elif isinstance(st, A.While):
+            out |= assigned_vars(st.body)
+        elif isinstance(st, A.For):
+            out |= assigned_vars(st.body) | {st.var}
+    return out
+
+
+# ============================================================================
+# Basic block builder: statements -> HOP DAG
+# ============================================================================
+class _BBuilder:
+    def __init__(self, tr: Translator, ctx: FileCtx, consts: dict):
+        self.tr = tr
+        self.ctx = ctx
+        self.consts = dict(consts)
+        self.env = {}            # var -> hop
+        self.treads = {}         # var -> tread hop
+        self.reads = set()
+        self.cse = {}
+        self.roots = []          # ordered sink hops (incl. fcalls)
+        self.stmt_count = 0
+        self.pos = None
+
+    def has_content(self):
+        return self.stmt_count > 0
+
+    # -- CSE-aware hop creation --------------------------------------------
+    def mk(self, op, inputs=(), p=None, named=None, dt="U", dim1=-1, dim2=-1, pos=None, cse=True):
+        h = Hop(op, inputs, p, named, dt, dim1, dim2, pos)
+        if cse:
+            k = h.key()
+            old = self.cse.get(k)
+            if old is not None:
+                return old
+            self.cse[k] = h
+        for c in h.inputs:
+            c.parents.append(h)
+        return h
+
+    def lit(self, v, pos=None):
+        h = lit(v, pos)
+        k = ("lit", S.vtype_of(v), "NaN" if isinstance(v, float) and v != v else v)
+        old = self.cse.get(k)
+        if old is not None:
+            return old
+        self.cse[k] = h
+        return h
+
+    # -- statements ----------------------------------------------------------------
+    def add(self, st):
+        self.stmt_count += 1
+        if self.pos is None:
+            self.pos = st.pos
+        if isinstance(st, A.Assign):
+            if st.ifdef is not None:
+                name = st.ifdef.name
+                if name in self.tr.args:
+                    val = self.lit(S.parse_literal_arg(self.tr.args[name]))
+                else:
+                    val = self.expr(st.value)
+            else:
+                val = self.expr(st.value)
+            t = st.target
+            if st.accumulate:
+                cur = self.var(t.name, st.pos) if isinstance(t, A.Ident) else self.expr(t)
+                val = self.binary("+", cur, val, st.pos)
+            if isinstance(t, A.Ident):
+                self.env[t.name] = val
+            elif isinstance(t, A.Indexed):
+                target = self.var(t.name, st.pos)
+                rl, ru, cl, cu = self.index_bounds(t)
+                h = self.mk("lix", [target, val, rl, ru, cl, cu], p={"list": t.cols is None},
+                            dt=target.dt, dim1=target.dim1, dim2=target.dim2, pos=st.pos, cse=False)
+                self.env[t.name] = h
+            elif isinstance(t, A.CmdParam):
+                raise LanguageError(f"{st.pos}: cannot assign to command-line parameter ${t.name}")
+        elif isinstance(st, A.MultiAssign):
+            call = st.value
+            fb = self.tr.resolve_function(self.ctx, call.namespace, call.name)
+            if fb is None:
+                # multi-return builtins (eigen, svd, qr, lu, transformencode, ...)
+                h = self.builtin_call(call, multi=True)
+            else:
+                h = self.fcall(fb, call)
+            self.roots.append(h)
+            for i, t in enumerate(st.targets):
+                if not isinstance(t, A.Ident):
+                    raise LanguageError(f"{st.pos}: multi-assignment targets must be identifiers")
+                self.env[t.name] = self.mk("fout", [h], p={"i": i}, pos=st.pos, cse=False)
+        elif isinstance(st, A.ExprStmt):
+            h = self.expr(st.call)
+            if h.op in ("sink", "fcall"):
+                if h not in self.roots:
+                    self.roots.append(h)
+            else:
+                # value discarded; still evaluate builtin calls for errors (cheap ones are DCE'd)
+                pass
+
+    def try_const(self, e):
+        """Evaluate expression to a constant if possible (without recording reads)."""
+        saved = (set(self.reads), dict(self.treads))
+        try:
+            h = self.expr(e)
+        except (LanguageError, DMLRuntimeError):
+            h = None
+        self.reads, self.treads = saved
+        if h is not None and h.op == "lit":
+            return h.value
+        return None
+
+    def out_consts(self):
+        c = dict(self.consts)
+        for k, h in self.env.items():
+            if h.op == "lit":
+                c[k] = h.value
+            else:
+                c.pop(k, None)
+        return c
+
+    def finish(self) -> BasicBlock:
+        bb = BasicBlock()
+        bb.pos = self.pos
+        bb.roots = list(self.roots)
+        bb.env_out = dict(self.env)
+        bb.reads = set(self.reads)
+        bb.writes = set(self.env.keys())
+        return bb
+
+    # -- expressions ---------------------------------------------------------------
+    def var(self, name, pos=None):
+        if name in self.env:
+            return self.env[name]
+        if name in self.consts:
+            return self.lit(self.consts[name], pos)
+        h = self.treads.get(name)
+        if h is None:
+            h = Hop("tread", p={"name": name}, pos=pos)
+            self.treads[name] = h
+        self.reads.add(name)
+        return h
+
+    def expr(self, e) -> Hop:
+        if isinstance(e, A.Literal):
+            v = e.value
+            if e.vtype == "DOUBLE":
+                v = float(v)
+            elif e.vtype == "INT":
+                v = int(v)
+            return self.lit(v, e.pos)
+        if isinstance(e, A.Ident):
+            if e.name not in self.env and e.name not in self.consts and e.name in BUILTIN_CONSTANTS \
+                    and e.name not in self.tr.inputs:
+                return self.lit(BUILTIN_CONSTANTS[e.name], e.pos)
+            return self.var(e.name, e.pos)
+        if isinstance(e, A.CmdParam):
+            if e.name not in self.tr.args:
+                raise LanguageError(f"{e.pos}: command-line parameter ${e.name} not specified")
+            return self.lit(S.parse_literal_arg(self.tr.args[e.name]), e.pos)
+        if isinstance(e, A.BinOp):
+            l = self.expr(e.left)
+            r = self.expr(e.right)
+            if e.op == "%*%":
+                return self.mk("mm", [l, r], dt="M", pos=e.pos)
+            return self.binary(e.op, l, r, e.pos)
+        if isinstance(e, A.UnOp):
+            x = self.expr(e.operand)
+            if e.op == "+":
+                return x
+            return self.unary("neg" if e.op == "-" else "not", x, e.pos)
+        if isinstance(e, A.Indexed):
+            src = self.var(e.name, e.pos)
+            rl, ru, cl, cu = self.index_bounds(e)
+            return self.mk("rix", [src, rl, ru, cl, cu], p={"list": e.cols is None}, pos=e.pos)
+        if isinstance(e, A.Call):
+            fb = self.tr.resolve_function(self.ctx, e.namespace, e.name)
+            if fb is not None:
+                h = self.fcall(fb, e)
+                self.roots.append(h)
+                return self.mk("fout", [h], p={"i": 0}, pos=e.pos, cse=False)
+            return self.builtin_call(e)
+        if isinstance(e, A.ExprList):
+            return self.mk("bi", [self.expr(x) for x in e.items], p={"name": "list"}, pos=e.pos)
+        raise LanguageError(f"unsupported expression {type(e).__name__}")
+
+    def index_bounds(self, e: A.Indexed):
+        none = self.lit(None)
+
+        def rng(r):
+            if r is None:
+                return none, none
+            lo = self.expr(r.lower) if r.lower is not None else none
+            if r.is_range:
+                hi = self.expr(r.upper) if r.upper is not None else none
+            else:
+                hi = lo
+            return lo, hi
+
+        rl, ru = rng(e.rows)
+        cl, cu = rng(e.cols)
+        return rl, ru, cl, cu
+
+    def binary(self, op, l, r, pos=None):
+        if l.op == "lit" and r.op == "lit" and l.value is not None and r.value is not None:
+            try:
+                return self.lit(S.binary(op, l.value, r.value), pos)
+            except DMLRuntimeError:
+                pass
+        dt = "M" if (l.dt == "M" or r.dt == "M") else ("S" if (l.dt == "S" and r.dt == "S") else "U")
+        return self.mk("b", [l, r], p={"o": op}, dt=dt, pos=pos)
+
+    def unary(self, op, x, pos=None):
+        if x.op == "lit" and op in SCALAR_FOLD_UNARY and x.value is not None:
+            try:
+                return self.lit(S.unary(op, x.value), pos)
+            except (DMLRuntimeError, TypeError, ValueError):
+                pass
+        return self.mk("u", [x], p={"o": op}, dt=x.dt, pos=pos)
+
+    def fcall(self, fb: FunctionBlock, call: A.Call):
+        names = [p.name for p in fb.inputs]
+        pos_args, named = [], {}
+        for a in call.args:
+            if a.name is None:
+                if named:
+                    raise LanguageError(f"{call.pos}: positional argument after named argument")
+                pos_args.append(self.expr(a.value))
+            else:
+                named[a.name] = self.expr(a.value)
+        if len(pos_args) > len(names):
+            raise LanguageError(f"{call.pos}: too many arguments for function {call.name}")
+        bound = dict(zip(names, pos_args))
+        for k, v in named.items():
+            if k not in names:
+                raise LanguageError(f"{call.pos}: unknown parameter '{k}' for function {call.name}")
+            bound[k] = v
+        inputs, given = [], []
+        for n in names:
+            if n in bound:
+                inputs.append(bound[n])
+                given.append(n)
+        return self.mk("fcall", inputs, p={"fkey": (fb.namespace, fb.name), "given": tuple(given)},
+                       pos=call.pos, cse=False)
+
+    def builtin_call(self, call: A.Call, multi=False) -> Hop:
+        name = call.name
+        pos = call.pos
+        args = call.args
+        pos_args = [self.expr(a.value) for a in args if a.name is None]
+        named = [(a.name, self.expr(a.value)) for a in args if a.name is not None]
+        nd = dict(named)
+
+        if name in UNARY_MATH and len(args) == 1:
+            return self.unary(name if name != "ceiling" else "ceil", pos_args[0] if pos_args else named[0][1], pos)
+        if name == "ceiling":
+            return self.unary("ceil", pos_args[0], pos)
+        if name == "log":
+            if len(pos_args) == 1 and not named:
+                return self.unary("log", pos_args[0], pos)
+            x = pos_args[0]
+            b = pos_args[1] if len(pos_args) > 1 else nd.get("base")
+            return self.binary("log", x, b, pos)
+        if name in CUMAGG:
+            return self.mk("u", [pos_args[0]], p={"o": name}, dt="M", pos=pos)
+        if name in FULL_AGG and len(pos_args) == 1 and not named:
+            x = pos_args[0]
+            if x.dt == "S" and name in ("sum", "mean", "prod"):
+                return x
+            return self.mk("agg", [x], p={"o": FULL_AGG[name], "dir": "all"}, dt="S", dim1=0, dim2=0, pos=pos)
+        if name in ROWCOL_AGG and len(pos_args) == 1:
+            o, d = ROWCOL_AGG[name]
+            return self.mk("agg", [pos_args[0]], p={"o": o, "dir": d}, dt="M", pos=pos)
+        if name in ("min", "max", "pmin", "pmax"):
+            o = "min" if name in ("min", "pmin") else "max"
+            allargs = pos_args + [h for _, h in named]
+            if len(allargs) == 1:
+                return self.mk("agg", [allargs[0]], p={"o": o, "dir": "all"}, dt="S", dim1=0, dim2=0, pos=pos)
+            h = allargs[0]
+            for x in allargs[1:]:
+                h = self.binary(o, h, x, pos)
+            return h
+        if name in ("nrow", "ncol", "length"):
+            x = pos_args[0]
+            return self.mk("u", [x], p={"o": name}, dt="S", pos=pos)
+        if name == "t":
+            return self.mk("t", [pos_args[0]], dt="M", pos=pos)
+        if name in CASTS:
+            x = pos_args[0]
+            o = CASTS[name]
+            if x.op == "lit" and o in ("cast_double", "cast_int", "cast_bool", "cast_scalar"):
+                return self.unary(o, x, pos)
+            return self.mk("u", [x], p={"o": o}, dt="S" if o not in ("cast_matrix", "cast_frame", "cast_list") else "M", pos=pos)
+        if name in BINARY_FNS and len(pos_args) == 2:
+            return self.binary(BINARY_FNS[name], pos_args[0], pos_args[1], pos)
+        if name == "ppred":
+            opmap = {">": ">", ">=": ">=", "<": "<", "<=": "<=", "==": "==", "!=": "!="}
+            o = pos_args[2].value if len(pos_args) > 2 else nd["op"].value
+            return self.binary(opmap[o], pos_args[0], pos_args[1], pos)
+        if name == "exists":
+            a = args[0].value
+            vn = a.name if isinstance(a, A.Ident) else None
+            if vn is not None:
+                return self.mk("bi", [], p={"name": "exists", "var": vn}, dt="S", pos=pos, cse=False)
+        if name == "ifelse" and all(h.op == "lit" for h in pos_args) and len(pos_args) == 3:
+            return pos_args[1] if S.as_bool(pos_args[0].value) else pos_args[2]
+        if name == "time":
+            return self.mk("bi", [], p={"name": "time"}, dt="S", pos=pos, cse=False)
+        if name == "eval":
+            # dynamic function call: resolve at runtime in this file context
+            return self._eval_call(pos_args, named, pos)
+        side = name in H.SIDE_EFFECT
+        nondet = name in H.NONDETERMINISTIC or (name in ("rand", "sample") and
+                                               not _has_literal_seed(nd))
+        inputs = pos_args + [h for _, h in named]
+        h = self.mk("sink" if side else "bi", inputs, p={"name": name, "npos": len(pos_args)},
+                    named=[n for n, _ in named], pos=pos, cse=not (side or nondet or multi))
+        if side:
+            self.roots.append(h)
+        return h
+
+    def _eval_call(self, pos_args, named, pos):
+        inputs = pos_args + [h for _, h in named]
+        return self.mk("bi", inputs, p={"name": "eval", "npos": len(pos_args), "nskey": self.ctx.key,
+                                        "imports": tuple(sorted(self.ctx.imports.items()))},
+                       named=[n for n, _ in named], pos=pos, cse=False)
+
+
+def _has_literal_seed(nd):
+    s = nd.get("seed")
+    return s is not None and s.op == "lit" and s.value is not None and s.value != -1
+
+
+# ============================================================================
+# Live variable analysis (reference: parser/LiveVariableAnalysis.java)
+# ============================================================================
+def _blocks_gen_kill(blocks):
+    """Upward-exposed reads (gen) and definite writes (kill) of a block list."""
+    gen, kill = set(), set()
+    for b in blocks:
+        g, k = _block_gen_kill(b)
+        gen |= (g - kill)
+        kill |= k
+    return gen, kill
+
+
+def _block_gen_kill(b):
+    if isinstance(b, BasicBlock):
+        return set(b.reads), set(b.writes)
+    if isinstance(b, IfBlock):
+        g1, k1 = _blocks_gen_kill(b.then_blocks)
+        g2, k2 = _blocks_gen_kill(b.else_blocks)
+        return b.pred.reads | g1 | g2, k1 & k2
+    if isinstance(b, WhileBlock):
+        g, _ = _blocks_gen_kill(b.body)
+        return b.pred.reads | g, set()
+    if isinstance(b, ForBlock):
+        g, _ = _blocks_gen_kill(b.body)
+        r = b.start.reads | b.end.reads | (b.incr.reads if b.incr else set())
+        return r | (g - {b.var}), set()
+    return set(), set()
+
+
+def liveness(blocks, live_out_final=None):
+    """Backward pass setting BasicBlock.live_out / rmvars. Returns live-in set of the list."""
+    live = set(live_out_final) if live_out_final is not None else set()
+    return _live_list(blocks, live)
+
+
+def _live_list(blocks, live_after):
+    live = set(live_after)
+    for b in reversed(blocks):
+        live = _live_block(b, live)
+    return live
+
+
+def _live_block(b, live_after):
+    if isinstance(b, BasicBlock):
+        b.live_out = set(live_after)
+        b.rmvars = sorted((b.reads | b.writes) - b.live_out)
+        return (b.live_out - b.writes) | b.reads
+    if isinstance(b, IfBlock):
+        l1 = _live_list(b.then_blocks, live_after)
+        l2 = _live_list(b.else_blocks, live_after)
+        return l1 | l2 | b.pred.reads
+    if isinstance(b, (WhileBlock, ForBlock)):
+        if isinstance(b, WhileBlock):
+            preds = set(b.pred.reads)
+        else:
+            preds = b.start.reads | b.end.reads | (b.incr.reads if b.incr else set())
+        end = set(live_after) | preds
+        for _ in range(10):
+            lin = _live_list(b.body, end)
+            new_end = set(live_after) | preds | lin
+            if isinstance(b, ForBlock):
+                new_end.discard(b.var)
+            if new_end == end:
+                break
+            end = new_end
+        lin = _live_list(b.body, end)
+        if isinstance(b, ForBlock):
+            b.result_vars = sorted(set(live_after) & _all_writes(b.body))
+            lin = lin - {b.var}
+        return lin | preds | set(live_after)
+    return set(live_after)
+
+
+def _all_writes(blocks):
+    out = set()
+    for b in blocks:
+        if isinstance(b, BasicBlock):
+            out |= b.writes
+        elif isinstance(b, IfBlock):
+            out |= _all_writes(b.then_blocks) | _all_writes(b.else_blocks)
+        elif isinstance(b, (WhileBlock, ForBlock)):
+            out |= _all_writes(b.body)
+            if isinstance(b, ForBlock):
+                out.add(b.var)
+    return out

@@ -1,0 +1,110 @@
+"""Matrix / frame / scalar writers (reference: runtime/io/{WriterTextCell,WriterTextCSV,
+WriterMatrixMarket,WriterBinaryBlock,FrameWriterTextCSV}.java).  Writes the data
+file plus a `.mtd` JSON metadata file; only rank 0 writes in SPMD mode."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ..parser.errors import DMLRuntimeError
+from ..runtime import scalars as S
+from ..runtime.data import FrameBlock, ListObject
+from . import mtd as M
+from .readers import BIN_MAGIC
+
+
+def _np(x):
+    from ..ops import core as C
+    if C.is_dist(x):
+        x = C._dist().gather(x)
+    if isinstance(x, torch.Tensor):
+        return x.detach().to("cpu").double().numpy()
+    raise DMLRuntimeError("write: expected a matrix")
+
+
+def write(ctx, x, fname, format="text", **kw):
+    fmt = str(format)
+    from ..ops import core as C
+    if C.is_dist(x):
+        x = C._dist().gather(x)
+    if ctx is not None and ctx.dist is not None and ctx.dist.rank != 0:
+        return
+    d = os.path.dirname(fname)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    if isinstance(x, (bool, int, float, str)):
+        with open(fname, "w") as f:
+            f.write(S.to_str(x))
+        M.write_mtd(fname, "scalar", S.vtype_of(x).lower(), 0, 0, fmt="text")
+        return
+    if isinstance(x, FrameBlock):
+        return write_frame(x, fname, fmt, **kw)
+    if isinstance(x, ListObject):
+        raise DMLRuntimeError("write of lists is not supported")
+    if fmt == "binary" and isinstance(x, torch.Tensor) and x.dtype == torch.bfloat16:
+        _write_binary_raw(x, fname, 2)
+        M.write_mtd(fname, "matrix", "double", x.shape[0], x.shape[1], fmt="binary")
+        return
+    a = _np(x)
+    r, c = a.shape
+    nnz = int(np.count_nonzero(a))
+    if fmt in ("text", "ijv"):
+        i, j = np.nonzero(a)
+        with open(fname, "w") as f:
+            if len(i) == 0:
+                pass
+            for ii, jj in zip(i, j):
+                f.write(f"{ii + 1} {jj + 1} {S.java_double_str(float(a[ii, jj]))}\n")
+    elif fmt == "csv":
+        sep = kw.get("sep", ",")
+        header = str(kw.get("header", False)).upper() == "TRUE"
+        with open(fname, "w") as f:
+            if header:
+                f.write(sep.join(f"C{k + 1}" for k in range(c)) + "\n")
+            for row in a:
+                f.write(sep.join(S.java_double_str(float(v)) for v in row) + "\n")
+    elif fmt == "mm":
+        i, j = np.nonzero(a)
+        with open(fname, "w") as f:
+            f.write("%%MatrixMarket matrix coordinate real general\n")
+            f.write(f"{r} {c} {len(i)}\n")
+            for ii, jj in zip(i, j):
+                f.write(f"{ii + 1} {jj + 1} {S.java_double_str(float(a[ii, jj]))}\n")
+    elif fmt == "binary":
+        _write_binary_raw(torch.from_numpy(a), fname, 0)
+    else:
+        raise DMLRuntimeError(f"write: unsupported format '{fmt}'")
+    M.write_mtd(fname, "matrix", "double", r, c, nnz, fmt=fmt)
+
+
+def _write_binary_raw(t, fname, code):
+    r, c = t.shape
+    with open(fname, "wb") as f:
+        f.write(BIN_MAGIC)
+        f.write(np.array([r, c], dtype=np.int64).tobytes())
+        f.write(np.array([code, 0], dtype=np.int32).tobytes())
+        if code == 2:
+            f.write(t.detach().cpu().contiguous().view(torch.int16).numpy().tobytes())
+        else:
+            f.write(t.detach().cpu().contiguous().numpy().astype(np.float64 if code == 0 else np.float32).tobytes())
+
+
+def write_frame(fr: FrameBlock, fname, fmt="csv", **kw):
+    sep = kw.get("sep", ",")
+    header = str(kw.get("header", False)).upper() == "TRUE"
+    r, c = fr.shape
+    with open(fname, "w") as f:
+        if fmt == "csv":
+            if header:
+                f.write(sep.join(fr.names) + "\n")
+            for i in range(r):
+                f.write(sep.join("" if v is None else S.to_str(v) for v in fr.row(i)) + "\n")
+        else:
+            for i in range(r):
+                for j in range(c):
+                    v = fr.columns[j][i]
+                    if v is not None and v != "":
+                        f.write(f"{i + 1} {j + 1} {S.to_str(v)}\n")
+    M.write_mtd(fname, "frame", "string", r, c, fmt=fmt, schema=",".join(fr.schema))

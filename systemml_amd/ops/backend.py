@@ -1,0 +1,69 @@
+"""Process-wide compute backend state: device, compute dtype, kernel library.
+
+The CP backend runs on host tensors in fp64 (reference LibMatrix* semantics);
+the GPU backend keeps matrices resident in MI355X HBM in the configured
+precision and routes the hot operators to the in-tree HIP kernels
+(`systemml_amd/ops/hip/*.hip` → `libsysml_hip.so`).
+"""
+from __future__ import annotations
+
+import os
+import torch
+
+
+class Backend:
+    def __init__(self):
+        self.device = torch.device("cpu")
+        self.dtype = torch.float64
+        self.use_kernels = False
+        self.bf16_min_cells = 0
+        self.stream_sync = False
+
+    @property
+    def on_gpu(self):
+        return self.device.type == "cuda"
+
+    def configure(self, config=None):
+        want_gpu = True if config is None else (config.gpu and not config.force_cpu)
+        if os.environ.get("SYSTEMML_AMD_FORCE_CPU") == "1":
+            want_gpu = False
+        if want_gpu and torch.cuda.is_available():
+            idx = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(idx)
+            self.device = torch.device("cuda", idx)
+            prec = "double" if config is None else config.precision
+            self.dtype = torch.float32 if prec in ("single", "float", "fp32", "bf16") else torch.float64
+            self.bf16_min_cells = 0 if config is None else config.bf16_storage_min_cells
+            want_k = True if config is None else config.hip_kernels
+            if want_k:
+                from . import kernels
+                kernels.load(required=True)
+                self.use_kernels = True
+            else:
+                self.use_kernels = False
+        else:
+            self.device = torch.device("cpu")
+            self.dtype = torch.float64
+            self.use_kernels = False
+            self.bf16_min_cells = 0
+        return self
+
+
+backend = Backend()
+
+
+def place(t: torch.Tensor) -> torch.Tensor:
+    """Move a freshly created/loaded matrix into the backend's memory + dtype."""
+    if t.dtype == torch.bfloat16:
+        return t.to(backend.device)
+    if t.device != backend.device or t.dtype != backend.dtype:
+        t = t.to(device=backend.device, dtype=backend.dtype)
+    return t
+
+
+def maybe_bf16(t: torch.Tensor) -> torch.Tensor:
+    """Store large read-only inputs in bf16 (fp32 accumulate in every kernel)."""
+    if backend.on_gpu and backend.bf16_min_cells > 0 and t.numel() >= backend.bf16_min_cells \
+            and t.dtype != torch.bfloat16:
+        return t.to(torch.bfloat16)
+    return t

@@ -1,0 +1,547 @@
+"""Local matrix operator library (reference: runtime/matrix/data/LibMatrixBincell.java,
+LibMatrixAgg.java, LibMatrixReorg.java, LibMatrixMult.java, and the GPU
+counterparts LibMatrixCUDA.java / LibMatrixCuMatMult.java).
+
+All functions accept DML runtime values: Python scalars (bool/int/float/str),
+2-D torch tensors (host or HBM) and row-partitioned DistMatrix objects (routed
+to systemml_amd.parallel.dist).  Hot GPU paths (skinny matmults, mmchain,
+row-fused Hessian-vector products, sum-of-squares aggregates, bf16-stored
+inputs) go to the hand-written HIP kernels in ops/kernels.py.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..parser.errors import DMLRuntimeError
+from ..runtime import scalars as S
+from .backend import backend
+
+Tensor = torch.Tensor
+_DIST = None
+
+
+def _dist():
+    global _DIST
+    if _DIST is None:
+        from ..parallel import dist as d
+        _DIST = d
+    return _DIST
+
+
+def is_dist(x):
+    return _DIST is not None and isinstance(x, _DIST.DistMatrix)
+
+
+def cvt(x: Tensor) -> Tensor:
+    """bf16 storage → compute dtype (materialises; kernels avoid this)."""
+    if x.dtype == torch.bfloat16:
+        return x.to(backend.dtype)
+    return x
+
+
+def _num(v):
+    if isinstance(v, bool):
+        return 1.0 if v else 0.0
+    if isinstance(v, str):
+        raise DMLRuntimeError(f"string '{v}' used in a matrix operation")
+    return v
+
+
+def _fdt(x: Tensor):
+    return x.dtype if x.dtype in (torch.float32, torch.float64) else backend.dtype
+
+
+# ----------------------------------------------------------------------------
+# binary cellwise
+# ----------------------------------------------------------------------------
+def _rel(fn):
+    def f(a, b):
+        r = fn(a, b)
+        return r.to(_out_dtype(a, b))
+    return f
+
+
+def _out_dtype(a, b):
+    for x in (a, b):
+        if isinstance(x, Tensor) and x.dtype in (torch.float32, torch.float64):
+            return x.dtype
+    return backend.dtype
+
+
+def _logical(fn):
+    def f(a, b):
+        a2 = (a != 0) if isinstance(a, Tensor) else bool(a != 0)
+        b2 = (b != 0) if isinstance(b, Tensor) else bool(b != 0)
+        if not isinstance(a2, Tensor):
+            a2 = torch.tensor(a2, device=b.device)
+        if not isinstance(b2, Tensor):
+            b2 = torch.tensor(b2, device=a.device)
+        return fn(a2, b2).to(_out_dtype(a, b))
+    return f
+
+
+def _min(a, b):
+    if not isinstance(a, Tensor):
+        a, b = b, a
+    if not isinstance(b, Tensor):
+        b = torch.tensor(b, dtype=a.dtype, device=a.device)
+    return torch.minimum(a, b)
+
+
+def _max(a, b):
+    if not isinstance(a, Tensor):
+        a, b = b, a
+    if not isinstance(b, Tensor):
+        b = torch.tensor(b, dtype=a.dtype, device=a.device)
+    return torch.maximum(a, b)
+
+
+def _pow(a, b):
+    if isinstance(b, (int, float)) and b == 2:
+        return a * a
+    if not isinstance(a, Tensor):
+        a = torch.tensor(float(a), dtype=b.dtype, device=b.device)
+    return torch.pow(a, b)
+
+
+def _mod(a, b):
+    if not isinstance(a, Tensor):
+        a = torch.tensor(float(a), dtype=b.dtype, device=b.device)
+    return torch.remainder(a, b)
+
+
+def _intdiv(a, b):
+    if not isinstance(a, Tensor):
+        a = torch.tensor(float(a), dtype=b.dtype, device=b.device)
+    return torch.floor(a / b)
+
+
+def _log2(a, b):
+    la = torch.log(a) if isinstance(a, Tensor) else math.log(a) if a > 0 else (-math.inf if a == 0 else math.nan)
+    lb = torch.log(b) if isinstance(b, Tensor) else math.log(b)
+    return la / lb
+
+
+def _bitw(fn):
+    def f(a, b):
+        ai = a.long() if isinstance(a, Tensor) else int(a)
+        bi = b.long() if isinstance(b, Tensor) else int(b)
+        return fn(ai, bi).to(_out_dtype(a, b))
+    return f
+
+
+BIN = {
+    "+": lambda a, b: a + b,
+    "-": lambda a, b: a - b,
+    "*": lambda a, b: a * b,
+    "/": lambda a, b: a / b,
+    "^": _pow,
+    "%%": _mod,
+    "%/%": _intdiv,
+    "==": _rel(lambda a, b: a == b),
+    "!=": _rel(lambda a, b: a != b),
+    "<": _rel(lambda a, b: a < b),
+    "<=": _rel(lambda a, b: a <= b),
+    ">": _rel(lambda a, b: a > b),
+    ">=": _rel(lambda a, b: a >= b),
+    "&": _logical(torch.logical_and),
+    "|": _logical(torch.logical_or),
+    "xor": _logical(torch.logical_xor),
+    "min": _min,
+    "max": _max,
+    "log": _log2,
+    "bitwAnd": _bitw(lambda a, b: a & b),
+    "bitwOr": _bitw(lambda a, b: a | b),
+    "bitwXor": _bitw(lambda a, b: a ^ b),
+    "bitwShiftL": _bitw(lambda a, b: a << b),
+    "bitwShiftR": _bitw(lambda a, b: a >> b),
+}
+
+
+def _check_bin_dims(a: Tensor, b: Tensor, op):
+    sa, sb = a.shape, b.shape
+    if sa == sb:
+        return
+    (ra, ca), (rb, cb) = sa, sb
+    ok = ((ra == rb and (ca == 1 or cb == 1)) or (ca == cb and (ra == 1 or rb == 1)) or
+          (ra == 1 and ca == 1) or (rb == 1 and cb == 1) or
+          (ca == 1 and rb == 1) or (ra == 1 and cb == 1))
+    if not ok:
+        raise DMLRuntimeError(f"Block sizes are not matched for binary cell operations: "
+                              f"{ra}x{ca} vs {rb}x{cb} (op {op})")
+
+
+def binary(op, a, b):
+    ta, tb = isinstance(a, Tensor), isinstance(b, Tensor)
+    if not ta and not tb:
+        if is_dist(a) or is_dist(b):
+            return _dist().binary(op, a, b)
+        if hasattr(a, "columns") or hasattr(b, "columns"):
+            raise DMLRuntimeError(f"operator {op} not supported on frames")
+        return S.binary(op, a, b)
+    if is_dist(a) or is_dist(b):
+        return _dist().binary(op, a, b)
+    fn = BIN.get(op)
+    if fn is None:
+        raise DMLRuntimeError(f"unknown binary operator {op}")
+    if ta and tb:
+        a, b = cvt(a), cvt(b)
+        if a.device != b.device:
+            b = b.to(a.device)
+        if a.dtype != b.dtype:
+            dt = torch.promote_types(a.dtype, b.dtype)
+            a, b = a.to(dt), b.to(dt)
+        _check_bin_dims(a, b, op)
+        return fn(a, b)
+    if ta:
+        return fn(cvt(a), _num(b))
+    return fn(_num(a), cvt(b))
+
+
+# ----------------------------------------------------------------------------
+# unary cellwise
+# ----------------------------------------------------------------------------
+def _round(x):
+    return torch.floor(x + 0.5)
+
+
+UN = {
+    "neg": lambda x: -x,
+    "not": lambda x: (x == 0).to(x.dtype),
+    "abs": torch.abs,
+    "exp": torch.exp,
+    "log": torch.log,
+    "sqrt": torch.sqrt,
+    "round": _round,
+    "floor": torch.floor,
+    "ceil": torch.ceil,
+    "sign": torch.sign,
+    "sin": torch.sin, "cos": torch.cos, "tan": torch.tan,
+    "asin": torch.asin, "acos": torch.acos, "atan": torch.atan,
+    "sinh": torch.sinh, "cosh": torch.cosh, "tanh": torch.tanh,
+    "cumsum": lambda x: torch.cumsum(x, dim=0),
+    "cumprod": lambda x: torch.cumprod(x, dim=0),
+    "cummin": lambda x: torch.cummin(x, dim=0).values,
+    "cummax": lambda x: torch.cummax(x, dim=0).values,
+    "sigmoid": torch.sigmoid,
+}
+
+
+def unary(op, x):
+    if isinstance(x, Tensor):
+        if op in ("nrow", "ncol", "length"):
+            r, c = x.shape
+            return {"nrow": r, "ncol": c, "length": r * c}[op]
+        if op == "cast_scalar" or op in ("cast_double", "cast_int", "cast_bool"):
+            if x.numel() != 1:
+                raise DMLRuntimeError(f"cannot cast {x.shape[0]}x{x.shape[1]} matrix to scalar")
+            v = float(x.reshape(-1)[0].item())
+            return S.unary(op, v) if op != "cast_scalar" else v
+        if op == "cast_matrix":
+            return x
+        if op == "cast_frame":
+            from ..runtime.data import FrameBlock
+            return FrameBlock.from_matrix(x)
+        fn = UN.get(op)
+        if fn is None:
+            raise DMLRuntimeError(f"unknown unary operator {op}")
+        return fn(cvt(x))
+    if is_dist(x):
+        return _dist().unary(op, x)
+    if op in ("nrow", "ncol", "length"):
+        if hasattr(x, "columns"):
+            r, c = x.shape
+            return {"nrow": r, "ncol": c, "length": r * c}[op]
+        if hasattr(x, "data") and hasattr(x, "names"):
+            return len(x) if op == "length" else (len(x) if op == "nrow" else 1)
+        if op == "length":
+            return 1
+        raise DMLRuntimeError(f"{op}() requires a matrix or frame argument")
+    if op == "cast_matrix":
+        if hasattr(x, "columns"):
+            return x.to_matrix(backend.dtype).to(backend.device)
+        if hasattr(x, "data") and hasattr(x, "names"):
+            vals = [float(v) for v in x.data]
+            return torch.tensor(vals, dtype=backend.dtype, device=backend.device).reshape(-1, 1)
+        return torch.full((1, 1), float(_num(x)), dtype=backend.dtype, device=backend.device)
+    if op == "cast_frame":
+        from ..runtime.data import FrameBlock
+        if hasattr(x, "columns"):
+            return x
+        return FrameBlock([[x]], [S.vtype_of(x)])
+    if op == "cast_scalar" and hasattr(x, "columns"):
+        return x.columns[0][0]
+    if op == "cast_list":
+        from ..runtime.data import ListObject
+        return x if hasattr(x, "names") and hasattr(x, "data") else ListObject([x])
+    return S.unary(op, x)
+
+
+# ----------------------------------------------------------------------------
+# aggregates
+# ----------------------------------------------------------------------------
+def _var(x, dim=None):
+    if dim is None:
+        n = x.numel()
+        if n <= 1:
+            return torch.zeros((), dtype=x.dtype, device=x.device)
+        return torch.var(x)
+    n = x.shape[dim]
+    if n <= 1:
+        shape = list(x.shape)
+        shape[dim] = 1
+        return torch.zeros(shape, dtype=x.dtype, device=x.device)
+    return torch.var(x, dim=dim, keepdim=True)
+
+
+def agg(o, d, x):
+    if not isinstance(x, Tensor):
+        if is_dist(x):
+            return _dist().agg(o, d, x)
+        if isinstance(x, (int, float, bool)):
+            v = _num(x)
+            if o in ("sum", "mean", "min", "max", "prod", "trace"):
+                return float(v)
+            if o == "sumsq":
+                return float(v) * float(v)
+            if o in ("var", "sd"):
+                return 0.0
+        raise DMLRuntimeError(f"aggregate {o} requires a matrix argument")
+    if o == "sumsq" and backend.use_kernels and x.is_cuda and x.numel() >= 1 << 16 and d in ("all", "row", "col"):
+        from . import kernels
+        return kernels.sumsq(x, d)
+    x = cvt(x)
+    if d == "all":
+        if x.numel() == 0:
+            if o in ("sum", "sumsq", "trace"):
+                return 0.0
+            raise DMLRuntimeError(f"aggregate {o} of an empty matrix")
+        if o == "sum":
+            r = torch.sum(x)
+        elif o == "sumsq":
+            r = torch.sum(x * x)
+        elif o == "mean":
+            r = torch.mean(x)
+        elif o == "prod":
+            r = torch.prod(x)
+        elif o == "min":
+            r = torch.min(x)
+        elif o == "max":
+            r = torch.max(x)
+        elif o == "var":
+            r = _var(x)
+        elif o == "sd":
+            r = torch.sqrt(_var(x))
+        elif o == "trace":
+            if x.shape[0] != x.shape[1]:
+                raise DMLRuntimeError("trace requires a square matrix")
+            r = torch.trace(x)
+        else:
+            raise DMLRuntimeError(f"unknown aggregate {o}")
+        return float(r.item())
+    dim = 1 if d == "row" else 0
+    if o == "sum":
+        return torch.sum(x, dim=dim, keepdim=True)
+    if o == "sumsq":
+        return torch.sum(x * x, dim=dim, keepdim=True)
+    if o == "mean":
+        return torch.mean(x, dim=dim, keepdim=True)
+    if o == "prod":
+        return torch.prod(x, dim=dim, keepdim=True)
+    if o == "min":
+        return torch.amin(x, dim=dim, keepdim=True)
+    if o == "max":
+        return torch.amax(x, dim=dim, keepdim=True)
+    if o == "var":
+        return _var(x, dim)
+    if o == "sd":
+        return torch.sqrt(_var(x, dim))
+    if o in ("imax", "imin"):
+        # 1-based index of the (last) extreme value per row, as LibMatrixAgg
+        xf = torch.flip(x, dims=[1])
+        idx = torch.argmax(xf, dim=1, keepdim=True) if o == "imax" else torch.argmin(xf, dim=1, keepdim=True)
+        return (x.shape[1] - idx).to(x.dtype)
+    raise DMLRuntimeError(f"unknown aggregate {o}")
+
+
+def tak(a, b):
+    """sum(a*b) without materialising the product (TernaryAggregate tak+*)."""
+    if is_dist(a) or is_dist(b):
+        return _dist().tak(a, b)
+    if not isinstance(a, Tensor) or not isinstance(b, Tensor):
+        return agg("sum", "all", binary("*", a, b))
+    if a.shape != b.shape:
+        return agg("sum", "all", binary("*", a, b))
+    a, b = cvt(a), cvt(b)
+    if b.dtype != a.dtype:
+        b = b.to(a.dtype)
+    return float(torch.dot(a.reshape(-1), b.reshape(-1)).item())
+
+
+# ----------------------------------------------------------------------------
+# matrix multiplication family
+# ----------------------------------------------------------------------------
+def _need_mat(x, what):
+    if not isinstance(x, Tensor):
+        if is_dist(x):
+            return x
+        raise DMLRuntimeError(f"{what}: expected a matrix, got {type(x).__name__}")
+    return x
+
+
+def mm(a, b, transA=False):
+    if is_dist(a) or is_dist(b):
+        return _dist().mm(a, b, transA)
+    a = _need_mat(a, "%*%")
+    b = _need_mat(b, "%*%")
+    ka = a.shape[0] if transA else a.shape[1]
+    if ka != b.shape[0]:
+        ra, ca = (a.shape[1], a.shape[0]) if transA else tuple(a.shape)
+        raise DMLRuntimeError(f"Matrix multiplication dimension mismatch: {ra}x{ca} %*% {b.shape[0]}x{b.shape[1]}")
+    if backend.use_kernels and a.is_cuda:
+        from . import kernels
+        r = kernels.try_mm(a, b, transA)
+        if r is not None:
+            return r
+    a, b = cvt(a), cvt(b)
+    if a.device != b.device:
+        b = b.to(a.device)
+    if a.dtype != b.dtype:
+        dt = torch.promote_types(a.dtype, b.dtype)
+        a, b = a.to(dt), b.to(dt)
+    return a.t() @ b if transA else a @ b
+
+
+def tsmm(x, left=True):
+    if is_dist(x):
+        return _dist().tsmm(x, left)
+    x = _need_mat(x, "tsmm")
+    if backend.use_kernels and x.is_cuda:
+        from . import kernels
+        r = kernels.try_tsmm(x, left)
+        if r is not None:
+            return r
+    x = cvt(x)
+    return x.t() @ x if left else x @ x.t()
+
+
+def mmchain(ctype, X, v, w=None):
+    """t(X) %*% f(X %*% v) fused chains (MapMultChain + codegen row template)."""
+    if is_dist(X):
+        return _dist().mmchain(ctype, X, v, w)
+    if backend.use_kernels and isinstance(X, Tensor) and X.is_cuda:
+        from . import kernels
+        r = kernels.try_mmchain(ctype, X, v, w)
+        if r is not None:
+            return r
+    return mmchain_ref(ctype, X, v, w)
+
+
+def mmchain_ref(ctype, X, v, w=None):
+    u = mm(X, v)
+    if ctype == "XtXv":
+        g = u
+    elif ctype == "XtwXv":
+        g = binary("*", w, u)
+    elif ctype == "XtXvy":
+        g = binary("-", u, w)
+    elif ctype == "XtPSXv":
+        q = binary("*", w, u)
+        g = binary("-", q, binary("*", w, agg("sum", "row", q)))
+    else:
+        raise DMLRuntimeError(f"unknown mmchain type {ctype}")
+    return mm(X, g, transA=True)
+
+
+# ----------------------------------------------------------------------------
+# reorg / indexing
+# ----------------------------------------------------------------------------
+def transpose(x):
+    if is_dist(x):
+        return _dist().transpose(x)
+    x = _need_mat(x, "t")
+    return cvt(x).t().contiguous()
+
+
+def _bound(v, default):
+    if v is None:
+        return default
+    if isinstance(v, Tensor):
+        v = v.reshape(-1)[0].item()
+    return int(S.as_double(v)) if not isinstance(v, int) else v
+
+
+def rix(x, rl, ru, cl, cu, list_mode=False):
+    from ..runtime.data import ListObject, FrameBlock
+    if isinstance(x, ListObject):
+        if isinstance(rl, str):
+            return x.get(rl)
+        lo = _bound(rl, 1)
+        hi = _bound(ru, len(x))
+        if lo == hi and (ru is rl or ru is None or list_mode):
+            return x.get(lo)
+        return x.slice(lo, hi)
+    if is_dist(x):
+        return _dist().rix(x, rl, ru, cl, cu)
+    if isinstance(x, FrameBlock):
+        nr, nc = x.shape
+        r0, r1 = _bound(rl, 1), _bound(ru, nr)
+        c0, c1 = _bound(cl, 1), _bound(cu, nc)
+        _check_range(r0, r1, c0, c1, nr, nc)
+        return x.slice(r0 - 1, r1, c0 - 1, c1)
+    if not isinstance(x, Tensor):
+        raise DMLRuntimeError("indexing requires a matrix, frame or list")
+    nr, nc = x.shape
+    r0, r1 = _bound(rl, 1), _bound(ru, nr)
+    c0, c1 = _bound(cl, 1), _bound(cu, nc)
+    _check_range(r0, r1, c0, c1, nr, nc)
+    out = x[r0 - 1:r1, c0 - 1:c1]
+    return out.clone() if out.data_ptr() == x.data_ptr() and out.shape == x.shape else out
+
+
+def _check_range(r0, r1, c0, c1, nr, nc):
+    if r0 < 1 or r1 > nr or r0 > r1 or c0 < 1 or c1 > nc or c0 > c1:
+        raise DMLRuntimeError(f"Invalid values for matrix indexing: [{r0}:{r1},{c0}:{c1}] "
+                              f"must be within matrix dimensions [{nr},{nc}]")
+
+
+def lix(x, y, rl, ru, cl, cu, list_mode=False):
+    from ..runtime.data import ListObject
+    if isinstance(x, ListObject):
+        i = _bound(rl, 1)
+        data = list(x.data)
+        names = list(x.names) if x.names else None
+        if isinstance(rl, str):
+            if names and rl in names:
+                data[names.index(rl)] = y
+            else:
+                data.append(y)
+                names = (names or [""] * (len(data) - 1)) + [rl]
+        else:
+            while len(data) < i:
+                data.append(None)
+            data[i - 1] = y
+        return ListObject(data, names)
+    if is_dist(x) or is_dist(y):
+        return _dist().lix(x, y, rl, ru, cl, cu)
+    if not isinstance(x, Tensor):
+        raise DMLRuntimeError("left indexing requires a matrix target")
+    nr, nc = x.shape
+    r0, r1 = _bound(rl, 1), _bound(ru, nr)
+    c0, c1 = _bound(cl, 1), _bound(cu, nc)
+    _check_range(r0, r1, c0, c1, nr, nc)
+    out = cvt(x).clone()
+    if isinstance(y, Tensor):
+        y = cvt(y)
+        if tuple(y.shape) != (r1 - r0 + 1, c1 - c0 + 1):
+            if y.numel() == 1:
+                y = y.reshape(())
+            else:
+                raise DMLRuntimeError(f"left indexing dimension mismatch: target [{r0}:{r1},{c0}:{c1}] "
+                                      f"vs source {y.shape[0]}x{y.shape[1]}")
+        out[r0 - 1:r1, c0 - 1:c1] = y.to(device=out.device, dtype=out.dtype)
+    else:
+        out[r0 - 1:r1, c0 - 1:c1] = float(_num(y))
+    return out

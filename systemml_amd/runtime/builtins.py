@@ -1,0 +1,952 @@
+"""Builtin function implementations dispatched by name from `bi` / `sink` HOPs.
+
+Reference: parser/BuiltinFunctionExpression.java + ParameterizedBuiltinFunctionExpression.java
+(signatures/defaults) and the CP instructions implementing them
+(runtime/instructions/cp/{DataGenCPInstruction,AppendCPInstruction,CtableCPInstruction,
+ParameterizedBuiltinCPInstruction,MultiReturnBuiltinCPInstruction,QuantilePickCPInstruction,
+CentralMomentCPInstruction,CovarianceCPInstruction,...}.java, LibCommonsMath.java).
+
+Every function takes the ExecutionContext first, then DML arguments (positional
+and named, with the reference's parameter names).
+"""
+from __future__ import annotations
+
+import math
+import time as _time
+
+import numpy as np
+import torch
+
+from ..parser.errors import DMLRuntimeError, DMLScriptStop
+from ..ops import core as C
+from ..ops.backend import backend, place
+from . import scalars as S
+from .data import ListObject, FrameBlock
+
+Tensor = torch.Tensor
+REGISTRY = {}
+MULTI_RETURN = set()
+
+
+def builtin(*names, multi=False):
+    def deco(fn):
+        for n in names:
+            REGISTRY[n] = fn
+            if multi:
+                MULTI_RETURN.add(n)
+        return fn
+    return deco
+
+
+def _dev():
+    return backend.device
+
+
+def _dt():
+    return backend.dtype
+
+
+def _mat(x, what="argument"):
+    if isinstance(x, Tensor):
+        return C.cvt(x)
+    if C.is_dist(x):
+        return C._dist().gather(x)
+    if isinstance(x, FrameBlock):
+        return place(x.to_matrix())
+    if isinstance(x, (int, float, bool)):
+        return torch.full((1, 1), float(x), dtype=_dt(), device=_dev())
+    raise DMLRuntimeError(f"{what}: expected a matrix")
+
+
+def _int(v, name="argument"):
+    if isinstance(v, Tensor):
+        v = v.reshape(-1)[0].item()
+    try:
+        return int(S.as_double(v)) if not isinstance(v, int) else v
+    except DMLRuntimeError:
+        raise DMLRuntimeError(f"{name}: expected an integer, got {v!r}")
+
+
+def _float(v):
+    if isinstance(v, Tensor):
+        return float(v.reshape(-1)[0].item())
+    return S.as_double(v)
+
+
+def _bool(v):
+    if isinstance(v, Tensor):
+        return bool(v.reshape(-1)[0].item() != 0)
+    return S.as_bool(v)
+
+
+# ============================================================================
+# printing / control
+# ============================================================================
+@builtin("print")
+def b_print(ctx, x="", *rest, **kw):
+    if rest:
+        # printf-style print("fmt %d", a, b)
+        s = _format(x, rest)
+    else:
+        s = to_display_string(x)
+    ctx.print(s)
+    return None
+
+
+def _format(fmt, args):
+    try:
+        vals = [(_float(a) if isinstance(a, Tensor) else a) for a in args]
+        return str(fmt) % tuple(vals)
+    except TypeError as e:
+        raise DMLRuntimeError(f"print format error: {e}")
+
+
+@builtin("printf")
+def b_printf(ctx, fmt, *args):
+    ctx.print(_format(fmt, args))
+
+
+def to_display_string(x):
+    if isinstance(x, Tensor) or C.is_dist(x):
+        return b_toString(None, x)
+    if isinstance(x, FrameBlock):
+        return b_toString(None, x)
+    if isinstance(x, ListObject):
+        return b_toString(None, x)
+    return S.to_str(x)
+
+
+@builtin("stop")
+def b_stop(ctx, msg=""):
+    raise DMLScriptStop(S.to_str(msg))
+
+
+@builtin("assert")
+def b_assert(ctx, cond):
+    if not _bool(cond):
+        raise DMLRuntimeError("assertion failed")
+
+
+@builtin("time")
+def b_time(ctx):
+    return int(_time.time_ns())
+
+
+@builtin("exists")
+def b_exists(ctx, *a, **kw):
+    return False
+
+
+@builtin("toString")
+def b_toString(ctx, target, rows=100, cols=100, decimal=3, sparse=False, sep=" ", linesep="\n"):
+    if isinstance(target, ListObject):
+        parts = []
+        for i, v in enumerate(target.data):
+            nm = target.names[i] if target.names else str(i + 1)
+            parts.append(f"[{nm}]: {to_display_string(v)}")
+        return "\n".join(parts)
+    if isinstance(target, FrameBlock):
+        r, c = target.shape
+        lines = ["# FRAME: nrow = %d, ncol = %d" % (r, c),
+                 "# " + sep.join(target.names), "# " + sep.join(target.schema)]
+        for i in range(min(r, _int(rows))):
+            lines.append(sep.join(S.to_str(v) if v is not None else "" for v in target.row(i)[:_int(cols)]))
+        return linesep.join(lines) + linesep
+    if not isinstance(target, Tensor) and not C.is_dist(target):
+        return S.to_str(target)
+    m = _mat(target).detach().cpu().double().numpy()
+    r, c = m.shape
+    r = min(r, _int(rows))
+    c = min(c, _int(cols))
+    d = _int(decimal)
+    out = []
+    if _bool(sparse):
+        for i in range(r):
+            for j in range(c):
+                if m[i, j] != 0:
+                    out.append(f"{i + 1}{sep}{j + 1}{sep}{_fmt_dec(m[i, j], d)}")
+        return linesep.join(out) + linesep
+    for i in range(r):
+        out.append(sep.join(_fmt_dec(m[i, j], d) for j in range(c)))
+    return linesep.join(out) + linesep
+
+
+def _fmt_dec(v, d):
+    if v != v:
+        return "NaN"
+    if v == math.inf:
+        return "Infinity"
+    if v == -math.inf:
+        return "-Infinity"
+    s = f"{v:.{d}f}"
+    if s.startswith("-") and float(s) == 0:
+        s = s[1:]
+    return s
+
+
+# ============================================================================
+# data generation (reference: LibMatrixDatagen.java, DataGenCPInstruction.java)
+# ============================================================================
+def _gen(seed):
+    seed = _int(seed) if seed is not None else -1
+    g = torch.Generator(device="cpu")
+    if seed is None or seed == -1:
+        g.seed()
+    else:
+        g.manual_seed(seed)
+    return g
+
+
+def _devgen(seed):
+    seed = _int(seed) if seed is not None else -1
+    dev = _dev()
+    g = torch.Generator(device=dev)
+    if seed == -1:
+        g.seed()
+    else:
+        g.manual_seed(seed)
+    return g
+
+
+@builtin("rand", "Rand")
+def b_rand(ctx, rows=None, cols=None, min=0.0, max=1.0, sparsity=1.0, pdf="uniform", seed=-1,
+           **kw):
+    lam = kw.get("lambda", 1.0)
+    if "dims" in kw:
+        raise DMLRuntimeError("tensor rand not supported")
+    r, c = _int(rows, "rows"), _int(cols, "cols")
+    lo, hi = _float(min), _float(max)
+    sp = _float(sparsity)
+    pdf = str(pdf).lower()
+    if ctx is not None and ctx.dist is not None and r >= ctx.config.dist_min_rows:
+        return C._dist().rand(ctx, r, c, lo, hi, sp, pdf, _int(seed), _float(lam))
+    return _rand_local(r, c, lo, hi, sp, pdf, _int(seed), _float(lam))
+
+
+def _rand_local(r, c, lo, hi, sp, pdf, seed, lam, device=None, row_offset=0):
+    device = device or _dev()
+    dt = _dt()
+    g = torch.Generator(device=device)
+    if seed == -1:
+        g.seed()
+    else:
+        g.manual_seed(seed + row_offset * 1000003)
+    if r == 0 or c == 0:
+        return torch.zeros((r, c), dtype=dt, device=device)
+    if pdf == "uniform":
+        if lo == hi:
+            m = torch.full((r, c), lo, dtype=dt, device=device)
+        else:
+            m = torch.rand((r, c), generator=g, dtype=dt, device=device) * (hi - lo) + lo
+    elif pdf == "normal":
+        m = torch.randn((r, c), generator=g, dtype=dt, device=device)
+    elif pdf == "poisson":
+        m = torch.poisson(torch.full((r, c), lam, dtype=dt, device=device), generator=g)
+    else:
+        raise DMLRuntimeError(f"unsupported pdf '{pdf}'")
+    if sp < 1.0:
+        mask = torch.rand((r, c), generator=g, dtype=dt, device=device) < sp
+        m = m * mask
+    return m
+
+
+@builtin("matrix")
+def b_matrix(ctx, data=None, rows=None, cols=None, byrow=True, dimnames=False, **kw):
+    if isinstance(data, str):
+        toks = data.replace(",", " ").split()
+        vals = [float(t) for t in toks]
+        r = _int(rows) if rows is not None else None
+        c = _int(cols) if cols is not None else None
+        if r is None and c is None:
+            r, c = len(vals), 1
+        elif r is None:
+            r = len(vals) // c
+        elif c is None:
+            c = len(vals) // r
+        if len(vals) != r * c:
+            if len(vals) == 1:
+                vals = vals * (r * c)
+            else:
+                raise DMLRuntimeError(f"matrix(): {len(vals)} values do not match {r}x{c}")
+        t = torch.tensor(vals, dtype=torch.float64).reshape(r, c) if _bool(byrow) else \
+            torch.tensor(vals, dtype=torch.float64).reshape(c, r).t()
+        return place(t.contiguous())
+    if isinstance(data, (Tensor,)) or C.is_dist(data):
+        m = _mat(data)
+        nr, nc = m.shape
+        r = _int(rows) if rows is not None else None
+        c = _int(cols) if cols is not None else None
+        if r is None:
+            r = nr * nc // c
+        if c is None:
+            c = nr * nc // r
+        if r * c != nr * nc:
+            raise DMLRuntimeError(f"reshape: cannot reshape {nr}x{nc} to {r}x{c}")
+        if _bool(byrow):
+            return m.contiguous().reshape(r, c)
+        return m.t().contiguous().reshape(c, r).t().contiguous()
+    if isinstance(data, FrameBlock):
+        return place(data.to_matrix())
+    v = _float(data if data is not None else 0.0)
+    r, c = _int(rows, "rows"), _int(cols, "cols")
+    if ctx is not None and ctx.dist is not None and r >= ctx.config.dist_min_rows:
+        return C._dist().full(ctx, r, c, v)
+    return torch.full((r, c), v, dtype=_dt(), device=_dev())
+
+
+@builtin("seq")
+def b_seq(ctx, frm=None, to=None, incr=None, **kw):
+    frm = kw.get("from", frm)
+    a, b = _float(frm), _float(to)
+    if incr is None:
+        inc = 1.0 if a <= b else -1.0
+    else:
+        inc = _float(incr)
+    if inc == 0 or (b - a) * inc < 0:
+        if a == b:
+            n = 1
+        else:
+            raise DMLRuntimeError(f"seq: wrong sign for increment ({a}, {b}, {inc})")
+    else:
+        n = int(math.floor((b - a) / inc + 1e-10)) + 1
+    if ctx is not None and ctx.dist is not None and n >= ctx.config.dist_min_rows:
+        return C._dist().seq(ctx, a, inc, n)
+    t = a + inc * torch.arange(n, dtype=torch.float64)
+    return place(t.reshape(n, 1))
+
+
+@builtin("sample")
+def b_sample(ctx, range_=None, size=None, replace=False, seed=-1, **kw):
+    rng = _int(kw.get("range", range_))
+    n = _int(size)
+    rep = _bool(replace) if not isinstance(replace, (int, float)) or isinstance(replace, bool) else False
+    if isinstance(replace, (int, float)) and not isinstance(replace, bool) and seed == -1:
+        seed = replace
+        rep = False
+    g = _gen(seed)
+    if rep:
+        v = torch.randint(1, rng + 1, (n,), generator=g, dtype=torch.int64)
+    else:
+        if n > rng:
+            raise DMLRuntimeError("sample: size > range without replacement")
+        v = torch.randperm(rng, generator=g)[:n] + 1
+    return place(v.double().reshape(n, 1))
+
+
+# ============================================================================
+# append / reorg
+# ============================================================================
+@builtin("cbind", "append")
+def b_cbind(ctx, *args, **kw):
+    if any(C.is_dist(a) for a in args):
+        return C._dist().cbind(args)
+    if isinstance(args[0], str):
+        # string append (reference: StringObject append joins with a newline)
+        return "\n".join(S.to_str(a) for a in args)
+    if isinstance(args[0], ListObject):
+        out = ListObject(args[0].data, args[0].names)
+        for a in args[1:]:
+            out.data.append(a)
+            if out.names is not None:
+                out.names.append("")
+        return out
+    if isinstance(args[0], FrameBlock):
+        cols, schema, names = [], [], []
+        for a in args:
+            cols += a.columns
+            schema += a.schema
+            names += a.names
+        return FrameBlock(cols, schema, names)
+    ms = [_mat(a) for a in args]
+    r = ms[0].shape[0]
+    for m in ms[1:]:
+        if m.shape[0] != r:
+            raise DMLRuntimeError(f"cbind: number of rows do not match ({r} vs {m.shape[0]})")
+    return torch.cat(ms, dim=1)
+
+
+@builtin("rbind")
+def b_rbind(ctx, *args, **kw):
+    if any(C.is_dist(a) for a in args):
+        return C._dist().rbind(args)
+    if isinstance(args[0], FrameBlock):
+        cols = [list(c) for c in args[0].columns]
+        for a in args[1:]:
+            for j, c in enumerate(a.columns):
+                cols[j] += c
+        return FrameBlock(cols, args[0].schema, args[0].names)
+    ms = [_mat(a) for a in args]
+    c = ms[0].shape[1]
+    for m in ms[1:]:
+        if m.shape[1] != c:
+            raise DMLRuntimeError(f"rbind: number of columns do not match ({c} vs {m.shape[1]})")
+    return torch.cat(ms, dim=0)
+
+
+@builtin("rev")
+def b_rev(ctx, x):
+    return torch.flip(_mat(x), dims=[0])
+
+
+@builtin("diag")
+def b_diag(ctx, x):
+    m = _mat(x)
+    r, c = m.shape
+    if c == 1:
+        return torch.diag(m.reshape(-1))
+    if r == c:
+        return torch.diagonal(m).reshape(-1, 1).clone()
+    raise DMLRuntimeError("diag requires a square matrix or a column vector")
+
+
+@builtin("lower.tri")
+def b_lower_tri(ctx, target=None, diag=False, values=False):
+    m = _mat(target)
+    k = 0 if _bool(diag) else -1
+    out = torch.tril(m, diagonal=k)
+    if not _bool(values):
+        out = (torch.tril(torch.ones_like(m), diagonal=k))
+    return out
+
+
+@builtin("upper.tri")
+def b_upper_tri(ctx, target=None, diag=False, values=False):
+    m = _mat(target)
+    k = 0 if _bool(diag) else 1
+    out = torch.triu(m, diagonal=k)
+    if not _bool(values):
+        out = torch.triu(torch.ones_like(m), diagonal=k)
+    return out
+
+
+@builtin("order")
+def b_order(ctx, target=None, by=1, decreasing=False, **kw):
+    m = _mat(target)
+    idx_ret = _bool(kw.get("index.return", False))
+    col = m[:, _int(by) - 1]
+    # stable sort (ties keep input order), as the reference
+    perm = torch.sort(col, descending=_bool(decreasing), stable=True).indices
+    if idx_ret:
+        return (perm + 1).to(m.dtype).reshape(-1, 1)
+    return m[perm]
+
+
+@builtin("removeEmpty")
+def b_removeEmpty(ctx, target=None, margin="rows", select=None, **kw):
+    m = _mat(target)
+    empty_return = _bool(kw.get("empty.return", True))
+    if margin == "rows":
+        keep = (m != 0).any(dim=1) if select is None else (_mat(select).reshape(-1) != 0)
+        out = m[keep]
+        if out.shape[0] == 0 and empty_return:
+            return torch.zeros((1, m.shape[1]), dtype=m.dtype, device=m.device)
+        return out
+    if margin == "cols":
+        keep = (m != 0).any(dim=0) if select is None else (_mat(select).reshape(-1) != 0)
+        out = m[:, keep]
+        if out.shape[1] == 0 and empty_return:
+            return torch.zeros((m.shape[0], 1), dtype=m.dtype, device=m.device)
+        return out
+    raise DMLRuntimeError(f"removeEmpty: invalid margin '{margin}'")
+
+
+@builtin("replace")
+def b_replace(ctx, target=None, pattern=None, replacement=None):
+    m = _mat(target).clone()
+    p = _float(pattern)
+    r = _float(replacement)
+    if p != p:
+        m[torch.isnan(m)] = r
+    else:
+        m[m == p] = r
+    return m
+
+
+@builtin("ifelse")
+def b_ifelse(ctx, test, yes, no):
+    if not any(isinstance(a, Tensor) or C.is_dist(a) for a in (test, yes, no)):
+        return yes if _bool(test) else no
+    t = test if isinstance(test, Tensor) else None
+    shape_src = next(a for a in (test, yes, no) if isinstance(a, Tensor))
+    def full(a):
+        if isinstance(a, Tensor):
+            return C.cvt(a)
+        return torch.full(shape_src.shape, float(C._num(a)), dtype=_dt(), device=shape_src.device)
+    tt, yy, nn = full(test), full(yes), full(no)
+    return torch.where(tt != 0, yy, nn)
+
+
+@builtin("outer")
+def b_outer(ctx, a, b, op):
+    x = _mat(a)
+    y = _mat(b)
+    if x.shape[1] != 1 or y.shape[0] != 1:
+        raise DMLRuntimeError("outer requires a column vector and a row vector")
+    return C.binary(str(op), x, y)
+
+
+@builtin("table", "ctable")
+def b_table(ctx, A=None, B=None, W=None, odim1=None, odim2=None, *rest, **kw):
+    if C.is_dist(A) or C.is_dist(B):
+        return C._dist().table(ctx, A, B, W, odim1, odim2)
+    # table(A, B, [W], [d1, d2])
+    args = [a for a in (A, B, W, odim1, odim2) + rest if a is not None]
+    if "weights" in kw:
+        W = kw["weights"]
+    A_, B_ = args[0], args[1]
+    w = None
+    dims = None
+    rem = args[2:]
+    if len(rem) in (1, 3):
+        w = rem[0]
+        rem = rem[1:]
+    if len(rem) == 2:
+        dims = (_int(rem[0]), _int(rem[1]))
+    a = _mat(A_).reshape(-1) if isinstance(A_, (Tensor,)) or C.is_dist(A_) else None
+    b = _mat(B_).reshape(-1) if isinstance(B_, (Tensor,)) or C.is_dist(B_) else None
+    n = a.numel() if a is not None else b.numel()
+    if a is None:
+        a = torch.full((n,), float(A_), dtype=_dt(), device=_dev())
+    if b is None:
+        b = torch.full((n,), float(B_), dtype=_dt(), device=_dev())
+    if w is None:
+        wv = torch.ones(n, dtype=_dt(), device=a.device)
+    elif isinstance(w, Tensor):
+        wv = C.cvt(w).reshape(-1).to(a.device)
+    else:
+        wv = torch.full((n,), float(w), dtype=_dt(), device=a.device)
+    return _ctable(a, b, wv, dims)
+
+
+def _ctable(a, b, wv, dims):
+    ai = torch.round(a).long()
+    bi = torch.round(b).long()
+    valid = (ai > 0) & (bi > 0)
+    if not bool(valid.all()):
+        if bool(((ai <= 0) | (bi <= 0)).any()):
+            raise DMLRuntimeError("ctable: invalid (non-positive) category values")
+    if dims is None:
+        d1 = int(ai.max().item()) if ai.numel() else 0
+        d2 = int(bi.max().item()) if bi.numel() else 0
+    else:
+        d1, d2 = dims
+        keep = (ai <= d1) & (bi <= d2)
+        ai, bi, wv = ai[keep], bi[keep], wv[keep]
+    out = torch.zeros(d1 * d2, dtype=_dt(), device=a.device)
+    out.index_add_(0, (ai - 1) * d2 + (bi - 1), wv.to(out.dtype))
+    return out.reshape(d1, d2)
+
+
+# ============================================================================
+# statistics (reference: CentralMomentCPInstruction, CovarianceCPInstruction,
+# QuantilePickCPInstruction, LibMatrixAgg grouped aggregates)
+# ============================================================================
+def _weights(w, n, like):
+    if w is None:
+        return None
+    return _mat(w).reshape(-1).to(like.dtype)
+
+
+@builtin("moment", "centralMoment")
+def b_moment(ctx, x, a2=None, a3=None):
+    v = _mat(x).reshape(-1)
+    if a3 is not None:
+        w = _mat(a2).reshape(-1).to(v.dtype)
+        order = _int(a3)
+    else:
+        w = None
+        order = _int(a2)
+    if w is None:
+        mu = v.mean()
+        return float(((v - mu) ** order).mean().item())
+    W = w.sum()
+    mu = (v * w).sum() / W
+    return float((w * (v - mu) ** order).sum().item() / W.item())
+
+
+@builtin("cov")
+def b_cov(ctx, x, y, w=None):
+    a = _mat(x).reshape(-1)
+    b = _mat(y).reshape(-1).to(a.dtype)
+    if w is None:
+        n = a.numel()
+        return float(((a - a.mean()) * (b - b.mean())).sum().item() / (n - 1))
+    wv = _mat(w).reshape(-1).to(a.dtype)
+    W = wv.sum()
+    ma = (a * wv).sum() / W
+    mb = (b * wv).sum() / W
+    return float(((a - ma) * (b - mb) * wv).sum().item() / (W.item() - 1))
+
+
+def _sorted_weighted(x, w):
+    v = _mat(x).reshape(-1)
+    if w is None:
+        return torch.sort(v).values, None
+    wv = _mat(w).reshape(-1).to(v.dtype)
+    s = torch.sort(v)
+    return s.values, wv[s.indices]
+
+
+def _quantile_pick(vals, wts, p):
+    """Reference semantics (QuantilePickCPInstruction): value at position ceil(p*n) in sorted order."""
+    if wts is None:
+        n = vals.numel()
+        pos = int(math.ceil(p * n)) - 1
+        pos = min(max(pos, 0), n - 1)
+        return float(vals[pos].item())
+    cw = torch.cumsum(wts, 0)
+    total = float(cw[-1].item())
+    target = math.ceil(p * total)
+    idx = int(torch.searchsorted(cw, torch.tensor(target, dtype=cw.dtype, device=cw.device)).item())
+    idx = min(max(idx, 0), vals.numel() - 1)
+    return float(vals[idx].item())
+
+
+@builtin("quantile")
+def b_quantile(ctx, x, a2, a3=None):
+    if a3 is not None:
+        vals, wts = _sorted_weighted(x, a2)
+        p = a3
+    else:
+        vals, wts = _sorted_weighted(x, None)
+        p = a2
+    if isinstance(p, Tensor):
+        ps = C.cvt(p).reshape(-1).tolist()
+        out = [_quantile_pick(vals, wts, q) for q in ps]
+        return place(torch.tensor(out, dtype=torch.float64).reshape(-1, 1))
+    return _quantile_pick(vals, wts, _float(p))
+
+
+@builtin("median")
+def b_median(ctx, x, w=None):
+    vals, wts = _sorted_weighted(x, w)
+    n = vals.numel() if wts is None else float(wts.sum().item())
+    if wts is None and n % 2 == 0:
+        # reference: average of the two middle values for even counts
+        return float((vals[n // 2 - 1] + vals[n // 2]).item() / 2)
+    return _quantile_pick(vals, wts, 0.5)
+
+
+@builtin("interQuantile")
+def b_interquantile(ctx, x, a2, a3=None):
+    if a3 is not None:
+        vals, wts = _sorted_weighted(x, a2)
+        p = _float(a3)
+    else:
+        vals, wts = _sorted_weighted(x, None)
+        p = _float(a2)
+    n = vals.numel()
+    lo = int(math.ceil(n * p))
+    hi = int(math.ceil(n * (1 - p)))
+    return place(vals[lo:hi].reshape(-1, 1).clone())
+
+
+@builtin("interQuartileMean")
+def b_iqm(ctx, x, w=None):
+    vals, wts = _sorted_weighted(x, w)
+    n = vals.numel()
+    if wts is None:
+        q1 = n * 0.25
+        q3 = n * 0.75
+        lo = int(math.ceil(q1))
+        hi = int(math.ceil(q3))
+        s = vals[lo:hi].sum().item()
+        # partial weights of boundary elements (reference: IQM with fractional ends)
+        s += (lo - q1) * vals[lo - 1].item() if lo > 0 else 0.0
+        s -= (hi - q3) * vals[hi - 1].item() if hi > 0 else 0.0
+        return float(s / (q3 - q1))
+    raise DMLRuntimeError("weighted interQuartileMean not supported")
+
+
+@builtin("aggregate")
+def b_aggregate(ctx, target=None, groups=None, fn="sum", weights=None, ngroups=None, **kw):
+    t = _mat(target).reshape(-1)
+    g = torch.round(_mat(groups).reshape(-1)).long()
+    k = _int(ngroups) if ngroups is not None else int(g.max().item())
+    keep = (g >= 1) & (g <= k)
+    t, g = t[keep], g[keep] - 1
+    w = _mat(weights).reshape(-1)[keep].to(t.dtype) if weights is not None else None
+    fn = str(fn)
+    dev = t.device
+    cnt = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, w if w is not None else torch.ones_like(t))
+    if fn == "count":
+        out = cnt
+    elif fn == "sum":
+        out = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, t * w if w is not None else t)
+    elif fn == "mean":
+        s = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, t * w if w is not None else t)
+        out = s / cnt
+    elif fn in ("variance", "var"):
+        ww = w if w is not None else torch.ones_like(t)
+        s = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, t * ww)
+        mu = s / cnt
+        d = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, ww * (t - mu[g]) ** 2)
+        out = d / (cnt - 1)
+    elif fn in ("min", "max"):
+        init = math.inf if fn == "min" else -math.inf
+        out = torch.full((k,), init, dtype=t.dtype, device=dev)
+        out = out.scatter_reduce(0, g, t, reduce="amin" if fn == "min" else "amax")
+    elif fn.startswith("centralmoment") or fn == "moment":
+        order = _int(kw.get("order", 2))
+        s = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, t)
+        mu = s / cnt
+        d = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, (t - mu[g]) ** order)
+        out = d / cnt
+    else:
+        raise DMLRuntimeError(f"aggregate: unsupported fn '{fn}'")
+    return out.reshape(-1, 1)
+
+
+# ============================================================================
+# distributions (reference: ParameterizedBuiltinCPInstruction cdf/invcdf)
+# ============================================================================
+def _dist_fn(dist, q=None, p=None, lower=True, **prm):
+    from scipy import stats as st
+    dist = str(dist).lower()
+    if dist == "normal":
+        d = st.norm(loc=_float(prm.get("mean", 0.0)), scale=_float(prm.get("sd", 1.0)))
+    elif dist == "exp":
+        d = st.expon(scale=1.0 / _float(prm.get("rate", 1.0)))
+    elif dist == "chisq":
+        d = st.chi2(_float(prm["df"]))
+    elif dist == "f":
+        d = st.f(_float(prm["df1"]), _float(prm["df2"]))
+    elif dist == "t":
+        d = st.t(_float(prm["df"]))
+    else:
+        raise DMLRuntimeError(f"unsupported distribution '{dist}'")
+    if q is not None:
+        v = _float(q)
+        return float(d.cdf(v) if lower else d.sf(v))
+    v = _float(p)
+    return float(d.ppf(v))
+
+
+@builtin("cdf")
+def b_cdf(ctx, target=None, dist="normal", **kw):
+    lower = _bool(kw.pop("lower.tail", True))
+    return _dist_fn(dist, q=target, lower=lower, **kw)
+
+
+@builtin("invcdf")
+def b_invcdf(ctx, target=None, dist="normal", **kw):
+    return _dist_fn(dist, p=target, **kw)
+
+
+def _mk_dist(name, dist, inverse):
+    def fn(ctx, target=None, **kw):
+        lower = _bool(kw.pop("lower.tail", True))
+        if inverse:
+            return _dist_fn(dist, p=target, **kw)
+        return _dist_fn(dist, q=target, lower=lower, **kw)
+    REGISTRY[name] = fn
+
+
+for _n, _d in (("pnorm", "normal"), ("pexp", "exp"), ("pchisq", "chisq"), ("pf", "f"), ("pt", "t")):
+    _mk_dist(_n, _d, False)
+for _n, _d in (("qnorm", "normal"), ("qexp", "exp"), ("qchisq", "chisq"), ("qf", "f"), ("qt", "t")):
+    _mk_dist(_n, _d, True)
+
+
+# ============================================================================
+# linear algebra (reference: LibCommonsMath.java)
+# ============================================================================
+def _la(x):
+    m = _mat(x)
+    return m.double() if m.dtype != torch.float64 else m
+
+
+@builtin("solve")
+def b_solve(ctx, A, b):
+    a, bb = _la(A), _la(b)
+    if a.shape[0] != a.shape[1]:
+        # least squares (reference: QR-based solve for non-square)
+        return torch.linalg.lstsq(a.cpu(), bb.cpu()).solution.to(_dev(), _dt())
+    return torch.linalg.solve(a, bb).to(_dt())
+
+
+@builtin("inv", "inverse")
+def b_inv(ctx, A):
+    a = _la(A)
+    if a.shape[0] != a.shape[1]:
+        raise DMLRuntimeError("inv requires a square matrix")
+    return torch.linalg.inv(a).to(_dt())
+
+
+@builtin("cholesky")
+def b_cholesky(ctx, A):
+    return torch.linalg.cholesky(_la(A)).to(_dt())
+
+
+@builtin("eigen", multi=True)
+def b_eigen(ctx, A):
+    a = _la(A)
+    w, v = torch.linalg.eigh(a)
+    return (w.reshape(-1, 1).to(_dt()), v.to(_dt()))
+
+
+@builtin("svd", multi=True)
+def b_svd(ctx, A):
+    a = _la(A)
+    U, Sv, Vh = torch.linalg.svd(a, full_matrices=False)
+    return (U.to(_dt()), torch.diag(Sv).to(_dt()), Vh.t().contiguous().to(_dt()))
+
+
+@builtin("qr", multi=True)
+def b_qr(ctx, A):
+    a = _la(A)
+    # reference returns Householder vectors H and R; we return Q-equivalent H = Q and R
+    Q, R = torch.linalg.qr(a, mode="complete")
+    return (Q.to(_dt()), R.to(_dt()))
+
+
+@builtin("lu", multi=True)
+def b_lu(ctx, A):
+    a = _la(A)
+    P, L, U = torch.linalg.lu(a)
+    return (P.t().contiguous().to(_dt()), L.to(_dt()), U.to(_dt()))
+
+
+# ============================================================================
+# lists / eval
+# ============================================================================
+@builtin("list")
+def b_list(ctx, *args, **kw):
+    if kw and not args:
+        return ListObject(list(kw.values()), list(kw.keys()))
+    if kw:
+        return ListObject(list(args) + list(kw.values()), [""] * len(args) + list(kw.keys()))
+    return ListObject(list(args))
+
+
+# ============================================================================
+# IO
+# ============================================================================
+@builtin("read")
+def b_read(ctx, fname, **kw):
+    from ..io import readers
+    return readers.read(ctx, S.to_str(fname), **kw)
+
+
+@builtin("write")
+def b_write(ctx, x, fname, **kw):
+    from ..io import writers
+    writers.write(ctx, x, S.to_str(fname), **kw)
+
+
+# ============================================================================
+# DNN builtins (reference: LibMatrixDNN*, ConvolutionCPInstruction)
+# ============================================================================
+def _nchw(x, C_, H, W):
+    return _mat(x).reshape(-1, C_, H, W)
+
+
+def _shape4(v):
+    if isinstance(v, ListObject):
+        return [_int(a) for a in v.data]
+    if isinstance(v, (list, tuple)):
+        return [_int(a) for a in v]
+    raise DMLRuntimeError("expected a list of 4 integers (e.g. input_shape=[N,C,H,W])")
+
+
+def _conv_params(kw):
+    ishape = _shape4(kw["input_shape"])
+    stride = _shape4(kw.get("stride", [1, 1]))
+    padding = _shape4(kw.get("padding", [0, 0]))
+    return ishape, stride, padding
+
+
+@builtin("conv2d")
+def b_conv2d(ctx, input=None, filter=None, **kw):
+    from ..ops import dnn
+    return dnn.conv2d(_mat(input), _mat(filter), **_conv_kw(kw))
+
+
+@builtin("conv2d_backward_filter")
+def b_conv2d_bwd_filter(ctx, input=None, dout=None, **kw):
+    from ..ops import dnn
+    return dnn.conv2d_backward_filter(_mat(input), _mat(dout), **_conv_kw(kw))
+
+
+@builtin("conv2d_backward_data")
+def b_conv2d_bwd_data(ctx, filter=None, dout=None, **kw):
+    from ..ops import dnn
+    return dnn.conv2d_backward_data(_mat(filter), _mat(dout), **_conv_kw(kw))
+
+
+def _conv_kw(kw):
+    out = {}
+    for k in ("input_shape", "filter_shape", "stride", "padding", "pool_size"):
+        if k in kw:
+            out[k] = _shape4(kw[k])
+    return out
+
+
+@builtin("max_pool", "avg_pool")
+def b_pool(ctx, input=None, **kw):
+    from ..ops import dnn
+    return dnn.pool(_mat(input), kind=kw.get("__name__", "max"), **_conv_kw(kw))
+
+
+def _pool_factory(kind, backward):
+    def fn(ctx, input=None, dout=None, **kw):
+        from ..ops import dnn
+        if backward:
+            return dnn.pool_backward(_mat(input), _mat(dout), kind=kind, **_conv_kw(kw))
+        return dnn.pool(_mat(input), kind=kind, **_conv_kw(kw))
+    return fn
+
+
+REGISTRY["max_pool"] = _pool_factory("max", False)
+REGISTRY["avg_pool"] = _pool_factory("avg", False)
+REGISTRY["max_pool_backward"] = _pool_factory("max", True)
+REGISTRY["avg_pool_backward"] = _pool_factory("avg", True)
+
+
+@builtin("bias_add")
+def b_bias_add(ctx, input, bias):
+    x = _mat(input)
+    b = _mat(bias).reshape(-1)
+    C_ = b.numel()
+    return (x.reshape(x.shape[0], C_, -1) + b.reshape(1, C_, 1)).reshape(x.shape[0], -1)
+
+
+@builtin("bias_multiply")
+def b_bias_mult(ctx, input, bias):
+    x = _mat(input)
+    b = _mat(bias).reshape(-1)
+    C_ = b.numel()
+    return (x.reshape(x.shape[0], C_, -1) * b.reshape(1, C_, 1)).reshape(x.shape[0], -1)
+
+
+# ============================================================================
+# frames / transform (reference: runtime/transform/*)
+# ============================================================================
+@builtin("transformencode", multi=True)
+def b_transformencode(ctx, target=None, spec=None):
+    from . import transform
+    return transform.encode(ctx, target, spec)
+
+
+@builtin("transformapply")
+def b_transformapply(ctx, target=None, spec=None, meta=None):
+    from . import transform
+    return transform.apply(ctx, target, spec, meta)
+
+
+@builtin("transformdecode")
+def b_transformdecode(ctx, target=None, spec=None, meta=None):
+    from . import transform
+    return transform.decode(ctx, target, spec, meta)
+
+
+@builtin("transformcolmap")
+def b_transformcolmap(ctx, target=None, spec=None):
+    from . import transform
+    return transform.colmap(ctx, target, spec)
+
+
+@builtin("transformmeta")
+def b_transformmeta(ctx, spec=None, meta=None):
+    from . import transform
+    return transform.read_meta(ctx, spec, meta)

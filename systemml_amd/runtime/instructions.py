@@ -1,0 +1,113 @@
+"""Instruction binding: HOP → executable closure (reference:
+runtime/instructions/InstructionParser + cp/*CPInstruction, gpu/*GPUInstruction).
+
+Each closure has the signature ``fn(ctx, args) -> value`` where ``args`` are the
+already-evaluated input values.  Exec-type (host CP vs. HBM GPU vs. row-
+partitioned DIST) is resolved by the operator library from where the operands
+live, so the same instruction stream runs on every backend.
+"""
+from __future__ import annotations
+
+from ..parser.errors import DMLRuntimeError
+from ..ops import core as C
+from . import builtins as B
+
+
+def make_impl(h):
+    op = h.op
+    p = h.p
+    if op == "lit":
+        v = p["v"]
+        return (lambda ctx, a: v), "lit"
+    if op == "tread":
+        name = p["name"]
+        pos = h.pos
+
+        def tread(ctx, a):
+            try:
+                return ctx.vars[name]
+            except KeyError:
+                raise DMLRuntimeError(f"{pos}: Variable '{name}' is not defined" if pos else
+                                      f"Variable '{name}' is not defined")
+        return tread, "tread"
+    if op == "b":
+        o = p["o"]
+        f = C.binary
+        return (lambda ctx, a: f(o, a[0], a[1])), o
+    if op == "u":
+        o = p["o"]
+        f = C.unary
+        return (lambda ctx, a: f(o, a[0])), o
+    if op == "agg":
+        o, d = p["o"], p["dir"]
+        f = C.agg
+        code = {"all": "ua", "row": "uar", "col": "uac"}[d] + o
+        return (lambda ctx, a: f(o, d, a[0])), code
+    if op == "mm":
+        tA = p.get("transA", False)
+        f = C.mm
+        return (lambda ctx, a: f(a[0], a[1], tA)), ("ba+*T" if tA else "ba+*")
+    if op == "tsmm":
+        left = p["left"]
+        return (lambda ctx, a: C.tsmm(a[0], left)), "tsmm"
+    if op == "mmchain":
+        t = p["type"]
+        return (lambda ctx, a: C.mmchain(t, a[0], a[1], a[2] if len(a) > 2 else None)), "mmchain-" + t
+    if op == "tak":
+        return (lambda ctx, a: C.tak(a[0], a[1])), "tak+*"
+    if op == "t":
+        return (lambda ctx, a: C.transpose(a[0])), "r'"
+    if op == "rix":
+        lm = p.get("list", False)
+        return (lambda ctx, a: C.rix(a[0], a[1], a[2], a[3], a[4], lm)), "rix"
+    if op == "lix":
+        lm = p.get("list", False)
+        return (lambda ctx, a: C.lix(a[0], a[1], a[2], a[3], a[4], a[5], lm)), "lix"
+    if op == "fout":
+        i = p["i"]
+
+        def fout(ctx, a):
+            r = a[0]
+            if not isinstance(r, tuple):
+                if i == 0:
+                    return r
+                raise DMLRuntimeError("function returned fewer outputs than requested")
+            if i >= len(r):
+                raise DMLRuntimeError("function returned fewer outputs than requested")
+            return r[i]
+        return fout, "fout"
+    if op == "fcall":
+        fkey = p["fkey"]
+        given = p["given"]
+        from . import program as PR
+        return (lambda ctx, a: PR.call_function(ctx, fkey, a, given)), f"fcall {fkey[1]}"
+    if op in ("bi", "sink"):
+        name = p["name"]
+        if name == "exists":
+            var = p.get("var")
+            return (lambda ctx, a: var in ctx.vars), "exists"
+        if name == "eval":
+            from . import program as PR
+            npos = p.get("npos", len(h.inputs))
+            named = list(h.named)
+            nskey = p["nskey"]
+            imports = dict(p["imports"])
+
+            def ev(ctx, a):
+                return PR.eval_call(ctx, a[0], list(a[1:npos]), dict(zip(named, a[npos:])), nskey, imports)
+            return ev, "eval"
+        fn = B.REGISTRY.get(name)
+        if fn is None:
+            pos = h.pos
+
+            def missing(ctx, a):
+                raise DMLRuntimeError(f"{pos}: unknown builtin function '{name}'")
+            return missing, name
+        npos = p.get("npos", len(h.inputs))
+        named = list(h.named)
+        if name in ("max_pool", "avg_pool", "max_pool_backward", "avg_pool_backward"):
+            pass
+        if not named:
+            return (lambda ctx, a: fn(ctx, *a)), name
+        return (lambda ctx, a: fn(ctx, *a[:npos], **dict(zip(named, a[npos:])))), name
+    raise DMLRuntimeError(f"cannot bind instruction for hop {h!r}")

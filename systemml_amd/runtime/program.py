@@ -1,0 +1,246 @@
+"""Program execution (reference: runtime/controlprogram/{Program,ProgramBlock,
+IfProgramBlock,WhileProgramBlock,ForProgramBlock,ParForProgramBlock,
+FunctionProgramBlock}.java, context/ExecutionContext.java).
+
+SPMD model for multi-GPU: every rank executes the same control program;
+row-partitioned matrices live in each rank's HBM and all scalars that steer
+control flow are produced by collectives, so ranks stay in lock-step without
+a driver/worker split.
+"""
+from __future__ import annotations
+
+import sys
+import time
+
+import torch
+
+from ..parser.errors import DMLRuntimeError, DMLScriptStop
+from ..compiler.blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
+from . import scalars as S
+
+
+class ExecutionContext:
+    def __init__(self, program, config, stats=None, out=None, dist=None):
+        self.vars = {}
+        self.program = program
+        self.config = config
+        self.stats = stats
+        self.dist = dist
+        self._out = out
+        self.depth = 0
+
+    def print(self, s):
+        if self.dist is not None and self.config.print_rank0_only and self.dist.rank != 0:
+            return
+        if self._out is not None:
+            self._out(s)
+        else:
+            sys.stdout.write(s + "\n")
+            sys.stdout.flush()
+
+
+# ----------------------------------------------------------------------------
+def _to_bool(v):
+    if isinstance(v, torch.Tensor):
+        if v.numel() != 1:
+            raise DMLRuntimeError("predicate must evaluate to a scalar")
+        return bool(v.reshape(-1)[0].item() != 0)
+    return S.as_bool(v)
+
+
+def _to_num(v):
+    if isinstance(v, torch.Tensor):
+        if v.numel() != 1:
+            raise DMLRuntimeError("loop bound must be a scalar")
+        return float(v.reshape(-1)[0].item())
+    if isinstance(v, bool):
+        return int(v)
+    if isinstance(v, str):
+        return S.parse_literal_arg(v)
+    return v
+
+
+def _attach_pos(e, pos):
+    msg = str(e)
+    if pos is not None and "line" not in msg:
+        return type(e)(f"{pos}: {msg}")
+    return e
+
+
+def exec_instrs(ctx, instrs, nslots):
+    slots = [None] * nslots
+    stats = ctx.stats
+    if stats is not None and stats.enabled:
+        sync = stats.sync
+        for ins in instrs:
+            t0 = time.perf_counter()
+            try:
+                r = ins.fn(ctx, [slots[i] for i in ins.ins])
+            except DMLScriptStop:
+                raise
+            except DMLRuntimeError as e:
+                raise _attach_pos(e, ins.hop.pos) from e
+            except (RuntimeError, ValueError, TypeError, IndexError, ZeroDivisionError) as e:
+                raise DMLRuntimeError(f"{ins.hop.pos}: error in {ins.opcode}: {e}") from e
+            if sync and torch.cuda.is_available() and isinstance(r, torch.Tensor) and r.is_cuda:
+                torch.cuda.synchronize()
+            stats.record(ins.opcode, time.perf_counter() - t0)
+            slots[ins.out] = r
+            for f in ins.free:
+                slots[f] = None
+        return slots
+    for ins in instrs:
+        try:
+            slots[ins.out] = ins.fn(ctx, [slots[i] for i in ins.ins])
+        except DMLScriptStop:
+            raise
+        except DMLRuntimeError as e:
+            raise _attach_pos(e, ins.hop.pos) from e
+        except (RuntimeError, ValueError, TypeError, IndexError, ZeroDivisionError) as e:
+            raise DMLRuntimeError(f"{ins.hop.pos}: error in {ins.opcode}: {e}") from e
+        for f in ins.free:
+            slots[f] = None
+    return slots
+
+
+def eval_pred(ctx, pred):
+    if pred.is_const:
+        return pred.const
+    slots = exec_instrs(ctx, pred.instrs, pred.nslots)
+    return slots[pred.out]
+
+
+def exec_blocks(ctx, blocks):
+    for b in blocks:
+        exec_block(ctx, b)
+
+
+def exec_block(ctx, b):
+    if isinstance(b, BasicBlock):
+        slots = exec_instrs(ctx, b.instrs, b.nslots)
+        vars_ = ctx.vars
+        for name, s in b.writes_slots:
+            vars_[name] = slots[s]
+        for name in b.rmvars:
+            vars_.pop(name, None)
+        return
+    if isinstance(b, IfBlock):
+        if _to_bool(eval_pred(ctx, b.pred)):
+            exec_blocks(ctx, b.then_blocks)
+        else:
+            exec_blocks(ctx, b.else_blocks)
+        return
+    if isinstance(b, WhileBlock):
+        while _to_bool(eval_pred(ctx, b.pred)):
+            exec_blocks(ctx, b.body)
+        return
+    if isinstance(b, ForBlock):
+        start = _to_num(eval_pred(ctx, b.start))
+        end = _to_num(eval_pred(ctx, b.end))
+        if b.incr is not None:
+            incr = _to_num(eval_pred(ctx, b.incr))
+        else:
+            incr = 1 if start <= end else -1
+        if incr == 0:
+            raise DMLRuntimeError("for loop increment must not be zero")
+        as_int = all(isinstance(x, int) or (isinstance(x, float) and x.is_integer()) for x in (start, end, incr)) \
+            and not any(isinstance(x, float) and not x.is_integer() for x in (start, incr))
+        if b.parfor and ctx.config.parallelism > 1:
+            from .parfor import exec_parfor
+            exec_parfor(ctx, b, start, end, incr, as_int)
+            return
+        i = start
+        cnt = 0
+        while (incr > 0 and i <= end) or (incr < 0 and i >= end):
+            ctx.vars[b.var] = int(i) if as_int else float(i)
+            exec_blocks(ctx, b.body)
+            cnt += 1
+            i = start + cnt * incr
+        return
+    raise DMLRuntimeError(f"unknown block type {type(b).__name__}")
+
+
+# ----------------------------------------------------------------------------
+# functions
+# ----------------------------------------------------------------------------
+def _coerce(v, param):
+    if param.dtype == "SCALAR" and not isinstance(v, torch.Tensor):
+        vt = param.vtype
+        try:
+            if vt == "DOUBLE" and isinstance(v, (int, bool)) :
+                return float(v)
+            if vt == "INT" and isinstance(v, float) and v.is_integer():
+                return int(v)
+            if vt == "BOOLEAN" and not isinstance(v, bool) and isinstance(v, (int, float)):
+                return bool(v)
+        except (TypeError, ValueError):
+            return v
+    return v
+
+
+def call_function(ctx, fkey, args, given):
+    fb = ctx.program.functions.get(fkey)
+    if fb is None:
+        raise DMLRuntimeError(f"function {fkey[1]} not found")
+    if fb.external:
+        from .udf import call_external
+        return call_external(ctx, fb, args, given)
+    new_vars = {}
+    params = {p.name: p for p in fb.inputs}
+    for name, v in zip(given, args):
+        new_vars[name] = _coerce(v, params[name])
+    saved = ctx.vars
+    for p in fb.inputs:
+        if p.name not in new_vars:
+            if p.name in fb.default_preds:
+                ctx.vars = new_vars
+                try:
+                    new_vars[p.name] = _coerce(eval_pred(ctx, fb.default_preds[p.name]), p)
+                finally:
+                    ctx.vars = saved
+            else:
+                raise DMLRuntimeError(f"missing argument '{p.name}' in call to function {fb.name}")
+    ctx.vars = new_vars
+    ctx.depth += 1
+    if ctx.depth > 500:
+        raise DMLRuntimeError("maximum function recursion depth exceeded")
+    try:
+        exec_blocks(ctx, fb.body)
+    finally:
+        ctx.vars = saved
+        ctx.depth -= 1
+    outs = []
+    for o in fb.outputs:
+        if o.name not in new_vars:
+            raise DMLRuntimeError(f"function {fb.name}: output variable '{o.name}' was not assigned")
+        outs.append(_coerce(new_vars[o.name], o))
+    return tuple(outs)
+
+
+def eval_call(ctx, fname, args, named, nskey, imports):
+    """DML `eval("fname", args...)` (reference: EvalNaryCPInstruction)."""
+    from . import builtins as B
+    fname = S.to_str(fname)
+    ns = None
+    if "::" in fname:
+        ns, fname = fname.split("::", 1)
+    key = imports.get(ns) if ns else nskey
+    fb = ctx.program.functions.get((key, fname))
+    if fb is None and ns is None:
+        fb = ctx.program.functions.get((".defaultNS", fname))
+    if fb is not None:
+        names = [p.name for p in fb.inputs]
+        given = names[:len(args)] + list(named.keys())
+        out = call_function(ctx, (fb.namespace, fb.name), list(args) + list(named.values()), given)
+        return out[0] if len(out) == 1 else out
+    fn = B.REGISTRY.get(fname)
+    if fn is None:
+        from ..ops import core as C
+        unary = {"abs", "exp", "log", "sqrt", "round", "floor", "ceil", "sign", "sin", "cos", "tan"}
+        if fname in unary:
+            return C.unary(fname, args[0])
+        agg = {"sum": "sum", "mean": "mean", "min": "min", "max": "max", "prod": "prod"}
+        if fname in agg:
+            return C.agg(agg[fname], "all", args[0])
+        raise DMLRuntimeError(f"eval: function '{fname}' not found")
+    return fn(ctx, *args, **named)

@@ -1,0 +1,306 @@
+"""DML scalar semantics: value types, arithmetic, comparison, casting and
+Java-compatible string formatting.
+
+Reference behaviour: runtime/instructions/cp/{Int,Double,Boolean,String}Object.java
+(Double.toString, Long.toString, upper-cased booleans), runtime/functionobjects/
+{Plus,Minus,Multiply,Divide,Power,Modulus,IntegerDivide,...}.java and
+ScalarObjectFactory (INT op INT stays INT except for '/' and '^').
+"""
+from __future__ import annotations
+
+import math
+from decimal import Decimal
+
+from ..parser.errors import DMLRuntimeError
+
+INF = float("inf")
+
+
+def java_double_str(d: float) -> str:
+    """Emulates java.lang.Double.toString."""
+    if d != d:
+        return "NaN"
+    if d == INF:
+        return "Infinity"
+    if d == -INF:
+        return "-Infinity"
+    if d == 0.0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    a = abs(d)
+    r = repr(float(d))
+    if 1e-3 <= a < 1e7:
+        if "e" in r or "E" in r:
+            r = format(Decimal(r), "f")
+        if "." not in r:
+            r += ".0"
+        return r
+    sign, digits, exp = Decimal(r).as_tuple()
+    digits = list(digits)
+    while len(digits) > 1 and digits[-1] == 0:
+        digits.pop()
+        exp += 1
+    e10 = len(digits) - 1 + exp
+    mant = str(digits[0]) + "." + ("".join(map(str, digits[1:])) or "0")
+    return ("-" if sign else "") + mant + "E" + str(e10)
+
+
+def to_str(v) -> str:
+    if isinstance(v, bool):
+        return "TRUE" if v else "FALSE"
+    if isinstance(v, int):
+        return str(v)
+    if isinstance(v, float):
+        return java_double_str(v)
+    if isinstance(v, str):
+        return v
+    return str(v)
+
+
+def vtype_of(v):
+    if isinstance(v, bool):
+        return "BOOLEAN"
+    if isinstance(v, int):
+        return "INT"
+    if isinstance(v, float):
+        return "DOUBLE"
+    if isinstance(v, str):
+        return "STRING"
+    return "UNKNOWN"
+
+
+def as_double(v):
+    if isinstance(v, str):
+        try:
+            return float(v)
+        except ValueError:
+            raise DMLRuntimeError(f"cannot cast string '{v}' to double")
+    return float(v)
+
+
+def as_int(v):
+    if isinstance(v, str):
+        try:
+            return int(float(v))
+        except ValueError:
+            raise DMLRuntimeError(f"cannot cast string '{v}' to int")
+    if isinstance(v, float):
+        if v != v or v in (INF, -INF):
+            raise DMLRuntimeError("cannot cast NaN/Inf to int")
+        return int(v)   # truncation like Java (long) cast
+    return int(v)
+
+
+def as_bool(v):
+    if isinstance(v, str):
+        u = v.strip().upper()
+        if u in ("TRUE", "T"):
+            return True
+        if u in ("FALSE", "F"):
+            return False
+        raise DMLRuntimeError(f"cannot cast string '{v}' to boolean")
+    return bool(v != 0)
+
+
+def _num(v):
+    if isinstance(v, bool):
+        return 1 if v else 0
+    return v
+
+
+def _r_mod(a, b):
+    # R semantics: a - floor(a/b)*b
+    if b == 0:
+        return float("nan")
+    return a - math.floor(a / b) * b
+
+
+def _r_intdiv(a, b):
+    if b == 0:
+        if a == 0:
+            return float("nan")
+        return INF if a > 0 else -INF
+    return math.floor(a / b)
+
+
+def _pow(a, b):
+    try:
+        r = math.pow(a, b)
+    except (OverflowError, ValueError):
+        try:
+            r = float(a) ** float(b)
+            if isinstance(r, complex):
+                return float("nan")
+        except OverflowError:
+            return INF
+        except ZeroDivisionError:
+            return INF
+    return r
+
+
+def _div(a, b):
+    a = float(a)
+    b = float(b)
+    if b == 0.0:
+        if a == 0.0 or a != a:
+            return float("nan")
+        return math.copysign(INF, a) * math.copysign(1.0, b)
+    return a / b
+
+
+def _cmp_prep(a, b):
+    if isinstance(a, str) or isinstance(b, str):
+        return to_str(a), to_str(b)
+    return _num(a), _num(b)
+
+
+def binary(op: str, a, b):
+    """Scalar-scalar binary operation with DML typing rules."""
+    if op == "+":
+        if isinstance(a, str) or isinstance(b, str):
+            return to_str(a) + to_str(b)
+        a, b = _num(a), _num(b)
+        return a + b
+    if op in ("==", "!=", "<", "<=", ">", ">="):
+        a, b = _cmp_prep(a, b)
+        if op == "==":
+            return a == b
+        if op == "!=":
+            return a != b
+        if op == "<":
+            return a < b
+        if op == "<=":
+            return a <= b
+        if op == ">":
+            return a > b
+        return a >= b
+    if op in ("&", "|", "xor"):
+        x, y = as_bool(a), as_bool(b)
+        if op == "&":
+            return x and y
+        if op == "|":
+            return x or y
+        return x != y
+    if isinstance(a, str) or isinstance(b, str):
+        raise DMLRuntimeError(f"operator '{op}' not supported for strings")
+    a, b = _num(a), _num(b)
+    both_int = isinstance(a, int) and isinstance(b, int)
+    if op == "-":
+        return a - b
+    if op == "*":
+        return a * b
+    if op == "/":
+        return _div(a, b)
+    if op == "^":
+        return _pow(float(a), float(b))
+    if op == "%%":
+        if both_int and b != 0:
+            return a - (a // b) * b
+        return _r_mod(float(a), float(b))
+    if op == "%/%":
+        if both_int and b != 0:
+            return a // b
+        return float(_r_intdiv(float(a), float(b)))
+    if op == "min":
+        return min(a, b) if both_int else float(min(a, b) if (a == a and b == b) else float("nan"))
+    if op == "max":
+        return max(a, b) if both_int else float(max(a, b) if (a == a and b == b) else float("nan"))
+    if op == "log":
+        return _log(float(a), float(b))
+    if op == "bitwAnd":
+        return int(a) & int(b)
+    if op == "bitwOr":
+        return int(a) | int(b)
+    if op == "bitwXor":
+        return int(a) ^ int(b)
+    if op == "bitwShiftL":
+        return int(a) << int(b)
+    if op == "bitwShiftR":
+        return int(a) >> int(b)
+    raise DMLRuntimeError(f"unknown scalar binary operator {op}")
+
+
+def _log(a, base=None):
+    if a < 0 or a != a:
+        return float("nan")
+    if a == 0:
+        return -INF
+    if base is None:
+        return math.log(a)
+    return math.log(a) / math.log(base)
+
+
+def _round_half_up(x):
+    # Java Math.round semantics (round half up) -> SystemML 'round' uses Math.round
+    if x != x or x in (INF, -INF):
+        return x
+    return float(math.floor(x + 0.5))
+
+
+def unary(op: str, a):
+    if op == "neg":
+        if isinstance(a, str):
+            raise DMLRuntimeError("cannot negate a string")
+        return -_num(a)
+    if op == "not":
+        return not as_bool(a)
+    if op == "ident":
+        return a
+    if op in ("cast_double",):
+        return as_double(a)
+    if op == "cast_int":
+        return as_int(a)
+    if op == "cast_bool":
+        return as_bool(a)
+    if op == "cast_scalar":
+        return a
+    x = float(_num(a))
+    if op == "abs":
+        v = abs(_num(a))
+        return v
+    if op == "exp":
+        try:
+            return math.exp(x)
+        except OverflowError:
+            return INF
+    if op == "log":
+        return _log(x)
+    if op == "sqrt":
+        return math.sqrt(x) if x >= 0 else float("nan")
+    if op == "round":
+        return _round_half_up(x)
+    if op == "floor":
+        return float(math.floor(x)) if math.isfinite(x) else x
+    if op == "ceil":
+        return float(math.ceil(x)) if math.isfinite(x) else x
+    if op == "sign":
+        return float((x > 0) - (x < 0)) if x == x else x
+    fn = {"sin": math.sin, "cos": math.cos, "tan": math.tan, "asin": math.asin, "acos": math.acos,
+          "atan": math.atan, "sinh": math.sinh, "cosh": math.cosh, "tanh": math.tanh}.get(op)
+    if fn is not None:
+        try:
+            return fn(x)
+        except (ValueError, OverflowError):
+            return float("nan") if op in ("asin", "acos") else (INF if x > 0 else -INF)
+    raise DMLRuntimeError(f"unknown scalar unary operator {op}")
+
+
+def parse_literal_arg(s: str):
+    """Type a command-line argument value (reference: DMLScript argument typing)."""
+    if isinstance(s, (bool, int, float)):
+        return s
+    t = s.strip()
+    if t in ("TRUE", "true", "True"):
+        return True
+    if t in ("FALSE", "false", "False"):
+        return False
+    try:
+        return int(t)
+    except ValueError:
+        pass
+    try:
+        return float(t)
+    except ValueError:
+        pass
+    if len(t) >= 2 and t[0] == t[-1] and t[0] in "\"'":
+        return t[1:-1]
+    return s
