@@ -48,10 +48,29 @@ def compile_script(source, args=None, inputs=(), outputs=(), config=None, pydml=
     prog = parse(source, pydml=pydml, filename=filename)
     t1 = time.perf_counter()
     tr = Translator(args or {}, config, base_dir=base_dir or (os.path.dirname(filename) if filename else None))
-    cp = tr.compile(prog, inputs=inputs, outputs=outputs)
+    input_types = {}
+    if isinstance(inputs, dict):
+        input_types = {k: value_dt(v) for k, v in inputs.items()}
+    cp = tr.compile(prog, inputs=list(inputs), outputs=outputs, input_types=input_types)
     compile_program(cp, make_impl, config)
     t2 = time.perf_counter()
     return CompiledScript(cp, config, set(inputs), list(outputs), t1 - t0, t2 - t1)
+
+
+def value_dt(v):
+    if isinstance(v, (bool, int, float, str, np.generic)):
+        return "S"
+    if isinstance(v, FrameBlock):
+        return "F"
+    if isinstance(v, ListObject):
+        return "L"
+    try:
+        import pandas as pd
+        if isinstance(v, pd.DataFrame) and not all(np.issubdtype(t, np.number) for t in v.dtypes):
+            return "F"
+    except ImportError:
+        pass
+    return "M"
 
 
 def convert_input(v, dist=None, config=None):
@@ -124,7 +143,7 @@ def execute(cs: CompiledScript, inputs=None, out=None, stats=None, dist=None):
 def run(source, args=None, inputs=None, outputs=(), config=None, pydml=False, filename="", out=None,
         stats=None):
     inputs = inputs or {}
-    cs = compile_script(source, args, inputs=inputs.keys(), outputs=outputs, config=config, pydml=pydml,
+    cs = compile_script(source, args, inputs=inputs, outputs=outputs, config=config, pydml=pydml,
                         filename=filename)
     res, _ = execute(cs, inputs, out=out, stats=stats)
     return res

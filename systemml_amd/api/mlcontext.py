@@ -1,0 +1,251 @@
+"""MLContext programmatic API (reference: api/mlcontext/{MLContext,Script,ScriptFactory,
+MLResults,Matrix,Frame,MatrixMetadata}.java and src/main/python/systemml/mlcontext.py).
+
+    from systemml_amd import MLContext, dml
+    ml = MLContext()
+    script = dml("y = X %*% w").input(X=np.ones((3, 2)), w=np.ones((2, 1))).output("y")
+    y = ml.execute(script).get("y").toNumPy()
+
+Inputs accept numpy arrays, torch tensors (host or HBM), pandas DataFrames,
+scipy sparse matrices, Python scalars/strings, FrameBlock / ListObject and
+row-partitioned DistMatrix objects.  Outputs come back as `Matrix` / `Frame`
+wrappers (lazy device→host conversion) or Python scalars.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ..conf import DMLConfig, get_default_config
+from ..runtime.data import FrameBlock, ListObject
+from ..utils.stats import Statistics
+from . import executor as EX
+
+SCRIPTS_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts")
+
+
+class Matrix:
+    """Result matrix handle (reference: api/mlcontext/Matrix.java)."""
+
+    def __init__(self, value):
+        self._v = value
+
+    def _tensor(self):
+        from ..ops import core as C
+        v = self._v
+        if C.is_dist(v):
+            v = C._dist().gather(v)
+        return v
+
+    def toNumPy(self):
+        return self._tensor().detach().to("cpu", torch.float64).numpy()
+
+    def toTorch(self):
+        return self._tensor()
+
+    def toDF(self):
+        import pandas as pd
+        return pd.DataFrame(self.toNumPy(), columns=[f"C{i + 1}" for i in range(self.shape[1])])
+
+    @property
+    def shape(self):
+        return tuple(self._v.shape)
+
+    def __repr__(self):
+        return f"Matrix{self.shape}"
+
+
+class Frame:
+    def __init__(self, fb: FrameBlock):
+        self._f = fb
+
+    def toDF(self):
+        import pandas as pd
+        return pd.DataFrame({n: c for n, c in zip(self._f.names, self._f.columns)})
+
+    def toFrameBlock(self):
+        return self._f
+
+    @property
+    def shape(self):
+        return self._f.shape
+
+
+def _wrap(v):
+    if isinstance(v, torch.Tensor):
+        return Matrix(v)
+    from ..ops import core as C
+    if C.is_dist(v):
+        return Matrix(v)
+    if isinstance(v, FrameBlock):
+        return Frame(v)
+    return v
+
+
+class MLResults:
+    def __init__(self, values, stats=None):
+        self._values = values
+        self.stats = stats
+
+    def get(self, *names):
+        out = [_wrap(self._values[n]) for n in names]
+        return out[0] if len(out) == 1 else tuple(out)
+
+    def getNumPyArray(self, name):
+        return self.get(name).toNumPy()
+
+    def getMatrix(self, name):
+        return self.get(name)
+
+    def getScalar(self, name):
+        return self._values[name]
+
+    def getDouble(self, name):
+        return float(self._values[name])
+
+    def getLong(self, name):
+        return int(self._values[name])
+
+    def getString(self, name):
+        from ..runtime import scalars as S
+        return S.to_str(self._values[name])
+
+    def getBoolean(self, name):
+        return bool(self._values[name])
+
+    def keys(self):
+        return list(self._values.keys())
+
+    def __getitem__(self, name):
+        return self.get(name)
+
+
+class Script:
+    def __init__(self, source, pydml=False, filename=""):
+        self.source = source
+        self.pydml = pydml
+        self.filename = filename
+        self._inputs = {}
+        self._outputs = []
+        self._args = {}
+
+    def input(self, *args, **kw):
+        if args:
+            if len(args) != 2:
+                raise ValueError("input(name, value) or input(name=value)")
+            kw = {args[0]: args[1]}
+        for k, v in kw.items():
+            if k.startswith("$"):
+                self._args[k[1:]] = v
+            else:
+                self._inputs[k] = v
+        return self
+
+    def output(self, *names):
+        self._outputs.extend(names)
+        return self
+
+    def args(self, **kw):
+        self._args.update({k: (v if isinstance(v, str) else v) for k, v in kw.items()})
+        return self
+
+    def setName(self, name):
+        self.filename = name
+        return self
+
+    def clearAll(self):
+        self._inputs.clear()
+        self._outputs.clear()
+        self._args.clear()
+        return self
+
+
+def dml(source):
+    return Script(source)
+
+
+def pydml(source):
+    return Script(source, pydml=True)
+
+
+def dmlFromFile(path):
+    with open(path) as f:
+        return Script(f.read(), filename=os.path.abspath(path))
+
+
+def pydmlFromFile(path):
+    with open(path) as f:
+        return Script(f.read(), pydml=True, filename=os.path.abspath(path))
+
+
+def dmlFromResource(rel):
+    """Load one of the bundled scripts (systemml_amd/scripts/...)."""
+    path = os.path.join(SCRIPTS_DIR, rel)
+    return dmlFromFile(path)
+
+
+class MLContext:
+    def __init__(self, sc=None, config: DMLConfig = None):
+        self.config = (config or get_default_config()).copy()
+        self._stats = False
+        self._explain = ""
+        self._out = None
+        self.last_stats = None
+
+    # configuration (reference method names)
+    def setStatistics(self, flag=True):
+        self._stats = bool(flag)
+        return self
+
+    def setExplain(self, flag=True, level="hops"):
+        self._explain = level if flag else ""
+        return self
+
+    def setExplainLevel(self, level):
+        self._explain = level
+        return self
+
+    def setGPU(self, flag=True):
+        self.config.gpu = bool(flag)
+        return self
+
+    def setForceGPU(self, flag=True):
+        self.config.gpu = bool(flag)
+        return self
+
+    def setConfigProperty(self, key, value):
+        self.config.set(key, value)
+        return self
+
+    def setConfig(self, path):
+        self.config = DMLConfig.from_xml(path)
+        return self
+
+    def setOutput(self, fn):
+        self._out = fn
+        return self
+
+    def execute(self, script: Script):
+        cfg = self.config
+        cfg.explain = self._explain
+        stats = Statistics(enabled=self._stats) if self._stats else None
+        cs = EX.compile_script(script.source, script._args, inputs=script._inputs,
+                               outputs=script._outputs, config=cfg, pydml=script.pydml,
+                               filename=script.filename)
+        values, ctx = EX.execute(cs, script._inputs, out=self._out, stats=stats)
+        if stats is not None:
+            from ..ops import kernels
+            for k, v in kernels.counters.items():
+                stats.counters[k] = v
+            ctx.print(stats.report(cfg.stats_count))
+        self.last_stats = stats
+        return MLResults(values, stats)
+
+    def close(self):
+        pass
+
+    def version(self):
+        from .. import __version__
+        return __version__

@@ -101,9 +101,12 @@ class Translator:
         return ctx
 
     # ------------------------------------------------------------------ compile
-    def compile(self, prog: A.Program, inputs=(), outputs=()):
+    def compile(self, prog: A.Program, inputs=(), outputs=(), input_types=None):
         main_ctx = self._register_file(prog, DEFAULT_NS, prog.source_path)
         self.inputs = set(inputs)
+        self.input_types = dict(input_types or {})
+        self.outputs = set(outputs)
+        self.main_ctx = main_ctx
         # compile all functions (bodies built lazily with empty const env)
         for (key, name), (fd, ctx) in list(self.func_defs.items()):
             self.functions[(key, name)] = FunctionBlock(name, key, fd.inputs, fd.outputs, None,
@@ -113,13 +116,15 @@ class Translator:
             fb = self.functions[(key, name)]
             if not fd.external:
                 consts = {}
-                fb.body = self.build_stmts(fd.body, ctx, consts, params=fd.inputs)
+                types = {p.name: p.dtype[0] if p.dtype in ("MATRIX", "SCALAR", "FRAME", "LIST") else "U"
+                         for p in fd.inputs}
+                fb.body = self.build_stmts(fd.body, ctx, consts, params=fd.inputs, types=types)
                 for p in fd.inputs:
                     if p.default is not None:
                         bb = _BBuilder(self, ctx, {})
                         h = bb.expr(p.default)
                         fb.default_preds[p.name] = Predicate(h, bb.reads)
-        blocks = self.build_stmts(prog.statements, main_ctx, {})
+        blocks = self.build_stmts(prog.statements, main_ctx, {}, types=dict(self.input_types))
         cp = CompiledProgram(blocks, self.functions, prog.source_path)
         # liveness
         for fb in self.functions.values():
@@ -134,10 +139,13 @@ class Translator:
         return cp
 
     # ------------------------------------------------------------------ blocks
-    def build_stmts(self, stmts, ctx, consts, params=None):
-        """Returns list of blocks. `consts` is updated in place with constants known at exit."""
+    def build_stmts(self, stmts, ctx, consts, params=None, types=None):
+        """Returns list of blocks. `consts` / `types` are updated in place with the scalar
+        constants and data types (M/S/F/L/U) known at exit."""
         blocks = []
-        cur = _BBuilder(self, ctx, consts)
+        if types is None:
+            types = {}
+        cur = _BBuilder(self, ctx, consts, types)
 
         def flush():
             nonlocal cur
@@ -146,7 +154,8 @@ class Translator:
                 blocks.append(bb)
                 consts.clear()
                 consts.update(cur.out_consts())
-            cur = _BBuilder(self, ctx, consts)
+                types.update(cur.out_types())
+            cur = _BBuilder(self, ctx, consts, types)
 
         def process(lst):
             nonlocal cur
@@ -161,56 +170,73 @@ class Translator:
                         process(st.then_body if S.as_bool(ph) else st.else_body)
                         continue
                     flush()
-                    pb = _BBuilder(self, ctx, consts)
+                    pb = _BBuilder(self, ctx, consts, types)
                     pred = Predicate(pb.expr(st.pred), pb.reads)
                     c1, c2 = dict(consts), dict(consts)
-                    tb = self.build_stmts(st.then_body, ctx, c1)
-                    eb = self.build_stmts(st.else_body, ctx, c2)
+                    t1, t2 = dict(types), dict(types)
+                    tb = self.build_stmts(st.then_body, ctx, c1, types=t1)
+                    eb = self.build_stmts(st.else_body, ctx, c2, types=t2)
                     blocks.append(IfBlock(pred, tb, eb, pos=st.pos))
                     merged = {k: v for k, v in c1.items() if k in c2 and _same(c2[k], v)}
                     consts.clear()
                     consts.update(merged)
-                    cur = _BBuilder(self, ctx, consts)
+                    for k in set(t1) | set(t2):
+                        types[k] = t1.get(k, "U") if t1.get(k, "U") == t2.get(k, "U") else "U"
+                    cur = _BBuilder(self, ctx, consts, types)
                 elif isinstance(st, A.While):
                     flush()
                     assigned = assigned_vars(st.body)
                     for v in assigned:
                         consts.pop(v, None)
-                    pb = _BBuilder(self, ctx, consts)
+                    self._loop_types(st.body, ctx, consts, types)
+                    pb = _BBuilder(self, ctx, consts, types)
                     pred = Predicate(pb.expr(st.pred), pb.reads)
-                    body = self.build_stmts(st.body, ctx, dict(consts))
+                    body = self.build_stmts(st.body, ctx, dict(consts), types=dict(types))
                     blocks.append(WhileBlock(pred, body, pos=st.pos))
-                    cur = _BBuilder(self, ctx, consts)
+                    cur = _BBuilder(self, ctx, consts, types)
                 elif isinstance(st, A.For):
                     flush()
                     assigned = assigned_vars(st.body) | {st.var}
-                    pb = _BBuilder(self, ctx, consts)
+                    pb = _BBuilder(self, ctx, consts, types)
                     p_from = Predicate(pb.expr(st.start), pb.reads)
-                    pb2 = _BBuilder(self, ctx, consts)
+                    pb2 = _BBuilder(self, ctx, consts, types)
                     p_to = Predicate(pb2.expr(st.end), pb2.reads)
                     p_incr = None
                     if st.incr is not None:
-                        pb3 = _BBuilder(self, ctx, consts)
+                        pb3 = _BBuilder(self, ctx, consts, types)
                         p_incr = Predicate(pb3.expr(st.incr), pb3.reads)
                     params = {}
                     for k, v in st.params.items():
-                        pbk = _BBuilder(self, ctx, consts)
+                        pbk = _BBuilder(self, ctx, consts, types)
                         hv = pbk.expr(v)
                         params[k] = hv.p.get("v") if hv.op == "lit" else None
                         if hv.op == "tread" or (hv.op != "lit" and isinstance(v, A.Ident)):
                             params[k] = v.name if isinstance(v, A.Ident) else None
                     for v in assigned:
                         consts.pop(v, None)
-                    body = self.build_stmts(st.body, ctx, dict(consts))
+                    types[st.var] = "S"
+                    self._loop_types(st.body, ctx, consts, types)
+                    body = self.build_stmts(st.body, ctx, dict(consts), types=dict(types))
                     fb = ForBlock(st.var, p_from, p_to, p_incr, body, parfor=st.parfor, params=params, pos=st.pos)
                     blocks.append(fb)
-                    cur = _BBuilder(self, ctx, consts)
+                    cur = _BBuilder(self, ctx, consts, types)
                 else:
                     raise LanguageError(f"unsupported statement {type(st).__name__}")
 
         process(stmts)
         flush()
         return blocks
+
+    def _loop_types(self, body, ctx, consts, types):
+        """Fixpoint of data types over a loop body (types assigned in the body that differ
+        from the entry types become unknown)."""
+        t = dict(types)
+        self.build_stmts(body, ctx, dict(consts), types=t)
+        for k, v in t.items():
+            if k in types and types[k] != v:
+                types[k] = "U"
+            elif k not in types:
+                types[k] = v
 
     def resolve_function(self, ctx: FileCtx, ns, name):
         if ns is not None:
@@ -269,10 +295,11 @@ def assigned_vars(stmts):
 # Basic block builder: statements -> HOP DAG
 # ============================================================================
 class _BBuilder:
-    def __init__(self, tr: Translator, ctx: FileCtx, consts: dict):
+    def __init__(self, tr: Translator, ctx: FileCtx, consts: dict, types=None):
         self.tr = tr
         self.ctx = ctx
         self.consts = dict(consts)
+        self.types = dict(types or {})
         self.env = {}            # var -> hop
         self.treads = {}         # var -> tread hop
         self.reads = set()
@@ -308,6 +335,15 @@ class _BBuilder:
 
     # -- statements ----------------------------------------------------------------
     def add(self, st):
+        # MLContext/JMLC semantics (reference: RewriteRemovePersistentReadWrite): a persistent
+        # read into a bound input variable, or a write of a bound output, becomes a no-op
+        if self.ctx is self.tr.main_ctx:
+            if isinstance(st, A.Assign) and isinstance(st.target, A.Ident) and st.target.name in self.tr.inputs \
+                    and isinstance(st.value, A.Call) and st.value.name == "read" and st.ifdef is None:
+                return
+            if isinstance(st, A.ExprStmt) and st.call.name == "write" and st.call.args and \
+                    isinstance(st.call.args[0].value, A.Ident) and st.call.args[0].value.name in self.tr.outputs:
+                return
         self.stmt_count += 1
         if self.pos is None:
             self.pos = st.pos
@@ -346,7 +382,8 @@ class _BBuilder:
             for i, t in enumerate(st.targets):
                 if not isinstance(t, A.Ident):
                     raise LanguageError(f"{st.pos}: multi-assignment targets must be identifiers")
-                self.env[t.name] = self.mk("fout", [h], p={"i": i}, pos=st.pos, cse=False)
+                dt = "M" if fb is None else _param_dt(fb.outputs[i] if i < len(fb.outputs) else None)
+                self.env[t.name] = self.mk("fout", [h], p={"i": i}, pos=st.pos, cse=False, dt=dt)
         elif isinstance(st, A.ExprStmt):
             h = self.expr(st.call)
             if h.op in ("sink", "fcall"):
@@ -377,6 +414,9 @@ class _BBuilder:
                 c.pop(k, None)
         return c
 
+    def out_types(self):
+        return {k: h.dt for k, h in self.env.items()}
+
     def finish(self) -> BasicBlock:
         bb = BasicBlock()
         bb.pos = self.pos
@@ -394,7 +434,7 @@ class _BBuilder:
             return self.lit(self.consts[name], pos)
         h = self.treads.get(name)
         if h is None:
-            h = Hop("tread", p={"name": name}, pos=pos)
+            h = Hop("tread", p={"name": name}, pos=pos, dt=self.types.get(name, "U"))
             self.treads[name] = h
         self.reads.add(name)
         return h
@@ -430,13 +470,15 @@ class _BBuilder:
         if isinstance(e, A.Indexed):
             src = self.var(e.name, e.pos)
             rl, ru, cl, cu = self.index_bounds(e)
-            return self.mk("rix", [src, rl, ru, cl, cu], p={"list": e.cols is None}, pos=e.pos)
+            dt = src.dt if src.dt in ("M", "F") else "U"
+            return self.mk("rix", [src, rl, ru, cl, cu], p={"list": e.cols is None}, pos=e.pos, dt=dt)
         if isinstance(e, A.Call):
             fb = self.tr.resolve_function(self.ctx, e.namespace, e.name)
             if fb is not None:
                 h = self.fcall(fb, e)
                 self.roots.append(h)
-                return self.mk("fout", [h], p={"i": 0}, pos=e.pos, cse=False)
+                return self.mk("fout", [h], p={"i": 0}, pos=e.pos, cse=False,
+                               dt=_param_dt(fb.outputs[0] if fb.outputs else None))
             return self.builtin_call(e)
         if isinstance(e, A.ExprList):
             return self.mk("bi", [self.expr(x) for x in e.items], p={"name": "list"}, pos=e.pos)
@@ -505,6 +547,11 @@ class _BBuilder:
         name = call.name
         pos = call.pos
         args = call.args
+        if name == "ifdef" and len(args) == 2 and isinstance(args[0].value, A.CmdParam):
+            pname = args[0].value.name
+            if pname in self.tr.args:
+                return self.lit(S.parse_literal_arg(self.tr.args[pname]), pos)
+            return self.expr(args[1].value)
         pos_args = [self.expr(a.value) for a in args if a.name is None]
         named = [(a.name, self.expr(a.value)) for a in args if a.name is not None]
         nd = dict(named)
@@ -567,12 +614,19 @@ class _BBuilder:
         if name == "eval":
             # dynamic function call: resolve at runtime in this file context
             return self._eval_call(pos_args, named, pos)
+        dt = _BI_DT.get(name, "U")
+        if name == "read":
+            dtn = nd.get("data_type")
+            if dtn is not None and dtn.op == "lit":
+                dt = {"frame": "F", "scalar": "S", "list": "L"}.get(str(dtn.value), "M")
+            else:
+                dt = "U"
         side = name in H.SIDE_EFFECT
         nondet = name in H.NONDETERMINISTIC or (name in ("rand", "sample") and
                                                not _has_literal_seed(nd))
         inputs = pos_args + [h for _, h in named]
         h = self.mk("sink" if side else "bi", inputs, p={"name": name, "npos": len(pos_args)},
-                    named=[n for n, _ in named], pos=pos, cse=not (side or nondet or multi))
+                    named=[n for n, _ in named], pos=pos, cse=not (side or nondet or multi), dt=dt)
         if side:
             self.roots.append(h)
         return h
@@ -582,6 +636,22 @@ class _BBuilder:
         return self.mk("bi", inputs, p={"name": "eval", "npos": len(pos_args), "nskey": self.ctx.key,
                                         "imports": tuple(sorted(self.ctx.imports.items()))},
                        named=[n for n, _ in named], pos=pos, cse=False)
+
+
+_M_BUILTINS = ("matrix rand seq sample cbind rbind table ctable diag rev removeEmpty replace order solve inv "
+               "inverse cholesky outer quantile interQuantile aggregate lower.tri upper.tri conv2d "
+               "conv2d_backward_filter conv2d_backward_data max_pool avg_pool max_pool_backward "
+               "avg_pool_backward bias_add bias_multiply transformapply transformcolmap").split()
+_S_BUILTINS = "toString median interQuartileMean moment centralMoment cov cdf invcdf pnorm qnorm pt qt pf qf " \
+              "pchisq qchisq pexp qexp exists time".split()
+_BI_DT = {**{n: "M" for n in _M_BUILTINS}, **{n: "S" for n in _S_BUILTINS}, "list": "L",
+          "transformdecode": "F", "transformmeta": "F"}
+
+
+def _param_dt(p):
+    if p is None:
+        return "U"
+    return {"MATRIX": "M", "SCALAR": "S", "FRAME": "F", "LIST": "L"}.get(p.dtype, "U")
 
 
 def _has_literal_seed(nd):

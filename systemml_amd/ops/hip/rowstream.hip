@@ -1,0 +1,361 @@
+// Row-streaming kernels for tall-skinny linear algebra on MI355X (gfx950).
+//
+// One launch reads a tall matrix X [N x D] (row-major; bf16, fp32 or fp64) exactly
+// once from HBM and performs one of:
+//   XV      : U[N x K]  = X %*% V                         (ba+* matrix-vector / skinny)
+//   XTG     : R[D x K]  = t(X) %*% G                      (ba+* with transposed LHS)
+//   XTXV    : R         = t(X) %*% (X %*% V)              (mmchain XtXv)
+//   XTWXV   : R         = t(X) %*% (w * (X %*% V))        (mmchain XtwXv)
+//   XTXVY   : R         = t(X) %*% ((X %*% V) - Y)        (mmchain XtXvy)
+//   XTPSXV  : R         = t(X) %*% (Q - P*rowSums(Q)),  Q = P*(X %*% V)
+//                                                         (multinomial logreg H*v, row template)
+//   ROWSSQ  : U[N x 1]  = rowSums(X^2)
+//   COLSSQ  : R[D x 1]  = colSums(X^2)
+//   COLSUM  : R[D x 1]  = colSums(X)
+//   ROWSUM  : U[N x 1]  = rowSums(X)
+//
+// Reference semantics: LibMatrixMult.matrixMultChain / matrixMult (CP) and the
+// codegen Row template (hops/codegen/template/TemplateRow.java); here fused so X
+// streams through the CU once (memory-bound: 1 byte of X per ~K FMAs).
+//
+// Mapping (wave64): a wave owns one row at a time.  Lane l owns the 8-column
+// chunks c = (j*64 + l)*8 .. +7, j < J (so D <= 512*J).  Row loads are 16-byte
+// vector loads (one 1-KiB coalesced wave-instruction per chunk for bf16); the next
+// row of the wave is prefetched into registers before the current row's wave
+// reductions so HBM latency overlaps the shuffle/FMA work.  V is staged once per
+// block in LDS; t(X)-side accumulators live in registers (J*8 x K per lane) and are
+// combined across the 4 waves through LDS, then one partial [D x K] per block is
+// written (reduced over blocks by the host wrapper).  Accumulation is fp32 for
+// bf16/fp32 X and fp64 for fp64 X.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sysml {
+
+enum Mode { XV = 0, XTG = 1, XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5,
+            ROWSSQ = 6, COLSSQ = 7, COLSUM = 8, ROWSUM = 9 };
+
+constexpr int WAVES = 4;
+constexpr int BLOCK = 64 * WAVES;
+
+template <int M> struct ModeInfo {
+  static constexpr bool needV   = (M == XV || M == XTXV || M == XTWXV || M == XTXVY || M == XTPSXV);
+  static constexpr bool accum   = (M == XTG || M == XTXV || M == XTWXV || M == XTXVY || M == XTPSXV ||
+                                   M == COLSSQ || M == COLSUM);
+  static constexpr bool rowOut  = (M == XV || M == ROWSSQ || M == ROWSUM);
+};
+
+// ---------------------------------------------------------------------------
+// element loads: 8 consecutive elements of one row into accumulator type A
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 16); }
+
+template <typename T> struct Raw8;
+template <> struct Raw8<uint16_t> { uint4 v; };
+template <> struct Raw8<float>    { float4 v[2]; };
+template <> struct Raw8<double>   { double2 v[4]; };
+
+template <typename T>
+__device__ __forceinline__ void load_raw(Raw8<T>& r, const T* __restrict__ row, int c0, int D, bool vec);
+
+template <>
+__device__ __forceinline__ void load_raw<uint16_t>(Raw8<uint16_t>& r, const uint16_t* __restrict__ row,
+                                                   int c0, int D, bool vec) {
+  if (vec && c0 + 8 <= D) {
+    r.v = *reinterpret_cast<const uint4*>(row + c0);
+  } else {
+    uint32_t e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = (c0 + i < D) ? row[c0 + i] : 0u;
+    r.v.x = e[0] | (e[1] << 16); r.v.y = e[2] | (e[3] << 16);
+    r.v.z = e[4] | (e[5] << 16); r.v.w = e[6] | (e[7] << 16);
+  }
+}
+
+template <>
+__device__ __forceinline__ void load_raw<float>(Raw8<float>& r, const float* __restrict__ row,
+                                                int c0, int D, bool vec) {
+  if (vec && c0 + 8 <= D) {
+    r.v[0] = *reinterpret_cast<const float4*>(row + c0);
+    r.v[1] = *reinterpret_cast<const float4*>(row + c0 + 4);
+  } else {
+    float e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = (c0 + i < D) ? row[c0 + i] : 0.f;
+    r.v[0] = make_float4(e[0], e[1], e[2], e[3]);
+    r.v[1] = make_float4(e[4], e[5], e[6], e[7]);
+  }
+}
+
+template <>
+__device__ __forceinline__ void load_raw<double>(Raw8<double>& r, const double* __restrict__ row,
+                                                 int c0, int D, bool vec) {
+  if (vec && c0 + 8 <= D) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.v[i] = *reinterpret_cast<const double2*>(row + c0 + 2 * i);
+  } else {
+    double e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = (c0 + i < D) ? row[c0 + i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.v[i] = make_double2(e[2 * i], e[2 * i + 1]);
+  }
+}
+
+template <typename A>
+__device__ __forceinline__ void unpack(const Raw8<uint16_t>& r, A* x) {
+  x[0] = bf2f(r.v.x & 0xffffu); x[1] = bf2f(r.v.x >> 16);
+  x[2] = bf2f(r.v.y & 0xffffu); x[3] = bf2f(r.v.y >> 16);
+  x[4] = bf2f(r.v.z & 0xffffu); x[5] = bf2f(r.v.z >> 16);
+  x[6] = bf2f(r.v.w & 0xffffu); x[7] = bf2f(r.v.w >> 16);
+}
+template <typename A>
+__device__ __forceinline__ void unpack(const Raw8<float>& r, A* x) {
+  x[0] = r.v[0].x; x[1] = r.v[0].y; x[2] = r.v[0].z; x[3] = r.v[0].w;
+  x[4] = r.v[1].x; x[5] = r.v[1].y; x[6] = r.v[1].z; x[7] = r.v[1].w;
+}
+template <typename A>
+__device__ __forceinline__ void unpack(const Raw8<double>& r, A* x) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { x[2 * i] = r.v[i].x; x[2 * i + 1] = r.v[i].y; }
+}
+
+template <typename A>
+__device__ __forceinline__ A wave_sum(A v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// main kernel
+// ---------------------------------------------------------------------------
+template <typename T, typename A, int K, int J, int MODE>
+__global__ void __launch_bounds__(BLOCK)
+rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
+                 const A* __restrict__ V, int ldv,          // D x K (row-major, ld ldv)
+                 const A* __restrict__ S, int lds, int sbc, // side input rows (G / w / Y / P)
+                 A* __restrict__ out, int ldo,              // U rows, or per-block partials
+                 int64_t rows_per_block) {
+  using MI = ModeInfo<MODE>;
+  constexpr int C = J * 8;                       // columns owned per lane
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  A* sV = reinterpret_cast<A*>(smem);            // [J*512][K] (zero padded)
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Dp = J * 512;
+
+  if constexpr (MI::needV) {
+    for (int i = threadIdx.x; i < Dp * K; i += BLOCK) {
+      int d = i / K, k = i - d * K;
+      sV[i] = (d < D) ? V[(int64_t)d * ldv + k] : A(0);
+    }
+    __syncthreads();
+  }
+
+  A acc[MI::accum ? C : 1][MI::accum ? K : 1];
+  if constexpr (MI::accum) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[c][k] = A(0);
+  }
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
+
+  Raw8<T> nxt[J];
+  int64_t r = r0 + wave;
+  if (r < r1) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) load_raw<T>(nxt[j], X + r * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+  }
+  for (; r < r1; r += WAVES) {
+    A x[C];
+#pragma unroll
+    for (int j = 0; j < J; ++j) unpack<A>(nxt[j], x + j * 8);
+    const int64_t rn = r + WAVES;
+    if (rn < r1) {   // prefetch the wave's next row before the reductions below
+#pragma unroll
+      for (int j = 0; j < J; ++j) load_raw<T>(nxt[j], X + rn * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+    }
+
+    if constexpr (MODE == ROWSSQ || MODE == ROWSUM) {
+      A s = A(0);
+#pragma unroll
+      for (int c = 0; c < C; ++c) s += (MODE == ROWSSQ) ? x[c] * x[c] : x[c];
+      s = wave_sum(s);
+      if (lane == 0) out[r * (int64_t)ldo] = s;
+      continue;
+    }
+    if constexpr (MODE == COLSSQ || MODE == COLSUM) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c][0] += (MODE == COLSSQ) ? x[c] * x[c] : x[c];
+      continue;
+    }
+
+    A g[K];
+    if constexpr (MI::needV) {
+      A u[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) u[k] = A(0);
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const A* vrow = sV + ((j * 64 + lane) * 8) * K;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+          for (int k = 0; k < K; ++k) u[k] += x[j * 8 + e] * vrow[e * K + k];
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) u[k] = wave_sum(u[k]);
+      if constexpr (MODE == XV) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (lane == k) out[r * (int64_t)ldo + k] = u[k];
+        continue;
+      } else if constexpr (MODE == XTXV) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[k] = u[k];
+      } else if constexpr (MODE == XTWXV) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[k] = S[r * (int64_t)lds + (sbc ? 0 : k)] * u[k];
+      } else if constexpr (MODE == XTXVY) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[k] = u[k] - S[r * (int64_t)lds + (sbc ? 0 : k)];
+      } else if constexpr (MODE == XTPSXV) {
+        A p[K], q[K], s = A(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) { p[k] = S[r * (int64_t)lds + k]; q[k] = p[k] * u[k]; s += q[k]; }
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[k] = q[k] - p[k] * s;
+      }
+    } else {  // XTG
+#pragma unroll
+      for (int k = 0; k < K; ++k) g[k] = S[r * (int64_t)lds + k];
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[c][k] += x[c] * g[k];
+  }
+
+  if constexpr (MI::accum) {
+    constexpr int KO = (MODE == COLSSQ || MODE == COLSUM) ? 1 : K;
+    // combine the 4 waves' register accumulators through LDS, then one partial per block
+    __syncthreads();
+    A* red = reinterpret_cast<A*>(smem);          // reuse: [J*512][KO]
+    for (int w = 0; w < WAVES; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int k = 0; k < KO; ++k) {
+              int idx = ((j * 64 + lane) * 8 + e) * KO + k;
+              red[idx] = (w == 0) ? acc[j * 8 + e][k] : red[idx] + acc[j * 8 + e][k];
+            }
+      }
+      __syncthreads();
+    }
+    A* dst = out + (int64_t)blockIdx.x * D * KO;
+    for (int i = threadIdx.x; i < D * KO; i += BLOCK) dst[i] = red[i];
+  }
+}
+
+}  // namespace sysml
+
+// ---------------------------------------------------------------------------
+// host entry points
+// ---------------------------------------------------------------------------
+using namespace sysml;
+
+template <typename T, typename A, int K, int J, int MODE>
+static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int ldv, const void* S,
+                    int lds, int sbc, void* out, int ldo, int grid, int64_t rpb, hipStream_t st) {
+  using MI = ModeInfo<MODE>;
+  if constexpr (sizeof(A) == 8 && K == 8 && J == 2 && MODE >= XTXV && MODE <= XTPSXV) {
+    return -1;  // fp64 x 8 columns x 1024 cols would spill: caller falls back to XV + XTG passes
+  } else {
+  constexpr int KO = (MODE == COLSSQ || MODE == COLSUM) ? 1 : K;
+  size_t shv = MI::needV ? (size_t)J * 512 * K * sizeof(A) : 0;
+  size_t shr = MI::accum ? (size_t)J * 512 * KO * sizeof(A) : 0;
+  size_t sh = shv > shr ? shv : shr;
+  hipLaunchKernelGGL((rowstream_kernel<T, A, K, J, MODE>), dim3(grid), dim3(BLOCK), sh, st,
+                     (const T*)X, N, D, vec, (const A*)V, ldv, (const A*)S, lds, sbc, (A*)out, ldo, rpb);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
+}
+
+template <typename T, typename A, int J, int MODE>
+static int launch_k(int K, const void* X, int64_t N, int D, int vec, const void* V, int ldv, const void* S,
+                    int lds, int sbc, void* out, int ldo, int grid, int64_t rpb, hipStream_t st) {
+  switch (K) {
+    case 1: return launch_t<T, A, 1, J, MODE>(X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+    case 2: return launch_t<T, A, 2, J, MODE>(X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+    case 4: return launch_t<T, A, 4, J, MODE>(X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+    case 8: return launch_t<T, A, 8, J, MODE>(X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+    default: return -1;
+  }
+}
+
+template <typename T, typename A, int MODE>
+static int launch_j(int J, int K, const void* X, int64_t N, int D, int vec, const void* V, int ldv,
+                    const void* S, int lds, int sbc, void* out, int ldo, int grid, int64_t rpb, hipStream_t st) {
+  if (J == 1) return launch_k<T, A, 1, MODE>(K, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+  if (J == 2) return launch_k<T, A, 2, MODE>(K, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+  return -1;
+}
+
+template <typename T, typename A>
+static int launch_mode(int mode, int J, int K, const void* X, int64_t N, int D, int vec, const void* V,
+                       int ldv, const void* S, int lds, int sbc, void* out, int ldo, int grid, int64_t rpb,
+                       hipStream_t st) {
+#define SYSML_CASE(M) case M: return launch_j<T, A, M>(J, K, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+  switch (mode) {
+    SYSML_CASE(XV) SYSML_CASE(XTG) SYSML_CASE(XTXV) SYSML_CASE(XTWXV) SYSML_CASE(XTXVY) SYSML_CASE(XTPSXV)
+    default: break;
+  }
+#undef SYSML_CASE
+  if (K != 1) return -1;
+  switch (mode) {
+    case ROWSSQ: return launch_j<T, A, ROWSSQ>(J, 1, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+    case COLSSQ: return launch_j<T, A, COLSSQ>(J, 1, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+    case COLSUM: return launch_j<T, A, COLSUM>(J, 1, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+    case ROWSUM: return launch_j<T, A, ROWSUM>(J, 1, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid, rpb, st);
+    default: return -1;
+  }
+}
+
+extern "C" {
+
+// xdtype: 0 = bf16 (fp32 accumulate), 1 = fp32, 2 = fp64.   Returns 0 on success.
+int sysml_rowstream(int mode, int xdtype, const void* X, int64_t N, int D, const void* V, int ldv,
+                    const void* S, int lds, int sbc, void* out, int ldo, int K, int grid,
+                    int64_t rows_per_block, void* stream) {
+  if (D <= 0 || D > 1024 || N <= 0 || grid <= 0) return -1;
+  const int J = (D <= 512) ? 1 : 2;
+  hipStream_t st = (hipStream_t)stream;
+  int vec;
+  if (xdtype == 0) {
+    vec = ((D % 8) == 0 && (((uintptr_t)X) & 15) == 0) ? 1 : 0;
+    return launch_mode<uint16_t, float>(mode, J, K, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid,
+                                        rows_per_block, st);
+  }
+  if (xdtype == 1) {
+    vec = ((D % 4) == 0 && (((uintptr_t)X) & 15) == 0) ? 1 : 0;
+    return launch_mode<float, float>(mode, J, K, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid,
+                                     rows_per_block, st);
+  }
+  if (xdtype == 2) {
+    vec = ((D % 2) == 0 && (((uintptr_t)X) & 15) == 0) ? 1 : 0;
+    return launch_mode<double, double>(mode, J, K, X, N, D, vec, V, ldv, S, lds, sbc, out, ldo, grid,
+                                       rows_per_block, st);
+  }
+  return -1;
+}
+
+int sysml_abi_version() { return 1; }
+
+}  // extern "C"

@@ -1,0 +1,273 @@
+"""Python bindings for the in-tree HIP kernel library (`ops/lib/libsysml_hip.so`,
+built from `ops/hip/*.hip` by `__graft_entry__.build()` / `python -m systemml_amd.ops.build`).
+
+The library is loaded with ctypes (no torch C++ ABI coupling); kernels are
+launched on PyTorch's current HIP stream so they order correctly with the
+surrounding torch ops and are capturable in HIP graphs.
+
+On a GPU box the library is REQUIRED: `load(required=True)` raises if it is
+missing or fails to load, so GPU runs never silently fall back to eager torch
+for the hot operators.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from ..parser.errors import DMLRuntimeError
+from .backend import backend
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsysml_hip.so")
+_lib = None
+
+# modes (must match ops/hip/rowstream.hip)
+XV, XTG, XTXV, XTWXV, XTXVY, XTPSXV, ROWSSQ, COLSSQ, COLSUM, ROWSUM = range(10)
+_CHAIN = {"XtXv": XTXV, "XtwXv": XTWXV, "XtXvy": XTXVY, "XtPSXv": XTPSXV}
+MIN_ROWS = 2048       # below this the launch + partial reduction is not worth it
+MAX_D = 1024
+
+counters = {}
+
+
+def _count(name):
+    counters[name] = counters.get(name, 0) + 1
+
+
+def load(required=False):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        if required:
+            raise DMLRuntimeError(f"HIP kernel library not built: {LIB_PATH} (run __graft_entry__.build())")
+        return None
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        if required:
+            raise DMLRuntimeError(f"cannot load HIP kernel library {LIB_PATH}: {e}")
+        return None
+    L.sysml_rowstream.restype = ctypes.c_int
+    L.sysml_rowstream.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                  ctypes.c_void_p]
+    _lib = L
+    return L
+
+
+def _xcode(x):
+    if x.dtype == torch.bfloat16:
+        return 0, torch.float32
+    if x.dtype == torch.float32:
+        return 1, torch.float32
+    if x.dtype == torch.float64:
+        return 2, torch.float64
+    return None, None
+
+
+def _kpad(k):
+    for p in (1, 2, 4, 8):
+        if k <= p:
+            return p
+    return None
+
+
+def _grid(n):
+    cus = 256
+    g = min((n + 63) // 64, cus * 4)
+    return max(g, 1)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _pad_cols(m, kp, dt):
+    m = m.to(dtype=dt)
+    if m.shape[1] == kp and m.is_contiguous():
+        return m
+    out = torch.zeros((m.shape[0], kp), dtype=dt, device=m.device)
+    out[:, :m.shape[1]] = m
+    return out
+
+
+def _launch(mode, X, V=None, S=None, sbc=0, K=1, out=None, ldo=1, grid=None):
+    L = load(required=True)
+    code, adt = _xcode(X)
+    N, D = X.shape
+    grid = grid or _grid(N)
+    rpb = (N + grid - 1) // grid
+    grid = (N + rpb - 1) // rpb
+    rc = L.sysml_rowstream(mode, code, ctypes.c_void_p(X.data_ptr()), N, D,
+                           ctypes.c_void_p(V.data_ptr() if V is not None else 0), V.shape[1] if V is not None else 0,
+                           ctypes.c_void_p(S.data_ptr() if S is not None else 0), S.shape[1] if S is not None else 0,
+                           sbc, ctypes.c_void_p(out.data_ptr()), ldo, K, grid, rpb, _stream())
+    return rc, grid
+
+
+def _ok_x(X):
+    return (X.is_cuda and X.dim() == 2 and X.is_contiguous() and X.shape[0] >= MIN_ROWS
+            and 0 < X.shape[1] <= MAX_D and _xcode(X)[0] is not None)
+
+
+def _result(t):
+    return t if t.dtype == backend.dtype else t.to(backend.dtype)
+
+
+def xv(X, V):
+    """U = X %*% V for tall X (N x D, D <= 1024) and skinny V (D x K, K <= 8)."""
+    K = V.shape[1]
+    kp = _kpad(K)
+    code, adt = _xcode(X)
+    Vp = _pad_cols(V, kp, adt).contiguous()
+    U = torch.empty((X.shape[0], kp), dtype=adt, device=X.device)
+    rc, _ = _launch(XV, X, V=Vp, K=kp, out=U, ldo=kp)
+    if rc != 0:
+        return None
+    _count("rowstream.xv")
+    return _result(U if kp == K else U[:, :K].contiguous())
+
+
+def xtg(X, G):
+    """R = t(X) %*% G for tall X and skinny G (N x K, K <= 8)."""
+    K = G.shape[1]
+    kp = _kpad(K)
+    code, adt = _xcode(X)
+    Gp = _pad_cols(G, kp, adt).contiguous()
+    grid = _grid(X.shape[0])
+    part = torch.empty((grid, X.shape[1] * kp), dtype=adt, device=X.device)
+    rc, g = _launch(XTG, X, S=Gp, K=kp, out=part, grid=grid)
+    if rc != 0:
+        return None
+    _count("rowstream.xtg")
+    R = part[:g].sum(0).reshape(X.shape[1], kp)
+    return _result(R if kp == K else R[:, :K].contiguous())
+
+
+def mmchain(ctype, X, V, W=None):
+    mode = _CHAIN[ctype]
+    K = V.shape[1]
+    kp = _kpad(K)
+    code, adt = _xcode(X)
+    Vp = _pad_cols(V, kp, adt).contiguous()
+    S = None
+    sbc = 0
+    if W is not None:
+        if W.shape[0] != X.shape[0]:
+            return None
+        if mode == XTWXV and W.shape[1] == 1:
+            S = W.to(adt).contiguous()
+            sbc = 1
+        elif W.shape[1] == K:
+            S = _pad_cols(W, kp, adt).contiguous()
+        else:
+            return None
+    grid = _grid(X.shape[0])
+    part = torch.empty((grid, X.shape[1] * kp), dtype=adt, device=X.device)
+    rc, g = _launch(mode, X, V=Vp, S=S, sbc=sbc, K=kp, out=part, grid=grid)
+    if rc != 0:
+        return None
+    _count("rowstream.mmchain." + ctype)
+    R = part[:g].sum(0).reshape(X.shape[1], kp)
+    return _result(R if kp == K else R[:, :K].contiguous())
+
+
+# ----------------------------------------------------------------------------
+# dispatch helpers used by ops/core.py
+# ----------------------------------------------------------------------------
+def try_mm(a, b, transA):
+    if not isinstance(b, torch.Tensor) or not b.is_cuda:
+        return None
+    if _ok_x(a):
+        K = b.shape[1]
+        if K <= 8:
+            if transA and b.shape[0] == a.shape[0]:
+                return xtg(a, b)
+            if not transA and b.shape[0] == a.shape[1]:
+                return xv(a, b)
+    if a.dtype == torch.bfloat16:
+        return _chunked_mm_bf16(a, b, transA)
+    return None
+
+
+def try_mmchain(ctype, X, v, w):
+    if not _ok_x(X) or not isinstance(v, torch.Tensor) or v.shape[1] > 8 or v.shape[0] != X.shape[1]:
+        return None
+    if w is not None and not isinstance(w, torch.Tensor):
+        return None
+    return mmchain(ctype, X, v, w)
+
+
+def try_tsmm(x, left):
+    if x.dtype == torch.bfloat16:
+        return _chunked_tsmm_bf16(x, left)
+    return None
+
+
+def sumsq(x, d):
+    if _ok_x(x):
+        code, adt = _xcode(x)
+        if d == "row":
+            U = torch.empty((x.shape[0], 1), dtype=adt, device=x.device)
+            rc, _ = _launch(ROWSSQ, x, K=1, out=U, ldo=1)
+            if rc == 0:
+                _count("rowstream.rowsumsq")
+                return _result(U)
+        elif d in ("col", "all"):
+            grid = _grid(x.shape[0])
+            part = torch.empty((grid, x.shape[1]), dtype=adt, device=x.device)
+            rc, g = _launch(COLSSQ, x, K=1, out=part, grid=grid)
+            if rc == 0:
+                _count("rowstream.colsumsq")
+                c = part[:g].sum(0).reshape(1, -1)
+                if d == "all":
+                    return float(c.sum().item())
+                return _result(c)
+    # generic: chunked to bound temporaries
+    from .core import cvt
+    if d == "all":
+        tot = 0.0
+        for s in range(0, x.shape[0], 1 << 16):
+            c = cvt(x[s:s + (1 << 16)])
+            tot += float(torch.sum(c * c).item())
+        return tot
+    xx = cvt(x)
+    return torch.sum(xx * xx, dim=1 if d == "row" else 0, keepdim=True)
+
+
+def _chunk_rows(x, budget_cells=1 << 26):
+    return max(1, budget_cells // max(1, x.shape[1]))
+
+
+def _chunked_mm_bf16(a, b, transA):
+    """bf16-stored operand without a full-size fp32 copy: row chunks upcast on the fly."""
+    dt = backend.dtype
+    b = b.to(dt) if b.dtype != torch.bfloat16 else b.to(dt)
+    step = _chunk_rows(a)
+    if transA:
+        out = None
+        for s in range(0, a.shape[0], step):
+            c = a[s:s + step].to(dt)
+            part = c.t() @ b[s:s + step]
+            out = part if out is None else out + part
+        return out
+    outs = [a[s:s + step].to(dt) @ b for s in range(0, a.shape[0], step)]
+    return torch.cat(outs, 0)
+
+
+def _chunked_tsmm_bf16(x, left):
+    dt = backend.dtype
+    if not left:
+        xx = x.to(dt)
+        return xx @ xx.t()
+    step = _chunk_rows(x)
+    out = None
+    for s in range(0, x.shape[0], step):
+        c = x[s:s + step].to(dt)
+        part = c.t() @ c
+        out = part if out is None else out + part
+    return out

@@ -1,5 +1,455 @@
-"""placeholder, replaced below"""
-class DistMatrix:  # noqa
-    pass
+"""Row-partitioned distributed matrices over one-process-per-GPU ranks.
+
+This replaces the reference's Spark/MR backends (runtime/instructions/spark/*,
+runtime/controlprogram/context/SparkExecutionContext.java) with an SPMD design
+for a single 8×MI355X node:
+
+* every rank runs the same compiled program (runtime/program.py);
+* matrices with >= `dist_min_rows` rows are split into contiguous row blocks,
+  one per rank, resident in that rank's HBM (`DistMatrix`); all other values
+  are replicated;
+* operators map to the reference's distributed physical operators:
+    - X %*% v (v replicated)           → local matmult, stays row-partitioned   (mapmm)
+    - t(X) %*% Y, Y co-partitioned     → local matmult + all-reduce             (cpmm / zipmm)
+    - t(X) %*% X                       → local tsmm + all-reduce                (tsmm)
+    - mmchain / row-fused H·v          → local fused kernel + all-reduce        (mapmmchain)
+    - full / column aggregates         → local aggregate + all-reduce
+    - row aggregates, cellwise ops     → purely local
+  so each iteration of a CG / trust-region solver moves only D×K-sized
+  vectors over xGMI (RCCL all-reduce); X never leaves its GPU.
+* anything else falls back to an all-gather (correct, slower), counted in
+  `fallback_gathers` so tests can assert the hot path stays distributed.
+
+Collectives use torch.distributed (backend "nccl" = RCCL on ROCm; "gloo" for
+CPU tests).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as tdist
+
+from ..parser.errors import DMLRuntimeError
+from ..runtime import scalars as S
+
+_CTX = None
+stats = {"allreduce": 0, "allgather": 0, "fallback_gathers": 0}
+
+
+class DistContext:
+    def __init__(self, rank, world, device, group=None):
+        self.rank = rank
+        self.world = world
+        self.device = device
+        self.group = group
+
+    def partition(self, n):
+        base, rem = divmod(n, self.world)
+        start = self.rank * base + min(self.rank, rem)
+        size = base + (1 if self.rank < rem else 0)
+        return start, start + size
+
+    def all_partitions(self, n):
+        out = []
+        base, rem = divmod(n, self.world)
+        s = 0
+        for r in range(self.world):
+            sz = base + (1 if r < rem else 0)
+            out.append((s, s + sz))
+            s += sz
+        return out
+
+    # -- collectives --------------------------------------------------------
+    def allreduce_(self, t, op="sum"):
+        stats["allreduce"] += 1
+        rop = {"sum": tdist.ReduceOp.SUM, "max": tdist.ReduceOp.MAX, "min": tdist.ReduceOp.MIN,
+               "prod": tdist.ReduceOp.PRODUCT}[op]
+        tdist.all_reduce(t, op=rop, group=self.group)
+        return t
+
+    def allreduce_scalar(self, v, op="sum", dtype=None, device=None):
+        dev = device if device is not None else self._coll_device()
+        t = torch.tensor([v], dtype=dtype or torch.float64, device=dev)
+        self.allreduce_(t, op)
+        return float(t.item())
+
+    def _coll_device(self):
+        return self.device if tdist.get_backend(self.group) != "gloo" else torch.device("cpu")
+
+    def barrier(self):
+        tdist.barrier(group=self.group)
+
+
 def get_context():
-    return None
+    return _CTX
+
+
+def init(backend=None, device=None):
+    """Initialise SPMD execution from torchrun-style env vars (RANK/WORLD_SIZE/MASTER_*)."""
+    global _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        _CTX = None
+        return None
+    rank = int(os.environ.get("RANK", "0"))
+    if not tdist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            local = int(os.environ.get("LOCAL_RANK", rank))
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        tdist.init_process_group(backend=backend, **kw)
+    if device is None:
+        if torch.cuda.is_available() and tdist.get_backend() == "nccl":
+            device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            device = torch.device("cpu")
+    _CTX = DistContext(rank, world, device)
+    return _CTX
+
+
+def shutdown():
+    global _CTX
+    _CTX = None
+    if tdist.is_initialized():
+        tdist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------
+class DistMatrix:
+    """Row block [start, end) of an (nrows x ncols) matrix held by this rank."""
+    __slots__ = ("local", "nrows", "ncols", "start", "ctx")
+
+    def __init__(self, local, nrows, ncols, start, ctx):
+        self.local = local
+        self.nrows = nrows
+        self.ncols = ncols
+        self.start = start
+        self.ctx = ctx
+
+    @property
+    def shape(self):
+        return (self.nrows, self.ncols)
+
+    def like(self, local):
+        return DistMatrix(local, self.nrows, local.shape[1], self.start, self.ctx)
+
+    def __repr__(self):
+        return f"DistMatrix({self.nrows}x{self.ncols}, rank {self.ctx.rank} rows [{self.start},{self.start + self.local.shape[0]}))"
+
+
+def _is_d(x):
+    return isinstance(x, DistMatrix)
+
+
+def _C():
+    from ..ops import core
+    return core
+
+
+def gather(x: DistMatrix):
+    """All-gather the row blocks into a replicated tensor."""
+    if not _is_d(x):
+        return x
+    ctx = x.ctx
+    stats["allgather"] += 1
+    parts = ctx.all_partitions(x.nrows)
+    loc = x.local.contiguous()
+    if tdist.get_backend(ctx.group) == "gloo" or loc.device.type == "cpu":
+        bufs = [torch.empty((e - s, x.ncols), dtype=loc.dtype, device=loc.device) for s, e in parts]
+        tdist.all_gather(bufs, loc, group=ctx.group)
+        return torch.cat(bufs, 0)
+    maxr = max(e - s for s, e in parts)
+    pad = torch.zeros((maxr, x.ncols), dtype=loc.dtype, device=loc.device)
+    pad[:loc.shape[0]] = loc
+    out = torch.empty((ctx.world * maxr, x.ncols), dtype=loc.dtype, device=loc.device)
+    tdist.all_gather_into_tensor(out, pad, group=ctx.group)
+    return torch.cat([out[r * maxr: r * maxr + (e - s)] for r, (s, e) in enumerate(parts)], 0)
+
+
+def _fallback(x):
+    stats["fallback_gathers"] += 1
+    return gather(x)
+
+
+def local_rows(ctx, t):
+    """Slice this rank's rows out of a replicated full tensor."""
+    s, e = ctx.partition(t.shape[0])
+    return DistMatrix(t[s:e].contiguous(), t.shape[0], t.shape[1], s, ctx)
+
+
+def scatter_rows_from_global(ctx, t):
+    from ..ops.backend import place, maybe_bf16
+    s, e = ctx.partition(t.shape[0])
+    loc = t[s:e]
+    if loc.dtype == torch.bfloat16:
+        loc = loc.to(ctx.device)
+    else:
+        loc = maybe_bf16(place(loc.contiguous()))
+    return DistMatrix(loc.contiguous(), t.shape[0], t.shape[1], s, ctx)
+
+
+def scatter_rows(exec_ctx, t):
+    return scatter_rows_from_global(exec_ctx.dist, t)
+
+
+def from_local(ctx, local, nrows):
+    s, e = ctx.partition(nrows)
+    if local.shape[0] != e - s:
+        raise DMLRuntimeError(f"local block has {local.shape[0]} rows, expected {e - s}")
+    return DistMatrix(local, nrows, local.shape[1], s, ctx)
+
+
+# ----------------------------------------------------------------------------
+# datagen
+# ----------------------------------------------------------------------------
+def rand(exec_ctx, r, c, lo, hi, sp, pdf, seed, lam):
+    from ..runtime.builtins import _rand_local
+    ctx = exec_ctx.dist
+    s, e = ctx.partition(r)
+    loc = _rand_local(e - s, c, lo, hi, sp, pdf, seed, lam, device=ctx.device, row_offset=s)
+    return DistMatrix(loc, r, c, s, ctx)
+
+
+def full(exec_ctx, r, c, v):
+    from ..ops.backend import backend
+    ctx = exec_ctx.dist
+    s, e = ctx.partition(r)
+    return DistMatrix(torch.full((e - s, c), v, dtype=backend.dtype, device=ctx.device), r, c, s, ctx)
+
+
+def seq(exec_ctx, a, inc, n):
+    from ..ops.backend import backend
+    ctx = exec_ctx.dist
+    s, e = ctx.partition(n)
+    loc = a + inc * torch.arange(s, e, dtype=torch.float64, device=ctx.device)
+    return DistMatrix(loc.to(backend.dtype).reshape(-1, 1), n, 1, s, ctx)
+
+
+# ----------------------------------------------------------------------------
+# operators
+# ----------------------------------------------------------------------------
+def _align(x, like: DistMatrix):
+    """Bring operand x to like's row partition (returns local tensor or scalar)."""
+    if _is_d(x):
+        if x.nrows != like.nrows:
+            raise DMLRuntimeError(f"dimension mismatch: {x.nrows} vs {like.nrows} rows")
+        return x.local
+    if isinstance(x, torch.Tensor):
+        if x.shape[0] == like.nrows and like.nrows != 1:
+            e = like.start + like.local.shape[0]
+            return x[like.start:e]
+        return x
+    return x
+
+
+def binary(op, a, b):
+    C = _C()
+    if _is_d(a):
+        ref = a
+    elif _is_d(b):
+        ref = b
+    else:
+        return C.binary(op, a, b)
+    if _is_d(a) and _is_d(b) and a.nrows != b.nrows:
+        # e.g. (N x 1) vs (1 x K) never distributed both; true mismatch
+        raise DMLRuntimeError(f"Block sizes are not matched for binary cell operations: {a.shape} vs {b.shape}")
+    la = _align(a, ref)
+    lb = _align(b, ref)
+    r = C.binary(op, la, lb)
+    return DistMatrix(r, ref.nrows, r.shape[1], ref.start, ref.ctx)
+
+
+def unary(op, x):
+    C = _C()
+    if op in ("nrow", "ncol", "length"):
+        return {"nrow": x.nrows, "ncol": x.ncols, "length": x.nrows * x.ncols}[op]
+    if op in ("cast_scalar", "cast_double", "cast_int", "cast_bool", "cast_frame"):
+        return C.unary(op, gather(x))
+    if op == "cast_matrix":
+        return x
+    if op in ("cumsum", "cumprod", "cummin", "cummax"):
+        return local_rows(x.ctx, C.unary(op, _fallback(x)))
+    r = C.unary(op, x.local)
+    return x.like(r)
+
+
+def agg(o, d, x: DistMatrix):
+    C = _C()
+    ctx = x.ctx
+    loc = x.local
+    if d == "row":
+        return x.like(C.agg(o, "row", loc))
+    if o in ("sum", "sumsq", "min", "max", "prod"):
+        if loc.shape[0] == 0:
+            init = {"sum": 0.0, "sumsq": 0.0, "min": float("inf"), "max": -float("inf"), "prod": 1.0}[o]
+            part = init if d == "all" else torch.full((1, x.ncols), init, dtype=torch.float64, device=ctx.device)
+        else:
+            part = C.agg(o, d, loc)
+        rop = {"sum": "sum", "sumsq": "sum", "min": "min", "max": "max", "prod": "prod"}[o]
+        if d == "all":
+            return ctx.allreduce_scalar(part, rop, device=loc.device if loc.is_cuda else None)
+        t = part.contiguous().clone()
+        ctx.allreduce_(t, rop)
+        return t
+    if o == "mean":
+        n = x.nrows * x.ncols if d == "all" else x.nrows
+        s = agg("sum", d, x)
+        return s / n if d == "all" else s / n
+    if o in ("var", "sd"):
+        n = x.nrows * x.ncols if d == "all" else x.nrows
+        s = agg("sum", d, x)
+        ss = agg("sumsq", d, x)
+        if d == "all":
+            v = (ss - s * s / n) / (n - 1) if n > 1 else 0.0
+            return v ** 0.5 if o == "sd" else v
+        v = (ss - s * s / n) / (n - 1)
+        return torch.sqrt(v) if o == "sd" else v
+    if o == "trace":
+        return C.agg(o, d, _fallback(x))
+    return C.agg(o, d, _fallback(x))
+
+
+def tak(a, b):
+    C = _C()
+    if _is_d(a) and _is_d(b):
+        part = C.tak(a.local, b.local) if a.local.shape[0] else 0.0
+        return a.ctx.allreduce_scalar(part, "sum", device=a.local.device if a.local.is_cuda else None)
+    ref = a if _is_d(a) else b
+    return agg("sum", "all", binary("*", a, b))
+
+
+def mm(a, b, transA=False):
+    C = _C()
+    if transA:
+        if _is_d(a):
+            lb = _align(b, a) if (_is_d(b) or (isinstance(b, torch.Tensor) and b.shape[0] == a.nrows)) else None
+            if lb is None:
+                raise DMLRuntimeError("t(X) %*% Y: row dimension mismatch")
+            r = C.mm(a.local, lb, True).contiguous()
+            a.ctx.allreduce_(r, "sum")
+            return r
+        return C.mm(_fallback(a) if _is_d(a) else a, _fallback(b) if _is_d(b) else b, True)
+    if _is_d(a) and not _is_d(b):
+        r = C.mm(a.local, b)
+        return DistMatrix(r, a.nrows, r.shape[1], a.start, a.ctx)
+    if _is_d(a) and _is_d(b):
+        # (N x M) %*% (M x K) with both row partitioned: B must be replicated
+        r = C.mm(a.local, _fallback(b))
+        return DistMatrix(r, a.nrows, r.shape[1], a.start, a.ctx)
+    # replicated A %*% distributed B: A[:, local rows] @ B_local, all-reduce
+    if _is_d(b):
+        e = b.start + b.local.shape[0]
+        r = C.mm(C.rix(a, None, None, b.start + 1, e, False) if b.local.shape[0] else a[:, :0], b.local).contiguous()
+        b.ctx.allreduce_(r, "sum")
+        return r
+    return C.mm(a, b, transA)
+
+
+def tsmm(x: DistMatrix, left=True):
+    C = _C()
+    if left:
+        r = C.tsmm(x.local, True).contiguous()
+        x.ctx.allreduce_(r, "sum")
+        return r
+    return C.tsmm(_fallback(x), False)
+
+
+def mmchain(ctype, X, v, w=None):
+    C = _C()
+    if not _is_d(X):
+        return C.mmchain(ctype, X, _fallback(v) if _is_d(v) else v, _fallback(w) if _is_d(w) else w)
+    if _is_d(v):
+        v = _fallback(v)
+    lw = _align(w, X) if w is not None else None
+    r = C.mmchain(ctype, X.local, v, lw).contiguous()
+    X.ctx.allreduce_(r, "sum")
+    return r
+
+
+def transpose(x):
+    return _C().transpose(_fallback(x))
+
+
+def _bnd(v):
+    if v is None:
+        return None
+    if isinstance(v, torch.Tensor):
+        v = v.reshape(-1)[0].item()
+    return int(S.as_double(v))
+
+
+def rix(x: DistMatrix, rl, ru, cl, cu):
+    C = _C()
+    r0, r1 = _bnd(rl), _bnd(ru)
+    if (r0 is None or r0 == 1) and (r1 is None or r1 == x.nrows):
+        c0 = _bnd(cl) or 1
+        c1 = _bnd(cu) or x.ncols
+        if c0 < 1 or c1 > x.ncols or c0 > c1:
+            raise DMLRuntimeError(f"Invalid values for matrix indexing: columns [{c0}:{c1}] of {x.ncols}")
+        return x.like(x.local[:, c0 - 1:c1])
+    return C.rix(_fallback(x), rl, ru, cl, cu)
+
+
+def lix(x, y, rl, ru, cl, cu):
+    C = _C()
+    r0, r1 = _bnd(rl), _bnd(ru)
+    if _is_d(x) and (r0 is None or r0 == 1) and (r1 is None or r1 == x.nrows):
+        ly = _align(y, x)
+        out = C.lix(x.local, ly, None, None, cl, cu) if x.local.shape[0] else x.local
+        return x.like(out)
+    xf = _fallback(x) if _is_d(x) else x
+    yf = _fallback(y) if _is_d(y) else y
+    r = C.lix(xf, yf, rl, ru, cl, cu)
+    if _is_d(x):
+        return local_rows(x.ctx, r)
+    return r
+
+
+def cbind(args):
+    ref = next(a for a in args if _is_d(a))
+    parts = []
+    for a in args:
+        la = _align(a, ref)
+        if not isinstance(la, torch.Tensor):
+            raise DMLRuntimeError("cbind of a distributed matrix with a scalar")
+        parts.append(_C().cvt(la))
+    r = torch.cat(parts, 1)
+    return DistMatrix(r, ref.nrows, r.shape[1], ref.start, ref.ctx)
+
+
+def rbind(args):
+    from ..runtime.builtins import b_rbind
+    full = b_rbind(None, *[gather(a) if _is_d(a) else a for a in args])
+    stats["fallback_gathers"] += 1
+    ctx = next(a for a in args if _is_d(a)).ctx
+    return local_rows(ctx, full)
+
+
+def table(exec_ctx, A, B, W, d1, d2):
+    """ctable(seq(1,N), y, N, K) → one-hot rows stay local; general case gathers."""
+    from ..runtime.builtins import _ctable, _int
+    from ..ops.backend import backend
+    if _is_d(A) and _is_d(B) and A.nrows == B.nrows and not isinstance(W, (torch.Tensor, DistMatrix)):
+        a = A.local.reshape(-1)
+        expect = torch.arange(A.start + 1, A.start + a.numel() + 1, dtype=a.dtype, device=a.device)
+        is_seq = bool(torch.equal(a, expect))
+        flag = A.ctx.allreduce_scalar(0.0 if is_seq else 1.0, "max", device=a.device if a.is_cuda else None)
+        if flag == 0.0 and d1 is not None and _int(d1) == A.nrows:
+            b = B.local.reshape(-1)
+            k = _int(d2) if d2 is not None else int(agg("max", "all", B))
+            w = 1.0 if W is None else float(W)
+            out = torch.zeros((a.numel(), k), dtype=backend.dtype, device=a.device)
+            bi = torch.round(b).long() - 1
+            keep = (bi >= 0) & (bi < k)
+            rows = torch.arange(a.numel(), device=a.device)
+            out[rows[keep], bi[keep]] = w
+            return DistMatrix(out, A.nrows, k, A.start, A.ctx)
+    from ..runtime.builtins import b_table
+    r = b_table(exec_ctx, gather(A) if _is_d(A) else A, gather(B) if _is_d(B) else B,
+                gather(W) if _is_d(W) else W, d1, d2)
+    stats["fallback_gathers"] += 1
+    return r
