@@ -27,6 +27,7 @@ _lib = None
 XV, XTG, XTXV, XTWXV, XTXVY, XTPSXV, ROWSSQ, COLSSQ, COLSUM, ROWSUM = range(10)
 _CHAIN = {"XtXv": XTXV, "XtwXv": XTWXV, "XtXvy": XTXVY, "XtPSXv": XTPSXV}
 MIN_ROWS = 2048       # below this the launch + partial reduction is not worth it
+MIN_D = 32            # a wave per row: narrower rows waste most lanes (torch handles those)
 MAX_D = 1024
 
 counters = {}
@@ -111,11 +112,12 @@ def _launch(mode, X, V=None, S=None, sbc=0, K=1, out=None, ldo=1, grid=None):
 
 def _ok_x(X):
     return (X.is_cuda and X.dim() == 2 and X.is_contiguous() and X.shape[0] >= MIN_ROWS
-            and 0 < X.shape[1] <= MAX_D and _xcode(X)[0] is not None)
+            and MIN_D <= X.shape[1] <= MAX_D and _xcode(X)[0] is not None)
 
 
 def _result(t):
-    return t if t.dtype == backend.dtype else t.to(backend.dtype)
+    # fp64 results (fp64 X) are kept exact; fp32 accumulations follow the backend dtype
+    return t if (t.dtype == backend.dtype or t.dtype == torch.float64) else t.to(backend.dtype)
 
 
 def xv(X, V):

@@ -1,0 +1,245 @@
+"""Runtime / builtin semantics on the CP backend vs numpy references
+(reference test strategy: functions/{binary,unary,aggregate,reorg,indexing,data}/*Test)."""
+import numpy as np
+import pytest
+
+from systemml_amd.api.executor import run
+from systemml_amd.conf import DMLConfig
+from systemml_amd.runtime.scalars import java_double_str
+
+CFG = DMLConfig(gpu=False)
+
+
+def R(src, inputs=None, outputs=(), **kw):
+    out = []
+    res = run(src, inputs=inputs or {}, outputs=outputs, config=CFG, out=out.append, **kw)
+    return res, out
+
+
+def M(res, k):
+    v = res[k]
+    return v.cpu().numpy() if hasattr(v, "cpu") else v
+
+
+def test_java_double_format():
+    assert java_double_str(1.0) == "1.0"
+    assert java_double_str(0.0001) == "1.0E-4"
+    assert java_double_str(123456789.0) == "1.23456789E8"
+    assert java_double_str(0.5) == "0.5"
+    assert java_double_str(float("nan")) == "NaN"
+    assert java_double_str(-2.5e-10) == "-2.5E-10"
+
+
+def test_scalar_semantics():
+    _, out = R("""
+      print(1 + 2); print(7 / 2); print(7 %/% 2); print(-7 %% 3); print(2 ^ 3)
+      print("a" + 1 + 2.5); print(TRUE & FALSE); print(5 > 3); print(as.integer(3.7))
+      x = 10; x += 5; print(x); print(max(3, 7, 2)); print(abs(-2))
+    """)
+    assert out == ["3", "3.5", "3", "2", "8.0", "a12.5", "FALSE", "TRUE", "3", "15", "7", "2"]
+
+
+def test_matrix_elementwise_broadcast():
+    A = np.arange(12, dtype=float).reshape(3, 4)
+    res, _ = R("""
+      B = A * 2 + 1; C = A - colMeans(A); D = A / rowSums(A); E = (A > 5) * A; F = A ^ 2 %% 7
+      G = min(A, 3); H = exp(-A); I = A %/% 3
+    """, {"A": A}, ["B", "C", "D", "E", "F", "G", "H", "I"])
+    np.testing.assert_allclose(M(res, "B"), A * 2 + 1)
+    np.testing.assert_allclose(M(res, "C"), A - A.mean(0))
+    np.testing.assert_allclose(M(res, "D"), A / A.sum(1, keepdims=True))
+    np.testing.assert_allclose(M(res, "E"), (A > 5) * A)
+    np.testing.assert_allclose(M(res, "F"), np.mod(A ** 2, 7))
+    np.testing.assert_allclose(M(res, "G"), np.minimum(A, 3))
+    np.testing.assert_allclose(M(res, "H"), np.exp(-A))
+    np.testing.assert_allclose(M(res, "I"), np.floor_divide(A, 3))
+
+
+def test_aggregates():
+    rng = np.random.default_rng(1)
+    A = rng.standard_normal((6, 5))
+    res, _ = R("""
+      s = sum(A); m = mean(A); v = var(A); sd0 = sd(A); mx = max(A); mn = min(A)
+      rs = rowSums(A); cs = colSums(A); rm = rowMeans(A); cmx = colMaxs(A); rv = rowVars(A)
+      csd = colSds(A); rim = rowIndexMax(A); ss = sum(A^2); tk = sum(A * A); pr = prod(A[1,])
+      cm = cumsum(A); tr = trace(A[1:5,])
+    """, {"A": A}, ["s", "m", "v", "sd0", "mx", "mn", "rs", "cs", "rm", "cmx", "rv", "csd", "rim", "ss", "tk",
+                    "pr", "cm", "tr"])
+    assert abs(res["s"] - A.sum()) < 1e-12
+    assert abs(res["m"] - A.mean()) < 1e-12
+    assert abs(res["v"] - A.var(ddof=1)) < 1e-12
+    assert abs(res["sd0"] - A.std(ddof=1)) < 1e-12
+    assert res["mx"] == A.max() and res["mn"] == A.min()
+    np.testing.assert_allclose(M(res, "rs"), A.sum(1, keepdims=True))
+    np.testing.assert_allclose(M(res, "cs"), A.sum(0, keepdims=True))
+    np.testing.assert_allclose(M(res, "rm"), A.mean(1, keepdims=True))
+    np.testing.assert_allclose(M(res, "cmx"), A.max(0, keepdims=True))
+    np.testing.assert_allclose(M(res, "rv"), A.var(1, ddof=1, keepdims=True))
+    np.testing.assert_allclose(M(res, "csd"), A.std(0, ddof=1, keepdims=True))
+    np.testing.assert_allclose(M(res, "rim").ravel(), A.argmax(1) + 1)
+    assert abs(res["ss"] - (A ** 2).sum()) < 1e-10 and abs(res["tk"] - (A ** 2).sum()) < 1e-10
+    assert abs(res["pr"] - A[0].prod()) < 1e-12
+    np.testing.assert_allclose(M(res, "cm"), np.cumsum(A, 0))
+    assert abs(res["tr"] - np.trace(A[:5])) < 1e-12
+
+
+def test_matmult_family_and_rewrites():
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((50, 7))
+    v = rng.standard_normal((7, 1))
+    w = rng.random((50, 1))
+    y = rng.standard_normal((50, 1))
+    res, _ = R("""
+      a = t(X) %*% (X %*% v); b = t(X) %*% (w * (X %*% v)); c = t(X) %*% ((X %*% v) - y)
+      d = t(X) %*% X; e = X %*% t(X); f = t(X) %*% y; g = t(t(X))
+    """, {"X": X, "v": v, "w": w, "y": y}, list("abcdefg"))
+    np.testing.assert_allclose(M(res, "a"), X.T @ (X @ v))
+    np.testing.assert_allclose(M(res, "b"), X.T @ (w * (X @ v)))
+    np.testing.assert_allclose(M(res, "c"), X.T @ (X @ v - y))
+    np.testing.assert_allclose(M(res, "d"), X.T @ X)
+    np.testing.assert_allclose(M(res, "e"), X @ X.T)
+    np.testing.assert_allclose(M(res, "f"), X.T @ y)
+    np.testing.assert_allclose(M(res, "g"), X)
+
+
+def test_row_fused_hessian_vector():
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((40, 6))
+    V = rng.standard_normal((6, 3))
+    P = rng.random((40, 4))
+    P /= P.sum(1, keepdims=True)
+    res, _ = R("""
+      K = 3
+      Q = P[, 1:K] * (X %*% V)
+      HV = t(X) %*% (Q - P[, 1:K] * (rowSums(Q) %*% matrix(1, rows = 1, cols = K)))
+    """, {"X": X, "V": V, "P": P}, ["HV"])
+    Pk = P[:, :3]
+    Q = Pk * (X @ V)
+    np.testing.assert_allclose(M(res, "HV"), X.T @ (Q - Pk * Q.sum(1, keepdims=True)))
+
+
+def test_indexing_and_left_indexing():
+    A = np.arange(20, dtype=float).reshape(4, 5)
+    res, _ = R("""
+      a = A[2, 3]; b = A[2:3, ]; c = A[, 2:4]; s = as.scalar(A[4, 5])
+      B = A; B[1, ] = matrix(0, rows = 1, cols = 5); B[2:3, 4:5] = matrix(7, rows = 2, cols = 2); B[4, 1] = -1
+    """, {"A": A}, ["a", "b", "c", "s", "B"])
+    assert M(res, "a").item() == A[1, 2]
+    np.testing.assert_allclose(M(res, "b"), A[1:3])
+    np.testing.assert_allclose(M(res, "c"), A[:, 1:4])
+    assert res["s"] == A[3, 4]
+    B = A.copy()
+    B[0] = 0
+    B[1:3, 3:5] = 7
+    B[3, 0] = -1
+    np.testing.assert_allclose(M(res, "B"), B)
+
+
+def test_datagen_and_reorg():
+    res, _ = R("""
+      A = matrix("1 2 3 4 5 6", rows = 2, cols = 3); B = matrix(A, rows = 3, cols = 2)
+      C = matrix(A, rows = 3, cols = 2, byrow = FALSE)
+      s = seq(1, 10, 3); s2 = seq(5, 1); R0 = rand(rows = 100, cols = 3, min = 2, max = 4, seed = 7)
+      R1 = rand(rows = 100, cols = 3, min = 2, max = 4, seed = 7); Z = rand(rows=50, cols=50, sparsity=0.2, seed=3)
+      D = diag(matrix("1 2 3", rows = 3, cols = 1)); d = diag(D); r = rev(s); T = t(A)
+      cb = cbind(A, A); rb = rbind(A, A)
+      o = order(target = matrix("3 1 2", rows = 3, cols = 1), by = 1)
+      oi = order(target = matrix("3 1 2", rows = 3, cols = 1), by = 1, decreasing = TRUE, index.return = TRUE)
+      re = removeEmpty(target = matrix("1 0 0 0 2 3", rows = 3, cols = 2), margin = "rows")
+      rp = replace(target = matrix("1 0 0 0 2 3", rows = 3, cols = 2), pattern = 0, replacement = 9)
+    """, outputs=["A", "B", "C", "s", "s2", "R0", "R1", "Z", "D", "d", "r", "T", "cb", "rb", "o", "oi", "re", "rp"])
+    A = np.array([[1, 2, 3], [4, 5, 6]], dtype=float)
+    np.testing.assert_allclose(M(res, "B"), A.reshape(3, 2))
+    np.testing.assert_allclose(M(res, "C"), A.reshape(-1, order="F").reshape(2, 3, order="F").reshape(3, 2, order="F")
+                               if False else A.flatten(order="F").reshape(3, 2, order="F"))
+    np.testing.assert_allclose(M(res, "s").ravel(), [1, 4, 7, 10])
+    np.testing.assert_allclose(M(res, "s2").ravel(), [5, 4, 3, 2, 1])
+    r0 = M(res, "R0")
+    assert r0.min() >= 2 and r0.max() <= 4 and np.array_equal(r0, M(res, "R1"))
+    z = M(res, "Z")
+    assert 0.1 < (z != 0).mean() < 0.3
+    np.testing.assert_allclose(M(res, "D"), np.diag([1, 2, 3]))
+    np.testing.assert_allclose(M(res, "d").ravel(), [1, 2, 3])
+    np.testing.assert_allclose(M(res, "T"), A.T)
+    assert M(res, "cb").shape == (2, 6) and M(res, "rb").shape == (4, 3)
+    np.testing.assert_allclose(M(res, "o").ravel(), [1, 2, 3])
+    np.testing.assert_allclose(M(res, "oi").ravel(), [1, 3, 2])
+    np.testing.assert_allclose(M(res, "re"), [[1, 0], [2, 3]])
+    np.testing.assert_allclose(M(res, "rp"), [[1, 9], [9, 9], [2, 3]])
+
+
+def test_table_and_stats():
+    res, _ = R("""
+      y = matrix("1 2 2 3 3 3", rows = 6, cols = 1)
+      T = table(seq(1, 6), y); c = table(y, y)
+      q = quantile(y, 0.5); med = median(y); mo = moment(y, 2); cv = cov(y, y)
+      ag = aggregate(target = y, groups = y, fn = "sum")
+    """, outputs=["T", "c", "q", "med", "mo", "cv", "ag"])
+    T = M(res, "T")
+    assert T.shape == (6, 3) and T.sum() == 6 and T[5, 2] == 1
+    np.testing.assert_allclose(np.diag(M(res, "c")), [1, 2, 3])
+    y = np.array([1, 2, 2, 3, 3, 3.0])
+    assert res["q"] == 2 and res["med"] == 2.5
+    assert abs(res["mo"] - y.var()) < 1e-12 and abs(res["cv"] - y.var(ddof=1)) < 1e-12
+    np.testing.assert_allclose(M(res, "ag").ravel(), [1, 4, 9])
+
+
+def test_linalg():
+    rng = np.random.default_rng(4)
+    A = rng.standard_normal((5, 5))
+    S = A @ A.T + 5 * np.eye(5)
+    b = rng.standard_normal((5, 1))
+    res, _ = R("""
+      x = solve(S, b); Ai = inv(S); L = cholesky(S); [ev, evec] = eigen(S)
+      [U, D, V] = svd(A)
+    """, {"S": S, "A": A, "b": b}, ["x", "Ai", "L", "ev", "evec", "U", "D", "V"])
+    np.testing.assert_allclose(M(res, "x"), np.linalg.solve(S, b))
+    np.testing.assert_allclose(M(res, "Ai"), np.linalg.inv(S), atol=1e-12)
+    np.testing.assert_allclose(M(res, "L"), np.linalg.cholesky(S))
+    np.testing.assert_allclose(np.sort(M(res, "ev").ravel()), np.sort(np.linalg.eigvalsh(S)))
+    U, D, V = M(res, "U"), M(res, "D"), M(res, "V")
+    np.testing.assert_allclose(U @ D @ V.T, A, atol=1e-10)
+
+
+def test_functions_control_flow():
+    _, out = R("""
+      fib = function(int n) return (int r) {
+        if (n <= 1) { r = n } else { [a] = fib(n - 1); [b] = fib(n - 2); r = a + b }
+      }
+      sq = function(matrix[double] X, double s = 2.0) return (matrix[double] Y) { Y = X ^ s }
+      x = fib(10); print(x)
+      M = sq(matrix(3, rows = 2, cols = 2)); print(sum(M))
+      M2 = sq(X = matrix(2, rows = 1, cols = 1), s = 3); print(as.scalar(M2))
+      i = 0; s = 0
+      while (i < 5) { i = i + 1; if (i == 3) { s = s + 100 } else { s = s + i } }
+      print(s)
+      acc = 0
+      for (k in seq(10, 1, -3)) { acc = acc + k }
+      print(acc)
+      l = list(a = 1, b = "x"); print(as.scalar(l["a"]) + 1)
+    """)
+    assert out == ["55", "36.0", "8.0", "112", "22", "2"]
+
+
+def test_constant_branch_removal_and_merge():
+    from systemml_amd.api.executor import compile_script
+    from systemml_amd.compiler.blocks import IfBlock
+    cs = compile_script("icpt = 0\nif (icpt == 2) { y = 1 } else { y = 2 }\nprint(y)", config=CFG)
+    assert not any(isinstance(b, IfBlock) for b in cs.cp.blocks)
+
+
+def test_undefined_variable_error():
+    from systemml_amd.parser.errors import DMLRuntimeError
+    with pytest.raises(DMLRuntimeError, match="not defined"):
+        R("print(undefined_var)")
+
+
+def test_stop():
+    from systemml_amd.parser.errors import DMLScriptStop
+    with pytest.raises(DMLScriptStop, match="bad"):
+        R("if (TRUE) { stop('bad') }")
+
+
+def test_toString_and_print_matrix():
+    _, out = R("print(toString(matrix('1 2 3 4', rows = 2, cols = 2)))")
+    assert out[0] == "1.000 2.000\n3.000 4.000\n"
