@@ -179,6 +179,15 @@ class Rewriter:
     def _rw_mm(self, h):
         a, b = h.inputs
         transA = h.p.get("transA", False)
+        # (-A) %*% B -> -(A %*% B): keeps t(X) visible to the transpose / fusion rules
+        if a.op == "u" and a.p["o"] == "neg" and a.dt == "M":
+            self._count("neg-pushdown")
+            inner = self._rw_mm(Hop("mm", [a.inputs[0], b], dict(h.p), dt="M", pos=h.pos))
+            return Hop("u", [inner], {"o": "neg"}, dt="M", pos=h.pos)
+        if b.op == "u" and b.p["o"] == "neg" and b.dt == "M":
+            self._count("neg-pushdown")
+            inner = self._rw_mm(Hop("mm", [a, b.inputs[0]], dict(h.p), dt="M", pos=h.pos))
+            return Hop("u", [inner], {"o": "neg"}, dt="M", pos=h.pos)
         if not transA and a.op == "t":
             X = a.inputs[0]
             if b is X:

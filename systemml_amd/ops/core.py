@@ -31,7 +31,7 @@ def _dist():
 
 
 def is_dist(x):
-    return _DIST is not None and isinstance(x, _DIST.DistMatrix)
+    return isinstance(x, _dist().DistMatrix)
 
 
 def cvt(x: Tensor) -> Tensor:

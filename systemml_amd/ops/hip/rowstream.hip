@@ -120,17 +120,33 @@ __device__ __forceinline__ void unpack(const Raw8<double>& r, A* x) {
   for (int i = 0; i < 4; ++i) { x[2 * i] = r.v[i].x; x[2 * i + 1] = r.v[i].y; }
 }
 
-template <typename A>
-__device__ __forceinline__ A wave_sum(A v) {
+// Wave-wide sum whose result is wave-uniform.  fp32: DPP butterflies inside each
+// 16-lane row (quad_perm xor1 / xor2, row_half_mirror, row_mirror: pure VALU, no LDS
+// crossbar) + 4 v_readlane for the cross-row total.  fp64 keeps the generic shuffle.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  v += dpp_f<0x140>(v);   // row_mirror  -> every lane holds its 16-lane row sum
+  const int iv = __float_as_int(v);
+  return (__int_as_float(__builtin_amdgcn_readlane(iv, 0)) + __int_as_float(__builtin_amdgcn_readlane(iv, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(iv, 32)) + __int_as_float(__builtin_amdgcn_readlane(iv, 48)));
+}
+__device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
 
 // ---------------------------------------------------------------------------
-// main kernel
+// main kernel: each wave streams R rows per iteration (rows r + i*WAVES), so R
+// independent reduction chains interleave and 2*R row loads are in flight.
 // ---------------------------------------------------------------------------
-template <typename T, typename A, int K, int J, int MODE>
+template <typename T, typename A, int K, int J, int MODE, int R>
 __global__ void __launch_bounds__(BLOCK)
 rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
                  const A* __restrict__ V, int ldv,          // D x K (row-major, ld ldv)
@@ -163,81 +179,123 @@ rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
 
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
+  constexpr int STEP = WAVES * R;
 
-  Raw8<T> nxt[J];
+  Raw8<T> nxt[R][J];
   int64_t r = r0 + wave;
-  if (r < r1) {
 #pragma unroll
-    for (int j = 0; j < J; ++j) load_raw<T>(nxt[j], X + r * (int64_t)D, (j * 64 + lane) * 8, D, vec);
-  }
-  for (; r < r1; r += WAVES) {
-    A x[C];
+  for (int i = 0; i < R; ++i) {
+    const int64_t ri = r + i * WAVES;
+    if (ri < r1) {
 #pragma unroll
-    for (int j = 0; j < J; ++j) unpack<A>(nxt[j], x + j * 8);
-    const int64_t rn = r + WAVES;
-    if (rn < r1) {   // prefetch the wave's next row before the reductions below
-#pragma unroll
-      for (int j = 0; j < J; ++j) load_raw<T>(nxt[j], X + rn * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+      for (int j = 0; j < J; ++j) load_raw<T>(nxt[i][j], X + ri * (int64_t)D, (j * 64 + lane) * 8, D, vec);
     }
+  }
+  for (; r < r1; r += STEP) {
+    A x[R][C];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < J; ++j) unpack<A>(nxt[i][j], x[i] + j * 8);
+    // prefetch the wave's next R rows before the reductions below
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int64_t rn = r + STEP + i * WAVES;
+      if (rn < r1) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) load_raw<T>(nxt[i][j], X + rn * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+      }
+    }
+    bool valid[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) valid[i] = (r + i * WAVES) < r1;   // wave-uniform
 
     if constexpr (MODE == ROWSSQ || MODE == ROWSUM) {
-      A s = A(0);
 #pragma unroll
-      for (int c = 0; c < C; ++c) s += (MODE == ROWSSQ) ? x[c] * x[c] : x[c];
-      s = wave_sum(s);
-      if (lane == 0) out[r * (int64_t)ldo] = s;
+      for (int i = 0; i < R; ++i) {
+        A s = A(0);
+#pragma unroll
+        for (int c = 0; c < C; ++c) s += (MODE == ROWSSQ) ? x[i][c] * x[i][c] : x[i][c];
+        s = wave_sum(s);
+        if (valid[i] && lane == 0) out[(r + i * WAVES) * (int64_t)ldo] = s;
+      }
       continue;
     }
     if constexpr (MODE == COLSSQ || MODE == COLSUM) {
 #pragma unroll
-      for (int c = 0; c < C; ++c) acc[c][0] += (MODE == COLSSQ) ? x[c] * x[c] : x[c];
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c][0] += (MODE == COLSSQ) ? x[i][c] * x[i][c] : x[i][c];
       continue;
     }
 
-    A g[K];
+    A g[R][K];
     if constexpr (MI::needV) {
-      A u[K];
+      A u[R][K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) u[k] = A(0);
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int k = 0; k < K; ++k) u[i][k] = A(0);
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const A* vrow = sV + ((j * 64 + lane) * 8) * K;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
 #pragma unroll
-          for (int k = 0; k < K; ++k) u[k] += x[j * 8 + e] * vrow[e * K + k];
+          for (int k = 0; k < K; ++k) {
+            const A vv = vrow[e * K + k];
+#pragma unroll
+            for (int i = 0; i < R; ++i) u[i][k] += x[i][j * 8 + e] * vv;
+          }
       }
 #pragma unroll
-      for (int k = 0; k < K; ++k) u[k] = wave_sum(u[k]);
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int i = 0; i < R; ++i) u[i][k] = wave_sum(u[i][k]);
       if constexpr (MODE == XV) {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-          if (lane == k) out[r * (int64_t)ldo + k] = u[k];
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if (valid[i] && lane == k) out[(r + i * WAVES) * (int64_t)ldo + k] = u[i][k];
         continue;
-      } else if constexpr (MODE == XTXV) {
+      } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k) g[k] = u[k];
-      } else if constexpr (MODE == XTWXV) {
+        for (int i = 0; i < R; ++i) {
+          const int64_t ri = r + i * WAVES;
+          const bool ok = valid[i];
+          if constexpr (MODE == XTXV) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) g[k] = S[r * (int64_t)lds + (sbc ? 0 : k)] * u[k];
-      } else if constexpr (MODE == XTXVY) {
+            for (int k = 0; k < K; ++k) g[i][k] = ok ? u[i][k] : A(0);
+          } else if constexpr (MODE == XTWXV) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) g[k] = u[k] - S[r * (int64_t)lds + (sbc ? 0 : k)];
-      } else if constexpr (MODE == XTPSXV) {
-        A p[K], q[K], s = A(0);
+            for (int k = 0; k < K; ++k) g[i][k] = ok ? S[ri * (int64_t)lds + (sbc ? 0 : k)] * u[i][k] : A(0);
+          } else if constexpr (MODE == XTXVY) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) { p[k] = S[r * (int64_t)lds + k]; q[k] = p[k] * u[k]; s += q[k]; }
+            for (int k = 0; k < K; ++k) g[i][k] = ok ? u[i][k] - S[ri * (int64_t)lds + (sbc ? 0 : k)] : A(0);
+          } else if constexpr (MODE == XTPSXV) {
+            A p[K], q[K], sq = A(0);
 #pragma unroll
-        for (int k = 0; k < K; ++k) g[k] = q[k] - p[k] * s;
+            for (int k = 0; k < K; ++k) { p[k] = ok ? S[ri * (int64_t)lds + k] : A(0); q[k] = p[k] * u[i][k]; sq += q[k]; }
+#pragma unroll
+            for (int k = 0; k < K; ++k) g[i][k] = q[k] - p[k] * sq;
+          }
+        }
       }
     } else {  // XTG
 #pragma unroll
-      for (int k = 0; k < K; ++k) g[k] = S[r * (int64_t)lds + k];
+      for (int i = 0; i < R; ++i) {
+        const int64_t ri = r + i * WAVES;
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[i][k] = valid[i] ? S[ri * (int64_t)lds + k] : A(0);
+      }
     }
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+    for (int i = 0; i < R; ++i)
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc[c][k] += x[c] * g[k];
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[c][k] += x[i][c] * g[i][k];
   }
 
   if constexpr (MI::accum) {
@@ -271,6 +329,8 @@ rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
 // ---------------------------------------------------------------------------
 using namespace sysml;
 
+static int g_rows_per_iter = 0;   // 0 = auto, else 1 / 2 (A/B tuning knob)
+
 template <typename T, typename A, int K, int J, int MODE>
 static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int ldv, const void* S,
                     int lds, int sbc, void* out, int ldo, int grid, int64_t rpb, hipStream_t st) {
@@ -282,8 +342,16 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
   size_t shv = MI::needV ? (size_t)J * 512 * K * sizeof(A) : 0;
   size_t shr = MI::accum ? (size_t)J * 512 * KO * sizeof(A) : 0;
   size_t sh = shv > shr ? shv : shr;
-  hipLaunchKernelGGL((rowstream_kernel<T, A, K, J, MODE>), dim3(grid), dim3(BLOCK), sh, st,
-                     (const T*)X, N, D, vec, (const A*)V, ldv, (const A*)S, lds, sbc, (A*)out, ldo, rpb);
+  const bool two = (g_rows_per_iter == 2) ||
+                   (g_rows_per_iter == 0 && sizeof(A) == 4 && (MODE == XV || MODE == XTXV || MODE == ROWSSQ ||
+                                                               MODE == ROWSUM || (K == 1 && MI::accum)));
+  if (sizeof(A) == 4 && K <= 4 && two) {
+    hipLaunchKernelGGL((rowstream_kernel<T, A, K, J, MODE, 2>), dim3(grid), dim3(BLOCK), sh, st,
+                       (const T*)X, N, D, vec, (const A*)V, ldv, (const A*)S, lds, sbc, (A*)out, ldo, rpb);
+  } else {
+    hipLaunchKernelGGL((rowstream_kernel<T, A, K, J, MODE, 1>), dim3(grid), dim3(BLOCK), sh, st,
+                       (const T*)X, N, D, vec, (const A*)V, ldv, (const A*)S, lds, sbc, (A*)out, ldo, rpb);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
   }
 }
@@ -356,6 +424,9 @@ int sysml_rowstream(int mode, int xdtype, const void* X, int64_t N, int D, const
   return -1;
 }
 
-int sysml_abi_version() { return 1; }
+int sysml_abi_version() { return 2; }
+
+// tuning knob for A/B runs: 0 = automatic, 1 or 2 rows per wave iteration
+void sysml_set_rows_per_iter(int r) { g_rows_per_iter = r; }
 
 }  // extern "C"

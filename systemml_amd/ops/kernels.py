@@ -56,6 +56,8 @@ def load(required=False):
                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                   ctypes.c_void_p]
+    L.sysml_set_rows_per_iter.argtypes = [ctypes.c_int]
+    L.sysml_set_rows_per_iter.restype = None
     _lib = L
     return L
 

@@ -429,18 +429,18 @@ def rbind(args):
     return local_rows(ctx, full)
 
 
-def table(exec_ctx, A, B, W, d1, d2):
-    """ctable(seq(1,N), y, N, K) → one-hot rows stay local; general case gathers."""
-    from ..runtime.builtins import _ctable, _int
+def table(exec_ctx, A, B, W, dims):
+    """ctable(seq(1,N), y, [w], N, K) → one-hot rows stay local; general case gathers."""
+    from ..runtime.builtins import b_table
     from ..ops.backend import backend
     if _is_d(A) and _is_d(B) and A.nrows == B.nrows and not isinstance(W, (torch.Tensor, DistMatrix)):
         a = A.local.reshape(-1)
         expect = torch.arange(A.start + 1, A.start + a.numel() + 1, dtype=a.dtype, device=a.device)
         is_seq = bool(torch.equal(a, expect))
         flag = A.ctx.allreduce_scalar(0.0 if is_seq else 1.0, "max", device=a.device if a.is_cuda else None)
-        if flag == 0.0 and d1 is not None and _int(d1) == A.nrows:
+        if flag == 0.0 and (dims is None or dims[0] == A.nrows):
             b = B.local.reshape(-1)
-            k = _int(d2) if d2 is not None else int(agg("max", "all", B))
+            k = dims[1] if dims is not None else int(agg("max", "all", B))
             w = 1.0 if W is None else float(W)
             out = torch.zeros((a.numel(), k), dtype=backend.dtype, device=a.device)
             bi = torch.round(b).long() - 1
@@ -448,8 +448,10 @@ def table(exec_ctx, A, B, W, d1, d2):
             rows = torch.arange(a.numel(), device=a.device)
             out[rows[keep], bi[keep]] = w
             return DistMatrix(out, A.nrows, k, A.start, A.ctx)
-    from ..runtime.builtins import b_table
-    r = b_table(exec_ctx, gather(A) if _is_d(A) else A, gather(B) if _is_d(B) else B,
-                gather(W) if _is_d(W) else W, d1, d2)
     stats["fallback_gathers"] += 1
-    return r
+    args = [gather(A) if _is_d(A) else A, gather(B) if _is_d(B) else B]
+    if W is not None:
+        args.append(gather(W) if _is_d(W) else W)
+    if dims is not None:
+        args += list(dims)
+    return b_table(exec_ctx, *args)

@@ -487,12 +487,10 @@ def b_outer(ctx, a, b, op):
 
 @builtin("table", "ctable")
 def b_table(ctx, A=None, B=None, W=None, odim1=None, odim2=None, *rest, **kw):
-    if C.is_dist(A) or C.is_dist(B):
-        return C._dist().table(ctx, A, B, W, odim1, odim2)
     # table(A, B, [W], [d1, d2])
     args = [a for a in (A, B, W, odim1, odim2) + rest if a is not None]
     if "weights" in kw:
-        W = kw["weights"]
+        args.insert(2, kw["weights"])
     A_, B_ = args[0], args[1]
     w = None
     dims = None
@@ -502,8 +500,10 @@ def b_table(ctx, A=None, B=None, W=None, odim1=None, odim2=None, *rest, **kw):
         rem = rem[1:]
     if len(rem) == 2:
         dims = (_int(rem[0]), _int(rem[1]))
-    a = _mat(A_).reshape(-1) if isinstance(A_, (Tensor,)) or C.is_dist(A_) else None
-    b = _mat(B_).reshape(-1) if isinstance(B_, (Tensor,)) or C.is_dist(B_) else None
+    if C.is_dist(A_) or C.is_dist(B_):
+        return C._dist().table(ctx, A_, B_, w, dims)
+    a = _mat(A_).reshape(-1) if isinstance(A_, Tensor) else None
+    b = _mat(B_).reshape(-1) if isinstance(B_, Tensor) else None
     n = a.numel() if a is not None else b.numel()
     if a is None:
         a = torch.full((n,), float(A_), dtype=_dt(), device=_dev())

@@ -1,0 +1,11 @@
+#!/bin/bash
+R=$GRAFT_REPO_ROOT
+cd $R
+mkdir -p gpurun_out
+timeout -k 10 400 python -m pytest tests/test_gpu_kernels.py -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
+echo "pytest rc=$?" > gpurun_out/progress3.txt
+timeout -k 10 300 python tools/bench_kernels.py --out gpurun_out/kbench.json > gpurun_out/kbench.log 2>&1
+rc=$?; echo "kbench rc=$rc" >> gpurun_out/progress3.txt
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_10m.log 2>&1
+echo "bench rc=$?" >> gpurun_out/progress3.txt
