@@ -62,6 +62,8 @@ def tokenize(src: str, pydml: bool = False, filename: str = ""):
 
     while i < n:
         c = src[i]
+        if pydml and at_line_start and paren_depth > 0:
+            at_line_start = False      # implicit line joining inside brackets
         if pydml and at_line_start and paren_depth == 0:
             # measure indentation of logical line
             j = i
