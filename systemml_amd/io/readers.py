@@ -35,6 +35,7 @@ def _files(fname):
 def read(ctx, fname, **kw):
     md = M.read_mtd(fname) or {}
     fmt = kw.get("format", md.get("format", None))
+    fmt = fmt.lower() if isinstance(fmt, str) else fmt
     dtype = kw.get("data_type", md.get("data_type", "matrix"))
     if fmt is None:
         fmt = _sniff(fname)

@@ -25,7 +25,7 @@ def _np(x):
 
 
 def write(ctx, x, fname, format="text", **kw):
-    fmt = str(format)
+    fmt = str(format).lower()
     from ..ops import core as C
     if C.is_dist(x):
         x = C._dist().gather(x)

@@ -660,41 +660,45 @@ def b_iqm(ctx, x, w=None):
 
 @builtin("aggregate")
 def b_aggregate(ctx, target=None, groups=None, fn="sum", weights=None, ngroups=None, **kw):
-    t = _mat(target).reshape(-1)
+    """Grouped aggregates (reference: ParameterizedBuiltin GROUPEDAGG); a multi-column
+    target is aggregated column-wise (result ngroups x ncol)."""
+    T = _mat(target)
     g = torch.round(_mat(groups).reshape(-1)).long()
+    if T.shape[0] != g.numel() and T.shape[1] == g.numel() and T.shape[0] == 1:
+        T = T.t()
     k = _int(ngroups) if ngroups is not None else int(g.max().item())
     keep = (g >= 1) & (g <= k)
-    t, g = t[keep], g[keep] - 1
-    w = _mat(weights).reshape(-1)[keep].to(t.dtype) if weights is not None else None
+    T, g = T[keep], g[keep] - 1
+    w = _mat(weights).reshape(-1)[keep].to(T.dtype) if weights is not None else None
     fn = str(fn)
-    dev = t.device
-    cnt = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, w if w is not None else torch.ones_like(t))
+    dev, dt = T.device, T.dtype
+    m = T.shape[1]
+    ww = (w if w is not None else torch.ones(T.shape[0], dtype=dt, device=dev)).reshape(-1, 1)
+
+    def gsum(v):
+        return torch.zeros((k, m), dtype=dt, device=dev).index_add_(0, g, v)
+
+    cnt = gsum(ww.expand(-1, m).contiguous())
     if fn == "count":
         out = cnt
     elif fn == "sum":
-        out = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, t * w if w is not None else t)
+        out = gsum(T * ww)
     elif fn == "mean":
-        s = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, t * w if w is not None else t)
-        out = s / cnt
+        out = gsum(T * ww) / cnt
     elif fn in ("variance", "var"):
-        ww = w if w is not None else torch.ones_like(t)
-        s = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, t * ww)
-        mu = s / cnt
-        d = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, ww * (t - mu[g]) ** 2)
-        out = d / (cnt - 1)
+        mu = gsum(T * ww) / cnt
+        out = gsum(ww * (T - mu[g]) ** 2) / (cnt - 1)
     elif fn in ("min", "max"):
         init = math.inf if fn == "min" else -math.inf
-        out = torch.full((k,), init, dtype=t.dtype, device=dev)
-        out = out.scatter_reduce(0, g, t, reduce="amin" if fn == "min" else "amax")
+        out = torch.full((k, m), init, dtype=dt, device=dev)
+        out = out.scatter_reduce(0, g.reshape(-1, 1).expand(-1, m), T, reduce="amin" if fn == "min" else "amax")
     elif fn.startswith("centralmoment") or fn == "moment":
         order = _int(kw.get("order", 2))
-        s = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, t)
-        mu = s / cnt
-        d = torch.zeros(k, dtype=t.dtype, device=dev).index_add_(0, g, (t - mu[g]) ** order)
-        out = d / cnt
+        mu = gsum(T) / cnt
+        out = gsum((T - mu[g]) ** order) / cnt
     else:
         raise DMLRuntimeError(f"aggregate: unsupported fn '{fn}'")
-    return out.reshape(-1, 1)
+    return out
 
 
 # ============================================================================
@@ -728,7 +732,7 @@ def b_cdf(ctx, target=None, dist="normal", **kw):
     return _dist_fn(dist, q=target, lower=lower, **kw)
 
 
-@builtin("invcdf")
+@builtin("invcdf", "icdf")
 def b_invcdf(ctx, target=None, dist="normal", **kw):
     return _dist_fn(dist, p=target, **kw)
 

@@ -56,10 +56,10 @@ def make_data(d, n=200, m=8, seed=3):
     T = np.hstack([np.abs(rng.standard_normal((n, 1))) * 10 + 1, (rng.random((n, 1)) < 0.7) * 1.0,
                    rng.integers(1, 3, (n, 1)) * 1.0, X[:, :3]])
     write(f"{d}/surv", T)
-    write(f"{d}/te", np.array([[1, 2]]))
+    write(f"{d}/te", np.array([[1], [2]]))
     write(f"{d}/gi", np.array([[3]]))
     write(f"{d}/si", np.array([[3]]))
-    write(f"{d}/F", X[:, :3])
+    write(f"{d}/F", np.array([[4], [5], [6]]))
     write(f"{d}/Xcs", np.sort(rng.random((30, 1)) * 10, 0))
     write(f"{d}/ycs", np.sin(np.sort(rng.random((30, 1)) * 10, 0)))
 
@@ -93,7 +93,7 @@ def cases(d):
         "bivar-stats": dict(X=f"{d}/X", index1=f"{d}/S1", index2=f"{d}/S2", types1=f"{d}/K1",
                             types2=f"{d}/K2", OUTDIR=f"{o}/bivar"),
         "ALS-CG": dict(X=f"{d}/R", U=f"{o}/U", V=f"{o}/V", rank=4, reg="L2", lambda_=0.01, maxi=10),
-        "ALS-DS": dict(V=f"{d}/R", L=f"{o}/L", R=f"{o}/Rf", rank=4, reg=0.01, maxi=10),
+        "ALS-DS": dict(V=f"{d}/R", L=f"{o}/L", R=f"{o}/Rf", rank=4, reg="L2", lambda_=0.01, maxi=10),
         "decision-tree": dict(X=f"{d}/X", Y=f"{d}/ycls", M=f"{o}/tree", bins=5, depth=4, num_leaf=5),
         "decision-tree-predict": dict(X=f"{d}/X", Y=f"{d}/ycls", M=f"{o}/tree", P=f"{o}/treeP",
                                       A=f"{o}/treeA", CM=f"{o}/treeCM"),
@@ -109,7 +109,7 @@ def cases(d):
         "StepLinearRegDS": dict(X=f"{d}/X", Y=f"{d}/y", B=f"{o}/stepB", S=f"{o}/stepS"),
         "StepGLM": dict(X=f"{d}/X", Y=f"{d}/counts", B=f"{o}/sglmB", S=f"{o}/sglmS", dfam=1, vpow=1.0, link=1,
                         lpow=0.0),
-        "stratstats": dict(X=f"{d}/X", Xcid=f"{d}/S1", Ycid=f"{d}/S2", S=1, O=f"{o}/strat"),
+        "stratstats": dict(X=f"{d}/Xint", Xcid=f"{d}/S1", Ycid=f"{d}/S2", S=f"{d}/gi", O=f"{o}/strat"),
     }
 
 
