@@ -322,6 +322,196 @@ rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Packed-fp32 variant for K in {2,4,8} (fp32 accumulate: bf16 / fp32 X).
+// The k dimension is carried in float2 pairs so every dot-product / accumulate
+// FMA is a v_pk_fma_f32 (2 FMAs per lane per instruction), and for C*K <= 64 the
+// lane's slice of V lives in registers for the whole launch (no per-row LDS
+// traffic).  Row-side values (g) are wave-uniform after the DPP reduction.
+// ---------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <typename T, int K, int J, int MODE, int R>
+__global__ void __launch_bounds__(BLOCK)
+rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
+                    const float* __restrict__ V, int ldv,
+                    const float* __restrict__ S, int lds, int sbc,
+                    float* __restrict__ out, int ldo, int64_t rows_per_block) {
+  using MI = ModeInfo<MODE>;
+  constexpr int C = J * 8;
+  constexpr int K2 = K / 2;
+  constexpr bool VREG = MI::needV && (C * K <= 64);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sV = reinterpret_cast<float*>(smem);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Dp = J * 512;
+
+  f2 vreg[VREG ? C : 1][VREG ? K2 : 1];
+  if constexpr (MI::needV) {
+    for (int i = threadIdx.x; i < Dp * K; i += BLOCK) {
+      int d = i / K, k = i - d * K;
+      sV[i] = (d < D) ? V[(int64_t)d * ldv + k] : 0.f;
+    }
+    __syncthreads();
+    if constexpr (VREG) {
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+          for (int kk = 0; kk < K2; ++kk) {
+            const float* p = sV + (((j * 64 + lane) * 8 + e) * K + 2 * kk);
+            vreg[j * 8 + e][kk] = f2{p[0], p[1]};
+          }
+    }
+  }
+
+  f2 acc[MI::accum ? C : 1][MI::accum ? K2 : 1];
+  if constexpr (MI::accum) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int kk = 0; kk < K2; ++kk) acc[c][kk] = f2{0.f, 0.f};
+  }
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
+  constexpr int STEP = WAVES * R;
+
+  Raw8<T> nxt[R][J];
+  int64_t r = r0 + wave;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int64_t ri = r + i * WAVES;
+    if (ri < r1) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) load_raw<T>(nxt[i][j], X + ri * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+    }
+  }
+  for (; r < r1; r += STEP) {
+    float x[R][C];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < J; ++j) unpack<float>(nxt[i][j], x[i] + j * 8);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int64_t rn = r + STEP + i * WAVES;
+      if (rn < r1) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) load_raw<T>(nxt[i][j], X + rn * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+      }
+    }
+    bool valid[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) valid[i] = (r + i * WAVES) < r1;
+
+    f2 g[R][K2];
+    if constexpr (MI::needV) {
+      f2 u[R][K2];
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk) u[i][kk] = f2{0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk) {
+          f2 vv;
+          if constexpr (VREG) {
+            vv = vreg[c][kk];
+          } else {
+            const float* p = sV + ((((c >> 3) * 64 + lane) * 8 + (c & 7)) * K + 2 * kk);
+            vv = f2{p[0], p[1]};
+          }
+#pragma unroll
+          for (int i = 0; i < R; ++i) u[i][kk] = __builtin_elementwise_fma(f2{x[i][c], x[i][c]}, vv, u[i][kk]);
+        }
+      }
+      float us[R][K];
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk) {
+          us[i][2 * kk] = wave_sum(u[i][kk].x);
+          us[i][2 * kk + 1] = wave_sum(u[i][kk].y);
+        }
+      if constexpr (MODE == XV) {
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if (valid[i] && lane == k) out[(r + i * WAVES) * (int64_t)ldo + k] = us[i][k];
+        continue;
+      } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const int64_t ri = r + i * WAVES;
+          const bool ok = valid[i];
+          float gs[K];
+          if constexpr (MODE == XTXV) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) gs[k] = ok ? us[i][k] : 0.f;
+          } else if constexpr (MODE == XTWXV) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) gs[k] = ok ? S[ri * (int64_t)lds + (sbc ? 0 : k)] * us[i][k] : 0.f;
+          } else if constexpr (MODE == XTXVY) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) gs[k] = ok ? us[i][k] - S[ri * (int64_t)lds + (sbc ? 0 : k)] : 0.f;
+          } else if constexpr (MODE == XTPSXV) {
+            float p[K], q[K], sq = 0.f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) { p[k] = ok ? S[ri * (int64_t)lds + k] : 0.f; q[k] = p[k] * us[i][k]; sq += q[k]; }
+#pragma unroll
+            for (int k = 0; k < K; ++k) gs[k] = q[k] - p[k] * sq;
+          }
+#pragma unroll
+          for (int kk = 0; kk < K2; ++kk) g[i][kk] = f2{gs[2 * kk], gs[2 * kk + 1]};
+        }
+      }
+    } else {  // XTG
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int64_t ri = r + i * WAVES;
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk)
+          g[i][kk] = valid[i] ? f2{S[ri * (int64_t)lds + 2 * kk], S[ri * (int64_t)lds + 2 * kk + 1]} : f2{0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk)
+          acc[c][kk] = __builtin_elementwise_fma(f2{x[i][c], x[i][c]}, g[i][kk], acc[c][kk]);
+  }
+
+  if constexpr (MI::accum) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    for (int w = 0; w < WAVES; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int kk = 0; kk < K2; ++kk) {
+              int idx = ((j * 64 + lane) * 8 + e) * K + 2 * kk;
+              f2 a = acc[j * 8 + e][kk];
+              if (w == 0) { red[idx] = a.x; red[idx + 1] = a.y; }
+              else { red[idx] += a.x; red[idx + 1] += a.y; }
+            }
+      }
+      __syncthreads();
+    }
+    float* dst = out + (int64_t)blockIdx.x * D * K;
+    for (int i = threadIdx.x; i < D * K; i += BLOCK) dst[i] = red[i];
+  }
+}
+
 }  // namespace sysml
 
 // ---------------------------------------------------------------------------
@@ -330,6 +520,7 @@ rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
 using namespace sysml;
 
 static int g_rows_per_iter = 0;   // 0 = auto, else 1 / 2 (A/B tuning knob)
+static int g_variant = 0;         // 0 = auto (packed fp32 where applicable), 1 = generic scalar kernel
 
 template <typename T, typename A, int K, int J, int MODE>
 static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int ldv, const void* S,
@@ -345,6 +536,21 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
   const bool two = (g_rows_per_iter == 2) ||
                    (g_rows_per_iter == 0 && sizeof(A) == 4 && (MODE == XV || MODE == XTXV || MODE == ROWSSQ ||
                                                                MODE == ROWSUM || (K == 1 && MI::accum)));
+  if constexpr (sizeof(A) == 4 && K >= 2 && MODE <= XTPSXV) {
+    if (g_variant != 1) {   // packed-fp32 kernel (default)
+      const bool two_pk = (g_rows_per_iter == 2) || (g_rows_per_iter == 0 && (MODE == XV || K == 2));
+      if (two_pk && K <= 4) {
+        hipLaunchKernelGGL((rowstream_pk_kernel<T, K, J, MODE, 2>), dim3(grid), dim3(BLOCK), sh, st,
+                           (const T*)X, N, D, vec, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out,
+                           ldo, rpb);
+      } else {
+        hipLaunchKernelGGL((rowstream_pk_kernel<T, K, J, MODE, 1>), dim3(grid), dim3(BLOCK), sh, st,
+                           (const T*)X, N, D, vec, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out,
+                           ldo, rpb);
+      }
+      return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+  }
   if (sizeof(A) == 4 && K <= 4 && two) {
     hipLaunchKernelGGL((rowstream_kernel<T, A, K, J, MODE, 2>), dim3(grid), dim3(BLOCK), sh, st,
                        (const T*)X, N, D, vec, (const A*)V, ldv, (const A*)S, lds, sbc, (A*)out, ldo, rpb);
@@ -428,5 +634,6 @@ int sysml_abi_version() { return 2; }
 
 // tuning knob for A/B runs: 0 = automatic, 1 or 2 rows per wave iteration
 void sysml_set_rows_per_iter(int r) { g_rows_per_iter = r; }
+void sysml_set_variant(int v) { g_variant = v; }
 
 }  // extern "C"

@@ -52,10 +52,13 @@ def main():
             cases["torch_mv_k1"] = lambda: X @ v1
             cases["torch_xtg_k4"] = lambda: X.t() @ g4
         times = {}
+        L.sysml_set_variant.argtypes = [ctypes.c_int]
         for rep in range(a.reps + 1):
             for name, fn in cases.items():
-                for R in ((1, 2) if not name.startswith("torch") else (0,)):
-                    L.sysml_set_rows_per_iter(R)
+                for R in ((1, 2, 11, 12) if not name.startswith("torch") else (0,)):
+                    # R = rows per wave iteration; 11/12 = generic scalar kernel (variant 1)
+                    L.sysml_set_variant(1 if R > 10 else 0)
+                    L.sysml_set_rows_per_iter(R % 10)
                     torch.cuda.synchronize()
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
