@@ -1,0 +1,142 @@
+"""nn library tests: numerical gradient checks of every layer's backward pass (the
+reference's scripts/nn/test/grad_check.dml strategy, driven from Python) plus the
+optimizers and a small end-to-end training run."""
+import numpy as np
+import pytest
+
+from systemml_amd.api.executor import run
+from systemml_amd.conf import DMLConfig
+
+CFG = DMLConfig(gpu=False)
+
+
+def dml(src, inputs, outputs):
+    res = run(src, inputs=inputs, outputs=outputs, config=CFG, out=lambda s: None)
+    return {k: (v.numpy() if hasattr(v, "numpy") else v) for k, v in res.items()}
+
+
+def gradcheck(layer, fwd_args, bwd_args, inputs, wrt, loss_w, extra_fwd_out="", h=1e-6, tol=1e-5):
+    """Check d(sum(out * loss_w))/d(wrt) from <layer>::backward against finite differences."""
+    src_f = f'source("nn/layers/{layer}.dml") as L\n[out{extra_fwd_out}] = L::forward({fwd_args})\nl = sum(out * LW)'
+    src_b = (f'source("nn/layers/{layer}.dml") as L\n[out{extra_fwd_out}] = L::forward({fwd_args})\n'
+             f'dout = LW\n{bwd_args}')
+    ins = dict(inputs)
+    ins["LW"] = loss_w
+    grads = dml(src_b, ins, ["d" + w for w in wrt])
+    rng = np.random.default_rng(0)
+    for w in wrt:
+        A = inputs[w]
+        G = grads["d" + w]
+        for _ in range(6):
+            i = rng.integers(0, A.shape[0])
+            j = rng.integers(0, A.shape[1])
+            Ap, Am = A.copy(), A.copy()
+            Ap[i, j] += h
+            Am[i, j] -= h
+            lp = dml(src_f, {**ins, w: Ap}, ["l"])["l"]
+            lm = dml(src_f, {**ins, w: Am}, ["l"])["l"]
+            num = (lp - lm) / (2 * h)
+            assert abs(num - G[i, j]) <= tol * max(1.0, abs(num)), (layer, w, i, j, num, G[i, j])
+
+
+rng = np.random.default_rng(42)
+
+
+def R(*s):
+    return rng.standard_normal(s)
+
+
+def test_affine():
+    gradcheck("affine", "X, W, b", "[dX, dW, db] = L::backward(dout, X, W, b)",
+              {"X": R(4, 5), "W": R(5, 3), "b": R(1, 3)}, ["X", "W", "b"], R(4, 3))
+
+
+@pytest.mark.parametrize("layer", ["relu", "sigmoid", "tanh"])
+def test_activations(layer):
+    gradcheck(layer, "X", "dX = L::backward(dout, X)", {"X": R(4, 5) + 0.01}, ["X"], R(4, 5))
+
+
+def test_softmax():
+    gradcheck("softmax", "X", "dX = L::backward(dout, X)", {"X": R(4, 5)}, ["X"], R(4, 5))
+
+
+def test_conv2d_builtin():
+    C, H, W, F, Hf = 2, 5, 5, 3, 3
+    gradcheck("conv2d_builtin", f"X, W, b, {C}, {H}, {W}, {Hf}, {Hf}, 1, 1, 1, 1", ", Hout, Wout".join(["", ""])
+              and f"[dX, dW, db] = L::backward(dout, Hout, Wout, X, W, b, {C}, {H}, {W}, {Hf}, {Hf}, 1, 1, 1, 1)",
+              {"X": R(2, C * H * W), "W": R(F, C * Hf * Hf), "b": R(F, 1)}, ["X", "W", "b"],
+              R(2, F * H * W), extra_fwd_out=", Hout, Wout")
+
+
+def test_max_pool():
+    C, H, W = 2, 4, 4
+    X = rng.permutation(2 * C * H * W).reshape(2, C * H * W).astype(float)   # no ties
+    gradcheck("max_pool2d_builtin", f"X, {C}, {H}, {W}, 2, 2, 2, 2, 0, 0",
+              f"dX = L::backward(dout, Hout, Wout, X, {C}, {H}, {W}, 2, 2, 2, 2, 0, 0)",
+              {"X": X}, ["X"], R(2, C * 4), extra_fwd_out=", Hout, Wout", h=1e-3)
+
+
+def test_batch_norm1d():
+    gradcheck("batch_norm1d", "X, g, b, 'train', em, ev, 0.9, 1e-5",
+              "[dX, dg, db] = L::backward(dout, out, a, bb, cm, cv, cn, X, g, b, 'train', em, ev, 0.9, 1e-5)",
+              {"X": R(6, 4), "g": R(1, 4), "b": R(1, 4), "em": np.zeros((1, 4)), "ev": np.ones((1, 4))},
+              ["X", "g", "b"], R(6, 4), extra_fwd_out=", a, bb, cm, cv, cn")
+
+
+def test_batch_norm2d():
+    C, H, W = 2, 3, 3
+    gradcheck("batch_norm2d", f"X, g, b, {C}, {H}, {W}, 'train', em, ev, 0.9, 1e-5",
+              f"[dX, dg, db] = L::backward(dout, out, a, bb, cm, cv, cn, X, g, b, {C}, {H}, {W}, 'train', em, ev, 0.9, 1e-5)",
+              {"X": R(4, C * H * W), "g": R(C, 1), "b": R(C, 1), "em": np.zeros((C, 1)), "ev": np.ones((C, 1))},
+              ["X", "g", "b"], R(4, C * H * W), extra_fwd_out=", a, bb, cm, cv, cn")
+
+
+def test_losses():
+    pred = np.abs(R(5, 3)) + 0.1
+    pred = pred / pred.sum(1, keepdims=True)
+    y = np.eye(3)[rng.integers(0, 3, 5)]
+    for layer in ("cross_entropy_loss", "l2_loss", "l1_loss"):
+        r = dml(f'source("nn/layers/{layer}.dml") as L\nl = L::forward(p, y)\nd = L::backward(p, y)',
+                {"p": pred, "y": y}, ["l", "d"])
+        h = 1e-6
+        P2 = pred.copy()
+        P2[1, 2] += h
+        r2 = dml(f'source("nn/layers/{layer}.dml") as L\nl = L::forward(p, y)', {"p": P2, "y": y}, ["l"])
+        assert abs((r2["l"] - r["l"]) / h - r["d"][1, 2]) < 1e-4
+
+
+def test_optimizers_decrease_quadratic():
+    for opt, call, init in [
+        ("sgd", "X = O::update(X, dX, 0.1)", ""),
+        ("sgd_momentum", "[X, v] = O::update(X, dX, 0.05, 0.9, v)", "v = O::init(X)"),
+        ("sgd_nesterov", "[X, v] = O::update(X, dX, 0.05, 0.9, v)", "v = O::init(X)"),
+        ("adagrad", "[X, c] = O::update(X, dX, 0.5, 1e-8, c)", "c = O::init(X)"),
+        ("rmsprop", "[X, c] = O::update(X, dX, 0.05, 0.9, 1e-8, c)", "c = O::init(X)"),
+        ("adam", "[X, m, v] = O::update(X, dX, 0.1, 0.9, 0.999, 1e-8, i - 1, m, v)", "[m, v] = O::init(X)"),
+    ]:
+        r = dml(f'source("nn/optim/{opt}.dml") as O\n{init}\nfor (i in 1:100) {{ dX = 2 * X\n {call} }}\n'
+                f'l = sum(X ^ 2)', {"X": np.ones((3, 2))}, ["l"])
+        assert r["l"] < 6 * 0.1, (opt, r["l"])
+
+
+def test_train_softmax_classifier():
+    X = R(200, 4)
+    y = np.eye(3)[np.argmax(X[:, :3], 1)]
+    src = '''
+source("nn/layers/affine.dml") as affine
+source("nn/layers/softmax.dml") as softmax
+source("nn/layers/cross_entropy_loss.dml") as ce
+source("nn/optim/sgd.dml") as sgd
+[W, b] = affine::init(4, 3)
+for (e in 1:200) {
+  s = affine::forward(X, W, b)
+  p = softmax::forward(s)
+  dp = ce::backward(p, Y)
+  ds = softmax::backward(dp, s)
+  [dX, dW, db] = affine::backward(ds, X, W, b)
+  W = sgd::update(W, dW, 0.5)
+  b = sgd::update(b, db, 0.5)
+}
+acc = mean(rowIndexMax(softmax::forward(affine::forward(X, W, b))) == rowIndexMax(Y))
+'''
+    assert dml(src, {"X": X, "Y": y}, ["acc"])["acc"] > 0.9
