@@ -140,3 +140,64 @@ for (e in 1:200) {
 acc = mean(rowIndexMax(softmax::forward(affine::forward(X, W, b))) == rowIndexMax(Y))
 '''
     assert dml(src, {"X": X, "Y": y}, ["acc"])["acc"] > 0.9
+
+
+def test_rnn():
+    N, T, D, M = 3, 4, 2, 3
+    gradcheck("rnn", f"X, W, b, {T}, {D}, TRUE, h0",
+              f"[dX, dW, db, dh0] = L::backward(dout, X, W, b, {T}, {D}, TRUE, h0, cache)",
+              {"X": R(N, T * D), "W": R(D + M, M) * 0.5, "b": R(1, M), "h0": R(N, M)}, ["X", "W", "b", "h0"],
+              R(N, T * M), extra_fwd_out=", cache")
+
+
+def test_lstm():
+    N, T, D, M = 2, 3, 2, 3
+    gradcheck("lstm", f"X, W, b, {T}, {D}, TRUE, h0, c0",
+              f"[dX, dW, db, dh0, dc0] = L::backward(dout, dc, X, W, b, {T}, {D}, TRUE, h0, c0, co, cc, cifog)",
+              {"X": R(N, T * D), "W": R(D + M, 4 * M) * 0.5, "b": R(1, 4 * M), "h0": R(N, M), "c0": R(N, M),
+               "dc": np.zeros((N, M))}, ["X", "W", "b", "h0", "c0"], R(N, T * M),
+              extra_fwd_out=", c, co, cc, cifog")
+
+
+def test_conv2d_transpose():
+    C, H, W, F, Hf = 2, 3, 3, 3, 3
+    Ho = 2 * (H - 1) - 2 + Hf + 1
+    gradcheck("conv2d_transpose", f"X, W, b, {C}, {H}, {W}, {Hf}, {Hf}, 2, 2, 1, 1, 1, 1",
+              f"[dX, dW, db] = L::backward(dout, Hout, Wout, X, W, b, {C}, {H}, {W}, {Hf}, {Hf}, 2, 2, 1, 1)",
+              {"X": R(2, C * H * W), "W": R(C, F * Hf * Hf), "b": R(F, 1)}, ["X", "W", "b"],
+              R(2, F * Ho * Ho), extra_fwd_out=", Hout, Wout")
+
+
+def test_upsample2d_and_fm():
+    gradcheck("upsample2d", "X, 2, 2, 3, 2, 2", "dX = L::backward(dout, 2, 2, 3, 2, 2)",
+              {"X": R(2, 12)}, ["X"], R(2, 48))
+    gradcheck("fm", "X, w0, W, V", "[dw0, dW, dV] = L::backward(dout, X, w0, W, V)",
+              {"X": R(5, 4), "w0": R(1, 1), "W": R(4, 1), "V": R(4, 2)}, ["w0", "W", "V"], R(5, 1))
+
+
+def test_depthwise():
+    C, H, W, M, Hf = 2, 4, 4, 2, 3
+    gradcheck("conv2d_depthwise", f"X, W, b, {H}, {W}, {M}, {Hf}, {Hf}, 1, 1, 1, 1",
+              f"[dX, dW, db] = L::backward(dout, Hout, Wout, X, W, b, {H}, {W}, {M}, {Hf}, {Hf}, 1, 1, 1, 1)",
+              {"X": R(2, C * H * W), "W": R(C, M * Hf * Hf), "b": R(C * M, 1)}, ["X", "W", "b"],
+              R(2, C * M * H * W), extra_fwd_out=", Hout, Wout")
+    gradcheck("conv2d_transpose_depthwise", f"X, W, b, 4, 3, 3, 2, 3, 3, 1, 1, 1, 1, 0, 0",
+              f"[dX, dW, db] = L::backward(dout, Hout, Wout, X, W, b, 4, 3, 3, 2, 3, 3, 1, 1, 1, 1)",
+              {"X": R(2, 4 * 9), "W": R(2, 2 * 9), "b": R(2, 1)}, ["X", "W", "b"],
+              R(2, 2 * 9), extra_fwd_out=", Hout, Wout")
+
+
+def test_lenet_example_trains_on_dummy_data():
+    src = '''
+source("nn/examples/mnist_lenet.dml") as lenet
+N = 128
+K = 10
+X = rand(rows = N, cols = 1 * 12 * 12, pdf = "normal", seed = 1)
+cls = rowIndexMax(X[, 1:K])
+Y = table(seq(1, N), cls, N, K)
+[W1, b1, W2, b2, W3, b3, W4, b4] = lenet::train(X, Y, X, Y, 1, 12, 12, 1)
+p = lenet::predict(X, 1, 12, 12, W1, b1, W2, b2, W3, b3, W4, b4)
+s = sum(p)
+'''
+    r = dml(src, {}, ["s"])
+    assert abs(r["s"] - 128) < 1e-6
