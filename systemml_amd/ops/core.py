@@ -526,6 +526,12 @@ def lix(x, y, rl, ru, cl, cu, list_mode=False):
         return ListObject(data, names)
     if is_dist(x) or is_dist(y):
         return _dist().lix(x, y, rl, ru, cl, cu)
+    if hasattr(x, "columns") and hasattr(x, "set_slice"):   # frame target
+        nr, nc = x.shape
+        r0, r1 = _bound(rl, 1), _bound(ru, nr)
+        c0, c1 = _bound(cl, 1), _bound(cu, nc)
+        _check_range(r0, r1, c0, c1, nr, nc)
+        return x.set_slice(r0 - 1, r1, c0 - 1, c1, y.cpu() if isinstance(y, Tensor) else y)
     if not isinstance(x, Tensor):
         raise DMLRuntimeError("left indexing requires a matrix target")
     nr, nc = x.shape

@@ -377,43 +377,43 @@ rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
 
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
+  // R = prefetch depth: each wave keeps R of its future rows in flight (packed, so a
+  // prefetched bf16 row costs 4*J VGPRs) while it processes one row; deeper rings put
+  // more bytes in flight per SIMD (Little's law at ~6 TB/s needs ~10 MB chip-wide).
   constexpr int STEP = WAVES * R;
 
-  Raw8<T> nxt[R][J];
-  int64_t r = r0 + wave;
+  // row-side operand (weights / targets / probabilities / g) for the same rows rides in
+  // the ring too, so its (wave-uniform) load latency is hidden behind R-1 rows of work
+  constexpr bool NEEDS = (MODE == XTWXV || MODE == XTXVY || MODE == XTPSXV || MODE == XTG);
+  constexpr int KS = NEEDS ? K : 1;
+  Raw8<T> ring[R][J];
+  float sring[R][KS];
+  auto load_s = [&](float (&dst)[KS], const int64_t rr) {
+    if constexpr (NEEDS) {
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int64_t ri = r + i * WAVES;
-    if (ri < r1) {
+      for (int k = 0; k < K; ++k) dst[k] = S[rr * (int64_t)lds + (((MODE == XTWXV || MODE == XTXVY) && sbc) ? 0 : k)];
+    }
+  };
+  int64_t base = r0 + wave;
 #pragma unroll
-      for (int j = 0; j < J; ++j) load_raw<T>(nxt[i][j], X + ri * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+  for (int p = 0; p < R; ++p) {
+    const int64_t rp = base + p * WAVES;
+    if (rp < r1) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) load_raw<T>(ring[p][j], X + rp * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+      load_s(sring[p], rp);
     }
   }
-  for (; r < r1; r += STEP) {
-    float x[R][C];
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-#pragma unroll
-      for (int j = 0; j < J; ++j) unpack<float>(nxt[i][j], x[i] + j * 8);
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const int64_t rn = r + STEP + i * WAVES;
-      if (rn < r1) {
-#pragma unroll
-        for (int j = 0; j < J; ++j) load_raw<T>(nxt[i][j], X + rn * (int64_t)D, (j * 64 + lane) * 8, D, vec);
-      }
-    }
-    bool valid[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) valid[i] = (r + i * WAVES) < r1;
 
-    f2 g[R][K2];
+  auto process = [&](const Raw8<T> (&cur)[J], const float (&sv)[KS], const int64_t r) {
+    float x[C];
+#pragma unroll
+    for (int j = 0; j < J; ++j) unpack<float>(cur[j], x + j * 8);
+    f2 g[K2];
     if constexpr (MI::needV) {
-      f2 u[R][K2];
+      f2 u[K2];
 #pragma unroll
-      for (int i = 0; i < R; ++i)
-#pragma unroll
-        for (int kk = 0; kk < K2; ++kk) u[i][kk] = f2{0.f, 0.f};
+      for (int kk = 0; kk < K2; ++kk) u[kk] = f2{0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < C; ++c) {
 #pragma unroll
@@ -422,70 +422,75 @@ rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
           if constexpr (VREG) {
             vv = vreg[c][kk];
           } else {
-            const float* p = sV + ((((c >> 3) * 64 + lane) * 8 + (c & 7)) * K + 2 * kk);
-            vv = f2{p[0], p[1]};
+            const float* pv = sV + ((((c >> 3) * 64 + lane) * 8 + (c & 7)) * K + 2 * kk);
+            vv = f2{pv[0], pv[1]};
           }
-#pragma unroll
-          for (int i = 0; i < R; ++i) u[i][kk] = __builtin_elementwise_fma(f2{x[i][c], x[i][c]}, vv, u[i][kk]);
+          u[kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, vv, u[kk]);
         }
       }
-      float us[R][K];
+      float us[K];
 #pragma unroll
-      for (int i = 0; i < R; ++i)
-#pragma unroll
-        for (int kk = 0; kk < K2; ++kk) {
-          us[i][2 * kk] = wave_sum(u[i][kk].x);
-          us[i][2 * kk + 1] = wave_sum(u[i][kk].y);
-        }
+      for (int kk = 0; kk < K2; ++kk) {
+        us[2 * kk] = wave_sum(u[kk].x);
+        us[2 * kk + 1] = wave_sum(u[kk].y);
+      }
       if constexpr (MODE == XV) {
 #pragma unroll
-        for (int i = 0; i < R; ++i)
-#pragma unroll
-          for (int k = 0; k < K; ++k)
-            if (valid[i] && lane == k) out[(r + i * WAVES) * (int64_t)ldo + k] = us[i][k];
-        continue;
+        for (int k = 0; k < K; ++k)
+          if (lane == k) out[r * (int64_t)ldo + k] = us[k];
+        return;
       } else {
+        float gs[K];
+        if constexpr (MODE == XTXV) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) {
-          const int64_t ri = r + i * WAVES;
-          const bool ok = valid[i];
-          float gs[K];
-          if constexpr (MODE == XTXV) {
+          for (int k = 0; k < K; ++k) gs[k] = us[k];
+        } else if constexpr (MODE == XTWXV) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) gs[k] = ok ? us[i][k] : 0.f;
-          } else if constexpr (MODE == XTWXV) {
+          for (int k = 0; k < K; ++k) gs[k] = sv[k] * us[k];
+        } else if constexpr (MODE == XTXVY) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) gs[k] = ok ? S[ri * (int64_t)lds + (sbc ? 0 : k)] * us[i][k] : 0.f;
-          } else if constexpr (MODE == XTXVY) {
+          for (int k = 0; k < K; ++k) gs[k] = us[k] - sv[k];
+        } else if constexpr (MODE == XTPSXV) {
+          float pr[K], q[K], sq = 0.f;
 #pragma unroll
-            for (int k = 0; k < K; ++k) gs[k] = ok ? us[i][k] - S[ri * (int64_t)lds + (sbc ? 0 : k)] : 0.f;
-          } else if constexpr (MODE == XTPSXV) {
-            float p[K], q[K], sq = 0.f;
+          for (int k = 0; k < K; ++k) { pr[k] = sv[k]; q[k] = pr[k] * us[k]; sq += q[k]; }
 #pragma unroll
-            for (int k = 0; k < K; ++k) { p[k] = ok ? S[ri * (int64_t)lds + k] : 0.f; q[k] = p[k] * us[i][k]; sq += q[k]; }
-#pragma unroll
-            for (int k = 0; k < K; ++k) gs[k] = q[k] - p[k] * sq;
-          }
-#pragma unroll
-          for (int kk = 0; kk < K2; ++kk) g[i][kk] = f2{gs[2 * kk], gs[2 * kk + 1]};
+          for (int k = 0; k < K; ++k) gs[k] = q[k] - pr[k] * sq;
         }
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk) g[kk] = f2{gs[2 * kk], gs[2 * kk + 1]};
       }
     } else {  // XTG
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const int64_t ri = r + i * WAVES;
-#pragma unroll
-        for (int kk = 0; kk < K2; ++kk)
-          g[i][kk] = valid[i] ? f2{S[ri * (int64_t)lds + 2 * kk], S[ri * (int64_t)lds + 2 * kk + 1]} : f2{0.f, 0.f};
-      }
+      for (int kk = 0; kk < K2; ++kk) g[kk] = f2{sv[2 * kk], sv[2 * kk + 1]};
     }
 #pragma unroll
-    for (int i = 0; i < R; ++i)
+    for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int c = 0; c < C; ++c)
+      for (int kk = 0; kk < K2; ++kk)
+        acc[c][kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, g[kk], acc[c][kk]);
+  };
+
+  for (; base < r1; base += STEP) {
 #pragma unroll
-        for (int kk = 0; kk < K2; ++kk)
-          acc[c][kk] = __builtin_elementwise_fma(f2{x[i][c], x[i][c]}, g[i][kk], acc[c][kk]);
+    for (int p = 0; p < R; ++p) {
+      const int64_t r = base + p * WAVES;   // wave-uniform
+      if (r < r1) {
+        Raw8<T> cur[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) cur[j] = ring[p][j];
+        float sv[KS];
+#pragma unroll
+        for (int k = 0; k < KS; ++k) sv[k] = sring[p][k];
+        const int64_t rn = r + STEP;
+        if (rn < r1) {
+#pragma unroll
+          for (int j = 0; j < J; ++j) load_raw<T>(ring[p][j], X + rn * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+          load_s(sring[p], rn);
+        }
+        process(cur, sv, r);
+      }
+    }
   }
 
   if constexpr (MI::accum) {
@@ -519,7 +524,13 @@ rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
 // ---------------------------------------------------------------------------
 using namespace sysml;
 
-static int g_rows_per_iter = 0;   // 0 = auto, else 1 / 2 (A/B tuning knob)
+static int g_rows_per_iter = 0;   // 0 = auto, else rows per iteration (generic) / prefetch depth (pk)
+#ifndef PF_DEFAULT_BF16
+#define PF_DEFAULT_BF16 3
+#endif
+#ifndef PF_DEFAULT_F32
+#define PF_DEFAULT_F32 2
+#endif
 static int g_variant = 0;         // 0 = auto (packed fp32 where applicable), 1 = generic scalar kernel
 
 template <typename T, typename A, int K, int J, int MODE>
@@ -538,16 +549,18 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
                                                                MODE == ROWSUM || (K == 1 && MI::accum)));
   if constexpr (sizeof(A) == 4 && K >= 2 && MODE <= XTPSXV) {
     if (g_variant != 1) {   // packed-fp32 kernel (default)
-      const bool two_pk = (g_rows_per_iter == 2) || (g_rows_per_iter == 0 && (MODE == XV || K == 2));
-      if (two_pk && K <= 4) {
-        hipLaunchKernelGGL((rowstream_pk_kernel<T, K, J, MODE, 2>), dim3(grid), dim3(BLOCK), sh, st,
-                           (const T*)X, N, D, vec, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out,
-                           ldo, rpb);
-      } else {
-        hipLaunchKernelGGL((rowstream_pk_kernel<T, K, J, MODE, 1>), dim3(grid), dim3(BLOCK), sh, st,
-                           (const T*)X, N, D, vec, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out,
-                           ldo, rpb);
+      // prefetch-ring depth: knob 1..4, else tuned default (bf16 rows are half the bytes,
+      // so they need twice the rows in flight for the same HBM occupancy)
+      int depth = g_rows_per_iter ? g_rows_per_iter : (sizeof(T) == 2 ? PF_DEFAULT_BF16 : PF_DEFAULT_F32);
+#define SYSML_PK(PF) hipLaunchKernelGGL((rowstream_pk_kernel<T, K, J, MODE, PF>), dim3(grid), dim3(BLOCK), sh, st, \
+          (const T*)X, N, D, vec, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, ldo, rpb)
+      switch (depth) {
+        case 1: SYSML_PK(1); break;
+        case 2: SYSML_PK(2); break;
+        case 3: SYSML_PK(3); break;
+        default: SYSML_PK(4); break;
       }
+#undef SYSML_PK
       return hipGetLastError() == hipSuccess ? 0 : -2;
     }
   }

@@ -351,12 +351,7 @@ def b_cbind(ctx, *args, **kw):
                 out.names.append("")
         return out
     if isinstance(args[0], FrameBlock):
-        cols, schema, names = [], [], []
-        for a in args:
-            cols += a.columns
-            schema += a.schema
-            names += a.names
-        return FrameBlock(cols, schema, names)
+        return FrameBlock.cbind([a if isinstance(a, FrameBlock) else C.unary("cast_frame", a) for a in args])
     ms = [_mat(a) for a in args]
     r = ms[0].shape[0]
     for m in ms[1:]:

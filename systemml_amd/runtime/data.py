@@ -46,12 +46,15 @@ class ListObject:
 class FrameBlock:
     """Column-oriented heterogeneous frame (schema per column)."""
 
-    def __init__(self, columns, schema=None, names=None):
+    def __init__(self, columns, schema=None, names=None, col_meta=None):
         # columns: list of python lists
         self.columns = [list(c) for c in columns]
         n = len(self.columns)
         self.schema = list(schema) if schema else ["STRING"] * n
         self.names = list(names) if names else [f"C{i + 1}" for i in range(n)]
+        # per-column transform metadata (reference: FrameBlock.ColumnMetadata:
+        # number of distinct values / bins and the missing-value replacement)
+        self.col_meta = [dict(m) for m in col_meta] if col_meta else [{} for _ in range(n)]
 
     @property
     def shape(self):
@@ -90,7 +93,32 @@ class FrameBlock:
 
     def slice(self, rl, ru, cl, cu):
         cols = [c[rl:ru] for c in self.columns[cl:cu]]
-        return FrameBlock(cols, self.schema[cl:cu], self.names[cl:cu])
+        return FrameBlock(cols, self.schema[cl:cu], self.names[cl:cu], self.col_meta[cl:cu])
+
+    def set_slice(self, rl, ru, cl, cu, src):
+        """Left indexing: rows [rl,ru) x cols [cl,cu) <- src (frame, matrix or scalar)."""
+        out = FrameBlock(self.columns, self.schema, self.names, self.col_meta)
+        for j in range(cl, cu):
+            col = out.columns[j]
+            for i in range(rl, ru):
+                if isinstance(src, FrameBlock):
+                    v = src.columns[j - cl][i - rl]
+                elif isinstance(src, torch.Tensor):
+                    v = float(src[i - rl, j - cl])
+                else:
+                    v = src
+                col[i] = v
+        return out
+
+    @staticmethod
+    def cbind(frames):
+        cols, schema, names, meta = [], [], [], []
+        for f in frames:
+            cols += f.columns
+            schema += f.schema
+            names += f.names
+            meta += f.col_meta
+        return FrameBlock(cols, schema, names, meta)
 
     def __repr__(self):
         return f"FrameBlock{self.shape}"

@@ -55,8 +55,8 @@ def main():
         L.sysml_set_variant.argtypes = [ctypes.c_int]
         for rep in range(a.reps + 1):
             for name, fn in cases.items():
-                for R in ((1, 2, 11, 12) if not name.startswith("torch") else (0,)):
-                    # R = rows per wave iteration; 11/12 = generic scalar kernel (variant 1)
+                for R in ((1, 2, 3, 4, 11) if not name.startswith("torch") else (0,)):
+                    # R = prefetch depth (pk kernel) / rows per iteration (generic); 11 = generic kernel
                     L.sysml_set_variant(1 if R > 10 else 0)
                     L.sysml_set_rows_per_iter(R % 10)
                     torch.cuda.synchronize()
