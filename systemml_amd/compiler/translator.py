@@ -615,6 +615,9 @@ class _BBuilder:
             # dynamic function call: resolve at runtime in this file context
             return self._eval_call(pos_args, named, pos)
         dt = _BI_DT.get(name, "U")
+        if name in _DIST_FNS:
+            tgt = nd.get("target", pos_args[0] if pos_args else None)
+            dt = "M" if tgt is not None and tgt.dt == "M" else ("U" if tgt is None or tgt.dt == "U" else "S")
         if name == "read":
             dtn = nd.get("data_type")
             if dtn is not None and dtn.op == "lit":
@@ -644,6 +647,7 @@ _M_BUILTINS = ("matrix rand seq sample cbind rbind table ctable diag rev removeE
                "avg_pool_backward bias_add bias_multiply transformapply transformcolmap").split()
 _S_BUILTINS = "toString median interQuartileMean moment centralMoment cov cdf invcdf pnorm qnorm pt qt pf qf " \
               "pchisq qchisq pexp qexp exists time".split()
+_DIST_FNS = set("cdf invcdf icdf pnorm qnorm pt qt pf qf pchisq qchisq pexp qexp".split())
 _BI_DT = {**{n: "M" for n in _M_BUILTINS}, **{n: "S" for n in _S_BUILTINS}, "list": "L",
           "transformdecode": "F", "transformmeta": "F"}
 

@@ -39,18 +39,24 @@ def build_hip(force=False, verbose=True):
     out = os.path.join(LIB, "libsysml_hip.so")
     if not force and not _stale(out, srcs + glob.glob(os.path.join(HERE, "hip", "*.h"))):
         return out
-    objs = []
+    objs, cmds = [], []
+    hdrs = glob.glob(os.path.join(HERE, "hip", "*.h"))
     for s in srcs:
         o = os.path.join(LIB, os.path.basename(s) + ".o")
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-c", s, "-o", o]
+        if force or _stale(o, [s] + hdrs):   # objects are kept: only edited units recompile
+            cmds.append([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-c", s, "-o", o])
+        objs.append(o)
+    # one hipcc per translation unit, in parallel (rowstream.hip alone is ~2 min)
+    procs = []
+    for cmd in cmds:
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.check_call(cmd)
-        objs.append(o)
+        procs.append(subprocess.Popen(cmd))
+    bad = [c for c, p in zip(cmds, procs) if p.wait() != 0]
+    if bad:
+        raise subprocess.CalledProcessError(1, bad[0])
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs
     subprocess.check_call(cmd)
-    for o in objs:
-        os.remove(o)
     return out
 
 

@@ -58,8 +58,78 @@ def load(required=False):
                                   ctypes.c_void_p]
     L.sysml_set_rows_per_iter.argtypes = [ctypes.c_int]
     L.sysml_set_rows_per_iter.restype = None
+    L.sysml_mchain.restype = ctypes.c_int
+    L.sysml_mchain.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                               ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.sysml_mchain_occupancy.restype = ctypes.c_int
+    L.sysml_mchain_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
     _lib = L
     return L
+
+
+# ----------------------------------------------------------------------------
+# MFMA chain kernels (ops/hip/mfma_chain.hip): bf16 X, D % 8 == 0, D <= 1024, K <= 4.
+# SYSML_MFMA=0 routes everything to the VALU row-streaming kernels (A/B switch).
+# ----------------------------------------------------------------------------
+MFMA = os.environ.get("SYSML_MFMA", "1") != "0"
+_occ = {}
+
+
+def _mfma_ok(X, kp):
+    return (MFMA and X.dtype == torch.bfloat16 and kp <= 4 and X.shape[1] % 8 == 0 and
+            X.shape[1] <= 1024 and X.is_contiguous() and X.data_ptr() % 16 == 0)
+
+
+def _mgrid(L, mode, X):
+    key = (mode, X.shape[1], X.device.index)
+    if key not in _occ:
+        occ = L.sysml_mchain_occupancy(mode, X.shape[1])
+        cus = torch.cuda.get_device_properties(X.device).multi_processor_count
+        _occ[key] = max(1, occ) * cus if occ > 0 else -1
+    ntiles = (X.shape[0] + 15) // 16
+    return min(_occ[key], ntiles)
+
+
+def _v3t(V, kp, D):
+    """V (D x K) -> [16][Dp] bf16: rows 4s+k hold rounding plane s (hi, lo, lo2) of V[:, k]."""
+    Dp = 256 * ((D + 255) // 256)
+    v = V.to(torch.float32)
+    planes = []
+    for _ in range(3):
+        h = v.to(torch.bfloat16)
+        planes.append(h)
+        v = v - h.to(torch.float32)
+    out = torch.zeros((16, Dp), dtype=torch.bfloat16, device=V.device)
+    for s_, h in enumerate(planes):
+        out[4 * s_:4 * s_ + V.shape[1], :D] = h.t()
+    return out
+
+
+def _mchain(mode, X, kp, V=None, S=None, sbc=0):
+    L = load(required=True)
+    N, D = X.shape
+    grid = _mgrid(L, mode, X)
+    if grid <= 0:
+        return None
+    V3 = _v3t(V, kp, D) if V is not None else None
+    if S is not None:
+        S = S.to(torch.float32).contiguous()
+    if mode == XV:
+        out = torch.empty((N, kp), dtype=torch.float32, device=X.device)
+        ldo = kp
+    else:
+        out = torch.empty((grid, D * kp), dtype=torch.float32, device=X.device)
+        ldo = 0
+    rc = L.sysml_mchain(mode, ctypes.c_void_p(X.data_ptr()), N, D,
+                        ctypes.c_void_p(V3.data_ptr() if V3 is not None else 0),
+                        ctypes.c_void_p(S.data_ptr() if S is not None else 0), S.shape[1] if S is not None else 0,
+                        sbc, kp, ctypes.c_void_p(out.data_ptr()), ldo, grid, _stream())
+    if rc != 0:
+        return None
+    if mode == XV:
+        return out
+    return out.sum(0).reshape(D, kp)
 
 
 def _xcode(x):
@@ -127,6 +197,11 @@ def xv(X, V):
     K = V.shape[1]
     kp = _kpad(K)
     code, adt = _xcode(X)
+    if _mfma_ok(X, kp):
+        U = _mchain(XV, X, kp, V=V)
+        if U is not None:
+            _count("mfma.xv")
+            return _result(U if kp == K else U[:, :K].contiguous())
     Vp = _pad_cols(V, kp, adt).contiguous()
     U = torch.empty((X.shape[0], kp), dtype=adt, device=X.device)
     rc, _ = _launch(XV, X, V=Vp, K=kp, out=U, ldo=kp)
@@ -142,6 +217,11 @@ def xtg(X, G):
     kp = _kpad(K)
     code, adt = _xcode(X)
     Gp = _pad_cols(G, kp, adt).contiguous()
+    if _mfma_ok(X, kp):
+        R = _mchain(XTG, X, kp, S=Gp)
+        if R is not None:
+            _count("mfma.xtg")
+            return _result(R if kp == K else R[:, :K].contiguous())
     grid = _grid(X.shape[0])
     part = torch.empty((grid, X.shape[1] * kp), dtype=adt, device=X.device)
     rc, g = _launch(XTG, X, S=Gp, K=kp, out=part, grid=grid)
@@ -170,6 +250,11 @@ def mmchain(ctype, X, V, W=None):
             S = _pad_cols(W, kp, adt).contiguous()
         else:
             return None
+    if _mfma_ok(X, kp):
+        R = _mchain(mode, X, kp, V=V, S=S, sbc=sbc)
+        if R is not None:
+            _count("mfma.mmchain." + ctype)
+            return _result(R if kp == K else R[:, :K].contiguous())
     grid = _grid(X.shape[0])
     part = torch.empty((grid, X.shape[1] * kp), dtype=adt, device=X.device)
     rc, g = _launch(mode, X, V=Vp, S=S, sbc=sbc, K=kp, out=part, grid=grid)

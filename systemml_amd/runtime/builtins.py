@@ -714,6 +714,19 @@ def _dist_fn(dist, q=None, p=None, lower=True, **prm):
         d = st.t(_float(prm["df"]))
     else:
         raise DMLRuntimeError(f"unsupported distribution '{dist}'")
+    x = q if q is not None else p
+    if isinstance(x, torch.Tensor):
+        # element-wise over a matrix (extension over the reference's scalar-only cdf):
+        # the normal family stays on the device via torch.special, others go through scipy
+        if dist == "normal":
+            mu, sd = _float(prm.get("mean", 0.0)), _float(prm.get("sd", 1.0))
+            if q is not None:
+                z = (x - mu) / sd
+                return torch.special.ndtr(z if lower else -z)
+            return torch.special.ndtri(x) * sd + mu
+        xn = x.detach().double().cpu().numpy()
+        r = (d.cdf(xn) if lower else d.sf(xn)) if q is not None else d.ppf(xn)
+        return torch.from_numpy(r).to(device=x.device, dtype=x.dtype)
     if q is not None:
         v = _float(q)
         return float(d.cdf(v) if lower else d.sf(v))

@@ -113,3 +113,102 @@ def test_pca_eigenvalues():
     r, _ = algo("PCA", dict(INPUT="A", K=2, CENTER=1, OUTPUT="/tmp/_pca_test", PROJDATA=0), {"A": A}, ["lam"])
     w = np.sort(np.linalg.eigvalsh(np.cov(A.T)))[::-1]
     np.testing.assert_allclose(r["lam"].ravel(), w[:2], rtol=1e-10)
+
+
+# ---------------------------------------------------------------------------
+# GLM (reference: test/integration/applications/GLMTest compares against R's glm();
+# here against a direct scipy minimisation of the same penalised deviance)
+# ---------------------------------------------------------------------------
+def _glm_data(kind, n=1500, m=4, seed=11):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, m))
+    beta = rng.standard_normal((m, 1)) * 0.3
+    eta = X @ beta + 0.5
+    if kind == "gauss":
+        y = eta + 0.1 * rng.standard_normal((n, 1))
+    elif kind == "poisson":
+        y = rng.poisson(np.exp(eta)).astype(float)
+    elif kind == "gamma":
+        y = rng.gamma(2.0, np.exp(eta) / 2.0)
+    else:
+        y = (rng.random((n, 1)) < 1 / (1 + np.exp(-eta))).astype(float)
+    return X, y
+
+
+def _glm_objective(kind, link, X, y, reg):
+    from scipy.special import ndtr
+    Xi = np.hstack([X, np.ones((X.shape[0], 1))])
+    yv = y.ravel()
+
+    def f(b):
+        eta = Xi @ b
+        if link == "log":
+            mu = np.exp(eta)
+        elif link == "id":
+            mu = eta
+        elif link == "logit":
+            mu = 1 / (1 + np.exp(-eta))
+        else:
+            mu = ndtr(eta)
+        if kind == "gauss":
+            dev = np.sum((yv - mu) ** 2)
+        elif kind == "poisson":
+            dev = 2 * np.sum(np.where(yv > 0, yv * np.log(np.where(yv > 0, yv, 1) / mu), 0) - (yv - mu))
+        elif kind == "gamma":
+            dev = 2 * np.sum(-np.log(yv / mu) + (yv - mu) / mu)
+        else:
+            mu = np.clip(mu, 1e-300, 1 - 1e-16)
+            dev = -2 * np.sum(yv * np.log(mu) + (1 - yv) * np.log(1 - mu))
+        return 0.5 * dev + 0.5 * reg * np.sum(b[:-1] ** 2)
+    return f
+
+
+@pytest.mark.parametrize("kind,args,link", [
+    ("gauss", dict(dfam=1, vpow=0.0), "id"),
+    ("poisson", dict(dfam=1, vpow=1.0), "log"),
+    ("gamma", dict(dfam=1, vpow=2.0, link=1, lpow=0.0), "log"),
+    ("binom", dict(dfam=2, link=2), "logit"),
+    ("binom", dict(dfam=2, link=3), "probit"),
+])
+def test_glm_matches_direct_minimisation(kind, args, link):
+    from scipy.optimize import minimize
+    X, y = _glm_data(kind)
+    reg = 0.5
+    r, out = algo("GLM", dict(X="X", Y="Y", B="B", icpt=1, reg=reg, tol=1e-12, moi=200, **args),
+                  {"X": X, "Y": y}, ["B"])
+    b = r["B"].ravel()
+    f = _glm_objective(kind, link, X, y, reg)
+    ref = minimize(f, np.zeros(X.shape[1] + 1), method="BFGS", options=dict(gtol=1e-9, maxiter=10000))
+    assert f(b) <= ref.fun * (1 + 1e-9) + 1e-9
+    np.testing.assert_allclose(b, ref.x, atol=2e-4)
+    assert "TERMINATION_CODE,1" in "\n".join(out)
+
+
+def test_glm_standardized_intercept_and_binomial_counts():
+    X, y = _glm_data("binom", seed=3)
+    r1, _ = algo("GLM", dict(X="X", Y="Y", B="B", icpt=1, dfam=2, link=2, tol=1e-12), {"X": X, "Y": y}, ["B"])
+    r2, _ = algo("GLM", dict(X="X", Y="Y", B="B", icpt=2, dfam=2, link=2, tol=1e-12), {"X": X, "Y": y}, ["B"])
+    assert r2["B"].shape == (X.shape[1] + 1, 2)
+    np.testing.assert_allclose(r2["B"][:, 0], r1["B"].ravel(), atol=1e-6)
+    # the same data as (#pos, #neg) counts, with yneg=-1 labels for the one-column form
+    Y2 = np.hstack([y, 1 - y])
+    r3, _ = algo("GLM", dict(X="X", Y="Y", B="B", icpt=1, dfam=2, link=2, tol=1e-12), {"X": X, "Y": Y2}, ["B"])
+    np.testing.assert_allclose(r3["B"], r1["B"], atol=1e-6)
+    r4, _ = algo("GLM", dict(X="X", Y="Y", B="B", icpt=1, dfam=2, link=2, yneg=-1.0, tol=1e-12),
+                 {"X": X, "Y": 2 * y - 1}, ["B"])
+    np.testing.assert_allclose(r4["B"], r1["B"], atol=1e-6)
+
+
+def test_glm_predict_means_and_r2():
+    X, y = _glm_data("poisson", seed=5)
+    r, _ = algo("GLM", dict(X="X", Y="Y", B="B", icpt=1, dfam=1, vpow=1.0, tol=1e-12), {"X": X, "Y": y}, ["B"])
+    B = r["B"]
+    p, out = algo("GLM-predict", dict(X="X", B="B", M="M", Y="Y", dfam=1, vpow=1.0, link=1, lpow=0.0),
+                  {"X": X, "B": B, "Y": y}, ["M"])
+    mu = np.exp(X @ B[:-1] + B[-1])
+    np.testing.assert_allclose(p["M"], mu, rtol=1e-12)
+    stats = dict((l.split(",")[0] + l.split(",")[1], float(l.split(",")[-1]))
+                 for l in "\n".join(out).split("\n") if l.count(",") == 3)
+    r2 = 1 - np.sum((y - mu) ** 2) / np.sum((y - y.mean()) ** 2)
+    np.testing.assert_allclose(stats["R21"], r2, rtol=1e-10)
+    np.testing.assert_allclose(stats["PEARSON_X2"], np.sum((y - mu) ** 2 / mu), rtol=1e-10)

@@ -94,8 +94,80 @@ def test_dml_uses_fused_kernels(gpu_config):
     from systemml_amd.ops import kernels
     X = np.random.rand(10000, 50)
     w = np.random.rand(50, 1)
-    before = kernels.counters.get("rowstream.mmchain.XtXv", 0)
+    cnt = lambda: sum(v for k, v in kernels.counters.items() if k.endswith("mmchain.XtXv"))
+    before = cnt()
     res = run("q = t(X) %*% (X %*% w)", inputs={"X": X, "w": w}, outputs=["q"], config=gpu_config)
-    after = kernels.counters.get("rowstream.mmchain.XtXv", 0)
+    after = cnt()
     assert after == before + 1
     np.testing.assert_allclose(res["q"].cpu().double().numpy(), X.T @ (X @ w), rtol=1e-4)
+
+
+# ---------------------------------------------------------------------------
+# MFMA chain kernels (ops/hip/mfma_chain.hip): exact small-integer data first (catches any
+# operand/accumulator layout slip, which would show up as a wrong element, not rounding),
+# then random data against an fp64 reference.
+# ---------------------------------------------------------------------------
+def _ints(shape, lo, hi, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return torch.randint(lo, hi + 1, shape, generator=g, device="cuda").to(torch.float64)
+
+
+@pytest.mark.parametrize("n", [1, 15, 17, 4099])
+@pytest.mark.parametrize("d", [8, 136, 256, 264, 1000])
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+def test_mfma_exact_integer_layout(K, n, d, k):
+    x = _ints((n, d), -3, 3, 10 + d).to(torch.bfloat16)
+    x64 = x.double()
+    v = _ints((d, k), -2, 2, 20 + k)
+    g = _ints((n, k), -2, 2, 30 + n)
+    c0 = dict(K.counters)
+    u = K.xv(x, v)
+    torch.testing.assert_close(u.double(), x64 @ v, rtol=0, atol=0)
+    r = K.xtg(x, g)
+    torch.testing.assert_close(r.double(), x64.t() @ g, rtol=0, atol=0)
+    r2 = K.mmchain("XtXv", x, v)
+    torch.testing.assert_close(r2.double(), x64.t() @ (x64 @ v), rtol=0, atol=0)
+    r3 = K.mmchain("XtXvy", x, v, g)
+    torch.testing.assert_close(r3.double(), x64.t() @ (x64 @ v - g), rtol=0, atol=0)
+    assert K.counters.get("mfma.xv", 0) > c0.get("mfma.xv", 0)
+    assert K.counters.get("mfma.xtg", 0) > c0.get("mfma.xtg", 0)
+    assert K.counters.get("mfma.mmchain.XtXv", 0) > c0.get("mfma.mmchain.XtXv", 0)
+
+
+@pytest.mark.parametrize("ctype", ["XtXv", "XtwXv", "XtXvy", "XtPSXv"])
+@pytest.mark.parametrize("k", [1, 2, 4])
+def test_mfma_matches_rowstream(K, ctype, k):
+    n, d = 50001, 1000
+    x = _mk(n, d, torch.bfloat16, seed=7)
+    x64 = x.double()
+    v = torch.randn((d, k), device="cuda", dtype=torch.float64)
+    w = None
+    if ctype == "XtwXv":
+        w = torch.rand((n, 1), device="cuda", dtype=torch.float64)
+    elif ctype == "XtXvy":
+        w = torch.randn((n, k), device="cuda", dtype=torch.float64)
+    elif ctype == "XtPSXv":
+        w = torch.softmax(torch.randn((n, k + 1), device="cuda", dtype=torch.float64), 1)[:, :k].contiguous()
+    u = x64 @ v
+    if ctype == "XtXv":
+        g = u
+    elif ctype == "XtwXv":
+        g = w * u
+    elif ctype == "XtXvy":
+        g = u - w
+    else:
+        q = w * u
+        g = q - w * q.sum(1, keepdim=True)
+    ref = x64.t() @ g
+    assert K._mfma_ok(x, k)
+    r_m = K.mmchain(ctype, x, v, w)
+    K.MFMA = False
+    try:
+        r_v = K.mmchain(ctype, x, v, w)
+    finally:
+        K.MFMA = True
+    scale = ref.abs().max().item()
+    err_m = (r_m.double() - ref).abs().max().item() / scale
+    err_v = (r_v.double() - ref).abs().max().item() / scale
+    # the split-bf16 MFMA path must be as accurate as the fp32 VALU path
+    assert err_m < max(2e-5, 2 * err_v), (err_m, err_v)

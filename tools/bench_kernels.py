@@ -46,6 +46,7 @@ def main():
             "xtg_k4": lambda: K.xtg(X, g4),
             "XtXv_k1": lambda: K.mmchain("XtXv", X, v1),
             "XtPSXv_k4": lambda: K.mmchain("XtPSXv", X, v4, P),
+            "XtXv_k4": lambda: K.mmchain("XtXv", X, v4),
             "rowsumsq": lambda: K.sumsq(X, "row"),
         }
         if dt == torch.float32:
@@ -55,10 +56,14 @@ def main():
         L.sysml_set_variant.argtypes = [ctypes.c_int]
         for rep in range(a.reps + 1):
             for name, fn in cases.items():
-                for R in ((1, 2, 3, 4, 11) if not name.startswith("torch") else (0,)):
-                    # R = prefetch depth (pk kernel) / rows per iteration (generic); 11 = generic kernel
-                    L.sysml_set_variant(1 if R > 10 else 0)
-                    L.sysml_set_rows_per_iter(R % 10)
+                variants = (0,) if name.startswith("torch") else (2, 3, 4, 11, 99) if dt == torch.bfloat16 \
+                    else (1, 2, 11)
+                for R in variants:
+                    # R = prefetch depth (pk kernel) / rows per iteration (generic); 11 = generic
+                    # kernel; 99 = MFMA chain kernel (bf16 only)
+                    K.MFMA = (R == 99)
+                    L.sysml_set_variant(1 if 10 < R < 99 else 0)
+                    L.sysml_set_rows_per_iter(R % 10 if R < 99 else 0)
                     torch.cuda.synchronize()
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
@@ -69,6 +74,7 @@ def main():
                     if rep > 0:
                         times.setdefault(f"{name}/R{R}", []).append(e0.elapsed_time(e1))
         L.sysml_set_rows_per_iter(0)
+        K.MFMA = True
         for k, ts in times.items():
             med = statistics.median(ts)
             results[f"{str(dt).split('.')[-1]}/{k}"] = {"ms": round(med, 3), "min_ms": round(min(ts), 3),
