@@ -32,6 +32,11 @@ def _files(fname):
     return [fname]
 
 
+def read_matrix(fname, **kw):
+    """Read a matrix file (any supported format, .mtd honoured) into a CPU fp64 tensor."""
+    return torch.as_tensor(read(None, fname, **kw)).double().cpu()
+
+
 def read(ctx, fname, **kw):
     md = M.read_mtd(fname) or {}
     fmt = kw.get("format", md.get("format", None))

@@ -212,3 +212,58 @@ def test_glm_predict_means_and_r2():
     r2 = 1 - np.sum((y - mu) ** 2) / np.sum((y - y.mean()) ** 2)
     np.testing.assert_allclose(stats["R21"], r2, rtol=1e-10)
     np.testing.assert_allclose(stats["PEARSON_X2"], np.sum((y - mu) ** 2 / mu), rtol=1e-10)
+
+
+def test_univar_stats():
+    rng = np.random.default_rng(8)
+    n = 501
+    X = np.hstack([rng.gamma(2.0, 1.5, (n, 1)), rng.integers(1, 5, (n, 1)).astype(float),
+                   rng.standard_normal((n, 1)) * 3 + 1, rng.integers(1, 3, (n, 1)).astype(float)])
+    types = np.array([[1, 2, 1, 3]], dtype=float)
+    r, _ = algo("Univar-Stats", dict(X="X", TYPES="T", STATS="/tmp/_univar_stats"), {"X": X, "K": types}, ["S"])
+    S = r["S"]
+    for j in (0, 2):
+        x = X[:, j]
+        mu, sd = x.mean(), x.std(ddof=1)
+        m2, m3, m4 = [np.mean((x - mu) ** k) for k in (2, 3, 4)]
+        exp = [x.min(), x.max(), np.ptp(x), mu, sd ** 2, sd, sd / np.sqrt(n), sd / mu, m3 / sd ** 3, m4 / sd ** 4 - 3]
+        np.testing.assert_allclose(S[:10, j], exp, rtol=1e-10)
+        np.testing.assert_allclose(S[12, j], np.median(x), rtol=1e-12)
+        xs = np.sort(x)   # inter-quartile mean of the middle half
+        assert np.quantile(x, 0.25) <= S[13, j] <= np.quantile(x, 0.75)
+    for j in (1, 3):
+        cnt = np.bincount(X[:, j].astype(int))[1:]
+        assert S[14, j] == len(cnt) and S[15, j] == np.argmax(cnt) + 1 and S[16, j] == np.sum(cnt == cnt.max())
+        assert np.all(S[:12, j] == 0)
+
+
+def test_bivar_stats(tmp_path):
+    from scipy import stats as st
+    from systemml_amd.io.readers import read_matrix
+    rng = np.random.default_rng(9)
+    n = 400
+    s1 = rng.standard_normal(n)
+    s2 = 0.6 * s1 + rng.standard_normal(n)
+    c1 = rng.integers(1, 4, n).astype(float)
+    o1 = np.clip(np.round(s1 + 2.5), 1, 5)
+    o2 = np.clip(np.round(s2 + 2.5), 1, 5)
+    X = np.column_stack([s1, s2, c1, o1, o2])
+    idx1, idx2 = np.array([[1, 3, 4]]), np.array([[2, 5]])
+    t1, t2 = np.array([[1, 2, 3]]), np.array([[1, 3]])
+    algo("bivar-stats", dict(X="X", index1="i1", index2="i2", types1="t1", types2="t2", OUTDIR=str(tmp_path)),
+         {"D": X, "S1": idx1, "S2": idx2, "K1": t1, "K2": t2}, [])
+    ss = read_matrix(str(tmp_path / "bivar.scale.scale.stats")).numpy()
+    r, _ = st.pearsonr(s1, s2)
+    np.testing.assert_allclose(ss[:, 0], [1, 2, r, np.cov(s1, s2)[0, 1], s1.std(ddof=1), s2.std(ddof=1)], rtol=1e-10)
+    nn = read_matrix(str(tmp_path / "bivar.nominal.nominal.stats")).numpy()
+    for col, (a, b) in enumerate([(c1, o2), (o1, o2)]):
+        tab = np.array([[np.sum((a == u) & (b == v)) for v in np.unique(b)] for u in np.unique(a)])
+        chi2, p, dof, _ = st.chi2_contingency(tab, correction=False)
+        np.testing.assert_allclose(nn[2:5, col], [chi2, dof, p], rtol=1e-8)
+    oo = read_matrix(str(tmp_path / "bivar.ordinal.ordinal.stats")).numpy()
+    np.testing.assert_allclose(oo[2, 0], st.spearmanr(o1, o2)[0], rtol=1e-10)
+    ns = read_matrix(str(tmp_path / "bivar.nominal.scale.stats")).numpy()
+    # scale column s1 against nominal c1 (ordinal o1 vs scale s2 handled the same way)
+    f, p = st.f_oneway(*[s2[c1 == u] for u in np.unique(c1)])
+    k = [i for i in range(ns.shape[1]) if ns[0, i] == 3 and ns[1, i] == 2][0]
+    np.testing.assert_allclose(ns[3:5, k], [f, p], rtol=1e-8)
