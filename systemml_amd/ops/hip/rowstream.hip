@@ -526,10 +526,10 @@ using namespace sysml;
 
 static int g_rows_per_iter = 0;   // 0 = auto, else rows per iteration (generic) / prefetch depth (pk)
 #ifndef PF_DEFAULT_BF16
-#define PF_DEFAULT_BF16 3
+#define PF_DEFAULT_BF16 4
 #endif
 #ifndef PF_DEFAULT_F32
-#define PF_DEFAULT_F32 2
+#define PF_DEFAULT_F32 1
 #endif
 static int g_variant = 0;         // 0 = auto (packed fp32 where applicable), 1 = generic scalar kernel
 
@@ -551,7 +551,11 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
     if (g_variant != 1) {   // packed-fp32 kernel (default)
       // prefetch-ring depth: knob 1..4, else tuned default (bf16 rows are half the bytes,
       // so they need twice the rows in flight for the same HBM occupancy)
-      int depth = g_rows_per_iter ? g_rows_per_iter : (sizeof(T) == 2 ? PF_DEFAULT_BF16 : PF_DEFAULT_F32);
+      // measured (profiles/rowstream_kbench_r1_prefetch.txt): bf16 chains like 4 rows in
+      // flight per wave, bf16 XV / XTG 3; fp32 rows are twice the bytes, 1 suffices
+      int depth = g_rows_per_iter ? g_rows_per_iter
+                                  : (sizeof(T) == 2 ? ((MODE == XV || MODE == XTG) ? 3 : PF_DEFAULT_BF16)
+                                                    : PF_DEFAULT_F32);
 #define SYSML_PK(PF) hipLaunchKernelGGL((rowstream_pk_kernel<T, K, J, MODE, PF>), dim3(grid), dim3(BLOCK), sh, st, \
           (const T*)X, N, D, vec, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, ldo, rpb)
       switch (depth) {

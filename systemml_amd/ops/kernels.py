@@ -73,12 +73,21 @@ def load(required=False):
 # SYSML_MFMA=0 routes everything to the VALU row-streaming kernels (A/B switch).
 # ----------------------------------------------------------------------------
 MFMA = os.environ.get("SYSML_MFMA", "1") != "0"
+MFMA_ALL = os.environ.get("SYSML_MFMA", "1") == "all"
 _occ = {}
 
 
-def _mfma_ok(X, kp):
-    return (MFMA and X.dtype == torch.bfloat16 and kp <= 4 and X.shape[1] % 8 == 0 and
-            X.shape[1] <= 1024 and X.is_contiguous() and X.data_ptr() % 16 == 0)
+def _mfma_ok(X, kp, mode=None):
+    """MFMA path eligibility.  By measurement (profiles/mfma_chain_experiments.md) the
+    matrix-core kernel wins for X %*% v with 1-2 columns and for t(X) %*% G; for the fused
+    chains the prefetching VALU row-stream kernel is faster, so they stay there unless
+    SYSML_MFMA=all."""
+    if not (MFMA and X.dtype == torch.bfloat16 and kp <= 4 and X.shape[1] % 8 == 0 and
+            X.shape[1] <= 1024 and X.is_contiguous() and X.data_ptr() % 16 == 0):
+        return False
+    if mode is None or MFMA_ALL:
+        return True
+    return mode == XTG or (mode == XV and kp <= 2)
 
 
 def _mgrid(L, mode, X):
@@ -197,7 +206,7 @@ def xv(X, V):
     K = V.shape[1]
     kp = _kpad(K)
     code, adt = _xcode(X)
-    if _mfma_ok(X, kp):
+    if _mfma_ok(X, kp, XV):
         U = _mchain(XV, X, kp, V=V)
         if U is not None:
             _count("mfma.xv")
@@ -217,7 +226,7 @@ def xtg(X, G):
     kp = _kpad(K)
     code, adt = _xcode(X)
     Gp = _pad_cols(G, kp, adt).contiguous()
-    if _mfma_ok(X, kp):
+    if _mfma_ok(X, kp, XTG):
         R = _mchain(XTG, X, kp, S=Gp)
         if R is not None:
             _count("mfma.xtg")
@@ -250,7 +259,7 @@ def mmchain(ctype, X, V, W=None):
             S = _pad_cols(W, kp, adt).contiguous()
         else:
             return None
-    if _mfma_ok(X, kp):
+    if _mfma_ok(X, kp, mode):
         R = _mchain(mode, X, kp, V=V, S=S, sbc=sbc)
         if R is not None:
             _count("mfma.mmchain." + ctype)

@@ -13,10 +13,11 @@ CFG = DMLConfig(gpu=False)
 
 
 def algo(name, args, inputs, outputs):
-    with open(os.path.join(SCRIPTS_DIR, "algorithms", name + ".dml")) as f:
+    path = os.path.join(SCRIPTS_DIR, "algorithms", name + ".dml")
+    with open(path) as f:
         src = f.read()
     out = []
-    res = run(src, args=args, inputs=inputs, outputs=outputs, config=CFG, out=out.append)
+    res = run(src, args=args, inputs=inputs, outputs=outputs, config=CFG, out=out.append, filename=path)
     return {k: (v.numpy() if hasattr(v, "numpy") else v) for k, v in res.items()}, out
 
 
@@ -267,3 +268,44 @@ def test_bivar_stats(tmp_path):
     f, p = st.f_oneway(*[s2[c1 == u] for u in np.unique(c1)])
     k = [i for i in range(ns.shape[1]) if ns[0, i] == 3 and ns[1, i] == 2][0]
     np.testing.assert_allclose(ns[3:5, k], [f, p], rtol=1e-8)
+
+
+def _tree_data(n=800, seed=12):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, 3))
+    cat = rng.integers(1, 4, n)
+    Xd = np.hstack([X, np.eye(3)[cat - 1]])
+    y = ((X[:, 0] > 0.3) & (cat != 2)).astype(int) + 1 + (X[:, 1] > 1).astype(int)
+    R = np.array([[1, 1, 1], [2, 2, 2], [3, 3, 3], [4, 4, 6]], dtype=float)
+    return Xd, np.eye(3)[y - 1], y, R
+
+
+def test_decision_tree_fit_and_predict():
+    Xd, Y, y, R = _tree_data()
+    r, out = algo("decision-tree", dict(X="X", Y="Y", R="R", M="M", bins=20, depth=8, num_leaf=5),
+                  {"X": Xd, "Y": Y, "R": R}, ["M"])
+    M = r["M"]
+    assert M.shape[0] == 6 and M[0, 0] == 1
+    # model consistency: children of internal node j sit at j + offset and j + offset + 1
+    for j in range(M.shape[1]):
+        if M[2, j] > 0:
+            lc = j + int(M[1, j])
+            assert M[0, lc] == 2 * M[0, j] and M[0, lc + 1] == 2 * M[0, j] + 1
+    p, pout = algo("decision-tree-predict", dict(X="X", Y="Y", R="R", M="M", P="P"),
+                   {"X": Xd, "Y": Y, "R": R, "M": M}, ["P"])
+    acc = (p["P"].ravel() == y).mean()
+    assert acc > 0.97
+    train_acc = float([l for l in out if "accuracy" in l][0].split(":")[1])
+    np.testing.assert_allclose(train_acc, 100 * acc)      # leaves' error counts match the replay
+
+
+def test_random_forest_votes():
+    Xd, Y, y, R = _tree_data(seed=13)
+    r, _ = algo("random-forest", dict(X="X", Y="Y", R="R", M="M", C="C", bins=16, depth=8, num_leaf=5,
+                                      num_trees=5, feature_subset=1.0), {"X": Xd, "Y": Y, "R": R}, ["M", "Cnt"])
+    M = r["M"]
+    assert M.shape[0] == 7 and set(np.unique(M[1])) == {1, 2, 3, 4, 5}
+    p, out = algo("random-forest-predict", dict(X="X", Y="Y", R="R", M="M", C="C", P="P"),
+                  {"X": Xd, "Y": Y, "R": R, "M": M, "Cnt": r["Cnt"]}, ["P"])
+    assert (p["P"].ravel() == y).mean() > 0.95
+    assert any(l.startswith("Out-Of-Bag error") for l in out)

@@ -107,6 +107,14 @@ def test_dml_uses_fused_kernels(gpu_config):
 # operand/accumulator layout slip, which would show up as a wrong element, not rounding),
 # then random data against an fp64 reference.
 # ---------------------------------------------------------------------------
+@pytest.fixture
+def mfma_all(K):
+    """Route every eligible op (incl. the fused chains) through the MFMA kernel."""
+    K.MFMA_ALL = True
+    yield
+    K.MFMA_ALL = False
+
+
 def _ints(shape, lo, hi, seed):
     g = torch.Generator(device="cuda").manual_seed(seed)
     return torch.randint(lo, hi + 1, shape, generator=g, device="cuda").to(torch.float64)
@@ -115,7 +123,7 @@ def _ints(shape, lo, hi, seed):
 @pytest.mark.parametrize("n", [1, 15, 17, 4099])
 @pytest.mark.parametrize("d", [8, 136, 256, 264, 1000])
 @pytest.mark.parametrize("k", [1, 2, 3, 4])
-def test_mfma_exact_integer_layout(K, n, d, k):
+def test_mfma_exact_integer_layout(K, n, d, k, mfma_all):
     x = _ints((n, d), -3, 3, 10 + d).to(torch.bfloat16)
     x64 = x.double()
     v = _ints((d, k), -2, 2, 20 + k)
@@ -136,7 +144,7 @@ def test_mfma_exact_integer_layout(K, n, d, k):
 
 @pytest.mark.parametrize("ctype", ["XtXv", "XtwXv", "XtXvy", "XtPSXv"])
 @pytest.mark.parametrize("k", [1, 2, 4])
-def test_mfma_matches_rowstream(K, ctype, k):
+def test_mfma_matches_rowstream(K, ctype, k, mfma_all):
     n, d = 50001, 1000
     x = _mk(n, d, torch.bfloat16, seed=7)
     x64 = x.double()

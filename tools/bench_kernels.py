@@ -56,12 +56,14 @@ def main():
         L.sysml_set_variant.argtypes = [ctypes.c_int]
         for rep in range(a.reps + 1):
             for name, fn in cases.items():
-                variants = (0,) if name.startswith("torch") else (2, 3, 4, 11, 99) if dt == torch.bfloat16 \
-                    else (1, 2, 11)
+                variants = (0,) if name.startswith("torch") else (0, 2, 3, 4, 99) if dt == torch.bfloat16 \
+                    else (0, 1, 2, 11)
                 for R in variants:
                     # R = prefetch depth (pk kernel) / rows per iteration (generic); 11 = generic
                     # kernel; 99 = MFMA chain kernel (bf16 only)
-                    K.MFMA = (R == 99)
+                    # R = 0: the default dispatch (MFMA where it wins, tuned prefetch depth)
+                    K.MFMA = R in (0, 99)
+                    K.MFMA_ALL = R == 99
                     L.sysml_set_variant(1 if 10 < R < 99 else 0)
                     L.sysml_set_rows_per_iter(R % 10 if R < 99 else 0)
                     torch.cuda.synchronize()
@@ -74,7 +76,7 @@ def main():
                     if rep > 0:
                         times.setdefault(f"{name}/R{R}", []).append(e0.elapsed_time(e1))
         L.sysml_set_rows_per_iter(0)
-        K.MFMA = True
+        K.MFMA, K.MFMA_ALL = True, False
         for k, ts in times.items():
             med = statistics.median(ts)
             results[f"{str(dt).split('.')[-1]}/{k}"] = {"ms": round(med, 3), "min_ms": round(min(ts), 3),
