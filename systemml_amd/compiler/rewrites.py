@@ -188,6 +188,10 @@ class Rewriter:
             self._count("neg-pushdown")
             inner = self._rw_mm(Hop("mm", [a, b.inputs[0]], dict(h.p), dt="M", pos=h.pos))
             return Hop("u", [inner], {"o": "neg"}, dt="M", pos=h.pos)
+        if not transA:
+            g = self._match_pmm(a, b, h)
+            if g is not None:
+                return g
         if not transA and a.op == "t":
             X = a.inputs[0]
             if b is X:
@@ -205,6 +209,27 @@ class Rewriter:
             if m is not None:
                 return m
         return h
+
+    def _match_pmm(self, a, b, h):
+        """table(seq(1, n), I [, n, L]) %*% B  ->  gather rows B[I] (0 where I is out of range).
+        The reference compiles this permutation-matrix product to PMMJ instead of
+        materialising the (sparse) selection matrix; a dense n x L selection matrix would
+        cost n*L cells here."""
+        if a.op != "bi" or a.p.get("name") not in ("table", "ctable") or a.named:
+            return None
+        npos = a.p.get("npos", len(a.inputs))
+        if npos not in (2, 4):
+            return None
+        sq = a.inputs[0]
+        if sq.op != "bi" or sq.p.get("name") != "seq" or sq.named:
+            return None
+        sargs = sq.inputs[:sq.p.get("npos", len(sq.inputs))]
+        if len(sargs) < 2 or not _is_lit(sargs[0], 1) or (len(sargs) > 2 and not _is_lit(sargs[2], 1)):
+            return None
+        nrows = a.inputs[2] if npos == 4 else sargs[1]
+        ncols = a.inputs[3] if npos == 4 else lit(-1)
+        self._count("pmm-gather")
+        return Hop("bi", [a.inputs[1], b, nrows, ncols], {"name": "_gather_rows", "npos": 4}, dt="M", pos=h.pos)
 
     def _match_mmchain(self, X, g):
         def is_xv(n):

@@ -480,6 +480,28 @@ def b_outer(ctx, a, b, op):
     return C.binary(str(op), x, y)
 
 
+@builtin("_gather_rows")
+def b_gather_rows(ctx, idx, B, nrows, ncols=-1):
+    """Rows of B selected by idx (1-based; rows with idx out of range are 0): the
+    permutation-matrix product table(seq(1,n), idx, n, L) %*% B without the n x L matrix."""
+    if C.is_dist(idx):
+        idx = C._dist().gather(idx)
+    if C.is_dist(B):
+        B = C._dist().gather(B)
+    I = _mat(idx).reshape(-1)
+    M = _mat(B)
+    n = int(nrows)
+    L = int(ncols) if ncols is not None and int(ncols) >= 0 else M.shape[0]
+    if L != M.shape[0]:
+        raise DMLRuntimeError(f"matrix multiplication: dimension mismatch ({n}x{L} %*% {M.shape[0]}x{M.shape[1]})")
+    if I.shape[0] != n:
+        raise DMLRuntimeError("table: seq length does not match the category vector")
+    k = I.round().long()
+    ok = (k >= 1) & (k <= L)
+    out = M.index_select(0, (k.clamp(1, max(L, 1)) - 1).to(M.device))
+    return out * ok.to(device=M.device, dtype=M.dtype).reshape(-1, 1)
+
+
 @builtin("table", "ctable")
 def b_table(ctx, A=None, B=None, W=None, odim1=None, odim2=None, *rest, **kw):
     # table(A, B, [W], [d1, d2])

@@ -309,3 +309,41 @@ def test_random_forest_votes():
                   {"X": Xd, "Y": Y, "R": R, "M": M, "Cnt": r["Cnt"]}, ["P"])
     assert (p["P"].ravel() == y).mean() > 0.95
     assert any(l.startswith("Out-Of-Bag error") for l in out)
+
+
+@pytest.mark.parametrize("name,a,b", [("ALS-CG", "U", "V"), ("ALS-DS", "L", "R")])
+@pytest.mark.parametrize("reg", ["L2", "wL2"])
+def test_als_recovers_low_rank(name, a, b, reg):
+    rng = np.random.default_rng(14)
+    m, n, k = 60, 40, 3
+    full = rng.standard_normal((m, k)) @ rng.standard_normal((k, n))
+    mask = rng.random((m, n)) < 0.6
+    X = np.where(mask, full, 0.0)
+    inp = "X" if name == "ALS-CG" else "Vm"
+    r, _ = algo(name, {"X" if name == "ALS-CG" else "V": "X", a: a, b: b, "rank": k, "reg": reg,
+                       "lambda": 1e-6, "maxi": 60, "check": False, "thr": 1e-12},
+                {inp: X}, [a, b])
+    P = r[a] @ r[b]
+    err = np.abs(P - full)[mask].max()
+    assert err < 1e-3, err
+    # held-out entries are recovered too (rank-3 structure)
+    assert np.abs(P - full)[~mask].max() < 1e-2
+
+
+def test_als_predict_and_topk(tmp_path):
+    rng = np.random.default_rng(15)
+    L = rng.standard_normal((6, 2))
+    R = rng.standard_normal((2, 5))
+    pairs = np.array([[1, 1], [6, 5], [3, 2]], dtype=float)
+    r, _ = algo("ALS_predict", dict(X="X", Y="Y", L="L", R="R", Vrows=6, Vcols=5),
+                {"X": pairs, "L": L, "R": R}, ["Y"])
+    S = L @ R
+    np.testing.assert_allclose(r["Y"][:, 2], [S[0, 0], S[5, 4], S[2, 1]])
+    V = np.zeros((6, 5))
+    V[1, np.argmax(S[1])] = 1          # user 2 already rated its best item
+    users = np.array([[2], [4]], dtype=float)
+    t, _ = algo("ALS_topk_predict", dict(X="X", Y=str(tmp_path / "Y"), L="L", R="R", V="V", K=2),
+                {"X": users, "L": L, "R": R, "V": V}, ["IDS", "SC"])
+    s2 = np.where(V[1] != 0, -np.inf, S[1])
+    np.testing.assert_array_equal(t["IDS"][0], np.argsort(-s2)[:2] + 1)
+    np.testing.assert_array_equal(t["IDS"][1], np.argsort(-S[3])[:2] + 1)
