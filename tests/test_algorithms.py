@@ -347,3 +347,33 @@ def test_als_predict_and_topk(tmp_path):
     s2 = np.where(V[1] != 0, -np.inf, S[1])
     np.testing.assert_array_equal(t["IDS"][0], np.argsort(-s2)[:2] + 1)
     np.testing.assert_array_equal(t["IDS"][1], np.argsort(-S[3])[:2] + 1)
+
+
+def test_step_linear_regression_selects_true_features():
+    rng = np.random.default_rng(16)
+    n, m = 500, 8
+    X = rng.standard_normal((n, m))
+    y = 3 * X[:, [2]] - 2 * X[:, [5]] + 0.5 * X[:, [0]] + 1.0 + 0.1 * rng.standard_normal((n, 1))
+    r, _ = algo("StepLinearRegDS", dict(X="X", Y="y", B="B", S="S", icpt=1, thr=0.001),
+                {"X": X, "y": y}, ["S", "Bfull"])
+    assert list(r["S"].ravel()[:3]) == [3, 6, 1]
+    B = r["Bfull"].ravel()
+    sel = [int(s) - 1 for s in r["S"].ravel()]
+    Xi = np.hstack([X[:, sel], np.ones((n, 1))])
+    ref = np.linalg.lstsq(Xi, y, rcond=None)[0].ravel()
+    np.testing.assert_allclose(B[sel], ref[:-1], atol=1e-8)
+    np.testing.assert_allclose(B[-1], ref[-1], atol=1e-8)
+    assert np.all(np.delete(B[:-1], sel) == 0)
+
+
+@pytest.mark.parametrize("name", ["CsplineDS", "CsplineCG"])
+def test_cubic_spline_matches_scipy(name):
+    from scipy.interpolate import CubicSpline
+    x = np.array([0.0, 0.7, 1.5, 2.0, 3.2, 4.0, 5.5])
+    y = np.sin(x) + 0.1 * x
+    cs = CubicSpline(x, y, bc_type="natural")
+    for xq in (0.3, 2.6, 5.0):
+        r, _ = algo(name, dict(X="X", Y="Y", K="K", O="O", inp_x=xq), {"X": x.reshape(-1, 1), "Y": y.reshape(-1, 1)},
+                    ["K", "q"])
+        np.testing.assert_allclose(r["K"].ravel(), cs(x, 1), rtol=1e-6, atol=1e-8)
+        np.testing.assert_allclose(r["q"], cs(xq), rtol=1e-6)
