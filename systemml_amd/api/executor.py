@@ -137,7 +137,18 @@ def execute(cs: CompiledScript, inputs=None, out=None, stats=None, dist=None):
             stats.t_exec += time.perf_counter() - t0
             stats.t_parse += cs.t_parse
             stats.t_compile += cs.t_compile
-    return {k: ctx.vars.get(k) for k in cs.outputs}, ctx
+            if ctx.pool is not None:
+                for k_, v_ in ctx.pool.stats.items():
+                    if isinstance(v_, int) and v_:
+                        stats.counters["bufferpool." + k_] = v_
+    from ..runtime.bufferpool import Evicted
+    res = {}
+    for k in cs.outputs:
+        v = ctx.vars.get(k)
+        if isinstance(v, Evicted):
+            v = ctx.pool.restore(ctx.vars, k, v)
+        res[k] = v
+    return res, ctx
 
 
 def run(source, args=None, inputs=None, outputs=(), config=None, pydml=False, filename="", out=None,

@@ -35,6 +35,11 @@ class DMLConfig:
     seed: int = -1
     hip_kernels: bool = True            # use in-tree HIP kernels for the hot ops on GPU
     hip_graphs: bool = False
+    # buffer pool (runtime/bufferpool.py): HBM -> pinned host -> local disk
+    bufferpool: bool = True
+    bufferpool_hbm_fraction: float = 0.85
+    bufferpool_host_bytes: int = 64 << 30
+    bufferpool_spill_dir: str = ""
     extra: dict = field(default_factory=dict)
 
     _XML_KEYS = {
@@ -47,6 +52,8 @@ class DMLConfig:
         "sysml.stats.maxHeavyHitters": ("stats_count", int),
         "sysml.codegen.enabled": ("fusion", lambda v: str(v).lower() == "true"),
         "sysml.gpu.hip.kernels": ("hip_kernels", lambda v: str(v).lower() == "true"),
+        "sysml.bufferpool.hbm.fraction": ("bufferpool_hbm_fraction", float),
+        "sysml.bufferpool.spill.dir": ("bufferpool_spill_dir", str),
     }
 
     def set(self, key, value):

@@ -167,7 +167,9 @@ def read_csv_matrix(fname, header=False, sep=",", fill=True, fill_value=0.0, na=
     from ..ops import native
     parts = []
     for k, f in enumerate(_files(fname)):
-        a = native.parse_csv(f, sep, header) if na is None else None
+        # native multi-threaded parser (ops/csrc/fastio.cpp) unless NA strings / a non-zero fill
+        a = native.parse_csv(f, sep, header, threads=os.cpu_count() or 8) \
+            if (na is None and fill and fill_value == 0.0) else None
         if a is None:
             rows = []
             with open(f) as fh:

@@ -8,6 +8,8 @@ live, so the same instruction stream runs on every backend.
 """
 from __future__ import annotations
 
+from .bufferpool import Evicted
+
 from ..parser.errors import DMLRuntimeError
 from ..ops import core as C
 from . import builtins as B
@@ -25,10 +27,16 @@ def make_impl(h):
 
         def tread(ctx, a):
             try:
-                return ctx.vars[name]
+                v = ctx.vars[name]
             except KeyError:
                 raise DMLRuntimeError(f"{pos}: Variable '{name}' is not defined" if pos else
                                       f"Variable '{name}' is not defined")
+            pool = ctx.pool
+            if pool is not None:
+                if type(v) is Evicted:
+                    v = pool.restore(ctx.vars, name, v)
+                pool.touch(ctx.vars, name)
+            return v
         return tread, "tread"
     if op == "b":
         o = p["o"]

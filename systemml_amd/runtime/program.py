@@ -28,6 +28,14 @@ class ExecutionContext:
         self.dist = dist
         self._out = out
         self.depth = 0
+        self.frame_stack = []        # callers' variable frames (buffer-pool eviction candidates)
+        self.pool = None
+        if config is not None and getattr(config, "bufferpool", False) and torch.cuda.is_available():
+            from .bufferpool import BufferPool
+            self.pool = BufferPool(config)
+
+    def frames(self):
+        return self.frame_stack + [self.vars]
 
     def print(self, s):
         if self.dist is not None and self.config.print_rank0_only and self.dist.rank != 0:
@@ -67,6 +75,16 @@ def _attach_pos(e, pos):
     return e
 
 
+def _run_ins(ctx, ins, slots):
+    try:
+        return ins.fn(ctx, [slots[i] for i in ins.ins])
+    except torch.OutOfMemoryError:
+        # reactive buffer-pool eviction (reference: CacheableData eviction on heap pressure)
+        if ctx.pool is None or not ctx.pool.on_oom(ctx.frames()):
+            raise
+        return ins.fn(ctx, [slots[i] for i in ins.ins])
+
+
 def exec_instrs(ctx, instrs, nslots):
     slots = [None] * nslots
     stats = ctx.stats
@@ -75,7 +93,7 @@ def exec_instrs(ctx, instrs, nslots):
         for ins in instrs:
             t0 = time.perf_counter()
             try:
-                r = ins.fn(ctx, [slots[i] for i in ins.ins])
+                r = _run_ins(ctx, ins, slots)
             except DMLScriptStop:
                 raise
             except DMLRuntimeError as e:
@@ -91,7 +109,7 @@ def exec_instrs(ctx, instrs, nslots):
         return slots
     for ins in instrs:
         try:
-            slots[ins.out] = ins.fn(ctx, [slots[i] for i in ins.ins])
+            slots[ins.out] = _run_ins(ctx, ins, slots)
         except DMLScriptStop:
             raise
         except DMLRuntimeError as e:
@@ -123,6 +141,8 @@ def exec_block(ctx, b):
             vars_[name] = slots[s]
         for name in b.rmvars:
             vars_.pop(name, None)
+        if ctx.pool is not None:
+            ctx.pool.maybe_evict(ctx.frames())
         return
     if isinstance(b, IfBlock):
         if _to_bool(eval_pred(ctx, b.pred)):
@@ -202,12 +222,14 @@ def call_function(ctx, fkey, args, given):
                 raise DMLRuntimeError(f"missing argument '{p.name}' in call to function {fb.name}")
     ctx.vars = new_vars
     ctx.depth += 1
+    ctx.frame_stack.append(saved)
     if ctx.depth > 500:
         raise DMLRuntimeError("maximum function recursion depth exceeded")
     try:
         exec_blocks(ctx, fb.body)
     finally:
         ctx.vars = saved
+        ctx.frame_stack.pop()
         ctx.depth -= 1
     outs = []
     for o in fb.outputs:

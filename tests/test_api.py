@@ -97,3 +97,27 @@ def test_cli_stop_returns_error(tmp_path):
     p = subprocess.run([sys.executable, "-m", "systemml_amd", "-s", "stop('boom')", "-cpu"], capture_output=True,
                        text=True, cwd=ROOT, env={**os.environ, "PYTHONPATH": ROOT})
     assert p.returncode == 1 and "boom" in p.stderr
+
+
+def test_native_csv_and_ijv_parsers(tmp_path):
+    import numpy as np
+    from systemml_amd.ops import native
+    if native.lib() is None:
+        pytest.skip("libsysml_native.so not built")
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((40000, 7))
+    A[3, 2] = 0.0
+    f = tmp_path / "a.csv"
+    with open(f, "w") as fh:
+        fh.write("h1,h2,h3,h4,h5,h6,h7\n")
+        for row in A:
+            fh.write(",".join(repr(float(v)) for v in row) + "\n")
+    B = native.parse_csv(str(f), ",", True, threads=8)     # > 1 MB: multi-threaded path
+    np.testing.assert_array_equal(A, B)
+    g = tmp_path / "b.ijv"
+    g.write_text("1 1 2.5\n3 2 -1e-3\n\n2 3 Infinity\n")
+    C = native.parse_ijv(str(g))
+    assert C.shape == (3, 3) and C[1, 2] == -1e-3 and np.isinf(C[2, 2])
+    h = tmp_path / "c.csv"
+    h.write_text("1,,3\n4,5\n")
+    np.testing.assert_array_equal(native.parse_csv(str(h), ",", False), [[1, 0, 3], [4, 5, 0]])

@@ -257,3 +257,29 @@ G = table(seq(1, 4), I, 4, 3) %*% B
     np.testing.assert_array_equal(r["G"].numpy(), [[3, 4], [0, 0], [5, 6], [1, 2]])
     cs = compile_script(src, outputs=["G"], config=DMLConfig(gpu=False))
     assert "_gather_rows" in cs.explain() if hasattr(cs, "explain") else True
+
+
+def test_buffer_pool_evicts_lru_and_restores(tmp_path):
+    import torch
+    from systemml_amd.runtime.bufferpool import BufferPool, Evicted
+    pool = BufferPool()
+    pool.host_tensors = True
+    pool.min_bytes = 0
+    main = {"A": torch.arange(12.0).reshape(3, 4), "B": torch.ones(2, 2)}
+    callee = {"C": torch.full((5, 1), 7.0)}
+    main["A2"] = main["A"]                      # alias: evicted together
+    pool.touch(main, "A")
+    pool.touch(callee, "C")
+    pool.touch(main, "B")
+    freed = pool.evict([main, callee], keep=(), need_bytes=1)
+    assert freed == 48 and isinstance(main["A"], Evicted) and main["A2"] is main["A"]
+    assert torch.is_tensor(main["B"]) and torch.is_tensor(callee["C"])
+    t = pool.restore(main, "A", main["A"])
+    assert torch.equal(t, torch.arange(12.0).reshape(3, 4)) and main["A"] is t
+    # second tier: spill to disk once the host budget is exhausted
+    pool.spill_dir = str(tmp_path)
+    pool.host_budget = 0
+    pool.evict([main, callee], keep=("C",))
+    assert isinstance(main["B"], Evicted) and main["B"].path is not None
+    assert torch.equal(pool.restore(main, "B", main["B"]), torch.ones(2, 2))
+    assert pool.stats["evict_disk"] >= 1 and "Buffer pool" in pool.report()
