@@ -98,6 +98,11 @@ def convert_input(v, dist=None, config=None):
     except ImportError:
         pass
     if hasattr(v, "toarray") and not isinstance(v, np.ndarray):   # scipy sparse
+        from ..ops import sparse as SP
+        coo = v.tocoo()
+        if dist is None and SP.want_sparse(coo.shape[0], coo.shape[1], coo.nnz):
+            return SP.from_ijv(coo.row, coo.col, coo.data, coo.shape[0], coo.shape[1], backend.dtype,
+                               backend.device)
         v = v.toarray()
     if isinstance(v, (list, tuple)):
         v = np.asarray(v, dtype=np.float64)

@@ -92,7 +92,16 @@ def _post(t, ctx):
     if ctx is not None and ctx.dist is not None and t.shape[0] >= ctx.config.dist_min_rows:
         from ..parallel import dist as D
         return D.scatter_rows(ctx, t)
+    from ..ops import sparse as SP
+    t = SP.maybe_sparse(t)
+    if SP.is_sparse(t):
+        return place_sparse(t)
     return maybe_bf16(place(t))
+
+
+def place_sparse(t):
+    from ..ops.backend import backend
+    return t.to(device=backend.device, dtype=backend.dtype)
 
 
 def _b(v):

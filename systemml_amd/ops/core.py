@@ -17,6 +17,7 @@ import torch
 from ..parser.errors import DMLRuntimeError
 from ..runtime import scalars as S
 from .backend import backend
+from . import sparse as SP
 
 Tensor = torch.Tensor
 _DIST = None
@@ -32,6 +33,12 @@ def _dist():
 
 def is_dist(x):
     return isinstance(x, _dist().DistMatrix)
+
+
+def cvt_sp(x):
+    if x.dtype != backend.dtype and x.dtype in (torch.float32, torch.float64):
+        return x.to(backend.dtype)
+    return x
 
 
 def cvt(x: Tensor) -> Tensor:
@@ -175,6 +182,15 @@ def _check_bin_dims(a: Tensor, b: Tensor, op):
 
 def binary(op, a, b):
     ta, tb = isinstance(a, Tensor), isinstance(b, Tensor)
+    if ta and SP.is_sparse(a):
+        if not tb and op in ("*", "/") and isinstance(b, (int, float)) and not isinstance(b, bool) \
+                and (op == "*" or b != 0):
+            return SP.scale(a, float(b), op)
+        a = SP.densify(a)
+    if tb and SP.is_sparse(b):
+        if not ta and op == "*" and isinstance(a, (int, float)) and not isinstance(a, bool):
+            return SP.scale(b, float(a), "*")
+        b = SP.densify(b)
     if not ta and not tb:
         if is_dist(a) or is_dist(b):
             return _dist().binary(op, a, b)
@@ -297,6 +313,11 @@ def _var(x, dim=None):
 
 
 def agg(o, d, x):
+    if isinstance(x, Tensor) and SP.is_sparse(x):
+        r = SP.agg(o, d, x)
+        if r is not None:
+            return r
+        x = SP.densify(x)
     if not isinstance(x, Tensor):
         if is_dist(x):
             return _dist().agg(o, d, x)
@@ -372,6 +393,7 @@ def tak(a, b):
         return _dist().tak(a, b)
     if not isinstance(a, Tensor) or not isinstance(b, Tensor):
         return agg("sum", "all", binary("*", a, b))
+    a, b = SP.densify(a), SP.densify(b)
     if a.shape != b.shape:
         return agg("sum", "all", binary("*", a, b))
     a, b = cvt(a), cvt(b)
@@ -396,6 +418,13 @@ def mm(a, b, transA=False):
         return _dist().mm(a, b, transA)
     a = _need_mat(a, "%*%")
     b = _need_mat(b, "%*%")
+    if SP.is_sparse(a) or SP.is_sparse(b):
+        ka = a.shape[0] if transA else a.shape[1]
+        if ka != b.shape[0]:
+            raise DMLRuntimeError(f"Matrix multiplication dimension mismatch: {a.shape} %*% {b.shape}")
+        if SP.is_sparse(a):
+            return SP.mm(cvt_sp(a), b, transA)
+        return mm(cvt(a), SP.densify(b), transA)
     ka = a.shape[0] if transA else a.shape[1]
     if ka != b.shape[0]:
         ra, ca = (a.shape[1], a.shape[0]) if transA else tuple(a.shape)
@@ -418,6 +447,8 @@ def tsmm(x, left=True):
     if is_dist(x):
         return _dist().tsmm(x, left)
     x = _need_mat(x, "tsmm")
+    if SP.is_sparse(x):
+        return SP.tsmm(x, left)
     if backend.use_kernels and x.is_cuda:
         from . import kernels
         r = kernels.try_tsmm(x, left)
@@ -431,7 +462,7 @@ def mmchain(ctype, X, v, w=None):
     """t(X) %*% f(X %*% v) fused chains (MapMultChain + codegen row template)."""
     if is_dist(X):
         return _dist().mmchain(ctype, X, v, w)
-    if backend.use_kernels and isinstance(X, Tensor) and X.is_cuda:
+    if backend.use_kernels and isinstance(X, Tensor) and X.is_cuda and not SP.is_sparse(X):
         from . import kernels
         r = kernels.try_mmchain(ctype, X, v, w)
         if r is not None:
@@ -462,6 +493,8 @@ def transpose(x):
     if is_dist(x):
         return _dist().transpose(x)
     x = _need_mat(x, "t")
+    if SP.is_sparse(x):
+        return SP.transpose(x)
     return cvt(x).t().contiguous()
 
 

@@ -1,0 +1,142 @@
+"""Sparse matrices (reference: runtime/matrix/data/{SparseBlock,SparseBlockCSR,SparseBlockMCSR}
+and the sparse paths of LibMatrixMult / LibMatrixAgg; MatrixBlock.evalSparseFormatInMemory
+decides dense vs sparse with a 0.4 sparsity turn point).
+
+Representation: a torch CSR tensor (`torch.sparse_csr`) on the backend device; on the
+MI355X the products run on hipSPARSE/rocSPARSE through torch.  Only the operations that
+benefit from sparsity keep the CSR form (matrix products incl. tsmm / mmchain, sum-type
+aggregates, transpose, scaling by a scalar, shape queries, write); every other operator
+receives a densified operand (instructions.make_impl), so semantics never depend on the
+format.
+"""
+from __future__ import annotations
+
+import torch
+
+SPARSITY_TURN_POINT = 0.4          # reference: MatrixBlock.SPARSITY_TURN_POINT
+MIN_CELLS = 1 << 16                # small matrices always stay dense
+
+
+def is_sparse(x) -> bool:
+    return isinstance(x, torch.Tensor) and x.layout in (torch.sparse_csr, torch.sparse_csc, torch.sparse_coo)
+
+
+def densify(x):
+    if is_sparse(x):
+        return x.to_dense()
+    return x
+
+
+def nnz(x) -> int:
+    if is_sparse(x):
+        return int(x._nnz()) if x.layout != torch.sparse_coo else int(x.coalesce()._nnz())
+    return int(torch.count_nonzero(x).item())
+
+
+def want_sparse(rows, cols, nz) -> bool:
+    cells = rows * cols
+    return cells >= MIN_CELLS and nz < SPARSITY_TURN_POINT * cells
+
+
+def maybe_sparse(x: torch.Tensor):
+    """Convert a dense matrix to CSR when it is sparse enough to pay off."""
+    if is_sparse(x) or x.dim() != 2 or x.dtype == torch.bfloat16:
+        return x
+    r, c = x.shape
+    if r * c < MIN_CELLS:
+        return x
+    nz = int(torch.count_nonzero(x).item())
+    return x.to_sparse_csr() if want_sparse(r, c, nz) else x
+
+
+def from_ijv(i, j, v, rows, cols, dtype, device):
+    """CSR matrix from 0-based COO triplets (duplicates summed)."""
+    idx = torch.stack([torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64)])
+    coo = torch.sparse_coo_tensor(idx, torch.as_tensor(v, dtype=dtype), (rows, cols)).coalesce()
+    return coo.to_sparse_csr().to(device)
+
+
+def rand_csr(rows, cols, sparsity, lo, hi, pdf, gen, dtype, device, chunk_cells=1 << 26):
+    """rand(..., sparsity < 0.4) generated directly in CSR, row-chunked so the dense
+    intermediate never exceeds `chunk_cells` cells."""
+    crow = [torch.zeros(1, dtype=torch.int64, device=device)]
+    cols_l, vals_l = [], []
+    step = max(1, chunk_cells // max(cols, 1))
+    base = 0
+    for r0 in range(0, rows, step):
+        r1 = min(rows, r0 + step)
+        mask = torch.rand((r1 - r0, cols), generator=gen, device=device, dtype=torch.float32) < sparsity
+        nzr, nzc = mask.nonzero(as_tuple=True)
+        k = nzr.numel()
+        if pdf == "normal":
+            v = torch.randn(k, generator=gen, device=device, dtype=dtype)
+        else:
+            v = torch.rand(k, generator=gen, device=device, dtype=dtype) * (hi - lo) + lo
+        counts = mask.sum(1, dtype=torch.int64)
+        crow.append(base + torch.cumsum(counts, 0))
+        base += k
+        cols_l.append(nzc.to(torch.int64))
+        vals_l.append(v)
+    crow_t = torch.cat(crow)
+    col_t = torch.cat(cols_l) if cols_l else torch.zeros(0, dtype=torch.int64, device=device)
+    val_t = torch.cat(vals_l) if vals_l else torch.zeros(0, dtype=dtype, device=device)
+    return torch.sparse_csr_tensor(crow_t, col_t, val_t, (rows, cols), device=device)
+
+
+# ----------------------------------------------------------------------------
+# sparse-aware operators (dense operands pass through untouched)
+# ----------------------------------------------------------------------------
+def _dense_rhs(b, dtype):
+    b = densify(b)
+    return b.to(dtype) if b.dtype != dtype else b
+
+
+def mm(a, b, transA=False):
+    """a %*% b (or t(a) %*% b) with a and/or b sparse."""
+    if is_sparse(a):
+        if transA:
+            a = a.t()                                  # CSR^T = CSC, consumed by spmm
+        return (a @ _dense_rhs(b, a.dtype)).contiguous()
+    # dense %*% sparse = t(t(b) %*% t(a))
+    at = a.t() if not transA else a
+    return (b.t() @ at.t().contiguous().to(b.dtype)).t().contiguous() if is_sparse(b) else None
+
+
+def tsmm(x, left=True):
+    """t(X) %*% X (left) or X %*% t(X) as a sparse x sparse product; the (small) result is dense."""
+    xt = x.t().to_sparse_csr()
+    r = (xt @ x) if left else (x @ xt)
+    return densify(r).contiguous()
+
+
+def agg(o, d, x):
+    """sum / sumsq / mean over all, rows or columns of a sparse matrix; None if unsupported."""
+    r, c = x.shape
+    if o not in ("sum", "sumsq", "mean"):
+        return None
+    vals = x.values()
+    if o == "sumsq":
+        xs = torch.sparse_csr_tensor(x.crow_indices(), x.col_indices(), vals * vals, x.shape) \
+            if x.layout == torch.sparse_csr else None
+        if xs is None:
+            return None
+        x = xs
+        vals = x.values()
+    if d == "all":
+        s = float(vals.sum().item())
+        return s / (r * c) if o == "mean" else s
+    if d == "row":
+        out = x @ torch.ones((c, 1), dtype=vals.dtype, device=vals.device)
+        return out / c if o == "mean" else out
+    out = (x.t() @ torch.ones((r, 1), dtype=vals.dtype, device=vals.device)).t().contiguous()
+    return out / r if o == "mean" else out
+
+
+def scale(x, s, op):
+    v = x.values()
+    nv = v * s if op == "*" else v / s
+    return torch.sparse_csr_tensor(x.crow_indices(), x.col_indices(), nv, x.shape)
+
+
+def transpose(x):
+    return x.t().to_sparse_csr()

@@ -233,6 +233,11 @@ def _rand_local(r, c, lo, hi, sp, pdf, seed, lam, device=None, row_offset=0):
         g.manual_seed(seed + row_offset * 1000003)
     if r == 0 or c == 0:
         return torch.zeros((r, c), dtype=dt, device=device)
+    from ..ops import sparse as SP
+    if sp < SP.SPARSITY_TURN_POINT and r * c >= SP.MIN_CELLS and pdf in ("uniform", "normal") \
+            and not (pdf == "uniform" and lo == hi == 0):
+        # sparse rand: CSR generated directly (reference: sparse MatrixBlocks below the turn point)
+        return SP.rand_csr(r, c, sp, lo, hi, pdf, g, dt, device)
     if pdf == "uniform":
         if lo == hi:
             m = torch.full((r, c), lo, dtype=dt, device=device)

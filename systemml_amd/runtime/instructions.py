@@ -12,10 +12,32 @@ from .bufferpool import Evicted
 
 from ..parser.errors import DMLRuntimeError
 from ..ops import core as C
+from ..ops import sparse as SP
 from . import builtins as B
 
 
+_SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak"}
+_SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
+
+
 def make_impl(h):
+    """Instruction implementation; operators that have no sparse path receive densified
+    operands (sparse matrices: ops/sparse.py)."""
+    fn, code = _make_impl(h)
+    if h.op in _SPARSE_OK_OPS or (h.op == "u" and h.p.get("o") in _SPARSE_OK_UNARY):
+        return fn, code
+    is_sp = SP.is_sparse
+    dense = SP.densify
+
+    def wrapped(ctx, a):
+        for x in a:
+            if is_sp(x):
+                return fn(ctx, [dense(y) for y in a])
+        return fn(ctx, a)
+    return wrapped, code
+
+
+def _make_impl(h):
     op = h.op
     p = h.p
     if op == "lit":

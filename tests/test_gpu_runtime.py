@@ -29,3 +29,23 @@ D = t(A) %*% B
     np.testing.assert_allclose(r["s"], ref_s, rtol=1e-4)
     np.testing.assert_allclose(r["D"].cpu().double().numpy(), A.T @ B, rtol=1e-3)
     assert st.counters.get("bufferpool.evict_host", 0) > 0 and st.counters.get("bufferpool.restore", 0) > 0
+
+
+def test_sparse_ops_on_gpu(gpu_config):
+    from systemml_amd.api.executor import run
+    from systemml_amd.ops import sparse as SP
+    r = run("""A = rand(rows=20000, cols=800, sparsity=0.01, seed=5)
+v = rand(rows=800, cols=1, seed=6)
+u = A %*% v
+g = t(A) %*% u
+B = t(A) %*% A
+s = sum(A)
+""", outputs=["A", "v", "u", "g", "B", "s"], config=gpu_config)
+    A = r["A"]
+    assert SP.is_sparse(A) and A.is_cuda
+    Ad = A.to_dense().double().cpu().numpy()
+    v = r["v"].double().cpu().numpy()
+    np.testing.assert_allclose(r["u"].double().cpu().numpy(), Ad @ v, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(r["g"].double().cpu().numpy(), Ad.T @ (Ad @ v), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(r["B"].double().cpu().numpy(), Ad.T @ Ad, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(r["s"], Ad.sum(), rtol=1e-5)

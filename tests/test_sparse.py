@@ -1,0 +1,67 @@
+"""Sparse matrix support (reference: test/integration/functions/sparse/* and the sparse /
+dense variants of the application tests): results must not depend on the format."""
+import numpy as np
+import pytest
+import scipy.sparse as sps
+import torch
+
+from systemml_amd.api.executor import run
+from systemml_amd.api.mlcontext import SCRIPTS_DIR
+from systemml_amd.conf import DMLConfig
+from systemml_amd.ops import sparse as SP
+
+CFG = DMLConfig(gpu=False)
+
+
+def test_sparse_rand_and_operators():
+    r = run("""A = rand(rows=1000, cols=500, sparsity=0.01, seed=3)
+s = sum(A)
+rs = rowSums(A)
+cs = colSums(A)
+m = mean(A)
+q = sum(A ^ 2)
+B = t(A) %*% A
+C = A %*% matrix(1, rows=500, cols=2)
+T = t(A)
+D = A * 2
+E = exp(A)
+F = A[1:10, ] + 1
+""", outputs=["A", "s", "rs", "cs", "m", "q", "B", "C", "T", "D", "E", "F"], config=CFG)
+    A = r["A"]
+    assert SP.is_sparse(A) and 3000 < A._nnz() < 7000
+    Ad = A.to_dense().numpy()
+    np.testing.assert_allclose(r["s"], Ad.sum())
+    np.testing.assert_allclose(r["rs"].numpy().ravel(), Ad.sum(1), atol=1e-12)
+    np.testing.assert_allclose(r["cs"].numpy().ravel(), Ad.sum(0), atol=1e-12)
+    np.testing.assert_allclose(r["m"], Ad.mean())
+    np.testing.assert_allclose(r["q"], (Ad ** 2).sum())
+    np.testing.assert_allclose(r["B"].numpy(), Ad.T @ Ad, atol=1e-12)
+    np.testing.assert_allclose(r["C"].numpy(), Ad @ np.ones((500, 2)), atol=1e-12)
+    assert SP.is_sparse(r["T"]) and SP.is_sparse(r["D"])
+    np.testing.assert_allclose(r["T"].to_dense().numpy(), Ad.T)
+    np.testing.assert_allclose(r["D"].to_dense().numpy(), 2 * Ad)
+    np.testing.assert_allclose(r["E"].numpy(), np.exp(Ad))
+    np.testing.assert_allclose(r["F"].numpy(), Ad[:10] + 1)
+
+
+def test_sparse_input_through_algorithm():
+    rng = np.random.default_rng(0)
+    X = sps.random(3000, 200, density=0.05, random_state=1, format="csr")
+    y = rng.standard_normal((3000, 1))
+    with open(f"{SCRIPTS_DIR}/algorithms/LinearRegCG.dml") as f:
+        src = f.read()
+    r = run(src, args=dict(X="X", Y="y", B="B", icpt=0, reg=1e-6, tol=1e-12, maxi=500),
+            inputs={"X": X, "y": y}, outputs=["beta"], config=CFG, out=lambda s: None)
+    ref = np.linalg.lstsq(X.toarray(), y, rcond=None)[0]
+    np.testing.assert_allclose(r["beta"].numpy(), ref, atol=1e-6)
+
+
+def test_sparse_read_text_cell(tmp_path):
+    rng = np.random.default_rng(1)
+    A = sps.random(400, 300, density=0.02, random_state=2, format="coo")
+    f = tmp_path / "A.ijv"
+    f.write_text("".join(f"{i + 1} {j + 1} {float(v)!r}\n" for i, j, v in zip(A.row, A.col, A.data)))
+    (tmp_path / "A.ijv.mtd").write_text('{"data_type": "matrix", "format": "text", "rows": 400, "cols": 300}')
+    r = run(f'X = read("{f}")\ns = sum(X %*% matrix(1, rows=300, cols=1))', outputs=["X", "s"], config=CFG)
+    assert SP.is_sparse(r["X"])
+    np.testing.assert_allclose(r["s"], A.sum())
