@@ -120,7 +120,8 @@ def convert_input(v, dist=None, config=None):
         return D.scatter_rows_from_global(dist, t)
     if t.dtype == torch.bfloat16:
         return t.to(backend.device)
-    return maybe_bf16(place(t))
+    from ..io.readers import maybe_compress
+    return maybe_compress(maybe_bf16(place(t)), config)
 
 
 def execute(cs: CompiledScript, inputs=None, out=None, stats=None, dist=None):

@@ -35,6 +35,8 @@ class DMLConfig:
     seed: int = -1
     hip_kernels: bool = True            # use in-tree HIP kernels for the hot ops on GPU
     hip_graphs: bool = False
+    # compressed linear algebra (ops/compress.py): "false" | "true" | "auto" (auto: ratio >= 3)
+    compressed_linalg: str = "false"
     # buffer pool (runtime/bufferpool.py): HBM -> pinned host -> local disk
     bufferpool: bool = True
     bufferpool_hbm_fraction: float = 0.85
@@ -53,6 +55,7 @@ class DMLConfig:
         "sysml.codegen.enabled": ("fusion", lambda v: str(v).lower() == "true"),
         "sysml.gpu.hip.kernels": ("hip_kernels", lambda v: str(v).lower() == "true"),
         "sysml.bufferpool.hbm.fraction": ("bufferpool_hbm_fraction", float),
+        "sysml.compressed.linalg": ("compressed_linalg", lambda v: str(v).lower()),
         "sysml.bufferpool.spill.dir": ("bufferpool_spill_dir", str),
     }
 

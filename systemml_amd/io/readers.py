@@ -96,7 +96,19 @@ def _post(t, ctx):
     t = SP.maybe_sparse(t)
     if SP.is_sparse(t):
         return place_sparse(t)
-    return maybe_bf16(place(t))
+    return maybe_compress(maybe_bf16(place(t)), ctx.config if ctx is not None else None)
+
+
+def maybe_compress(t, config):
+    """Compressed linear algebra for read-only inputs (reference: sysml.compressed.linalg)."""
+    mode = getattr(config, "compressed_linalg", "false") if config is not None else "false"
+    if mode not in ("true", "auto") or not isinstance(t, torch.Tensor) or t.dim() != 2:
+        return t
+    from ..ops import compress as CMP
+    c = CMP.compress(t)
+    if CMP.is_compressed(c) and (mode == "true" or c.ratio() >= 3.0):
+        return c
+    return t
 
 
 def place_sparse(t):

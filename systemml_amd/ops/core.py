@@ -18,6 +18,7 @@ from ..parser.errors import DMLRuntimeError
 from ..runtime import scalars as S
 from .backend import backend
 from . import sparse as SP
+from . import compress as CMP
 
 Tensor = torch.Tensor
 _DIST = None
@@ -181,6 +182,14 @@ def _check_bin_dims(a: Tensor, b: Tensor, op):
 
 
 def binary(op, a, b):
+    if CMP.is_compressed(a):
+        if op in ("*", "/") and isinstance(b, (int, float)) and not isinstance(b, bool) and (op == "*" or b != 0):
+            return a.scale(float(b) if op == "*" else 1.0 / float(b))
+        a = a.decompress()
+    if CMP.is_compressed(b):
+        if op == "*" and isinstance(a, (int, float)) and not isinstance(a, bool):
+            return b.scale(float(a))
+        b = b.decompress()
     ta, tb = isinstance(a, Tensor), isinstance(b, Tensor)
     if ta and SP.is_sparse(a):
         if not tb and op in ("*", "/") and isinstance(b, (int, float)) and not isinstance(b, bool) \
@@ -246,6 +255,11 @@ UN = {
 
 
 def unary(op, x):
+    if CMP.is_compressed(x):
+        if op in ("nrow", "ncol", "length"):
+            r, c = x.shape
+            return {"nrow": r, "ncol": c, "length": r * c}[op]
+        x = x.decompress()
     if isinstance(x, Tensor):
         if op in ("nrow", "ncol", "length"):
             r, c = x.shape
@@ -313,6 +327,16 @@ def _var(x, dim=None):
 
 
 def agg(o, d, x):
+    if CMP.is_compressed(x):
+        if o in ("sum", "sumsq", "mean"):
+            sq = o == "sumsq"
+            r, c = x.shape
+            if d == "all":
+                v = float(x.colsums(sq).sum().item())
+                return v / (r * c) if o == "mean" else v
+            out = x.rowsums(sq) if d == "row" else x.colsums(sq)
+            return out / (c if d == "row" else r) if o == "mean" else out
+        x = x.decompress()
     if isinstance(x, Tensor) and SP.is_sparse(x):
         r = SP.agg(o, d, x)
         if r is not None:
@@ -391,6 +415,7 @@ def tak(a, b):
     """sum(a*b) without materialising the product (TernaryAggregate tak+*)."""
     if is_dist(a) or is_dist(b):
         return _dist().tak(a, b)
+    a, b = SP.densify(a), SP.densify(b)
     if not isinstance(a, Tensor) or not isinstance(b, Tensor):
         return agg("sum", "all", binary("*", a, b))
     a, b = SP.densify(a), SP.densify(b)
@@ -416,6 +441,14 @@ def _need_mat(x, what):
 def mm(a, b, transA=False):
     if is_dist(a) or is_dist(b):
         return _dist().mm(a, b, transA)
+    if CMP.is_compressed(a):
+        b = SP.densify(_need_mat(b, "%*%"))
+        k = a.shape[0] if transA else a.shape[1]
+        if k != b.shape[0]:
+            raise DMLRuntimeError(f"Matrix multiplication dimension mismatch: {a.shape} %*% {tuple(b.shape)}")
+        return a.tmatmul(cvt(b)) if transA else a.matmul(cvt(b))
+    if CMP.is_compressed(b):
+        b = b.decompress()
     a = _need_mat(a, "%*%")
     b = _need_mat(b, "%*%")
     if SP.is_sparse(a) or SP.is_sparse(b):
@@ -446,6 +479,8 @@ def mm(a, b, transA=False):
 def tsmm(x, left=True):
     if is_dist(x):
         return _dist().tsmm(x, left)
+    if CMP.is_compressed(x):
+        x = x.decompress()
     x = _need_mat(x, "tsmm")
     if SP.is_sparse(x):
         return SP.tsmm(x, left)
@@ -492,6 +527,8 @@ def mmchain_ref(ctype, X, v, w=None):
 def transpose(x):
     if is_dist(x):
         return _dist().transpose(x)
+    if CMP.is_compressed(x):
+        x = x.decompress()
     x = _need_mat(x, "t")
     if SP.is_sparse(x):
         return SP.transpose(x)

@@ -22,9 +22,17 @@ def is_sparse(x) -> bool:
 
 
 def densify(x):
+    """Dense tensor of a sparse (CSR) or compressed (ops/compress.py) matrix."""
     if is_sparse(x):
         return x.to_dense()
+    if type(x).__name__ == "CompressedMatrix":
+        return x.decompress()
     return x
+
+
+def is_special(x) -> bool:
+    """Sparse or compressed representation (operators without a native path densify it)."""
+    return is_sparse(x) or type(x).__name__ == "CompressedMatrix"
 
 
 def nnz(x) -> int:

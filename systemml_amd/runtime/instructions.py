@@ -26,7 +26,7 @@ def make_impl(h):
     fn, code = _make_impl(h)
     if h.op in _SPARSE_OK_OPS or (h.op == "u" and h.p.get("o") in _SPARSE_OK_UNARY):
         return fn, code
-    is_sp = SP.is_sparse
+    is_sp = SP.is_special
     dense = SP.densify
 
     def wrapped(ctx, a):
