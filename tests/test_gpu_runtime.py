@@ -27,7 +27,8 @@ D = t(A) %*% B
     B = 2 * A
     ref_s = sum((B + i).sum() for i in (1, 2, 3))
     np.testing.assert_allclose(r["s"], ref_s, rtol=1e-4)
-    np.testing.assert_allclose(r["D"].cpu().double().numpy(), A.T @ B, rtol=1e-3)
+    ref_d = A.T @ B
+    np.testing.assert_allclose(r["D"].cpu().double().numpy(), ref_d, rtol=1e-3, atol=1e-5 * np.abs(ref_d).max())
     assert st.counters.get("bufferpool.evict_host", 0) > 0 and st.counters.get("bufferpool.restore", 0) > 0
 
 
