@@ -24,6 +24,11 @@ def _np(x):
     raise DMLRuntimeError("write: expected a matrix")
 
 
+def write_matrix(x, fname, format="binary", **kw):
+    """Write a matrix (tensor / numpy) with its .mtd file, outside of a DML program."""
+    return write(None, x, fname, format=format, **kw)
+
+
 def write(ctx, x, fname, format="text", **kw):
     fmt = str(format).lower()
     from ..ops import core as C
