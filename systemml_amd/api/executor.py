@@ -54,7 +54,9 @@ def compile_script(source, args=None, inputs=(), outputs=(), config=None, pydml=
     cp = tr.compile(prog, inputs=list(inputs), outputs=outputs, input_types=input_types)
     compile_program(cp, make_impl, config)
     t2 = time.perf_counter()
-    return CompiledScript(cp, config, set(inputs), list(outputs), t1 - t0, t2 - t1)
+    cs = CompiledScript(cp, config, set(inputs), list(outputs), t1 - t0, t2 - t1)
+    cs.source = source
+    return cs
 
 
 def value_dt(v):

@@ -79,6 +79,9 @@ def compile_basic_block(bb: BasicBlock, make_impl, config=None):
                 continue     # x = x: nothing to write
             tail.append((name, h))
     bb.instrs, bb.writes_slots, bb.nslots = _linearize(bb.roots, tail, make_impl)
+    # variable -> slot of its last assignment in this block (debugger symbol table)
+    out_of = {ins.hop.id: ins.out for ins in bb.instrs}
+    bb.debug_slots = {name: out_of[h.id] for name, h in bb.env_out.items() if h.id in out_of}
 
 
 def compile_predicate(pred: Predicate, make_impl, config=None):

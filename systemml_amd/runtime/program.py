@@ -29,6 +29,7 @@ class ExecutionContext:
         self._out = out
         self.depth = 0
         self.frame_stack = []        # callers' variable frames (buffer-pool eviction candidates)
+        self.debugger = None         # utils/debugger.Debugger when run with -debug
         self.pool = None
         if config is not None and getattr(config, "bufferpool", False) and torch.cuda.is_available():
             from .bufferpool import BufferPool
@@ -76,6 +77,8 @@ def _attach_pos(e, pos):
 
 
 def _run_ins(ctx, ins, slots):
+    if ctx.debugger is not None:
+        ctx.debugger.on_instruction(ctx, ins, slots)
     try:
         return ins.fn(ctx, [slots[i] for i in ins.ins])
     except torch.OutOfMemoryError:
@@ -135,6 +138,8 @@ def exec_blocks(ctx, blocks):
 
 def exec_block(ctx, b):
     if isinstance(b, BasicBlock):
+        if ctx.debugger is not None:
+            ctx.debugger.cur_block = b
         slots = exec_instrs(ctx, b.instrs, b.nslots)
         vars_ = ctx.vars
         for name, s in b.writes_slots:

@@ -121,3 +121,20 @@ def test_native_csv_and_ijv_parsers(tmp_path):
     h = tmp_path / "c.csv"
     h.write_text("1,,3\n4,5\n")
     np.testing.assert_array_equal(native.parse_csv(str(h), ",", False), [[1, 0, 3], [4, 5, 0]])
+
+
+def test_debugger_breakpoints_step_and_print():
+    import io
+    from systemml_amd.api.executor import compile_script
+    from systemml_amd.conf import DMLConfig
+    from systemml_amd.utils.debugger import Debugger
+    src = "A = rand(rows=3, cols=2, seed=1)\nB = A * 2\nC = B + 1\ns = sum(C)\nprint(s)\n"
+    cs = compile_script(src, config=DMLConfig(gpu=False))
+    inp = io.StringIO("b 3\ni\nr\nw B\nl\ns\nc\n")
+    out = io.StringIO()
+    ctx = Debugger(cs, inp=inp, out=out).run()
+    log = out.getvalue()
+    assert "Breakpoint set at line 3" in log and "Breakpoint at line 3" in log
+    assert "Program finished." in log
+    assert "=>   3  C = B + 1" in log
+    assert "matrix[torch.float64] 3x2" in log        # whatis B inside the running block
