@@ -644,7 +644,7 @@ class _BBuilder:
 _M_BUILTINS = ("matrix rand seq sample cbind rbind table ctable diag rev removeEmpty replace order solve inv "
                "inverse cholesky outer quantile interQuantile aggregate lower.tri upper.tri conv2d "
                "conv2d_backward_filter conv2d_backward_data max_pool avg_pool max_pool_backward "
-               "avg_pool_backward bias_add bias_multiply transformapply transformcolmap").split()
+               "avg_pool_backward bias_add bias_multiply transformapply transformcolmap transform").split()
 _S_BUILTINS = "toString median interQuartileMean moment centralMoment cov cdf invcdf pnorm qnorm pt qt pf qf " \
               "pchisq qchisq pexp qexp exists time".split()
 _DIST_FNS = set("cdf invcdf icdf pnorm qnorm pt qt pf qf pchisq qchisq pexp qexp".split())

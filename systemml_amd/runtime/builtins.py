@@ -967,6 +967,12 @@ def b_transformencode(ctx, target=None, spec=None):
     return transform.encode(ctx, target, spec)
 
 
+@builtin("transform")
+def b_transform(ctx, target=None, **kw):
+    from . import transform
+    return transform.legacy_transform(ctx, target, **kw)
+
+
 @builtin("transformapply")
 def b_transformapply(ctx, target=None, spec=None, meta=None):
     from . import transform

@@ -408,6 +408,66 @@ def read_meta_dir(spec, path, sep=","):
     return FrameBlock(cols, ["STRING"] * ncol, colnames, cmeta)
 
 
+def write_meta_dir(meta: FrameBlock, spec, path, sep=","):
+    """Inverse of read_meta_dir: the on-disk transform metadata layout of the reference's
+    legacy transform (column.names, Recode/<col>.map|.ndistinct, Bin/<col>.bin,
+    Impute/<col>.impute)."""
+    sp = Spec(spec, meta.names, meta.ncol())
+    os.makedirs(path, exist_ok=True)
+    with open(os.path.join(path, "column.names"), "w") as f:
+        f.write(sep.join(meta.names) + "\n")
+    for c in sp.recode:
+        name = meta.names[c - 1]
+        d = os.path.join(path, "Recode")
+        os.makedirs(d, exist_ok=True)
+        m = _recode_map(meta, c - 1)
+        with open(os.path.join(d, name + ".map"), "w") as f:
+            for tok, code in sorted(m.items(), key=lambda kv: kv[1]):
+                f.write(f'"{tok}"{sep}{code}\n')
+        with open(os.path.join(d, name + ".ndistinct"), "w") as f:
+            f.write(f"{len(m)}\n")
+    for c in sp.bin:
+        name = meta.names[c - 1]
+        d = os.path.join(path, "Bin")
+        os.makedirs(d, exist_ok=True)
+        lo, hi = _bin_bounds(meta, c - 1)
+        w = (hi[-1] - lo[0]) / len(lo)
+        with open(os.path.join(d, name + ".bin"), "w") as f:
+            f.write(sep.join(str(x) for x in (c, repr(float(lo[0])), repr(float(hi[-1])), repr(float(w)), len(lo))))
+    for c in sp.impute:
+        rep = meta.col_meta[c - 1].get("mv") if meta.col_meta[c - 1] else None
+        if rep is None:
+            continue
+        d = os.path.join(path, "Impute")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, meta.names[c - 1] + ".impute"), "w") as f:
+            f.write(f"{c}{sep}{rep}")
+    with open(os.path.join(path, "spec.json"), "w") as f:
+        json.dump(sp.js, f)
+
+
+def legacy_transform(ctx, target, transformPath=None, spec=None, applyTransformPath=None, outputNames=None, **kw):
+    """Legacy `transform()` builtin (reference: ParameterizedBuiltin transform with
+    transformPath / applyTransformPath): encode and write the metadata directory, or apply a
+    previously written one."""
+    fr = _frame_of(target)
+    from ..ops.backend import place
+    if applyTransformPath is not None:
+        path = applyTransformPath
+        with open(os.path.join(path, "spec.json")) as f:
+            js = json.load(f)
+        meta = _meta_for(read_meta_dir(js, path), fr)
+        return place(apply_meta(fr, Spec(js, fr.names, fr.ncol()), meta))
+    sp = Spec(spec, fr.names, fr.ncol())
+    meta = build_meta(fr, sp)
+    if transformPath is not None:
+        write_meta_dir(meta, sp.js, transformPath)
+    if outputNames is not None:
+        with open(str(outputNames), "w") as f:
+            f.write(",".join(fr.names) + "\n")
+    return place(apply_meta(fr, sp, meta))
+
+
 # ---------------------------------------------------------------------------
 # builtin entry points
 # ---------------------------------------------------------------------------

@@ -174,3 +174,21 @@ G = transformdecode(target=X, spec="{ids: true, recode: [1]}", meta=M)
     G = r["G"]
     assert G.columns[0] == ["par", "ber"]
     assert G.columns[1] == [7.0, 9.0]
+
+
+@needs_ref
+def test_legacy_transform_and_apply_scripts(homes, tmp_path):
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    spec = os.path.join(HOMES, "homes.tfspec_recode_dummy.json")
+    tdir = tmp_path / "tf"
+    src = open(os.path.join(SCRIPTS_DIR, "algorithms", "transform.dml")).read()
+    _run(src, DATA_PATH=str(homes / "homes.csv"), TRANSFORM_SPEC_PATH=spec, TRANSFORM_PATH=str(tdir),
+         OUTPUT_NAMES=str(tmp_path / "names"), OUTPUT_DATA_PATH=str(tmp_path / "A.csv"))
+    assert (tdir / "Recode" / "zipcode.map").exists() and (tdir / "column.names").exists()
+    src2 = open(os.path.join(SCRIPTS_DIR, "algorithms", "apply-transform.dml")).read()
+    _run(src2, DATA_PATH=str(homes / "homes.csv"), TRANSFORM_PATH=str(tdir), APPLY_TRANSFORM_PATH=str(tdir),
+         OUTPUT_DATA_PATH=str(tmp_path / "B.csv"))
+    A = np.loadtxt(tmp_path / "A.csv", delimiter=",")
+    B = np.loadtxt(tmp_path / "B.csv", delimiter=",")
+    assert A.shape == (148, 14)
+    np.testing.assert_array_equal(A, B)
