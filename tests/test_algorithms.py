@@ -377,3 +377,33 @@ def test_cubic_spline_matches_scipy(name):
                     ["K", "q"])
         np.testing.assert_allclose(r["K"].ravel(), cs(x, 1), rtol=1e-6, atol=1e-8)
         np.testing.assert_allclose(r["q"], cs(xq), rtol=1e-6)
+
+
+def test_stratstats_against_numpy():
+    from scipy import stats as st
+    rng = np.random.default_rng(21)
+    n = 600
+    s = rng.integers(1, 5, n).astype(float)
+    x = rng.standard_normal(n) + s
+    y = 0.7 * x + 0.5 * s + rng.standard_normal(n)
+    x[5] = np.nan
+    y[9] = np.nan
+    X = np.column_stack([s, x, y])
+    r, _ = algo("stratstats", dict(X="X", O="O", Xcid="xc", Ycid="yc", Scid=1),
+                {"X": X, "Xcid": np.array([[2]]), "Ycid": np.array([[3]])}, ["OUT"])
+    row = r["OUT"][0]
+    ok = ~np.isnan(x) & ~np.isnan(y)
+    xs, ys, ss = x[ok], y[ok], s[ok]
+    res = st.linregress(xs, ys)
+    np.testing.assert_allclose(row[[20, 21, 23, 25, 27]], [ok.sum(), res.slope, res.rvalue, res.rvalue ** 2,
+                                                          res.pvalue], rtol=1e-9)
+    np.testing.assert_allclose(row[22], res.stderr, rtol=1e-9)
+    # stratified slope = within-stratum (fixed effects) regression
+    xd = xs - np.array([xs[ss == k].mean() for k in ss])
+    yd = ys - np.array([ys[ss == k].mean() for k in ss])
+    np.testing.assert_allclose(row[31], (xd @ yd) / (xd @ xd), rtol=1e-9)
+    # covariate x vs strata: one-way ANOVA
+    xv = x[~np.isnan(x)]
+    f, p = st.f_oneway(*[xv[s[~np.isnan(x)] == k] for k in (1, 2, 3, 4)])
+    np.testing.assert_allclose(row[7], p, rtol=1e-6)
+    assert row[0] == 2 and row[10] == 3 and row[38] == 4
