@@ -24,3 +24,10 @@ def gpu_config():
         pytest.skip("no GPU")
     from systemml_amd.conf import DMLConfig
     return DMLConfig(gpu=True, precision="single")
+
+
+@pytest.fixture(autouse=True)
+def _isolated_cwd(tmp_path, monkeypatch):
+    """Scripts write their $-named outputs relative to the working directory; keep them
+    out of the repository."""
+    monkeypatch.chdir(tmp_path)

@@ -407,3 +407,88 @@ def test_stratstats_against_numpy():
     f, p = st.f_oneway(*[xv[s[~np.isnan(x)] == k] for k in (1, 2, 3, 4)])
     np.testing.assert_allclose(row[7], p, rtol=1e-6)
     assert row[0] == 2 and row[10] == 3 and row[38] == 4
+
+
+def _km_ref(t, e):
+    ut = np.unique(t)
+    n_risk = np.array([(t >= u).sum() for u in ut], float)
+    d = np.array([e[t == u].sum() for u in ut], float)
+    s = np.cumprod(1 - d / n_risk)
+    gw = np.cumsum(d / np.maximum(n_risk * (n_risk - d), 1e-300) * (n_risk > d))
+    return ut, n_risk, d, s, s * np.sqrt(gw)
+
+
+def test_kaplan_meier_and_logrank():
+    from scipy.stats import CensoredData, ecdf, logrank
+    rng = np.random.default_rng(5)
+    n = 120
+    g = rng.integers(1, 3, n)
+    t = np.round(rng.exponential(np.where(g == 1, 5.0, 9.0)), 1) + 0.1
+    e = (rng.random(n) < 0.75).astype(float)
+    X = np.column_stack([t, e, g])
+    TE = np.array([[1.0, 2.0]])
+    r, out = algo("KM", dict(X="X", TE="TE", GI="GI", O="O", M="M", T="T", ttype="log-rank",
+                             etype="greenwood", ctype="log"),
+                  {"X": X, "TE": TE, "GI": np.array([[3.0]])}, ["KM", "Mout", "Tout"])
+    KM, M, T = r["KM"], r["Mout"], r["Tout"]
+    for gi in (1, 2):
+        sel = g == gi
+        ut, nr, d, s, se = _km_ref(t[sel], e[sel])
+        blk = KM[:len(ut), 7 * (gi - 1):7 * gi]
+        np.testing.assert_allclose(blk[:, 0], ut)
+        np.testing.assert_allclose(blk[:, 1], nr)
+        np.testing.assert_allclose(blk[:, 2], d)
+        np.testing.assert_allclose(blk[:, 3], s, atol=1e-12)
+        np.testing.assert_allclose(blk[:, 4], se, atol=1e-12)
+        # survival also matches scipy's KM estimator
+        cd = CensoredData(uncensored=t[sel][e[sel] == 1], right=t[sel][e[sel] == 0])
+        np.testing.assert_allclose(blk[:, 3], ecdf(cd).sf.evaluate(ut), atol=1e-12)
+        med = ut[np.argmax(s <= 0.5)] if (s <= 0.5).any() else np.nan
+        assert M[gi - 1, 0] == gi and M[gi - 1, 1] == sel.sum() and M[gi - 1, 2] == e[sel].sum()
+        np.testing.assert_allclose(M[gi - 1, 3], med)
+    c1 = CensoredData(uncensored=t[(g == 1) & (e == 1)], right=t[(g == 1) & (e == 0)])
+    c2 = CensoredData(uncensored=t[(g == 2) & (e == 1)], right=t[(g == 2) & (e == 0)])
+    lr = logrank(c1, c2)
+    np.testing.assert_allclose(T[0, 2], lr.statistic ** 2, rtol=1e-10)
+    np.testing.assert_allclose(T[0, 3], lr.pvalue, rtol=1e-8)
+    assert T[0, 0] == 2 and T[0, 1] == 1
+
+
+def test_kaplan_meier_strata_wilcoxon():
+    rng = np.random.default_rng(6)
+    n = 90
+    g = rng.integers(1, 4, n)
+    s = rng.integers(1, 3, n)
+    t = rng.integers(1, 30, n).astype(float)
+    e = (rng.random(n) < 0.8).astype(float)
+    X = np.column_stack([t, e, g, s])
+    r, _ = algo("KM", dict(X="X", TE="TE", GI="GI", SI="SI", O="O", M="M", T="T", ttype="wilcoxon"),
+                {"X": X, "TE": np.array([[1.0, 2.0]]), "GI": np.array([[3.0]]), "SI": np.array([[4.0]])},
+                ["KM", "Mout", "Tout"])
+    KM, M, T = r["KM"], r["Mout"], r["Tout"]
+    assert KM.shape[1] == 7 * 6 and M.shape == (6, 2 + 5)
+    for gi in (1, 2, 3):
+        for si in (1, 2):
+            c = (gi - 1) * 2 + si
+            sel = (g == gi) & (s == si)
+            ut, nr, d, sv, _ = _km_ref(t[sel], e[sel])
+            np.testing.assert_allclose(KM[:len(ut), 7 * (c - 1) + 3], sv, atol=1e-12)
+            assert M[c - 1, 0] == gi and M[c - 1, 1] == si
+    # stratified Gehan-Wilcoxon reference
+    O = np.zeros(3); E = np.zeros(3); V = np.zeros((3, 3))
+    for si in (1, 2):
+        ms = s == si
+        for u in np.unique(t[ms]):
+            risk = np.array([((t >= u) & ms & (g == k)).sum() for k in (1, 2, 3)], float)
+            dk = np.array([(e * ((t == u) & ms & (g == k))).sum() for k in (1, 2, 3)])
+            N, D = risk.sum(), dk.sum()
+            if D == 0:
+                continue
+            w = N
+            O += w * dk
+            E += w * risk * D / N
+            f = w ** 2 * D * (N - D) / max(N - 1, 1) / N ** 2
+            V += f * (np.diag(risk * N) - np.outer(risk, risk))
+    oe = (O - E)[:2]
+    stat = oe @ np.linalg.solve(V[:2, :2], oe)
+    np.testing.assert_allclose(T[0, 2], stat, rtol=1e-9)
