@@ -492,3 +492,88 @@ def test_kaplan_meier_strata_wilcoxon():
     oe = (O - E)[:2]
     stat = oe @ np.linalg.solve(V[:2, :2], oe)
     np.testing.assert_allclose(T[0, 2], stat, rtol=1e-9)
+
+
+def _cox_ref(t, e, Z, b):
+    """Breslow partial likelihood, score and information by explicit risk-set loops."""
+    l, g, I = 0.0, np.zeros(Z.shape[1]), np.zeros((Z.shape[1],) * 2)
+    w = np.exp(Z @ b)
+    for u in np.unique(t[e == 1]):
+        R = t >= u
+        D = (t == u) & (e == 1)
+        s0 = w[R].sum()
+        s1 = (w[R, None] * Z[R]).sum(0)
+        s2 = (w[R, None, None] * Z[R, :, None] * Z[R, None, :]).sum(0)
+        dk = D.sum()
+        l += (Z[D] @ b).sum() - dk * np.log(s0)
+        g += Z[D].sum(0) - dk * s1 / s0
+        I += dk * (s2 / s0 - np.outer(s1, s1) / s0 ** 2)
+    return l, g, I
+
+
+def test_cox_regression_and_predict():
+    from scipy.optimize import minimize
+    from scipy.stats import chi2
+    rng = np.random.default_rng(7)
+    n = 150
+    Z = rng.standard_normal((n, 3))
+    fac = rng.integers(0, 3, n)
+    F = np.eye(3)[fac]                                   # one factor, 3 levels
+    beta = np.array([0.6, -0.4, 0.2, 0.5, -0.3])
+    full = np.hstack([Z, F[:, 1:]])
+    t = np.round(rng.exponential(1.0 / np.exp(full @ beta)), 2) + 0.01
+    e = (rng.random(n) < 0.8).astype(float)
+    X = np.column_stack([t, e, Z, F])                    # cols 1,2 | 3..5 | 6..8
+    r, _ = algo("Cox", dict(X="X", TE="TE", R="R", M="M", S="S", T="T", COV="COV", RT="RT",
+                            XO="XO", MF="MF", tol=1e-12),
+                {"X": X, "TE": np.array([[1.0], [2.0]]), "R": np.array([[6.0, 8.0]])},
+                ["M", "St", "Tst", "COV", "XO", "RT", "MF"])
+    M, St, Tst, COV, MF = r["M"], r["St"], r["Tst"], r["COV"], r["MF"]
+    # the most frequent factor level is the baseline
+    base = 6 + int(np.argmax(np.bincount(fac, minlength=3)[::-1]) * -1 + 2)
+    kept = [c for c in (6, 7, 8) if c != base]
+    np.testing.assert_array_equal(MF.ravel(), [1, 2, 3, 4, 5] + kept)
+    Zk = X[:, [c - 1 for c in MF.ravel()[2:].astype(int)]]
+    Zk = Zk - Zk.mean(0)
+    ref = minimize(lambda b: -_cox_ref(t, e, Zk, b)[0], np.zeros(5),
+                   jac=lambda b: -_cox_ref(t, e, Zk, b)[1], method="BFGS",
+                   options=dict(gtol=1e-10))
+    np.testing.assert_allclose(M[:, 0], ref.x, atol=1e-6)
+    l, g, I = _cox_ref(t, e, Zk, M[:, 0])
+    np.testing.assert_allclose(COV, np.linalg.inv(I), rtol=1e-8)
+    np.testing.assert_allclose(M[:, 2], np.sqrt(np.diag(np.linalg.inv(I))), rtol=1e-8)
+    l0, g0, I0 = _cox_ref(t, e, Zk, np.zeros(5))
+    np.testing.assert_allclose(St.ravel()[:4], [n, e.sum(), l, -2 * l + 10], rtol=1e-10)
+    np.testing.assert_allclose(Tst[:, 0], [2 * (l - l0), M[:, 0] @ I @ M[:, 0],
+                                           g0 @ np.linalg.solve(I0, g0)], rtol=1e-8)
+    np.testing.assert_allclose(Tst[0, 2], chi2.sf(2 * (l - l0), 5), rtol=1e-8)
+
+    # prediction on new records (original column layout)
+    Y = X[:7].copy()
+    Y[:, 0] = [0.001, 0.05, 0.3, 1.0, 2.5, t.max() + 1, np.median(t)]
+    p, _ = algo("Cox-predict", dict(X="XO", RT="RT", M="M", Y="Y", COV="COV", MF="MF", P="P"),
+                {"X": r["XO"], "RT": r["RT"], "M": M, "Y": Y, "COV": COV, "MF": MF}, ["P"])
+    P = p["P"]
+    cols = MF.ravel()[2:].astype(int) - 1
+    mu = X[:, cols].mean(0)
+    b = M[:, 0]
+    Zc = X[:, cols] - mu
+    w = np.exp(Zc @ b)
+    for i in range(7):
+        z = Y[i, cols] - mu
+        lp = z @ b
+        H0 = VH = 0.0
+        Qv = np.zeros(5)
+        for u in np.unique(t[e == 1]):
+            if u > Y[i, 0]:
+                continue
+            R = t >= u
+            dk = ((t == u) & (e == 1)).sum()
+            s0 = w[R].sum()
+            H0 += dk / s0
+            VH += dk / s0 ** 2
+            Qv += dk * (w[R, None] * Zc[R]).sum(0) / s0 ** 2
+        dq = z * H0 - Qv
+        exp_row = [lp, np.sqrt(z @ COV @ z), np.exp(lp), np.exp(lp) * np.sqrt(z @ COV @ z),
+                   H0 * np.exp(lp), np.exp(lp) * np.sqrt(VH + dq @ COV @ dq)]
+        np.testing.assert_allclose(P[i], exp_row, rtol=1e-8, atol=1e-12)
