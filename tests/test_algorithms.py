@@ -577,3 +577,37 @@ def test_cox_regression_and_predict():
         exp_row = [lp, np.sqrt(z @ COV @ z), np.exp(lp), np.exp(lp) * np.sqrt(z @ COV @ z),
                    H0 * np.exp(lp), np.exp(lp) * np.sqrt(VH + dq @ COV @ dq)]
         np.testing.assert_allclose(P[i], exp_row, rtol=1e-8, atol=1e-12)
+
+
+@pytest.mark.parametrize("link,icpt", [(2, 1), (3, 2), (4, 0)])
+def test_step_glm_bernoulli(link, icpt):
+    from scipy.optimize import minimize
+    from scipy.stats import norm
+    rng = np.random.default_rng(11)
+    n, m = 600, 6
+    X = rng.standard_normal((n, m)) + 0.3
+    eta = 1.4 * X[:, 1] - 1.1 * X[:, 4] + (0.3 if icpt else 0.0)
+    inv = {2: lambda e: 1 / (1 + np.exp(-e)), 3: norm.cdf, 4: lambda e: 1 - np.exp(-np.exp(e))}[link]
+    y = (rng.random(n) < inv(eta)).astype(float) * 2 - 1       # labels -1 / 1
+    r, out = algo("StepGLM", dict(X="X", Y="Y", B="B", S="S", link=link, yneg=-1.0, icpt=icpt,
+                                  tol=1e-12, thr=0.001),
+                  {"X": X, "Y": y.reshape(-1, 1)}, ["Bout", "S", "dev"])
+    S = r["S"].ravel().astype(int)
+    assert set(S[:2]) == {2, 5}
+    cols = S - 1
+    A = X[:, cols]
+    if icpt:
+        A = np.hstack([A, np.ones((n, 1))])
+    y01 = (y > 0).astype(float)
+
+    def nll(b):
+        mu = np.clip(inv(A @ b), 1e-12, 1 - 1e-12)
+        return -np.sum(y01 * np.log(mu) + (1 - y01) * np.log(1 - mu))
+    ref = minimize(nll, np.zeros(A.shape[1]), method="BFGS", options=dict(gtol=1e-9))
+    B = r["Bout"]
+    got = B[cols, 0]
+    if icpt:
+        got = np.append(got, B[m, 0])
+    np.testing.assert_allclose(got, ref.x, atol=2e-4)
+    np.testing.assert_allclose(r["dev"], 2 * ref.fun, rtol=1e-6)
+    assert np.all(B[[c for c in range(m) if c not in cols], 0] == 0)
