@@ -102,6 +102,24 @@ __device__ __forceinline__ void load_raw<double>(Raw8<double>& r, const double* 
   }
 }
 
+// unconditional 16-B-aligned loads of 8 elements (vector path of the packed kernel)
+template <typename T>
+__device__ __forceinline__ void load_vec(Raw8<T>& r, const T* __restrict__ p);
+template <>
+__device__ __forceinline__ void load_vec<uint16_t>(Raw8<uint16_t>& r, const uint16_t* __restrict__ p) {
+  r.v = *reinterpret_cast<const uint4*>(p);
+}
+template <>
+__device__ __forceinline__ void load_vec<float>(Raw8<float>& r, const float* __restrict__ p) {
+  r.v[0] = *reinterpret_cast<const float4*>(p);
+  r.v[1] = *reinterpret_cast<const float4*>(p + 4);
+}
+template <>
+__device__ __forceinline__ void load_vec<double>(Raw8<double>& r, const double* __restrict__ p) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.v[i] = *reinterpret_cast<const double2*>(p + 2 * i);
+}
+
 template <typename A>
 __device__ __forceinline__ void unpack(const Raw8<uint16_t>& r, A* x) {
   x[0] = bf2f(r.v.x & 0xffffu); x[1] = bf2f(r.v.x >> 16);
@@ -323,97 +341,95 @@ rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
 }
 
 // ---------------------------------------------------------------------------
-// Packed-fp32 variant for K in {2,4,8} (fp32 accumulate: bf16 / fp32 X).
-// The k dimension is carried in float2 pairs so every dot-product / accumulate
-// FMA is a v_pk_fma_f32 (2 FMAs per lane per instruction), and for C*K <= 64 the
-// lane's slice of V lives in registers for the whole launch (no per-row LDS
-// traffic).  Row-side values (g) are wave-uniform after the DPP reduction.
+// Packed-fp32 kernels for K in {2,4,8} (fp32 accumulate: bf16 / fp32 X), vector rows
+// only (D % 8 == 0, 16-B aligned; the host routes everything else to rowstream_kernel).
+//
+// The k dimension is carried in float2 pairs so every dot-product / accumulate FMA is a
+// v_pk_fma_f32 (2 FMAs per lane per instruction), and for C*K <= 64 the lane's slice of
+// V lives in registers for the whole launch (no per-row LDS traffic).  Row-side values
+// (g) are wave-uniform after the DPP reduction.  The per-row math lives in RowOps and is
+// shared by the two streaming front ends:
+//
+//  * rowstream_dma_kernel (every accumulating mode: XTG and the fused chains) — each wave
+//    owns an R-slot ring in LDS that is filled by LDS-DMA (global_load_lds_dwordx4 for the
+//    X row, global_load_lds_dword for the row-side operand S) and drained with a COUNTED
+//    s_waitcnt vmcnt((R-1) * loads_per_row): R rows per wave stay in flight across the
+//    whole loop.  The LDS reads are inline asm (data and lgkmcnt wait in one statement) so
+//    hipcc's waitcnt pass, which would otherwise drain vmcnt(0) before any ds_read while
+//    an LDS-DMA is outstanding, sees no LDS access to protect.  (Register-staged rings do
+//    not survive hipcc: it sinks the prefetch loads into the consuming iteration and waits
+//    vmcnt(0) there — profiles/mfma_chain_experiments.md.)
+//  * rowstream_pk_kernel (XV, whose per-row stores would share vmcnt with the ring) —
+//    register prefetch ring with unconditional (clamped) loads.
+//
+// Out-of-range handling without branches: a row index past the block's range re-reads
+// the block's last row, a column chunk past D re-reads the row's last chunk.  Those values
+// meet zero V rows (phase 1), a zero row weight (phase 2) or accumulator columns that are
+// never written out.
 // ---------------------------------------------------------------------------
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) char lds_char;
 
-template <typename T, int K, int J, int MODE, int R>
-__global__ void __launch_bounds__(BLOCK)
-rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
-                    const float* __restrict__ V, int ldv,
-                    const float* __restrict__ S, int lds, int sbc,
-                    float* __restrict__ out, int ldo, int64_t rows_per_block) {
+template <typename T, int K, int J, int MODE>
+struct RowOps {
   using MI = ModeInfo<MODE>;
-  constexpr int C = J * 8;
-  constexpr int K2 = K / 2;
-  constexpr bool VREG = MI::needV && (C * K <= 64);
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sV = reinterpret_cast<float*>(smem);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int Dp = J * 512;
+  static constexpr int C = J * 8;
+  static constexpr int K2 = K / 2;
+  static constexpr bool VREG = MI::needV && (C * K <= 64);
+  static constexpr bool NEEDS = (MODE == XTWXV || MODE == XTXVY || MODE == XTPSXV || MODE == XTG);
 
   f2 vreg[VREG ? C : 1][VREG ? K2 : 1];
-  if constexpr (MI::needV) {
-    for (int i = threadIdx.x; i < Dp * K; i += BLOCK) {
-      int d = i / K, k = i - d * K;
-      sV[i] = (d < D) ? V[(int64_t)d * ldv + k] : 0.f;
-    }
-    __syncthreads();
-    if constexpr (VREG) {
-#pragma unroll
-      for (int j = 0; j < J; ++j)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-#pragma unroll
-          for (int kk = 0; kk < K2; ++kk) {
-            const float* p = sV + (((j * 64 + lane) * 8 + e) * K + 2 * kk);
-            vreg[j * 8 + e][kk] = f2{p[0], p[1]};
-          }
-    }
-  }
-
   f2 acc[MI::accum ? C : 1][MI::accum ? K2 : 1];
-  if constexpr (MI::accum) {
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int kk = 0; kk < K2; ++kk) acc[c][kk] = f2{0.f, 0.f};
-  }
+  const float* sV;
+  int lane;
 
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
-  // R = prefetch depth: each wave keeps R of its future rows in flight (packed, so a
-  // prefetched bf16 row costs 4*J VGPRs) while it processes one row; deeper rings put
-  // more bytes in flight per SIMD (Little's law at ~6 TB/s needs ~10 MB chip-wide).
-  constexpr int STEP = WAVES * R;
-
-  // row-side operand (weights / targets / probabilities / g) for the same rows rides in
-  // the ring too, so its (wave-uniform) load latency is hidden behind R-1 rows of work
-  constexpr bool NEEDS = (MODE == XTWXV || MODE == XTXVY || MODE == XTPSXV || MODE == XTG);
-  constexpr int KS = NEEDS ? K : 1;
-  Raw8<T> ring[R][J];
-  float sring[R][KS];
-  auto load_s = [&](float (&dst)[KS], const int64_t rr) {
-    if constexpr (NEEDS) {
+  // stage V (D x K, zero-padded to J*512 rows) in LDS, then the lane's slice in registers
+  __device__ __forceinline__ void init(const float* __restrict__ V, int ldv, int D, float* smemV, int ln) {
+    lane = ln;
+    sV = smemV;
+    constexpr int Dp = J * 512;
+    if constexpr (MI::needV) {
+      for (int i = threadIdx.x; i < Dp * K; i += BLOCK) {
+        int d = i / K, k = i - d * K;
+        smemV[i] = (d < D) ? V[(int64_t)d * ldv + k] : 0.f;
+      }
+      __syncthreads();
+      if constexpr (VREG) {
 #pragma unroll
-      for (int k = 0; k < K; ++k) dst[k] = S[rr * (int64_t)lds + (((MODE == XTWXV || MODE == XTXVY) && sbc) ? 0 : k)];
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int kk = 0; kk < K2; ++kk) {
+              const float* p = smemV + (((j * 64 + lane) * 8 + e) * K + 2 * kk);
+              vreg[j * 8 + e][kk] = f2{p[0], p[1]};
+            }
+      }
     }
-  };
-  int64_t base = r0 + wave;
+    if constexpr (MI::accum) {
 #pragma unroll
-  for (int p = 0; p < R; ++p) {
-    const int64_t rp = base + p * WAVES;
-    if (rp < r1) {
+      for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int j = 0; j < J; ++j) load_raw<T>(ring[p][j], X + rp * (int64_t)D, (j * 64 + lane) * 8, D, vec);
-      load_s(sring[p], rp);
+        for (int kk = 0; kk < K2; ++kk) acc[c][kk] = f2{0.f, 0.f};
     }
   }
 
-  auto process = [&](const Raw8<T> (&cur)[J], const float (&sv)[KS], const int64_t r) {
+  // one row: cur = the lane's 8*J elements, sl = lane k's S[r][k]
+  __device__ __forceinline__ void process(const Raw8<T> (&cur)[J], const float sl, const int64_t r,
+                                          const bool valid, float* __restrict__ out, int ldo) {
     float x[C];
 #pragma unroll
     for (int j = 0; j < J; ++j) unpack<float>(cur[j], x + j * 8);
+    float sv[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      sv[k] = NEEDS ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sl), k)) : 0.f;
     f2 g[K2];
     if constexpr (MI::needV) {
-      f2 u[K2];
+      // two partial sums per k pair: halves the dependent-FMA chain of the dot products
+      f2 u0[K2], u1[K2];
 #pragma unroll
-      for (int kk = 0; kk < K2; ++kk) u[kk] = f2{0.f, 0.f};
+      for (int kk = 0; kk < K2; ++kk) { u0[kk] = f2{0.f, 0.f}; u1[kk] = f2{0.f, 0.f}; }
 #pragma unroll
       for (int c = 0; c < C; ++c) {
 #pragma unroll
@@ -425,19 +441,23 @@ rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
             const float* pv = sV + ((((c >> 3) * 64 + lane) * 8 + (c & 7)) * K + 2 * kk);
             vv = f2{pv[0], pv[1]};
           }
-          u[kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, vv, u[kk]);
+          if (c & 1) u1[kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, vv, u1[kk]);
+          else       u0[kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, vv, u0[kk]);
         }
       }
       float us[K];
 #pragma unroll
       for (int kk = 0; kk < K2; ++kk) {
-        us[2 * kk] = wave_sum(u[kk].x);
-        us[2 * kk + 1] = wave_sum(u[kk].y);
+        const f2 u = u0[kk] + u1[kk];
+        us[2 * kk] = wave_sum(u.x);
+        us[2 * kk + 1] = wave_sum(u.y);
       }
       if constexpr (MODE == XV) {
+        if (valid) {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-          if (lane == k) out[r * (int64_t)ldo + k] = us[k];
+          for (int k = 0; k < K; ++k)
+            if (lane == k) out[r * (int64_t)ldo + k] = us[k];
+        }
         return;
       } else {
         float gs[K];
@@ -458,63 +478,237 @@ rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
           for (int k = 0; k < K; ++k) gs[k] = q[k] - pr[k] * sq;
         }
 #pragma unroll
-        for (int kk = 0; kk < K2; ++kk) g[kk] = f2{gs[2 * kk], gs[2 * kk + 1]};
+        for (int kk = 0; kk < K2; ++kk)
+          g[kk] = valid ? f2{gs[2 * kk], gs[2 * kk + 1]} : f2{0.f, 0.f};
       }
     } else {  // XTG
 #pragma unroll
-      for (int kk = 0; kk < K2; ++kk) g[kk] = f2{sv[2 * kk], sv[2 * kk + 1]};
+      for (int kk = 0; kk < K2; ++kk) g[kk] = valid ? f2{sv[2 * kk], sv[2 * kk + 1]} : f2{0.f, 0.f};
     }
+    if constexpr (MI::accum) {
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+      for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int kk = 0; kk < K2; ++kk)
-        acc[c][kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, g[kk], acc[c][kk]);
+        for (int kk = 0; kk < K2; ++kk)
+          acc[c][kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, g[kk], acc[c][kk]);
+    }
+  }
+
+  // combine the 4 waves' accumulators through LDS (red: J*512*K floats), one partial per block
+  __device__ __forceinline__ void reduce(float* red, int wave, float* __restrict__ out, int D) {
+    if constexpr (MI::accum) {
+      __syncthreads();
+      for (int w = 0; w < WAVES; ++w) {
+        if (wave == w) {
+#pragma unroll
+          for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+#pragma unroll
+              for (int kk = 0; kk < K2; ++kk) {
+                int idx = ((j * 64 + lane) * 8 + e) * K + 2 * kk;
+                f2 a = acc[j * 8 + e][kk];
+                if (w == 0) { red[idx] = a.x; red[idx + 1] = a.y; }
+                else { red[idx] += a.x; red[idx + 1] += a.y; }
+              }
+        }
+        __syncthreads();
+      }
+      float* dst = out + (int64_t)blockIdx.x * D * K;
+      for (int i = threadIdx.x; i < D * K; i += BLOCK) dst[i] = red[i];
+    }
+  }
+};
+
+// lane's clamped element offset of its 8-element chunk j (D % 8 == 0)
+__device__ __forceinline__ int chunk_off(int j, int lane, int D) {
+  const int c0 = (j * 64 + lane) * 8;
+  return (c0 < D) ? c0 : D - 8;
+}
+
+// ---------------------------------------------------------------------------
+// register-ring front end (XV)
+// ---------------------------------------------------------------------------
+template <typename T, int K, int J, int MODE, int R>
+__global__ void __launch_bounds__(BLOCK)
+rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D,
+                    const float* __restrict__ V, int ldv,
+                    const float* __restrict__ S, int lds, int sbc,
+                    float* __restrict__ out, int ldo, int64_t rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using OPS = RowOps<T, K, J, MODE>;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  OPS ops;
+  ops.init(V, ldv, D, reinterpret_cast<float*>(smem), lane);
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
+  const int64_t rlast = r1 - 1;
+  constexpr int STEP = WAVES * R;
+  int coff[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) coff[j] = chunk_off(j, lane, D);
+  const int scol = ((MODE == XTWXV || MODE == XTXVY) && sbc) ? 0 : (lane < K ? lane : K - 1);
+
+  Raw8<T> ring[R][J];
+  float sring[R];
+  auto fetch = [&](Raw8<T> (&dst)[J], float& sdst, int64_t rr) {
+    rr = (rr < rlast) ? rr : rlast;
+    const T* row = X + rr * (int64_t)D;
+#pragma unroll
+    for (int j = 0; j < J; ++j) load_vec<T>(dst[j], row + coff[j]);
+    if constexpr (OPS::NEEDS) {
+      sdst = S[rr * (int64_t)lds + scol];
+    } else {
+      sdst = 0.f;
+    }
   };
+  int64_t base = r0 + wave;
+#pragma unroll
+  for (int p = 0; p < R; ++p) fetch(ring[p], sring[p], base + p * WAVES);
 
   for (; base < r1; base += STEP) {
 #pragma unroll
     for (int p = 0; p < R; ++p) {
       const int64_t r = base + p * WAVES;   // wave-uniform
-      if (r < r1) {
-        Raw8<T> cur[J];
+      Raw8<T> cur[J];
 #pragma unroll
-        for (int j = 0; j < J; ++j) cur[j] = ring[p][j];
-        float sv[KS];
-#pragma unroll
-        for (int k = 0; k < KS; ++k) sv[k] = sring[p][k];
-        const int64_t rn = r + STEP;
-        if (rn < r1) {
-#pragma unroll
-          for (int j = 0; j < J; ++j) load_raw<T>(ring[p][j], X + rn * (int64_t)D, (j * 64 + lane) * 8, D, vec);
-          load_s(sring[p], rn);
-        }
-        process(cur, sv, r);
-      }
+      for (int j = 0; j < J; ++j) cur[j] = ring[p][j];
+      const float sl = sring[p];
+      fetch(ring[p], sring[p], r + STEP);
+      ops.process(cur, sl, r, r < r1, out, ldo);
     }
   }
+  ops.reduce(reinterpret_cast<float*>(smem), wave, out, D);
+}
 
-  if constexpr (MI::accum) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);
-    for (int w = 0; w < WAVES; ++w) {
-      if (wave == w) {
+// ---------------------------------------------------------------------------
+// LDS-DMA front end (XTG and the fused chains)
+// ---------------------------------------------------------------------------
+template <typename T> struct DmaShape {
+  static constexpr int PIECES = (int)sizeof(T) / 2;   // 16-B pieces per 8-element chunk
+};
+
+__device__ __forceinline__ uint4 lds_read_b128(uint32_t addr) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(addr) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_read_row_bf16(Raw8<uint16_t> (&cur)[1], float& s, uint32_t xa, uint32_t sa) {
+  uint4 v;
+  uint32_t t;
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(v), "=&v"(t) : "v"(xa), "v"(sa) : "memory");
+  cur[0].v = v;
+  s = __uint_as_float(t);
+}
+__device__ __forceinline__ void lds_read_row_bf16(Raw8<uint16_t> (&cur)[2], float& s, uint32_t xa, uint32_t sa) {
+  uint4 v0, v1;
+  uint32_t t;
+  asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:1024\n\tds_read_b32 %2, %4\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(v0), "=&v"(v1), "=&v"(t) : "v"(xa), "v"(sa) : "memory");
+  cur[0].v = v0;
+  cur[1].v = v1;
+  s = __uint_as_float(t);
+}
+template <int J>
+__device__ __forceinline__ void lds_read_row_f32(Raw8<float> (&cur)[J], float& s, uint32_t xa, uint32_t sa) {
 #pragma unroll
-        for (int j = 0; j < J; ++j)
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-#pragma unroll
-            for (int kk = 0; kk < K2; ++kk) {
-              int idx = ((j * 64 + lane) * 8 + e) * K + 2 * kk;
-              f2 a = acc[j * 8 + e][kk];
-              if (w == 0) { red[idx] = a.x; red[idx + 1] = a.y; }
-              else { red[idx] += a.x; red[idx + 1] += a.y; }
-            }
-      }
-      __syncthreads();
-    }
-    float* dst = out + (int64_t)blockIdx.x * D * K;
-    for (int i = threadIdx.x; i < D * K; i += BLOCK) dst[i] = red[i];
+  for (int j = 0; j < J; ++j) {
+    const uint4 a = lds_read_b128(xa + (2 * j) * 1024);
+    const uint4 b = lds_read_b128(xa + (2 * j + 1) * 1024);
+    cur[j].v[0] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+    cur[j].v[1] = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
   }
+  uint32_t t;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(t) : "v"(sa) : "memory");
+  s = __uint_as_float(t);
+}
+
+template <int N> __device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+
+// LDS bytes of the DMA front end: reduction / V region + WAVES rings of R slots
+template <typename T, int K, int J, int R>
+constexpr size_t dma_lds_bytes() {
+  return (size_t)J * 512 * K * 4 + (size_t)WAVES * R * (J * DmaShape<T>::PIECES * 1024 + 256);
+}
+
+template <typename T, int K, int J, int MODE, int R>
+__global__ void __launch_bounds__(BLOCK)
+rowstream_dma_kernel(const T* __restrict__ X, int64_t N, int D,
+                     const float* __restrict__ V, int ldv,
+                     const float* __restrict__ S, int lds, int sbc,
+                     float* __restrict__ out, int64_t rows_per_block) {
+  static_assert(MODE != XV, "row-output mode uses the register-ring front end");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using OPS = RowOps<T, K, J, MODE>;
+  constexpr int PIECES = DmaShape<T>::PIECES;
+  constexpr int XB = J * PIECES * 1024;       // X bytes of one slot (lane-linear 16-B pieces)
+  constexpr int SLOT = XB + 256;              // + S: 64 lanes x 4 B
+  constexpr int NPR = J * PIECES + (OPS::NEEDS ? 1 : 0);   // LDS-DMA instructions per row
+  constexpr int STEP = WAVES * R;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  OPS ops;
+  ops.init(V, ldv, D, reinterpret_cast<float*>(smem), lane);
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
+  const int64_t rlast = r1 - 1;
+  int coff[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) coff[j] = chunk_off(j, lane, D);
+  const int scol = ((MODE == XTWXV || MODE == XTXVY) && sbc) ? 0 : (lane < K ? lane : K - 1);
+
+  const int ring_off = J * 512 * K * 4 + wave * (R * SLOT);
+  lds_char* ring = (lds_char*)(smem) + ring_off;
+  const uint32_t ring_addr = (uint32_t)(uintptr_t)ring;
+
+  auto fetch = [&](int slot, int64_t rr) {
+    rr = (rr < rlast) ? rr : rlast;
+    const T* row = X + rr * (int64_t)D;
+    lds_char* sb = ring + slot * SLOT;
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int h = 0; h < PIECES; ++h)
+        __builtin_amdgcn_global_load_lds((const void*)(row + coff[j] + h * (8 / PIECES)),
+                                         (void __attribute__((address_space(3)))*)(sb + (j * PIECES + h) * 1024),
+                                         16, 0, 0);
+    if constexpr (OPS::NEEDS)
+      __builtin_amdgcn_global_load_lds((const void*)(S + rr * (int64_t)lds + scol),
+                                       (void __attribute__((address_space(3)))*)(sb + XB), 4, 0, 0);
+  };
+
+  int64_t base = r0 + wave;
+#pragma unroll
+  for (int p = 0; p < R; ++p) fetch(p, base + p * WAVES);
+
+  for (; base < r1; base += STEP) {
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
+      const int64_t r = base + p * WAVES;   // wave-uniform
+      wait_vmcnt<(R - 1) * NPR>();          // slot p landed; R-1 rows stay in flight
+      Raw8<T> cur[J];
+      float sl;
+      const uint32_t xa = ring_addr + p * SLOT + lane * 16;
+      const uint32_t sa = ring_addr + p * SLOT + XB + lane * 4;
+      if constexpr (sizeof(T) == 2) {
+        lds_read_row_bf16(cur, sl, xa, sa);
+      } else {
+        lds_read_row_f32<J>(cur, sl, xa, sa);
+      }
+      if constexpr (!OPS::NEEDS) sl = 0.f;
+      fetch(p, r + STEP);                   // refill the slot (its LDS reads have retired)
+      ops.process(cur, sl, r, r < r1, out, 0);
+    }
+  }
+  wait_vmcnt<0>();                          // no LDS-DMA may outlive the block's LDS
+  ops.reduce(reinterpret_cast<float*>(smem), wave, out, D);
 }
 
 }  // namespace sysml
@@ -525,12 +719,6 @@ rowstream_pk_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
 using namespace sysml;
 
 static int g_rows_per_iter = 0;   // 0 = auto, else rows per iteration (generic) / prefetch depth (pk)
-#ifndef PF_DEFAULT_BF16
-#define PF_DEFAULT_BF16 4
-#endif
-#ifndef PF_DEFAULT_F32
-#define PF_DEFAULT_F32 1
-#endif
 static int g_variant = 0;         // 0 = auto (packed fp32 where applicable), 1 = generic scalar kernel
 
 template <typename T, typename A, int K, int J, int MODE>
@@ -548,23 +736,22 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
                    (g_rows_per_iter == 0 && sizeof(A) == 4 && (MODE == XV || MODE == XTXV || MODE == ROWSSQ ||
                                                                MODE == ROWSUM || (K == 1 && MI::accum)));
   if constexpr (sizeof(A) == 4 && K >= 2 && MODE <= XTPSXV) {
-    if (g_variant != 1) {   // packed-fp32 kernel (default)
-      // prefetch-ring depth: knob 1..4, else tuned default (bf16 rows are half the bytes,
-      // so they need twice the rows in flight for the same HBM occupancy)
-      // measured (profiles/rowstream_kbench_r1_prefetch.txt): bf16 chains like 4 rows in
-      // flight per wave, bf16 XV / XTG 3; fp32 rows are twice the bytes, 1 suffices
-      int depth = g_rows_per_iter ? g_rows_per_iter
-                                  : (sizeof(T) == 2 ? ((MODE == XV || MODE == XTG) ? 3 : PF_DEFAULT_BF16)
-                                                    : PF_DEFAULT_F32);
+    if (g_variant != 1 && vec && (D % 8) == 0) {   // packed-fp32 kernels (vector rows only)
+      // rows in flight per wave: knob (1-2 -> 2, 3+ -> 4), else bf16 4 / fp32 2 (same bytes)
+      const int knob = g_rows_per_iter;
+      const bool deep = knob ? (knob > 2) : (sizeof(T) == 2);
+      if constexpr (MODE == XV) {
 #define SYSML_PK(PF) hipLaunchKernelGGL((rowstream_pk_kernel<T, K, J, MODE, PF>), dim3(grid), dim3(BLOCK), sh, st, \
-          (const T*)X, N, D, vec, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, ldo, rpb)
-      switch (depth) {
-        case 1: SYSML_PK(1); break;
-        case 2: SYSML_PK(2); break;
-        case 3: SYSML_PK(3); break;
-        default: SYSML_PK(4); break;
-      }
+          (const T*)X, N, D, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, ldo, rpb)
+        if (deep) SYSML_PK(4); else SYSML_PK(2);
 #undef SYSML_PK
+      } else {
+        const size_t shd = deep ? dma_lds_bytes<T, K, J, 4>() : dma_lds_bytes<T, K, J, 2>();
+#define SYSML_DMA(PF) hipLaunchKernelGGL((rowstream_dma_kernel<T, K, J, MODE, PF>), dim3(grid), dim3(BLOCK), shd, st, \
+          (const T*)X, N, D, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, rpb)
+        if (deep) SYSML_DMA(4); else SYSML_DMA(2);
+#undef SYSML_DMA
+      }
       return hipGetLastError() == hipSuccess ? 0 : -2;
     }
   }
