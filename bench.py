@@ -9,8 +9,8 @@ on a 10M x 1K dense synthetic matrix (perftest settings), on N GPUs of one node.
 One step = compile + execute scripts/algorithms/LinearRegCG.dml (icpt=0, maxi=20,
 tol=1e-4, reg=0.01) followed by compile + execute scripts/algorithms/MultiLogReg.dml
 (k=5 classes, icpt=0, moi=20, mii=5, tol=1e-4, reg=0.01) — the reference's
-scripts/perftest/runLinearRegCG.sh / runMultiLogReg.sh settings.  Synthetic data is
-generated directly in HBM (dense, sparsity 0.9 as genMultinomialData.sh), row-
+scripts/perftest/runLinearRegCG.sh / runMultiLogReg.sh settings.  The inputs follow the
+perftest data generators (gen_data below), are generated directly in HBM and row-
 partitioned across ranks (strong scaling: total work fixed), outside the timed region.
 X is stored bf16 (fp32 accumulation in every kernel); all vectors/iterates are fp32.
 """
@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -29,39 +30,60 @@ import torch  # noqa: E402
 METRIC = "end-to-end sec for LinregCG + MLogReg on 10Mx1K dense (perftest) at 1/2/4/8 GPU"
 
 
-def gen_data(ctx, rows, cols, classes, dtype, seed=7):
-    """Dense synthetic X (90% non-zeros), regression target y and class labels, row-partitioned."""
+def gen_data(ctx, rows, cols, classes, dtype, sparsity=0.9, seed=7):
+    """The perftest inputs, generated directly in HBM and row-partitioned across ranks
+    (each rank draws its rows from its own generator stream; model weights come from a
+    shared seed so every rank uses the same ones):
+
+    * LinregCG runs on the binomial data of scripts/perftest/genBinomialData.sh ->
+      scripts/datagen/genRandData4LogisticRegression.dml (N 1000 maxFeature=5 maxWeight=5,
+      addNoise=1, no intercept, sparsity 0.9, labels 1/2):
+        X = 5 * U(-1, 1) with 90% non-zeros,  w = 5 * U(-1, 1),
+        y = 1 + (sigmoid(X w) >= r),  r ~ U(0, 1)
+    * MultiLogReg runs on the multinomial data of genMultinomialData.sh ->
+      scripts/datagen/genRandData4Multinomial.dml (N 1000 sparsity 0.9, 5 categories, no
+      intercept):
+        X = U(1, 5) with 90% non-zeros,  B = U(-1, 1) * 3 / sqrt(1000 * 0.9)  (D x 4),
+        P = exp(X B) / (1 + rowSums(exp(X B))),  y = 1 + rowSums(cumsum(P) < r),
+        and the last 5 rows take labels 1..5 so every class occurs.
+    """
     from systemml_amd.parallel import dist as D
-    from systemml_amd.ops import core as C
     dev = torch.device("cuda", torch.cuda.current_device())
-    if ctx is not None:
-        s, e = ctx.partition(rows)
-    else:
-        s, e = 0, rows
+    s, e = ctx.partition(rows) if ctx is not None else (0, rows)
     n = e - s
     g = torch.Generator(device=dev)
     g.manual_seed(seed + 7919 * s)
-    X = torch.empty((n, cols), dtype=dtype, device=dev)
-    step = 1 << 19
+    gw = torch.Generator(device=dev)
+    gw.manual_seed(seed)
+    w = (torch.rand((cols, 1), generator=gw, device=dev) * 2 - 1) * 5.0
+    B = (torch.rand((cols, classes - 1), generator=gw, device=dev) * 2 - 1) * (3.0 / math.sqrt(cols * sparsity))
+    X1 = torch.empty((n, cols), dtype=dtype, device=dev)
+    X2 = torch.empty((n, cols), dtype=dtype, device=dev)
+    y1 = torch.empty((n, 1), device=dev)
+    y2 = torch.empty((n, 1), device=dev)
+    step = 1 << 18
     for a in range(0, n, step):
         b = min(n, a + step)
-        blk = torch.rand((b - a, cols), generator=g, device=dev)
-        blk.mul_(torch.rand((b - a, cols), generator=g, device=dev) < 0.9)
-        X[a:b] = blk.to(dtype)
-        del blk
-    gw = torch.Generator(device=dev)
-    gw.manual_seed(seed)            # identical model weights on every rank
-    w = torch.randn((cols, 1), generator=gw, device=dev)
-    W = torch.randn((cols, classes), generator=gw, device=dev)
-    y = C.mm(X, w) + 0.1 * torch.randn((n, 1), generator=g, device=dev)
-    sc = C.mm(X, W)
-    sc = sc - sc.mean(1, keepdim=True)
-    gum = -torch.log(-torch.log(torch.rand((n, classes), generator=g, device=dev).clamp_min(1e-20)))
-    lab = (torch.argmax(sc / sc.std() * 2.0 + gum, 1, keepdim=True) + 1).float()
+        m = b - a
+        blk = torch.rand((m, cols), generator=g, device=dev).mul_(10.0).sub_(5.0)
+        blk.mul_(torch.rand((m, cols), generator=g, device=dev) < sparsity)
+        xb = blk.to(dtype)
+        X1[a:b] = xb
+        prob = torch.sigmoid(xb.float() @ w)
+        y1[a:b] = 1.0 + (prob >= torch.rand((m, 1), generator=g, device=dev)).float()
+        blk = torch.rand((m, cols), generator=g, device=dev).mul_(4.0).add_(1.0)
+        blk.mul_(torch.rand((m, cols), generator=g, device=dev) < sparsity)
+        xb = blk.to(dtype)
+        X2[a:b] = xb
+        E = torch.exp(xb.float() @ B)
+        P = torch.cumsum(E / (1.0 + E.sum(1, keepdim=True)), 1)
+        y2[a:b] = 1.0 + (P < torch.rand((m, 1), generator=g, device=dev)).float().sum(1, keepdim=True)
+        del blk, xb, prob, E, P
+    if e == rows and n >= classes:
+        y2[n - classes:] = torch.arange(1, classes + 1, device=dev, dtype=torch.float32).reshape(-1, 1)
     if ctx is not None:
-        return (D.from_local(ctx, X, rows), D.from_local(ctx, y.contiguous(), rows),
-                D.from_local(ctx, lab.contiguous(), rows))
-    return X, y.contiguous(), lab.contiguous()
+        return tuple(D.from_local(ctx, t, rows) for t in (X1, y1, X2, y2))
+    return X1, y1, X2, y2
 
 
 def main():
@@ -78,6 +100,8 @@ def main():
     ap.add_argument("--mii", type=int, default=5)
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--stats", action="store_true")
+    ap.add_argument("--gpu-min-cells", type=int, default=None,
+                    help="host-placement threshold for small matrices (default: config default)")
     a = ap.parse_args()
 
     from systemml_amd.parallel import dist as D
@@ -96,6 +120,8 @@ def main():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
 
     cfg = DMLConfig(precision="single", dist_min_rows=100_000)
+    if a.gpu_min_cells is not None:
+        cfg.gpu_min_cells = a.gpu_min_cells
     from systemml_amd.ops.backend import backend
     backend.configure(cfg)
     xdt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[a.xdtype]
@@ -104,7 +130,7 @@ def main():
         backend.configure(cfg)
 
     t0 = time.perf_counter()
-    X, y, lab = gen_data(ctx, a.rows, a.cols, a.classes, xdt)
+    X1, y1, X2, lab = gen_data(ctx, a.rows, a.cols, a.classes, xdt)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
 
@@ -118,10 +144,10 @@ def main():
     out = (lambda s: log.append(s)) if not a.verbose else (lambda s: print(s, file=sys.stderr))
 
     def step(stats=None):
-        cs1 = EX.compile_script(src_lr, args_lr, inputs={"X": X, "y": y}, outputs=["B_out"], config=cfg)
-        r1, _ = EX.execute(cs1, {"X": X, "y": y}, out=out, dist=ctx, stats=stats)
-        cs2 = EX.compile_script(src_mlr, args_mlr, inputs={"X": X, "Y_vec": lab}, outputs=["B_out"], config=cfg)
-        r2, _ = EX.execute(cs2, {"X": X, "Y_vec": lab}, out=out, dist=ctx, stats=stats)
+        cs1 = EX.compile_script(src_lr, args_lr, inputs={"X": X1, "y": y1}, outputs=["B_out"], config=cfg)
+        r1, _ = EX.execute(cs1, {"X": X1, "y": y1}, out=out, dist=ctx, stats=stats)
+        cs2 = EX.compile_script(src_mlr, args_mlr, inputs={"X": X2, "Y_vec": lab}, outputs=["B_out"], config=cfg)
+        r2, _ = EX.execute(cs2, {"X": X2, "Y_vec": lab}, out=out, dist=ctx, stats=stats)
         return r1["B_out"], r2["B_out"]
 
     for _ in range(a.warmup):
@@ -149,7 +175,8 @@ def main():
             "metric": METRIC, "value": round(sec, 4), "unit": "s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(sec * 1000, 2), "higher_is_better": False,
             "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if a.xdtype == "bf16" else a.xdtype,
-            "data": "synthetic (in-HBM datagen, dense sparsity 0.9)",
+            "data": "synthetic (perftest generators genRandData4LogisticRegression / genRandData4Multinomial, "
+                    "sparsity 0.9, generated in HBM)",
             "config": {"model": "LinregCG+MultiLogReg (perftest: maxi=%d; k=%d moi=%d mii=%d)"
                                 % (a.maxi, a.classes, a.moi, a.mii),
                        "global_batch": a.rows, "seq_len": a.cols, "rows": a.rows, "cols": a.cols,

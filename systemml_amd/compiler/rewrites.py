@@ -128,6 +128,8 @@ class Rewriter:
             return self._rw_agg(h)
         if op == "mm":
             return self._rw_mm(h)
+        if op == "bi" and h.p.get("name") in ("table", "ctable"):
+            return self._match_onehot(h)
         return h
 
     def _rw_binary(self, h):
@@ -215,6 +217,12 @@ class Rewriter:
         The reference compiles this permutation-matrix product to PMMJ instead of
         materialising the (sparse) selection matrix; a dense n x L selection matrix would
         cost n*L cells here."""
+        if a.op == "bi" and a.p.get("name") == "_onehot":     # already rewritten seq-ctable
+            y, n, k = a.inputs
+            if _is_lit(n, -1):
+                return None
+            self._count("pmm-gather")
+            return Hop("bi", [y, b, n, k], {"name": "_gather_rows", "npos": 4}, dt="M", pos=h.pos)
         if a.op != "bi" or a.p.get("name") not in ("table", "ctable") or a.named:
             return None
         npos = a.p.get("npos", len(a.inputs))
@@ -230,6 +238,28 @@ class Rewriter:
         ncols = a.inputs[3] if npos == 4 else lit(-1)
         self._count("pmm-gather")
         return Hop("bi", [a.inputs[1], b, nrows, ncols], {"name": "_gather_rows", "npos": 4}, dt="M", pos=h.pos)
+
+    def _match_onehot(self, h):
+        """table(seq(1, N), y [, N, K])  ->  one-hot of y (no materialised row-index sequence;
+        the reference's ctable with a sequence input is the same special case,
+        CtableCPInstruction / LibMatrixReorg 'seq-ctable')."""
+        if h.named:
+            return h
+        npos = h.p.get("npos", len(h.inputs))
+        if npos not in (2, 4):
+            return h
+        sq = h.inputs[0]
+        if sq.op != "bi" or sq.p.get("name") != "seq" or sq.named or h.inputs[1].dt == "S":
+            return h
+        sargs = sq.inputs[:sq.p.get("npos", len(sq.inputs))]
+        if len(sargs) < 2 or not _is_lit(sargs[0], 1) or (len(sargs) > 2 and not _is_lit(sargs[2], 1)):
+            return h
+        n = h.inputs[2] if npos == 4 else sargs[1]
+        k = h.inputs[3] if npos == 4 else lit(-1)
+        if npos == 2:
+            n = lit(-1)      # as many rows as labels (seq(1, nrow(y)) is the usual form)
+        self._count("seq-ctable")
+        return Hop("bi", [h.inputs[1], n, k], {"name": "_onehot", "npos": 3}, dt="M", pos=h.pos)
 
     def _match_mmchain(self, X, g):
         def is_xv(n):

@@ -126,6 +126,9 @@ class Translator:
                         fb.default_preds[p.name] = Predicate(h, bb.reads)
         blocks = self.build_stmts(prog.statements, main_ctx, {}, types=dict(self.input_types))
         cp = CompiledProgram(blocks, self.functions, prog.source_path)
+        if self.config is None or getattr(self.config, "rewrites", True):
+            from .loops import hoist_program
+            cp.licm_stats = hoist_program(cp)      # before liveness: adds blocks / variables
         # liveness
         for fb in self.functions.values():
             if fb.body is not None:

@@ -21,6 +21,7 @@ class DMLConfig:
     precision: str = "double"           # 'double' | 'single' : compute dtype of matrices on GPU
     bf16_storage_min_cells: int = 0     # >0: large read-only inputs stored bf16 (fp32 accumulate)
     dist_min_rows: int = 100_000        # row-partition matrices with >= rows across ranks (SPMD)
+    gpu_min_cells: int = 16384          # GPU backend: smaller matrices (and their operators) stay on host
     parallelism: int = 8                # parfor local workers
     # compiler
     rewrites: bool = True
@@ -48,6 +49,7 @@ class DMLConfig:
         "sysml.floating.point.precision": ("precision", str),
         "sysml.gpu.storage.bf16.mincells": ("bf16_storage_min_cells", int),
         "sysml.dist.minrows": ("dist_min_rows", int),
+        "sysml.gpu.mincells": ("gpu_min_cells", int),
         "sysml.parallel.ops": ("parallelism", lambda v: 8 if str(v).lower() == "true" else 1),
         "sysml.localtmpdir": ("scratch", str),
         "sysml.scratch": ("scratch", str),

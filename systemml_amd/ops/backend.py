@@ -18,6 +18,7 @@ class Backend:
         self.use_kernels = False
         self.bf16_min_cells = 0
         self.stream_sync = False
+        self.small_cells = 0        # GPU backend: matrices below this many cells live on the host
 
     @property
     def on_gpu(self):
@@ -34,6 +35,7 @@ class Backend:
             prec = "double" if config is None else config.precision
             self.dtype = torch.float32 if prec in ("single", "float", "fp32", "bf16") else torch.float64
             self.bf16_min_cells = 0 if config is None else config.bf16_storage_min_cells
+            self.small_cells = 16384 if config is None else int(config.gpu_min_cells)
             want_k = True if config is None else config.hip_kernels
             if want_k:
                 from . import kernels
@@ -46,18 +48,31 @@ class Backend:
             self.dtype = torch.float64
             self.use_kernels = False
             self.bf16_min_cells = 0
+            self.small_cells = 0
         return self
 
 
 backend = Backend()
 
 
+def home(numel: int) -> torch.device:
+    """Where a matrix of `numel` cells lives: HBM, or host memory for small matrices on a GPU
+    backend (hybrid CP / GPU placement, runtime/instructions.py:_placed)."""
+    if backend.small_cells > 0 and numel < backend.small_cells:
+        return _CPU
+    return backend.device
+
+
+_CPU = torch.device("cpu")
+
+
 def place(t: torch.Tensor) -> torch.Tensor:
     """Move a freshly created/loaded matrix into the backend's memory + dtype."""
     if t.dtype == torch.bfloat16:
         return t.to(backend.device)
-    if t.device != backend.device or t.dtype != backend.dtype:
-        t = t.to(device=backend.device, dtype=backend.dtype)
+    dev = home(t.numel())
+    if t.device != dev or t.dtype != backend.dtype:
+        t = t.to(device=dev, dtype=backend.dtype)
     return t
 
 

@@ -18,6 +18,7 @@ import torch
 
 from ..parser.errors import DMLRuntimeError
 from .backend import backend
+from . import sparse as SP
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libsysml_hip.so")
@@ -100,16 +101,16 @@ def _mgrid(L, mode, X):
     return min(_occ[key], ntiles)
 
 
-def _v3t(V, kp, D):
+def _v3t(V, kp, D, device):
     """V (D x K) -> [16][Dp] bf16: rows 4s+k hold rounding plane s (hi, lo, lo2) of V[:, k]."""
     Dp = 256 * ((D + 255) // 256)
-    v = V.to(torch.float32)
+    v = V.to(device=device, dtype=torch.float32)
     planes = []
     for _ in range(3):
         h = v.to(torch.bfloat16)
         planes.append(h)
         v = v - h.to(torch.float32)
-    out = torch.zeros((16, Dp), dtype=torch.bfloat16, device=V.device)
+    out = torch.zeros((16, Dp), dtype=torch.bfloat16, device=device)
     for s_, h in enumerate(planes):
         out[4 * s_:4 * s_ + V.shape[1], :D] = h.t()
     return out
@@ -121,9 +122,9 @@ def _mchain(mode, X, kp, V=None, S=None, sbc=0):
     grid = _mgrid(L, mode, X)
     if grid <= 0:
         return None
-    V3 = _v3t(V, kp, D) if V is not None else None
+    V3 = _v3t(V, kp, D, X.device) if V is not None else None
     if S is not None:
-        S = S.to(torch.float32).contiguous()
+        S = S.to(device=X.device, dtype=torch.float32).contiguous()
     if mode == XV:
         out = torch.empty((N, kp), dtype=torch.float32, device=X.device)
         ldo = kp
@@ -168,8 +169,8 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def _pad_cols(m, kp, dt):
-    m = m.to(dtype=dt)
+def _pad_cols(m, kp, dt, device=None):
+    m = m.to(dtype=dt) if device is None else m.to(device=device, dtype=dt)
     if m.shape[1] == kp and m.is_contiguous():
         return m
     out = torch.zeros((m.shape[0], kp), dtype=dt, device=m.device)
@@ -217,7 +218,7 @@ def xv(X, V):
         if U is not None:
             _count("mfma.xv")
             return _result(U if kp == K else U[:, :K].contiguous())
-    Vp = _pad_cols(V, kp, adt).contiguous()
+    Vp = _pad_cols(V, kp, adt, X.device).contiguous()
     U = torch.empty((X.shape[0], kp), dtype=adt, device=X.device)
     rc, _ = _launch(XV, X, V=Vp, K=kp, out=U, ldo=kp)
     if rc != 0:
@@ -231,7 +232,7 @@ def xtg(X, G):
     K = G.shape[1]
     kp = _kpad(K)
     code, adt = _xcode(X)
-    Gp = _pad_cols(G, kp, adt).contiguous()
+    Gp = _pad_cols(G, kp, adt, X.device).contiguous()
     if _mfma_ok(X, kp, XTG):
         R = _mchain(XTG, X, kp, S=Gp)
         if R is not None:
@@ -252,17 +253,17 @@ def mmchain(ctype, X, V, W=None):
     K = V.shape[1]
     kp = _kpad(K)
     code, adt = _xcode(X)
-    Vp = _pad_cols(V, kp, adt).contiguous()
+    Vp = _pad_cols(V, kp, adt, X.device).contiguous()
     S = None
     sbc = 0
     if W is not None:
         if W.shape[0] != X.shape[0]:
             return None
         if mode == XTWXV and W.shape[1] == 1:
-            S = W.to(adt).contiguous()
+            S = W.to(device=X.device, dtype=adt).contiguous()
             sbc = 1
         elif W.shape[1] == K:
-            S = _pad_cols(W, kp, adt).contiguous()
+            S = _pad_cols(W, kp, adt, X.device).contiguous()
         else:
             return None
     if _mfma_ok(X, kp, mode):
@@ -284,8 +285,10 @@ def mmchain(ctype, X, V, W=None):
 # dispatch helpers used by ops/core.py
 # ----------------------------------------------------------------------------
 def try_mm(a, b, transA):
-    if not isinstance(b, torch.Tensor) or not b.is_cuda:
+    if not isinstance(b, torch.Tensor) or SP.is_sparse(b):
         return None
+    if not b.is_cuda:
+        b = b.to(a.device)
     if _ok_x(a):
         K = b.shape[1]
         if K <= 8:

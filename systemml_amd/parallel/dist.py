@@ -429,6 +429,18 @@ def rbind(args):
     return local_rows(ctx, full)
 
 
+def onehot(exec_ctx, y, n, k):
+    """Row-aligned one-hot of a row-partitioned label vector (table(seq(1,N), y, N, K))."""
+    from ..runtime import builtins as B
+    if n is not None and int(n) >= 0 and int(n) != y.nrows:
+        return B.b_onehot(exec_ctx, gather(y), n, k)
+    if k is None or int(k) < 0:
+        loc = y.local
+        kmax = float(loc.max().item()) if loc.numel() else 0.0
+        k = int(y.ctx.allreduce_scalar(kmax, "max", device=loc.device if loc.is_cuda else None))
+    return y.like(B.b_onehot(exec_ctx, y.local, y.local.shape[0], k))
+
+
 def table(exec_ctx, A, B, W, dims):
     """ctable(seq(1,N), y, [w], N, K) → one-hot rows stay local; general case gathers."""
     from ..runtime.builtins import b_table

@@ -316,7 +316,8 @@ def b_seq(ctx, frm=None, to=None, incr=None, **kw):
         n = int(math.floor((b - a) / inc + 1e-10)) + 1
     if ctx is not None and ctx.dist is not None and n >= ctx.config.dist_min_rows:
         return C._dist().seq(ctx, a, inc, n)
-    t = a + inc * torch.arange(n, dtype=torch.float64)
+    from ..ops.backend import home
+    t = a + inc * torch.arange(n, dtype=torch.float64, device=home(n))   # generated where it lives
     return place(t.reshape(n, 1))
 
 
@@ -538,6 +539,31 @@ def b_table(ctx, A=None, B=None, W=None, odim1=None, odim2=None, *rest, **kw):
     else:
         wv = torch.full((n,), float(w), dtype=_dt(), device=a.device)
     return _ctable(a, b, wv, dims)
+
+
+@builtin("_onehot")
+def b_onehot(ctx, y, n=None, k=None):
+    """table(seq(1, N), y [, N, K]) without materialising seq (rewrites.py _match_onehot):
+    row i gets a 1 in column round(y[i]); rows beyond N / categories beyond K are dropped.
+    Non-positive categories are an error, as in ctable."""
+    if C.is_dist(y):
+        return C._dist().onehot(ctx, y, n, k)
+    yv = _mat(y).reshape(-1)
+    yi = torch.round(yv).long()
+    if yi.numel() and bool((yi <= 0).any()):
+        raise DMLRuntimeError("ctable: invalid (non-positive) category values")
+    rows = yi.numel() if n is None or _int(n) < 0 else _int(n)
+    cols = (int(yi.max().item()) if yi.numel() else 0) if k is None or _int(k) < 0 else _int(k)
+    m = min(rows, yi.numel())
+    yi = yi[:m]
+    out = torch.zeros((rows, cols), dtype=_dt(), device=yv.device)
+    keep = yi <= cols
+    if not bool(keep.all()):
+        idx = torch.nonzero(keep).reshape(-1)
+        out[idx, yi[idx] - 1] = 1.0
+    else:
+        out[:m].scatter_(1, (yi - 1).reshape(-1, 1), 1.0)
+    return out
 
 
 def _ctable(a, b, wv, dims):

@@ -18,12 +18,19 @@ from . import builtins as B
 
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
+# operators that compute on matrix operands (placement applies); the rest move values around
+_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "tak", "t", "rix", "lix", "bi"}
+_NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
+                "read"}
 
 
 def make_impl(h):
     """Instruction implementation; operators that have no sparse path receive densified
-    operands (sparse matrices: ops/sparse.py)."""
+    operands (sparse matrices: ops/sparse.py), and compute operators run under the
+    hybrid host/HBM placement of `_placed` on a GPU backend."""
     fn, code = _make_impl(h)
+    if h.op in _COMPUTE_OPS and not (h.op == "bi" and h.p.get("name") in _NO_PLACE_BI):
+        fn = _placed(fn)
     if h.op in _SPARSE_OK_OPS or (h.op == "u" and h.p.get("o") in _SPARSE_OK_UNARY):
         return fn, code
     is_sp = SP.is_special
@@ -35,6 +42,47 @@ def make_impl(h):
                 return fn(ctx, [dense(y) for y in a])
         return fn(ctx, a)
     return wrapped, code
+
+
+def _placed(fn):
+    """Hybrid CP / GPU execution (reference: the per-operator CP vs GPU exec-type choice of
+    hops/Hop.java#findExecTypeByMemEstimate with the GPU operator threshold): matrices below
+    `sysml.gpu.mincells` cells live in host memory and their operators run on the CPU, where a
+    small op costs a few microseconds and its scalars are available without a device sync;
+    larger matrices stay resident in HBM.  An operator that mixes the two runs where its
+    largest operand lives (small operands are copied over), and a small result produced in HBM
+    (e.g. the D x K output of a fused t(X) %*% f(X %*% V) pass) is moved to host memory."""
+    import torch
+    from ..ops.backend import backend
+    Tensor = torch.Tensor
+
+    def run(ctx, a):
+        small = backend.small_cells
+        if small <= 0:
+            return fn(ctx, a)
+        dev = None
+        mixed = False
+        for x in a:
+            if type(x) is Tensor:
+                d = x.device.type
+            elif hasattr(x, "local") and type(getattr(x, "local", None)) is Tensor:
+                d = x.local.device.type      # row-partitioned DistMatrix block
+            else:
+                continue
+            if dev is None:
+                dev = d
+            elif d != dev:
+                mixed = True
+        if mixed:
+            gpu = backend.device
+            a = [x.to(gpu, non_blocking=True) if (type(x) is Tensor and x.device.type != "cuda") else x
+                 for x in a]
+        r = fn(ctx, a)
+        if type(r) is Tensor and r.is_cuda and r.numel() < small and r.dtype != torch.bfloat16 \
+                and not r.is_sparse and r.layout == torch.strided:
+            return r.to("cpu")
+        return r
+    return run
 
 
 def _make_impl(h):

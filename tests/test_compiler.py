@@ -1,0 +1,65 @@
+"""Compiler passes: loop-invariant code motion, seq-ctable one-hot rewrite, inter-procedural
+analysis (inlining, literal propagation, unused-function removal), size propagation /
+memory estimates / exec types, and matrix-multiplication chain ordering."""
+import numpy as np
+import pytest
+
+from systemml_amd.api.executor import run, compile_script, explain
+from systemml_amd.conf import DMLConfig
+
+CFG = DMLConfig(gpu=False)
+
+
+def _run(src, inputs=None, outputs=(), **kw):
+    res = run(src, inputs=inputs or {}, outputs=list(outputs), config=CFG, out=lambda s: None, **kw)
+    return {k: (v.numpy() if hasattr(v, "numpy") else v) for k, v in res.items()}
+
+
+def test_licm_hoists_invariant_slice():
+    src = """
+    s = 0
+    i = 0
+    while (i < 3) {
+      Pk = P[, 1:K]
+      s = s + sum(Pk * (i + 1))
+      i = i + 1
+    }
+    """
+    P = np.random.default_rng(0).random((40, 5))
+    r = _run(src, {"P": P, "K": 4}, ["s"])
+    assert np.isclose(r["s"], P[:, :4].sum() * 6)
+    cs = compile_script(src, inputs={"P": P, "K": 4}, outputs=["s"], config=CFG)
+    assert cs.cp.licm_stats.get("hoisted", 0) == 1
+    assert "_licm" in explain(cs.cp)
+
+
+def test_licm_keeps_loop_variant_expressions():
+    src = """
+    s = 0
+    for (i in 1:3) {
+      Q = P[, 1:i]
+      s = s + sum(Q)
+      P = P * 2
+    }
+    """
+    P = np.ones((10, 4))
+    r = _run(src, {"P": P}, ["s"])
+    assert np.isclose(r["s"], 10 * 1 + 10 * 2 * 2 + 10 * 3 * 4)
+    cs = compile_script(src, inputs={"P": P}, outputs=["s"], config=CFG)
+    assert cs.cp.licm_stats.get("hoisted", 0) == 0
+
+
+def test_seq_ctable_becomes_onehot():
+    y = np.array([[2], [1], [3], [3]], float)
+    src = "Y = table(seq(1, nrow(y)), y)\nZ = table(seq(1, 4), y, 4, 2)"
+    r = _run(src, {"y": y}, ["Y", "Z"])
+    np.testing.assert_array_equal(r["Y"], np.eye(3)[[1, 0, 2, 2]])
+    np.testing.assert_array_equal(r["Z"], np.eye(3)[[1, 0, 2, 2]][:, :2] * (y <= 2))
+    cs = compile_script(src, inputs={"y": y}, outputs=["Y"], config=CFG)
+    assert "_onehot" in explain(cs.cp)
+
+
+def test_onehot_rejects_nonpositive_labels():
+    from systemml_amd.parser.errors import DMLRuntimeError
+    with pytest.raises(DMLRuntimeError):
+        _run("Y = table(seq(1, nrow(y)), y)", {"y": np.array([[1.0], [0.0]])}, ["Y"])
