@@ -181,7 +181,28 @@ def _check_bin_dims(a: Tensor, b: Tensor, op):
                               f"{ra}x{ca} vs {rb}x{cb} (op {op})")
 
 
+_PYNUM = (int, float, bool)
+_STRIDED = torch.strided
+
+
 def binary(op, a, b):
+    # fast paths: two Python scalars; dense same-device same-dtype tensors (or tensor-scalar)
+    ta_, tb_ = type(a), type(b)
+    if ta_ in _PYNUM and tb_ in _PYNUM:
+        return S.binary(op, a, b)
+    if ta_ is Tensor and a.layout is _STRIDED and a.dtype is not torch.bfloat16:
+        fn = BIN.get(op)
+        if fn is not None:
+            if tb_ is Tensor:
+                if b.layout is _STRIDED and b.dtype is a.dtype and b.device == a.device:
+                    _check_bin_dims(a, b, op)
+                    return fn(a, b)
+            elif tb_ is int or tb_ is float:
+                return fn(a, b)
+    elif tb_ is Tensor and (ta_ is int or ta_ is float) and b.layout is _STRIDED and b.dtype is not torch.bfloat16:
+        fn = BIN.get(op)
+        if fn is not None:
+            return fn(a, b)
     if CMP.is_compressed(a):
         if op in ("*", "/") and isinstance(b, (int, float)) and not isinstance(b, bool) and (op == "*" or b != 0):
             return a.scale(float(b) if op == "*" else 1.0 / float(b))
