@@ -127,6 +127,8 @@ class Translator:
         blocks = self.build_stmts(prog.statements, main_ctx, {}, types=dict(self.input_types))
         cp = CompiledProgram(blocks, self.functions, prog.source_path)
         if self.config is None or getattr(self.config, "rewrites", True):
+            from . import ipa
+            ipa.run(cp, self.config)                # inter-procedural analysis (inlining, ...)
             from .loops import hoist_program
             cp.licm_stats = hoist_program(cp)      # before liveness: adds blocks / variables
         # liveness

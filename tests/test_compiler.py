@@ -63,3 +63,66 @@ def test_onehot_rejects_nonpositive_labels():
     from systemml_amd.parser.errors import DMLRuntimeError
     with pytest.raises(DMLRuntimeError):
         _run("Y = table(seq(1, nrow(y)), y)", {"y": np.array([[1.0], [0.0]])}, ["Y"])
+
+
+# ---------------------------------------------------------------------------- IPA
+def test_ipa_inlines_small_functions_and_keeps_semantics():
+    src = """
+    scale = function(matrix[double] A, double s) return (matrix[double] B) {
+      B = A * s + 1
+    }
+    half = function(int n) return (double h) {
+      h = n / 2
+    }
+    unused = function(matrix[double] A) return (matrix[double] B) { B = t(A) }
+    Y = scale(X, 2)
+    Z = scale(X, 3)
+    h = half(3)
+    """
+    X = np.arange(6.0).reshape(3, 2)
+    r = _run(src, {"X": X}, ["Y", "Z", "h"])
+    np.testing.assert_allclose(r["Y"], X * 2 + 1)
+    np.testing.assert_allclose(r["Z"], X * 3 + 1)
+    assert r["h"] == 1.5
+    cs = compile_script(src, inputs={"X": X}, outputs=["Y"], config=CFG)
+    assert cs.cp.ipa_stats.get("inlined", 0) == 3
+    assert cs.cp.ipa_stats.get("removed", 0) >= 1
+    e = explain(cs.cp)
+    assert "fcall" not in e and "unused" not in e
+
+
+def test_ipa_keeps_recursive_and_side_effect_functions():
+    src = """
+    fact = function(int n) return (int f) {
+      if (n <= 1) { f = 1 } else { f = n * fact(n - 1) }
+    }
+    noisy = function(double a) return (double b) {
+      print("noisy " + a)
+      b = a + 1
+    }
+    f = fact(5)
+    b = noisy(1.5)
+    """
+    out = []
+    res = run(src, outputs=["f", "b"], config=CFG, out=out.append)
+    assert res["f"] == 120 and res["b"] == 2.5 and out == ["noisy 1.5"]
+    cs = compile_script(src, outputs=["f"], config=CFG)
+    assert cs.cp.ipa_stats.get("inlined", 0) == 0
+    assert any(fb.recursive for fb in cs.cp.functions.values())
+
+
+def test_ipa_propagates_constant_arguments():
+    src = """
+    step = function(matrix[double] A, int k) return (matrix[double] B) {
+      B = A
+      for (i in 1:k) { B = B * 2 }
+    }
+    Y = step(X, 3)
+    Z = step(X + 1, 3)
+    """
+    X = np.ones((2, 2))
+    r = _run(src, {"X": X}, ["Y", "Z"])
+    np.testing.assert_allclose(r["Y"], 8 * X)
+    np.testing.assert_allclose(r["Z"], 16 * X)
+    cs = compile_script(src, inputs={"X": X}, outputs=["Y"], config=CFG)
+    assert cs.cp.ipa_stats.get("literals", 0) == 1
