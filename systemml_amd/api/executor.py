@@ -52,7 +52,12 @@ def compile_script(source, args=None, inputs=(), outputs=(), config=None, pydml=
     if isinstance(inputs, dict):
         input_types = {k: value_dt(v) for k, v in inputs.items()}
     cp = tr.compile(prog, inputs=list(inputs), outputs=outputs, input_types=input_types)
+    from ..compiler import cost
+    shapes = inputs if isinstance(inputs, dict) else None
+    if getattr(config, "rewrites", True):
+        cost.reorder_chains(cp, shapes)          # size-dependent mm-chain order (needs raw DAGs)
     compile_program(cp, make_impl, config)
+    cost.annotate(cp, shapes, config)            # dims, memory estimates, exec types
     t2 = time.perf_counter()
     cs = CompiledScript(cp, config, set(inputs), list(outputs), t1 - t0, t2 - t1)
     cs.source = source

@@ -1,0 +1,413 @@
+"""Size propagation, memory estimates, execution-type selection and the size-dependent
+matrix-multiplication chain optimization (reference: hops/Hop.java refreshSizeInformation
+/ computeMemEstimate / findExecTypeByMemEstimate, hops/OptimizerUtils.java,
+hops/rewrite/RewriteMatrixMultChainOptimization.java, hops/recompile/Recompiler.java).
+
+* `annotate(cp, input_shapes, config)` walks the program in statement order with the
+  known dimensions of every live variable (inputs bound through MLContext / JMLC / the
+  bench, or literals), infers the output dimensions of every HOP, attaches a worst-case
+  dense memory estimate and picks an execution type:
+      CP   scalars and matrices below `gpu_min_cells` (host memory, CPU operators)
+      GPU  larger matrices on a GPU backend (HBM-resident, HIP kernels)
+      DIST matrices with at least `dist_min_rows` rows in an SPMD run (row-partitioned)
+  `-explain hops` prints the dimensions, estimates and exec types.
+* Matrix-multiplication chains A1 %*% ... %*% An (n >= 3) whose dimensions are known are
+  re-parenthesised by the classic O(n^3) dynamic program over the flop count, and the
+  block is re-rewritten so the new shape can become fused operators (for example
+  t(X) %*% X %*% v -> t(X) %*% (X %*% v) -> mmchain, never forming t(X) %*% X).
+* Blocks whose chains have unknown dimensions at compile time are flagged for dynamic
+  recompilation: runtime/program.py re-plans them at first execution from the actual
+  operand shapes (`recompile_block`), cached per shape signature.
+"""
+from __future__ import annotations
+
+from . import hops as H
+from .hops import Hop
+from .blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
+
+UNK = (-1, -1)
+SCALAR = (0, 0)
+
+
+def _lv(h):
+    return h.value if h.op == "lit" else None
+
+
+def _known(d):
+    return d[0] >= 0 and d[1] >= 0
+
+
+def _int_or(v, default=-1):
+    if isinstance(v, bool) or v is None:
+        return default
+    if isinstance(v, (int, float)) and v == v and v >= 0:
+        return int(v)
+    return default
+
+
+def infer(h, dims, env):
+    """Output (rows, cols) of hop h given input dims; (0, 0) for scalars, -1 unknown."""
+    op = h.op
+    ins = [dims.get(c.id, UNK) for c in h.inputs]
+    if op == "lit" or h.dt == "S":
+        return SCALAR
+    if op == "tread":
+        return env.get(h.p["name"], UNK)
+    if op == "b":
+        a, b = ins
+        if a == SCALAR:
+            return b
+        if b == SCALAR:
+            return a
+        if _known(a) and _known(b):
+            return (max(a[0], b[0]), max(a[1], b[1]))
+        return a if _known(a) else b
+    if op == "u":
+        o = h.p["o"]
+        if o in ("nrow", "ncol", "length", "cast_scalar", "cast_double", "cast_int", "cast_bool"):
+            return SCALAR
+        if o == "cast_matrix":
+            return (1, 1) if ins[0] == SCALAR else ins[0]
+        return ins[0]
+    if op == "agg":
+        r, c = ins[0]
+        d = h.p["dir"]
+        return SCALAR if d == "all" else ((r, 1) if d == "row" else (1, c))
+    if op == "mm":
+        (ra, ca), (rb, cb) = ins
+        return (ca if h.p.get("transA") else ra, cb)
+    if op == "tsmm":
+        r, c = ins[0]
+        return (c, c) if h.p.get("left") else (r, r)
+    if op == "mmchain":
+        return (ins[0][1], ins[1][1])
+    if op == "tak":
+        return SCALAR
+    if op == "t":
+        return (ins[0][1], ins[0][0])
+    if op == "lix":
+        return ins[0]
+    if op == "rix":
+        r, c = ins[0]
+        rl, ru, cl, cu = (_lv(x) for x in h.inputs[1:5])
+
+        def span(lo, hi, n):
+            if lo is None and hi is None:
+                return n
+            lo_, hi_ = _int_or(lo, 1 if lo is None else -1), _int_or(hi, n if hi is None else -1)
+            return hi_ - lo_ + 1 if lo_ >= 0 and hi_ >= 0 else -1
+        lists = h.p.get("list", False)
+        return (span(rl, ru, r), c if lists and cl is None else span(cl, cu, c))
+    if op == "bi":
+        return _infer_bi(h, ins)
+    return UNK
+
+
+def _bi_arg(h, i, name):
+    npos = h.p.get("npos", len(h.inputs) - len(h.named))
+    if i < npos:
+        return h.inputs[i]
+    if name in h.named:
+        return h.inputs[npos + h.named.index(name)]
+    return None
+
+
+def _infer_bi(h, ins):
+    name = h.p.get("name")
+    if name in ("matrix", "rand"):
+        if name == "matrix":
+            data = _bi_arg(h, 0, "data")
+            r, c = _bi_arg(h, 1, "rows"), _bi_arg(h, 2, "cols")
+        else:
+            r, c = _bi_arg(h, 99, "rows"), _bi_arg(h, 99, "cols")
+        rv = _int_or(_lv(r)) if r is not None else -1
+        cv = _int_or(_lv(c)) if c is not None else -1
+        return (rv, cv)
+    if name == "seq":
+        a, b = (_lv(x) for x in h.inputs[:2]) if len(h.inputs) >= 2 else (None, None)
+        inc = _lv(h.inputs[2]) if len(h.inputs) > 2 else None
+        if isinstance(a, (int, float)) and isinstance(b, (int, float)):
+            inc = inc if isinstance(inc, (int, float)) and inc else (1 if b >= a else -1)
+            return (int((b - a) / inc) + 1, 1)
+        return (-1, 1)
+    if name in ("cbind", "append"):
+        if all(_known(d) for d in ins):
+            return (ins[0][0], sum(d[1] for d in ins))
+        return (ins[0][0] if ins else -1, -1)
+    if name == "rbind":
+        if all(_known(d) for d in ins):
+            return (sum(d[0] for d in ins), ins[0][1])
+        return (-1, ins[0][1] if ins else -1)
+    if name == "diag":
+        r, c = ins[0]
+        if c == 1:
+            return (r, r)
+        return (r, 1) if r >= 0 else UNK
+    if name == "solve":
+        return (ins[0][1], ins[1][1])
+    if name in ("inv", "inverse", "cholesky", "rev", "replace", "lower.tri", "upper.tri", "exp", "abs"):
+        return ins[0]
+    if name == "_onehot":
+        return (_int_or(_lv(h.inputs[1])), _int_or(_lv(h.inputs[2])))
+    if name == "outer":
+        return (ins[0][0], ins[1][1])
+    return UNK
+
+
+# ----------------------------------------------------------------------------
+def mem_estimate(d, bytes_per_cell=8):
+    """Worst-case dense size in bytes of a matrix output; None when unknown."""
+    if d == SCALAR:
+        return 0
+    if not _known(d):
+        return None
+    return d[0] * d[1] * bytes_per_cell
+
+
+def exec_type(h, d, in_dims, config):
+    if h.dt == "S" or d == SCALAR:
+        return "CP"
+    cells = [x[0] * x[1] for x in [d] + list(in_dims) if _known(x)]
+    unknown = not _known(d) or any(not _known(x) for x in in_dims if x != SCALAR)
+    gpu = config is not None and getattr(config, "gpu", False)
+    if config is not None and _known(d) and getattr(config, "dist_min_rows", 0) and \
+            d[0] >= config.dist_min_rows and getattr(config, "_world", 1) > 1:
+        return "DIST"
+    small = getattr(config, "gpu_min_cells", 16384) if config is not None else 16384
+    if gpu and (unknown or max(cells or [0]) >= small):
+        return "GPU"
+    return "CP"
+
+
+def annotate_dag(roots, env, config=None):
+    """Infer dims for a DAG (mutating hop.dim1/dim2, .exec_type, .mem); returns id -> dims."""
+    dims = {}
+    for h in H.walk(roots):
+        d = infer(h, dims, env)
+        if d == UNK and h.dim1 >= 0 and h.dim2 >= 0:
+            d = (h.dim1, h.dim2)
+        dims[h.id] = d
+        h.dim1, h.dim2 = d
+        h.exec_type = exec_type(h, d, [dims.get(c.id, UNK) for c in h.inputs], config)
+    return dims
+
+
+# ----------------------------------------------------------------------------
+# matrix multiplication chains
+# ----------------------------------------------------------------------------
+def _chain_operands(h, consumers):
+    """Flatten a left/right-nested tree of plain mm hops into its operand list."""
+    ops = []
+
+    def rec(x, top):
+        if x.op == "mm" and not x.p.get("transA") and (top or consumers.get(x.id, 0) <= 1):
+            rec(x.inputs[0], False)
+            rec(x.inputs[1], False)
+        else:
+            ops.append(x)
+    rec(h, True)
+    return ops
+
+
+def mmchain_order(dimsv):
+    """Classic DP: dimsv = [d0, d1, ..., dn] for n matrices; returns split table."""
+    n = len(dimsv) - 1
+    cost = [[0.0] * n for _ in range(n)]
+    split = [[0] * n for _ in range(n)]
+    for ln in range(1, n):
+        for i in range(n - ln):
+            j = i + ln
+            best = None
+            for k in range(i, j):
+                c = cost[i][k] + cost[k + 1][j] + float(dimsv[i]) * dimsv[k + 1] * dimsv[j + 1]
+                if best is None or c < best:
+                    best, split[i][j] = c, k
+            cost[i][j] = best
+    return split, cost[0][n - 1] if n > 1 else 0.0
+
+
+def _build(ops, split, i, j, pos):
+    if i == j:
+        return ops[i]
+    k = split[i][j]
+    return Hop("mm", [_build(ops, split, i, k, pos), _build(ops, split, k + 1, j, pos)], {}, dt="M", pos=pos)
+
+
+def _tree_cost(h, dims, consumers):
+    """Flops of the current parenthesisation of a chain rooted at h."""
+    if h.op == "mm" and not h.p.get("transA") and consumers.get(h.id, 0) <= 1:
+        a, b = h.inputs
+        (ra, ca), (_, cb) = dims[a.id], dims[b.id]
+        return _tree_cost(a, dims, consumers) + _tree_cost(b, dims, consumers) + float(ra) * ca * cb
+    return 0.0
+
+
+def optimize_mm_chains(roots, env, stats):
+    """Re-parenthesise mm chains of >= 3 operands with known dims. Returns (roots, changed,
+    has_unknown_chain)."""
+    dims = annotate_dag(roots, env)
+    consumers = {}
+    for h in H.walk(roots):
+        for c in h.inputs:
+            consumers[c.id] = consumers.get(c.id, 0) + 1
+    memo = {}
+    changed = False
+    unknown = False
+
+    def rec(h):
+        nonlocal changed, unknown
+        r = memo.get(h.id)
+        if r is not None:
+            return r
+        if h.op == "mm" and not h.p.get("transA"):
+            ops = _chain_operands(h, consumers)
+            if len(ops) >= 3:
+                ods = [dims.get(o.id, UNK) for o in ops]
+                if all(_known(d) and d != SCALAR for d in ods):
+                    dv = [ods[0][0]] + [d[1] for d in ods]
+                    split, best = mmchain_order(dv)
+                    if best < _tree_cost(h, dims, consumers) * 0.999:
+                        new_ops = [rec(o) for o in ops]
+                        nh = _build(new_ops, split, 0, len(ops) - 1, h.pos)
+                        memo[h.id] = nh
+                        changed = True
+                        stats["mmchain_reorder"] = stats.get("mmchain_reorder", 0) + 1
+                        return nh
+                else:
+                    unknown = True
+        h.inputs = [rec(c) for c in h.inputs]
+        memo[h.id] = h
+        return h
+
+    new_roots = [rec(h) for h in roots]
+    return new_roots, changed, unknown, memo
+
+
+def _chain_block(bb, env, stats):
+    tops = list(bb.roots) + list(bb.env_out.values())
+    _, changed, unknown, memo = optimize_mm_chains(tops, env, stats)
+    if changed:
+        bb.roots = [memo.get(h.id, h) for h in bb.roots]
+        bb.env_out = {k: memo.get(v.id, v) for k, v in bb.env_out.items()}
+    return changed, unknown
+
+
+# ----------------------------------------------------------------------------
+# program-level pass
+# ----------------------------------------------------------------------------
+def _shape_of(v):
+    if isinstance(v, (bool, int, float, str)):
+        return SCALAR
+    sh = getattr(v, "shape", None)
+    if sh is not None and len(sh) == 2:
+        return (int(sh[0]), int(sh[1]))
+    return UNK
+
+
+def _deep_copy(roots, env_out):
+    import copy
+    memo = {}
+
+    def cp_(h):
+        r = memo.get(h.id)
+        if r is None:
+            r = copy.copy(h)
+            r.inputs = [cp_(c) for c in h.inputs]
+            memo[h.id] = r
+        return r
+    return [cp_(h) for h in roots], {k: cp_(v) for k, v in env_out.items()}
+
+
+def _walk_program(cp, env, visit_bb):
+    from .loops import assigned_in
+
+    def blocks(bl, env):
+        for b in bl:
+            if isinstance(b, BasicBlock):
+                dims = visit_bb(b, env)
+                for k, h in b.env_out.items():
+                    env[k] = dims.get(h.id, UNK)
+            elif isinstance(b, IfBlock):
+                e1, e2 = dict(env), dict(env)
+                blocks(b.then_blocks, e1)
+                blocks(b.else_blocks, e2)
+                for k in set(e1) | set(e2):
+                    env[k] = e1.get(k, UNK) if e1.get(k, UNK) == e2.get(k, UNK) else UNK
+            elif isinstance(b, (WhileBlock, ForBlock)):
+                if isinstance(b, ForBlock):
+                    env[b.var] = SCALAR
+                body_env = dict(env)
+                blocks(b.body, body_env)
+                for k in assigned_in(b.body):
+                    if body_env.get(k, UNK) != env.get(k, UNK):
+                        env[k] = UNK
+    blocks(cp.blocks, env)
+    for fb in cp.functions.values():
+        if fb.body is not None:
+            fenv = {p.name: (SCALAR if p.dtype == "SCALAR" else UNK) for p in fb.inputs}
+            blocks(fb.body, fenv)
+
+
+def reorder_chains(cp, inputs=None):
+    """Before the HOP rewrites: re-parenthesise mm chains with known dims; flag blocks whose
+    chains have unknown dims for dynamic recompilation (keeping their raw DAG)."""
+    stats = {}
+    env = {k: _shape_of(v) for k, v in (inputs or {}).items()}
+
+    def visit(bb, env):
+        changed, unknown = _chain_block(bb, env, stats)
+        if unknown:
+            bb.recompile = True
+            bb._raw = _deep_copy(list(bb.roots), dict(bb.env_out))
+            stats["recompile_blocks"] = stats.get("recompile_blocks", 0) + 1
+        return annotate_dag(list(bb.roots) + list(bb.env_out.values()), env)
+
+    _walk_program(cp, env, visit)
+    cp.chain_stats = stats
+    return stats
+
+
+def annotate(cp, inputs=None, config=None):
+    """After instruction generation: dims, memory estimates and exec types of the final
+    (rewritten) HOP DAGs, for -explain and the cost statistics."""
+    env = {k: _shape_of(v) for k, v in (inputs or {}).items()}
+    counts = {}
+
+    def visit(bb, env):
+        dims = annotate_dag(list(bb.roots) + list(bb.env_out.values()), env, config)
+        for h in H.walk(list(bb.roots) + list(bb.env_out.values())):
+            if h.exec_type and h.op not in ("lit", "tread"):
+                counts[h.exec_type] = counts.get(h.exec_type, 0) + 1
+        return dims
+
+    _walk_program(cp, env, visit)
+    cp.exec_types = counts
+    return counts
+
+
+def recompile_block(bb, vars_, make_impl, config):
+    """Dynamic recompilation (reference: Recompiler.recompileHopsDag): re-plan a flagged
+    block's mm chains from the actual shapes of its live-in variables.  Plans are cached
+    per shape signature; returns True when a re-planned instruction list is in use."""
+    from .lops import compile_basic_block
+    names = sorted(bb.reads)
+    sig = tuple((n, _shape_of(vars_.get(n))) for n in names)
+    cache = getattr(bb, "_plans", None)
+    if cache is None:
+        cache = bb._plans = {}
+        bb._orig_plan = (bb.instrs, bb.writes_slots, bb.nslots, getattr(bb, "debug_slots", {}))
+    plan = cache.get(sig)
+    if plan is None:
+        roots, env_out = _deep_copy(*bb._raw)
+        tmp = BasicBlock()
+        tmp.roots, tmp.env_out = roots, env_out
+        tmp.live_out = bb.live_out
+        changed, _ = _chain_block(tmp, dict(sig), {})
+        if changed:
+            compile_basic_block(tmp, make_impl, config)
+            plan = (tmp.instrs, tmp.writes_slots, tmp.nslots, getattr(tmp, "debug_slots", {}))
+        else:
+            plan = bb._orig_plan
+        cache[sig] = plan
+    bb.instrs, bb.writes_slots, bb.nslots, bb.debug_slots = plan
+    return plan is not bb._orig_plan

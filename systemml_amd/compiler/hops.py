@@ -126,5 +126,8 @@ def explain_dag(roots, indent=""):
     lines = []
     for h in walk(roots):
         et = f" {h.exec_type}" if h.exec_type else ""
+        if h.dt == "M" and h.dim1 >= 0 and h.dim2 >= 0:
+            mb = h.dim1 * h.dim2 * 8 / 1e6
+            et += f" [{mb:.3g}MB]"
         lines.append(f"{indent}{h!r}{et}")
     return "\n".join(lines)

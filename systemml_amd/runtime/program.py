@@ -140,6 +140,11 @@ def exec_block(ctx, b):
     if isinstance(b, BasicBlock):
         if ctx.debugger is not None:
             ctx.debugger.cur_block = b
+        if b.recompile:
+            from ..compiler.cost import recompile_block
+            from .instructions import make_impl
+            if recompile_block(b, ctx.vars, make_impl, ctx.config) and ctx.stats is not None:
+                ctx.stats.count("recompiled blocks")
         slots = exec_instrs(ctx, b.instrs, b.nslots)
         vars_ = ctx.vars
         for name, s in b.writes_slots:

@@ -126,3 +126,42 @@ def test_ipa_propagates_constant_arguments():
     np.testing.assert_allclose(r["Z"], 16 * X)
     cs = compile_script(src, inputs={"X": X}, outputs=["Y"], config=CFG)
     assert cs.cp.ipa_stats.get("literals", 0) == 1
+
+
+# ---------------------------------------------------------------------------- sizes / chains
+def test_size_propagation_and_exec_types():
+    X = np.random.default_rng(1).random((50, 4))
+    src = "Y = t(X) %*% X\nz = sum(Y)\nW = matrix(0, rows=3, cols=2)"
+    cs = compile_script(src, inputs={"X": X}, outputs=["Y", "z"], config=DMLConfig(gpu=True, gpu_min_cells=100))
+    e = explain(cs.cp)
+    assert "tsmm" in e and "M[4x4]" in e and "M[3x2]" in e
+    assert cs.cp.exec_types.get("CP", 0) >= 1
+
+
+def test_mm_chain_reordered_into_mmchain():
+    X = np.random.default_rng(2).random((200, 30))
+    v = np.random.default_rng(3).random((30, 1))
+    src = "q = t(X) %*% X %*% v"
+    cs = compile_script(src, inputs={"X": X, "v": v}, outputs=["q"], config=CFG)
+    assert cs.cp.chain_stats.get("mmchain_reorder", 0) == 1
+    assert "mmchain" in explain(cs.cp) and "tsmm" not in explain(cs.cp)
+    r = _run(src, {"X": X, "v": v}, ["q"])
+    np.testing.assert_allclose(r["q"], X.T @ X @ v, rtol=1e-10)
+
+
+def test_dynamic_recompile_of_unknown_chain():
+    from systemml_amd.utils.stats import Statistics
+    src = """
+    n = nrow(A)
+    if (n > 0) { B = rand(rows=n, cols=40, seed=4) } else { B = A }
+    for (i in 1:2) {
+      q = t(B) %*% B %*% v
+    }
+    """
+    v = np.ones((40, 1))
+    A = np.ones((300, 40))
+    st = Statistics(enabled=True)
+    res = run(src, inputs={"A": A, "v": v}, outputs=["q", "B"], config=CFG, stats=st, out=lambda s: None)
+    B = res["B"].numpy()
+    np.testing.assert_allclose(res["q"].numpy(), B.T @ B @ v, rtol=1e-9)
+    assert st.counters.get("recompiled blocks", 0) >= 1
