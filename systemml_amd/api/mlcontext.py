@@ -180,6 +180,58 @@ def pydmlFromFile(path):
         return Script(f.read(), pydml=True, filename=os.path.abspath(path))
 
 
+def pydmlFromResource(rel):
+    path = os.path.join(SCRIPTS_DIR, rel)
+    return pydmlFromFile(path)
+
+
+def getHopDAG(ml, script, lines=None, conf=None, apply_rewrites=True, with_subgraph=False):
+    """Graphviz DOT text of the script's HOP DAGs (reference: mlcontext.getHopDAG, which
+    renders through the JVM).  `lines` restricts the output to basic blocks starting on
+    those script lines; `apply_rewrites=False` shows the DAGs before the HOP rewrites;
+    `with_subgraph` draws one cluster per basic block."""
+    from ..compiler.blocks import BasicBlock
+    from ..compiler import hops as H
+    cfg = (conf or (ml.config if ml is not None else get_default_config())).copy()
+    cfg.rewrites = bool(apply_rewrites)
+    cfg.fusion = bool(apply_rewrites)
+    cs = EX.compile_script(script.source, script._args, inputs=script._inputs, outputs=script._outputs,
+                           config=cfg, pydml=script.pydml, filename=script.filename)
+    out = ["digraph HopDAG {", "  node [shape=box, fontname=Helvetica];"]
+    seen = set()
+    idx = [0]
+
+    def emit(blocks):
+        for b in blocks:
+            if isinstance(b, BasicBlock):
+                line = b.pos.line if b.pos else None
+                if lines is not None and line not in lines:
+                    continue
+                roots = list(b.roots) + list(b.env_out.values())
+                if with_subgraph:
+                    out.append(f"  subgraph cluster_{idx[0]} {{ label=\"lines {line}\";")
+                    idx[0] += 1
+                for h in H.walk(roots):
+                    if h.id in seen:
+                        continue
+                    seen.add(h.id)
+                    label = repr(h).split(" [")[0].replace('"', "'")
+                    et = f"\\n{h.exec_type}" if h.exec_type else ""
+                    out.append(f'    h{h.id} [label="{label}{et}"];')
+                    for c in h.inputs:
+                        out.append(f"    h{c.id} -> h{h.id};")
+                for name, h in b.env_out.items():
+                    out.append(f'    v_{h.id}_{name} [label="{name}", shape=ellipse]; h{h.id} -> v_{h.id}_{name};')
+                if with_subgraph:
+                    out.append("  }")
+            for attr in ("then_blocks", "else_blocks", "body"):
+                if hasattr(b, attr):
+                    emit(getattr(b, attr))
+    emit(cs.cp.blocks)
+    out.append("}")
+    return "\n".join(out)
+
+
 def dmlFromResource(rel):
     """Load one of the bundled scripts (systemml_amd/scripts/...)."""
     path = os.path.join(SCRIPTS_DIR, rel)

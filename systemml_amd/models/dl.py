@@ -510,6 +510,23 @@ class Caffe2DML(BaseSystemMLClassifier):
                   filename=os.path.join(SCRIPTS_DIR, "caffe2dml_predict.dml"))
         return _out(res["P"])
 
+    def load(self, weights=None, sep="/", ignore_weights=None, eager=False):
+        """Warm start from a directory of <layer>_weight.mtx / <layer>_bias.mtx matrices
+        (as written by converters.convert_caffemodel); layers in ignore_weights keep their
+        initialisation (reference: Caffe2DML.load in the Python mllearn API)."""
+        from ..io.readers import read_matrix
+        ignore = set(ignore_weights or [])
+        found = {}
+        for L in _params(self.layers):
+            if L.name in ignore:
+                continue
+            for part, key in (("weight", "W"), ("bias", "b")):
+                path = f"{weights}{sep}{L.name}_{part}.mtx"
+                if os.path.exists(path):
+                    found[f"{key}_{L.name}"] = _np(read_matrix(path))
+        self.init_weights_ = found or None
+        return self
+
     @property
     def model_keys(self):
         return [f"{v}_{L.name}" for L in _params(self.layers) for v in ("W", "b")]

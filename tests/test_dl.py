@@ -65,3 +65,24 @@ def test_keras2dml_from_json_and_weights():
     m.fit(X, y)
     assert m.score(X, y) > 0.9
     assert set(m.model_) == {"W_c1", "b_c1", "W_d1", "b_d1"}
+
+
+def test_caffe2dml_load_converted_caffemodel(tmp_path):
+    """convert_caffemodel output (<layer>_weight/_bias.mtx) warm-starts Caffe2DML."""
+    from systemml_amd.io.writers import write_matrix
+    import torch
+    (tmp_path / "net.prototxt").write_text(NET)
+    (tmp_path / "solver.prototxt").write_text('net: "net.prototxt"\nbase_lr: 0.0\nmax_iter: 1\ntype: "SGD"\n')
+    m = Caffe2DML(solver=str(tmp_path / "solver.prototxt"), input_shape=(1, 8, 8))
+    rng = np.random.default_rng(3)
+    w = {"conv1_weight": rng.standard_normal((4, 9)), "conv1_bias": rng.standard_normal((4, 1)),
+         "ip1_weight": rng.standard_normal((64, 16)), "ip1_bias": rng.standard_normal((1, 16))}
+    d = tmp_path / "weights"
+    d.mkdir()
+    for k, v in w.items():
+        write_matrix(torch.from_numpy(v), str(d / (k + ".mtx")), "csv")
+    m.load(str(d), ignore_weights=["ip1"])
+    assert set(m.init_weights_) == {"W_conv1", "b_conv1"}
+    np.testing.assert_allclose(m.init_weights_["W_conv1"], w["conv1_weight"])
+    m.load(str(d))
+    assert set(m.init_weights_) == {"W_conv1", "b_conv1", "W_ip1", "b_ip1"}
