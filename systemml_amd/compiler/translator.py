@@ -35,7 +35,7 @@ BUILTIN_CONSTANTS = {"NaN": float("nan"), "Inf": float("inf"), "pi": math.pi, "I
                      "NAN": float("nan"), "PI": math.pi}
 
 UNARY_MATH = {"abs", "exp", "sqrt", "round", "floor", "ceil", "sign", "sin", "cos", "tan", "asin",
-              "acos", "atan", "sinh", "cosh", "tanh"}
+              "acos", "atan", "sinh", "cosh", "tanh", "sigmoid"}
 CUMAGG = {"cumsum", "cumprod", "cummin", "cummax"}
 FULL_AGG = {"sum": "sum", "prod": "prod", "mean": "mean", "avg": "mean", "var": "var", "sd": "sd",
             "trace": "trace"}
@@ -262,8 +262,8 @@ def _package_script_candidates(path):
     out = [os.path.join(scripts, p)]
     if p.startswith("scripts/"):
         out.append(os.path.join(here, p))
-    if p.startswith("nn/"):
-        out.append(os.path.join(scripts, p))
+    # library directories of the shipped scripts (e.g. "scalable_linalg/...", "utils/...")
+    out += [os.path.join(scripts, sub, p) for sub in ("staging", "algorithms", "utils")]
     return out
 
 

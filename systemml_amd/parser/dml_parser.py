@@ -216,15 +216,20 @@ class DMLParser(BaseParser):
         if not (self.accept_op("=") or self.accept_op("<-")):
             self.error("expected assignment")
         if self.is_kw("ifdef") and self.is_op("(", self.peek()):
+            start = self.i
             self.i += 2
             cp = self._parse_data_identifier()
             if not isinstance(cp, A.CmdParam):
                 self.error("ifdef requires a command-line parameter ($name)")
             self.expect_op(",")
             dflt = self.parse_expr()
+            close = self.tok
             self.expect_op(")")
-            self.skip_semis()
-            return A.Assign(target, dflt, ifdef=cp, pos=p)
+            nxt = self.tok
+            if nxt.kind == "EOF" or nxt.line != close.line or (nxt.kind == "OP" and nxt.value in (";", "}")):
+                self.skip_semis()
+                return A.Assign(target, dflt, ifdef=cp, pos=p)
+            self.i = start          # ifdef(...) inside a larger expression
         val = self.parse_expr()
         self.skip_semis()
         return A.Assign(target, val, pos=p)

@@ -859,10 +859,17 @@ def b_svd(ctx, A):
 
 @builtin("qr", multi=True)
 def b_qr(ctx, A):
+    """[H, R] = qr(A): H (m x n) holds the Householder vectors column by column (lower
+    trapezoidal, unit leading entry; reflector j is I - 2 v v'/(v'v)), R (m x n) is upper
+    trapezoidal, A = H_1 ... H_n R (reference LibCommonsMath.computeQR semantics)."""
     a = _la(A)
-    # reference returns Householder vectors H and R; we return Q-equivalent H = Q and R
-    Q, R = torch.linalg.qr(a, mode="complete")
-    return (Q.to(_dt()), R.to(_dt()))
+    m, n = a.shape
+    f, tau = torch.geqrf(a)
+    H = torch.tril(f, -1)
+    k = min(m, n)
+    idx = torch.arange(k, device=H.device)
+    H[idx, idx] = torch.where(tau[:k] != 0, torch.ones_like(tau[:k]), torch.zeros_like(tau[:k]))
+    return (H.to(_dt()), torch.triu(f).to(_dt()))
 
 
 @builtin("lu", multi=True)

@@ -275,7 +275,8 @@ def unary(op: str, a):
     if op == "sign":
         return float((x > 0) - (x < 0)) if x == x else x
     fn = {"sin": math.sin, "cos": math.cos, "tan": math.tan, "asin": math.asin, "acos": math.acos,
-          "atan": math.atan, "sinh": math.sinh, "cosh": math.cosh, "tanh": math.tanh}.get(op)
+          "atan": math.atan, "sinh": math.sinh, "cosh": math.cosh, "tanh": math.tanh,
+          "sigmoid": lambda v: 1.0 / (1.0 + math.exp(-v)) if v > -700 else 0.0}.get(op)
     if fn is not None:
         try:
             return fn(x)
