@@ -204,7 +204,8 @@ def _inline_in_block(bb, candidates, ncalls, stats):
 
     def sub(h):
         if h.op == "fout" and h.inputs and h.inputs[0].id in repl:
-            return repl[h.inputs[0].id][h.p["i"]]
+            # the inlined body may itself consume outputs of other calls inlined here
+            return sub(repl[h.inputs[0].id][h.p["i"]])
         r = memo.get(h.id)
         if r is not None:
             return r

@@ -165,3 +165,21 @@ def test_dynamic_recompile_of_unknown_chain():
     B = res["B"].numpy()
     np.testing.assert_allclose(res["q"].numpy(), B.T @ B @ v, rtol=1e-9)
     assert st.counters.get("recompiled blocks", 0) >= 1
+
+
+def test_inlining_of_chained_calls_keeps_single_definition():
+    """Inlining a call whose arguments are outputs of other calls inlined in the same block
+    must substitute through (regression: the inner call stayed as a second, independent
+    definition, so a random matrix was drawn twice)."""
+    src = """
+randn = function(Integer r, Integer c) return (Matrix[Double] M) { M = rand(rows = r, cols = c, pdf = "normal") }
+lin = function(Matrix[Double] X, Matrix[Double] W) return (Matrix[Double] Y) { Y = X %*% W }
+f = function() return (Double d) {
+  X = randn(3, 4); W = randn(4, 5)
+  D = randn(3, 4)
+  d = sum(lin(X + D, W)) - sum(lin(X, W)) - sum(D %*% W)
+}
+d = f()
+"""
+    r = _run(src, outputs=("d",))
+    assert abs(r["d"]) < 1e-9

@@ -201,3 +201,50 @@ s = sum(p)
 '''
     r = dml(src, {}, ["s"])
     assert abs(r["s"] - 128) < 1e-6
+
+
+def test_dml_nn_test_suite():
+    """scripts/nn/test/run_tests.dml: directional-derivative grad checks of every layer plus
+    unit tests (the reference's in-DML test suite) report zero failures."""
+    import os
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    path = os.path.join(SCRIPTS_DIR, "nn", "test", "run_tests.dml")
+    out = []
+    run(open(path).read(), config=CFG, out=out.append, filename=path)
+    errors = [s for s in out if s.startswith("ERROR")]
+    assert not errors, errors
+    assert out[-1] == "NN TESTS FAILED: 0"
+
+
+def test_nn_example_drivers(tmp_path):
+    """Softmax / LeNet train + predict drivers, the data-parallel LeNet and the FM dummy-data
+    drivers run end to end on small synthetic CSV data."""
+    import os
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.io.readers import read_matrix
+    import torch
+    from systemml_amd.io.writers import write_matrix
+    ex = os.path.join(SCRIPTS_DIR, "nn", "examples")
+    g = np.random.default_rng(0)
+    lab = g.integers(0, 10, (60, 1)).astype(float)
+    data = np.hstack([lab, g.integers(0, 256, (60, 64)).astype(float)])
+    write_matrix(torch.from_numpy(data), str(tmp_path / "train.csv"), "csv")
+
+    def go(name, args):
+        p = os.path.join(ex, name)
+        out = []
+        run(open(p).read(), args=args, config=CFG, out=out.append, filename=p)
+        return out
+
+    out = go("mnist_softmax-train.dml", dict(train=str(tmp_path / "train.csv"), test=str(tmp_path / "train.csv"),
+                                             out_dir=str(tmp_path)))
+    assert any(s.startswith("Test Accuracy") for s in out)
+    write_matrix(torch.from_numpy(data[:, 1:]), str(tmp_path / "X.csv"), "csv")
+    go("mnist_softmax-predict.dml", dict(X=str(tmp_path / "X.csv"), model_dir=str(tmp_path), out_dir=str(tmp_path)))
+    P = read_matrix(str(tmp_path / "probs")).numpy()
+    np.testing.assert_allclose(P.sum(axis=1), 1, atol=1e-9)
+    out = go("mnist_lenet_distrib_sgd-train-dummy-data.dml", dict(N=16, Nval=8, Hin=8, Win=8, batch_size=4,
+                                                                  parallel_batches=2, epochs=1))
+    assert any("Dummy data validation" in s for s in out)
+    out = go("fm-regression-dummy-data.dml", dict(n=50, d=3))
+    assert any("Validation loss" in s for s in out)
