@@ -341,7 +341,107 @@ def rewrite_block(bb, config=None):
     roots, visit = cse(bb.roots)
     bb.roots = roots
     bb.env_out = {k: visit(v) for k, v in bb.env_out.items()}
+    if rw.enabled and rw.fuse:
+        n = fuse_softmax_grad(bb)
+        if n:
+            rw.stats["softmax-grad"] = n
     return rw.stats
+
+
+# ----------------------------------------------------------------------------
+# two-output row template: X %*% V and t(X) %*% (softmax(cbind(X %*% V, 0))[, 1:K] - Y)
+# ----------------------------------------------------------------------------
+def _agg_row(h, o):
+    return h.op == "agg" and h.p.get("o") == o and h.p.get("dir") == "row"
+
+
+def _match_softmax_grad(G):
+    """G = mm(X, g, transA) with g = P[, 1:cu] - Y, P = E / rowSums(E), E = exp(L - rowMaxs(L)),
+    L = cbind(U, matrix(0, N, 1)), U = X %*% V  ->  (X, U, V, Y, cu) or None.
+    This is the candidate-point evaluation of MultiLogReg's trust-region step (the
+    reference's codegen forms a Row template for it, hops/codegen/template/TemplateRow.java)."""
+    if G.op != "mm" or not G.p.get("transA"):
+        return None
+    X, g = G.inputs
+    if g.op != "b" or g.p.get("o") != "-" or g.inputs[0].op != "rix":
+        return None
+    rx, Y = g.inputs
+    P, rl, ru, cl, cu = rx.inputs
+    def empty(x):
+        return x.op == "lit" and x.value is None
+    if not (empty(rl) and empty(ru) and _is_lit(cl, 1)) or Y.dt != "M":
+        return None
+    if P.op != "b" or P.p.get("o") != "/":
+        return None
+    E, s = P.inputs
+    if not (_agg_row(s, "sum") and s.inputs[0] is E and E.op == "u" and E.p.get("o") == "exp"):
+        return None
+    L2 = E.inputs[0]
+    if L2.op != "b" or L2.p.get("o") != "-":
+        return None
+    L, mx = L2.inputs
+    if not (_agg_row(mx, "max") and mx.inputs[0] is L and L.op == "bi" and L.p.get("name") == "cbind"
+            and len(L.inputs) == 2 and not L.named):
+        return None
+    U, Z = L.inputs
+    if not (U.op == "mm" and not U.p.get("transA") and U.inputs[0] is X):
+        return None
+    if not (Z.op == "bi" and Z.p.get("name") == "matrix" and Z.inputs and _is_lit(Z.inputs[0], 0)):
+        return None
+    zc = _bi_args(Z).get("cols")
+    if zc is None or not _is_lit(zc, 1):
+        return None
+    return X, U, U.inputs[1], Y, cu
+
+
+def fuse_softmax_grad(bb):
+    """Replace every matched (U, G) pair by the outputs of one `smgrad` hop (one pass over X)."""
+    seen = set()
+    order = []
+
+    def walk(h):
+        if h.id in seen:
+            return
+        seen.add(h.id)
+        for c in h.inputs:
+            walk(c)
+        order.append(h)
+
+    for r in list(bb.roots) + list(bb.env_out.values()):
+        walk(r)
+    repl = {}
+    for h in order:
+        m = _match_softmax_grad(h)
+        if m is None:
+            continue
+        X, U, V, Y, cu = m
+        if U.id in repl:
+            continue
+        F = Hop("smgrad", [X, V, Y, cu], {}, dt="U", pos=h.pos)
+        repl[U.id] = Hop("fout", [F], {"i": 0}, dt="M", pos=U.pos)
+        repl[h.id] = Hop("fout", [F], {"i": 1}, dt="M", pos=h.pos)
+    if not repl:
+        return 0
+    memo = {}
+
+    def sub(h):
+        r = repl.get(h.id)
+        if r is not None:
+            return r
+        if h.id in memo:
+            return h
+        memo[h.id] = True
+        h.inputs = [sub(c) for c in h.inputs]
+        return h
+
+    # the fused hop's own inputs must not be rewritten to its outputs
+    for r in repl.values():
+        F = r.inputs[0]
+        memo[F.id] = True
+        F.inputs = [sub(c) for c in F.inputs]
+    bb.roots = [sub(h) for h in bb.roots]
+    bb.env_out = {k: sub(v) for k, v in bb.env_out.items()}
+    return len(repl) // 2
 
 
 def rewrite_pred(pred, config=None):

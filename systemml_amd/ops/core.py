@@ -526,6 +526,34 @@ def mmchain(ctype, X, v, w=None):
     return mmchain_ref(ctype, X, v, w)
 
 
+def smgrad(X, V, Y, cu=None):
+    """Fused multinomial-logreg candidate evaluation: returns (U, G) with U = X %*% V and
+    G = t(X) %*% (P[, 1:cu] - Y), P = row-softmax of cbind(U, 0)  (the row template the
+    compiler forms from MultiLogReg's line-search step, see rewrites.fuse_softmax_grad)."""
+    if is_dist(X):
+        return _dist().smgrad(X, V, Y, cu)
+    K = V.shape[1] if hasattr(V, "shape") else None
+    kc = K if cu is None else int(S.as_double(cu))
+    if backend.use_kernels and isinstance(X, Tensor) and X.is_cuda and not SP.is_sparse(X) and kc == K \
+            and isinstance(V, Tensor) and isinstance(Y, Tensor) and not SP.is_sparse(Y):
+        from . import kernels
+        r = kernels.smgrad(X, V, Y)
+        if r is not None:
+            return r
+    return smgrad_ref(X, V, Y, kc)
+
+
+def smgrad_ref(X, V, Y, kc):
+    u = mm(X, V)
+    lt = cvt(u) if not isinstance(u, Tensor) or SP.is_sparse(u) else u
+    lt = torch.cat([lt, torch.zeros((lt.shape[0], 1), dtype=lt.dtype, device=lt.device)], dim=1)
+    lt = lt - lt.max(dim=1, keepdim=True).values
+    e = torch.exp(lt)
+    p = e / e.sum(dim=1, keepdim=True)
+    g = binary("-", p[:, :kc], Y)
+    return u, mm(X, g, transA=True)
+
+
 def mmchain_ref(ctype, X, v, w=None):
     u = mm(X, v)
     if ctype == "XtXv":

@@ -9,6 +9,9 @@
 //   XTXVY   : R         = t(X) %*% ((X %*% V) - Y)        (mmchain XtXvy)
 //   XTPSXV  : R         = t(X) %*% (Q - P*rowSums(Q)),  Q = P*(X %*% V)
 //                                                         (multinomial logreg H*v, row template)
+//   XTSMG   : U = X %*% V and R = t(X) %*% (softmax([U, 0])[, 1:K] - Y)
+//                                                         (multinomial logreg gradient at a candidate
+//                                                          point, two outputs, one pass)
 //   ROWSSQ  : U[N x 1]  = rowSums(X^2)
 //   COLSSQ  : R[D x 1]  = colSums(X^2)
 //   COLSUM  : R[D x 1]  = colSums(X)
@@ -33,15 +36,16 @@
 namespace sysml {
 
 enum Mode { XV = 0, XTG = 1, XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5,
-            ROWSSQ = 6, COLSSQ = 7, COLSUM = 8, ROWSUM = 9 };
+            ROWSSQ = 6, COLSSQ = 7, COLSUM = 8, ROWSUM = 9, XTSMG = 10 };
 
 constexpr int WAVES = 4;
 constexpr int BLOCK = 64 * WAVES;
 
 template <int M> struct ModeInfo {
-  static constexpr bool needV   = (M == XV || M == XTXV || M == XTWXV || M == XTXVY || M == XTPSXV);
+  static constexpr bool needV   = (M == XV || M == XTXV || M == XTWXV || M == XTXVY || M == XTPSXV ||
+                                   M == XTSMG);
   static constexpr bool accum   = (M == XTG || M == XTXV || M == XTWXV || M == XTXVY || M == XTPSXV ||
-                                   M == COLSSQ || M == COLSUM);
+                                   M == COLSSQ || M == COLSUM || M == XTSMG);
   static constexpr bool rowOut  = (M == XV || M == ROWSSQ || M == ROWSUM);
 };
 
@@ -376,7 +380,8 @@ struct RowOps {
   static constexpr int C = J * 8;
   static constexpr int K2 = K / 2;
   static constexpr bool VREG = MI::needV && (C * K <= 64);
-  static constexpr bool NEEDS = (MODE == XTWXV || MODE == XTXVY || MODE == XTPSXV || MODE == XTG);
+  static constexpr bool NEEDS = (MODE == XTWXV || MODE == XTXVY || MODE == XTPSXV || MODE == XTG ||
+                                 MODE == XTSMG);
 
   f2 vreg[VREG ? C : 1][VREG ? K2 : 1];
   f2 acc[MI::accum ? C : 1][MI::accum ? K2 : 1];
@@ -415,8 +420,9 @@ struct RowOps {
   }
 
   // one row: cur = the lane's 8*J elements, sl = lane k's S[r][k]
+  // XTSMG: out/ldo = the U output, kact = number of real (unpadded) columns
   __device__ __forceinline__ void process(const Raw8<T> (&cur)[J], const float sl, const int64_t r,
-                                          const bool valid, float* __restrict__ out, int ldo) {
+                                          const bool valid, float* __restrict__ out, int ldo, int kact = 0) {
     float x[C];
 #pragma unroll
     for (int j = 0; j < J; ++j) unpack<float>(cur[j], x + j * 8);
@@ -476,6 +482,22 @@ struct RowOps {
           for (int k = 0; k < K; ++k) { pr[k] = sv[k]; q[k] = pr[k] * us[k]; sq += q[k]; }
 #pragma unroll
           for (int k = 0; k < K; ++k) gs[k] = q[k] - pr[k] * sq;
+        } else if constexpr (MODE == XTSMG) {
+          // softmax over [u_1..u_kact, 0] (the baseline class has linear term 0)
+          float m = 0.f;
+#pragma unroll
+          for (int k = 0; k < K; ++k) m = (k < kact) ? fmaxf(m, us[k]) : m;
+          float e[K], s = __expf(-m);
+#pragma unroll
+          for (int k = 0; k < K; ++k) { e[k] = (k < kact) ? __expf(us[k] - m) : 0.f; s += e[k]; }
+          const float inv = 1.f / s;
+#pragma unroll
+          for (int k = 0; k < K; ++k) gs[k] = (k < kact) ? e[k] * inv - sv[k] : 0.f;
+          if (valid) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+              if (lane == k && k < kact) out[r * (int64_t)ldo + k] = us[k];
+          }
         }
 #pragma unroll
         for (int kk = 0; kk < K2; ++kk)
@@ -642,7 +664,8 @@ __global__ void __launch_bounds__(BLOCK)
 rowstream_dma_kernel(const T* __restrict__ X, int64_t N, int D,
                      const float* __restrict__ V, int ldv,
                      const float* __restrict__ S, int lds, int sbc,
-                     float* __restrict__ out, int64_t rows_per_block) {
+                     float* __restrict__ out, int64_t rows_per_block,
+                     float* __restrict__ uout, int ldu) {
   static_assert(MODE != XV, "row-output mode uses the register-ring front end");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using OPS = RowOps<T, K, J, MODE>;
@@ -662,7 +685,8 @@ rowstream_dma_kernel(const T* __restrict__ X, int64_t N, int D,
   int coff[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) coff[j] = chunk_off(j, lane, D);
-  const int scol = ((MODE == XTWXV || MODE == XTXVY) && sbc) ? 0 : (lane < K ? lane : K - 1);
+  int scol = ((MODE == XTWXV || MODE == XTXVY) && sbc) ? 0 : (lane < K ? lane : K - 1);
+  if constexpr (MODE == XTSMG) scol = lane < sbc ? lane : sbc - 1;   // Y has only kact columns
 
   const int ring_off = J * 512 * K * 4 + wave * (R * SLOT);
   lds_char* ring = (lds_char*)(smem) + ring_off;
@@ -704,7 +728,7 @@ rowstream_dma_kernel(const T* __restrict__ X, int64_t N, int D,
       }
       if constexpr (!OPS::NEEDS) sl = 0.f;
       fetch(p, r + STEP);                   // refill the slot (its LDS reads have retired)
-      ops.process(cur, sl, r, r < r1, out, 0);
+      ops.process(cur, sl, r, r < r1, uout, ldu, sbc);
     }
   }
   wait_vmcnt<0>();                          // no LDS-DMA may outlive the block's LDS
@@ -720,6 +744,8 @@ using namespace sysml;
 
 static int g_rows_per_iter = 0;   // 0 = auto, else rows per iteration (generic) / prefetch depth (pk)
 static int g_variant = 0;         // 0 = auto (packed fp32 where applicable), 1 = generic scalar kernel
+static float* g_uout = nullptr;   // XTSMG: row output U (set by sysml_rowstream_smg around the launch)
+static int g_ldu = 0;
 
 template <typename T, typename A, int K, int J, int MODE>
 static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int ldv, const void* S,
@@ -727,6 +753,8 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
   using MI = ModeInfo<MODE>;
   if constexpr (sizeof(A) == 8 && K == 8 && J == 2 && MODE >= XTXV && MODE <= XTPSXV) {
     return -1;  // fp64 x 8 columns x 1024 cols would spill: caller falls back to XV + XTG passes
+  } else if constexpr (MODE == XTSMG && (sizeof(A) != 4 || K < 2 || K > 4)) {
+    return -1;  // fused softmax gradient: packed-fp32 LDS-DMA kernel only (caller runs it unfused)
   } else {
   constexpr int KO = (MODE == COLSSQ || MODE == COLSUM) ? 1 : K;
   size_t shv = MI::needV ? (size_t)J * 512 * K * sizeof(A) : 0;
@@ -735,7 +763,7 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
   const bool two = (g_rows_per_iter == 2) ||
                    (g_rows_per_iter == 0 && sizeof(A) == 4 && (MODE == XV || MODE == XTXV || MODE == ROWSSQ ||
                                                                MODE == ROWSUM || (K == 1 && MI::accum)));
-  if constexpr (sizeof(A) == 4 && K >= 2 && MODE <= XTPSXV) {
+  if constexpr (sizeof(A) == 4 && K >= 2 && (MODE <= XTPSXV || MODE == XTSMG)) {
     if (g_variant != 1 && vec && (D % 8) == 0) {   // packed-fp32 kernels (vector rows only)
       // rows in flight per wave: knob (1-2 -> 2, 3+ -> 4), else bf16 4 / fp32 2 (same bytes)
       const int knob = g_rows_per_iter;
@@ -748,13 +776,16 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
       } else {
         const size_t shd = deep ? dma_lds_bytes<T, K, J, 4>() : dma_lds_bytes<T, K, J, 2>();
 #define SYSML_DMA(PF) hipLaunchKernelGGL((rowstream_dma_kernel<T, K, J, MODE, PF>), dim3(grid), dim3(BLOCK), shd, st, \
-          (const T*)X, N, D, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, rpb)
+          (const T*)X, N, D, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, rpb, g_uout, g_ldu)
         if (deep) SYSML_DMA(4); else SYSML_DMA(2);
 #undef SYSML_DMA
       }
       return hipGetLastError() == hipSuccess ? 0 : -2;
     }
   }
+  if constexpr (MODE == XTSMG) {
+    return -1;  // no generic-kernel variant of the two-output mode
+  } else {
   if (sizeof(A) == 4 && K <= 4 && two) {
     hipLaunchKernelGGL((rowstream_kernel<T, A, K, J, MODE, 2>), dim3(grid), dim3(BLOCK), sh, st,
                        (const T*)X, N, D, vec, (const A*)V, ldv, (const A*)S, lds, sbc, (A*)out, ldo, rpb);
@@ -763,6 +794,7 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
                        (const T*)X, N, D, vec, (const A*)V, ldv, (const A*)S, lds, sbc, (A*)out, ldo, rpb);
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   }
 }
 
@@ -834,7 +866,33 @@ int sysml_rowstream(int mode, int xdtype, const void* X, int64_t N, int D, const
   return -1;
 }
 
-int sysml_abi_version() { return 2; }
+// Fused multinomial-logreg candidate evaluation (mode XTSMG): U = X %*% V (N x kact, written
+// to U with leading dimension ldu) and partial[grid][D x K] of t(X) %*% (softmax([U,0])[,1:kact]
+// - Y[,1:kact]) in one pass over X.  V is D x K (K = kact padded to 2 or 4, zero columns),
+// Y is N x >= kact (leading dimension ldy).  bf16 / fp32 X only.  Returns 0 on success.
+int sysml_rowstream_smg(int xdtype, const void* X, int64_t N, int D, const void* V, int ldv,
+                        const void* Y, int ldy, int kact, void* U, int ldu, void* partial, int K,
+                        int grid, int64_t rows_per_block, void* stream) {
+  if (D <= 0 || D > 1024 || N <= 0 || grid <= 0 || kact < 1 || kact > K || (xdtype != 0 && xdtype != 1))
+    return -1;
+  const int J = (D <= 512) ? 1 : 2;
+  const int align = xdtype == 0 ? 8 : 4;
+  const int vec = ((D % align) == 0 && (((uintptr_t)X) & 15) == 0) ? 1 : 0;
+  g_uout = (float*)U;
+  g_ldu = ldu;
+  int rc;
+  if (xdtype == 0)
+    rc = launch_j<uint16_t, float, XTSMG>(J, K, X, N, D, vec, V, ldv, Y, ldy, kact, partial, 0, grid,
+                                          rows_per_block, (hipStream_t)stream);
+  else
+    rc = launch_j<float, float, XTSMG>(J, K, X, N, D, vec, V, ldv, Y, ldy, kact, partial, 0, grid,
+                                       rows_per_block, (hipStream_t)stream);
+  g_uout = nullptr;
+  g_ldu = 0;
+  return rc;
+}
+
+int sysml_abi_version() { return 3; }
 
 // tuning knob for A/B runs: 0 = automatic, 1 or 2 rows per wave iteration
 void sysml_set_rows_per_iter(int r) { g_rows_per_iter = r; }

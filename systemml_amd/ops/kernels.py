@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libsysml_hip.so")
 _lib = None
 
 # modes (must match ops/hip/rowstream.hip)
-XV, XTG, XTXV, XTWXV, XTXVY, XTPSXV, ROWSSQ, COLSSQ, COLSUM, ROWSUM = range(10)
+XV, XTG, XTXV, XTWXV, XTXVY, XTPSXV, ROWSSQ, COLSSQ, COLSUM, ROWSUM, XTSMG = range(11)
 _CHAIN = {"XtXv": XTXV, "XtwXv": XTWXV, "XtXvy": XTXVY, "XtPSXv": XTPSXV}
 MIN_ROWS = 2048       # below this the launch + partial reduction is not worth it
 MIN_D = 32            # a wave per row: narrower rows waste most lanes (torch handles those)
@@ -57,6 +57,11 @@ def load(required=False):
                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                   ctypes.c_void_p]
+    L.sysml_rowstream_smg.restype = ctypes.c_int
+    L.sysml_rowstream_smg.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                      ctypes.c_void_p]
     L.sysml_set_rows_per_iter.argtypes = [ctypes.c_int]
     L.sysml_set_rows_per_iter.restype = None
     L.sysml_mchain.restype = ctypes.c_int
@@ -279,6 +284,37 @@ def mmchain(ctype, X, V, W=None):
     _count("rowstream.mmchain." + ctype)
     R = part[:g].sum(0).reshape(X.shape[1], kp)
     return _result(R if kp == K else R[:, :K].contiguous())
+
+
+def smgrad(X, V, Y):
+    """(U, G) with U = X %*% V and G = t(X) %*% (softmax([U, 0])[, 1:K] - Y) in one pass over X
+    (mode XTSMG: the multinomial-logreg objective / gradient at a candidate point).  V is
+    D x K with K <= 4, Y is N x K.  Returns None when the kernel does not apply."""
+    if not _ok_x(X) or X.dtype not in (torch.bfloat16, torch.float32):
+        return None
+    K = V.shape[1]
+    if K > 4 or Y.shape != (X.shape[0], K) or V.shape[0] != X.shape[1]:
+        return None
+    kp = _kpad(K)
+    kp = max(kp, 2)
+    L = load(required=True)
+    code, adt = _xcode(X)
+    N, D = X.shape
+    Vp = _pad_cols(V, kp, torch.float32, X.device).contiguous()
+    Yc = Y.to(device=X.device, dtype=torch.float32).contiguous()
+    U = torch.empty((N, K), dtype=torch.float32, device=X.device)
+    grid = _grid(N)
+    rpb = (N + grid - 1) // grid
+    grid = (N + rpb - 1) // rpb
+    part = torch.empty((grid, D * kp), dtype=torch.float32, device=X.device)
+    rc = L.sysml_rowstream_smg(code, ctypes.c_void_p(X.data_ptr()), N, D, ctypes.c_void_p(Vp.data_ptr()), kp,
+                               ctypes.c_void_p(Yc.data_ptr()), K, K, ctypes.c_void_p(U.data_ptr()), K,
+                               ctypes.c_void_p(part.data_ptr()), kp, grid, rpb, _stream())
+    if rc != 0:
+        return None
+    _count("rowstream.smgrad")
+    G = part.sum(0).reshape(D, kp)
+    return _result(U), _result(G if kp == K else G[:, :K].contiguous())
 
 
 # ----------------------------------------------------------------------------

@@ -370,6 +370,20 @@ def mmchain(ctype, X, v, w=None):
     return r
 
 
+def smgrad(X, V, Y, cu=None):
+    """Row-partitioned fused softmax gradient: each rank streams its rows of X once, U stays
+    row-distributed, the D x K gradient partials are all-reduced."""
+    C = _C()
+    if not _is_d(X):
+        return C.smgrad(X, _fallback(V) if _is_d(V) else V, _fallback(Y) if _is_d(Y) else Y, cu)
+    if _is_d(V):
+        V = _fallback(V)
+    u, g = C.smgrad(X.local, V, _align(Y, X), cu)
+    g = g.contiguous()
+    X.ctx.allreduce_(g, "sum")
+    return DistMatrix(u, X.nrows, u.shape[1], X.start, X.ctx), g
+
+
 def transpose(x):
     return _C().transpose(_fallback(x))
 

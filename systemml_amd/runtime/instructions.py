@@ -19,7 +19,7 @@ from . import builtins as B
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
 # operators that compute on matrix operands (placement applies); the rest move values around
-_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "tak", "t", "rix", "lix", "bi"}
+_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "tak", "t", "rix", "lix", "bi"}
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
 
@@ -78,7 +78,12 @@ def _placed(fn):
             a = [x.to(gpu, non_blocking=True) if (type(x) is Tensor and x.device.type != "cuda") else x
                  for x in a]
         r = fn(ctx, a)
-        if type(r) is Tensor and r.is_cuda and r.numel() < small and r.dtype != torch.bfloat16 \
+        if type(r) is tuple:                 # multi-output fused operators
+            return tuple(demote(x) for x in r)
+        return demote(r)
+
+    def demote(r):
+        if type(r) is Tensor and r.is_cuda and r.numel() < backend.small_cells and r.dtype != torch.bfloat16 \
                 and not r.is_sparse and r.layout == torch.strided:
             return r.to("cpu")
         return r
@@ -131,6 +136,8 @@ def _make_impl(h):
     if op == "mmchain":
         t = p["type"]
         return (lambda ctx, a: C.mmchain(t, a[0], a[1], a[2] if len(a) > 2 else None)), "mmchain-" + t
+    if op == "smgrad":
+        return (lambda ctx, a: C.smgrad(a[0], a[1], a[2], a[3] if len(a) > 3 else None)), "smgrad"
     if op == "tak":
         return (lambda ctx, a: C.tak(a[0], a[1])), "tak+*"
     if op == "t":

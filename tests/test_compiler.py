@@ -183,3 +183,24 @@ d = f()
 """
     r = _run(src, outputs=("d",))
     assert abs(r["d"]) < 1e-9
+
+
+def test_softmax_gradient_fusion_matches_unfused():
+    """MultiLogReg's candidate evaluation (X %*% B and t(X) %*% (softmax - Y)) is fused into
+    one smgrad operator; results equal the unfused plan."""
+    import os
+    from systemml_amd.api import executor as EX
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    src = open(os.path.join(SCRIPTS_DIR, "algorithms", "MultiLogReg.dml")).read()
+    g = np.random.default_rng(3)
+    X = g.standard_normal((400, 7))
+    y = (np.argmax(X[:, :3] + 0.5 * g.standard_normal((400, 3)), axis=1) + 1).astype(float)[:, None]
+    args = dict(X="X", Y="Y", B="B", icpt=0, reg=0.01, tol=1e-9, moi=6, mii=3)
+    outs = {}
+    for fuse in (True, False):
+        cfg = DMLConfig(gpu=False, fusion=fuse)
+        cs = EX.compile_script(src, args, inputs={"X": X, "Y_vec": y}, outputs=["B_out"], config=cfg)
+        assert ("smgrad" in EX.explain(cs.cp if hasattr(cs, "cp") else cs.program, "hops")) == fuse
+        res, _ = EX.execute(cs, {"X": X, "Y_vec": y}, out=lambda s: None)
+        outs[fuse] = res["B_out"].numpy()
+    np.testing.assert_allclose(outs[True], outs[False], rtol=1e-10, atol=1e-12)

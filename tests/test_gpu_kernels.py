@@ -179,3 +179,26 @@ def test_mfma_matches_rowstream(K, ctype, k, mfma_all):
     err_v = (r_v.double() - ref).abs().max().item() / scale
     # the split-bf16 MFMA path must be as accurate as the fp32 VALU path
     assert err_m < max(2e-5, 2 * err_v), (err_m, err_v)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("d", [1000, 512, 64])
+@pytest.mark.parametrize("k", [4, 3, 2])
+def test_smgrad_fused_softmax_gradient(K, dt, d, k):
+    """Mode XTSMG: U = X V and t(X) (softmax([U, 0])[:, :k] - Y) in one pass vs fp64 torch."""
+    n = 30011
+    x = _mk(n, d, dt, seed=5)
+    x64 = x.double()
+    v = torch.randn((d, k), device="cuda", dtype=torch.float64) * 0.05
+    lab = torch.randint(0, k + 1, (n,), device="cuda")
+    y = torch.nn.functional.one_hot(lab, k + 1)[:, :k].double()
+    r = K.smgrad(x, v, y)
+    assert r is not None
+    u, g = r
+    u_ref = x64 @ v
+    lt = torch.cat([u_ref, torch.zeros((n, 1), device="cuda", dtype=torch.float64)], 1)
+    p = torch.softmax(lt, dim=1)[:, :k]
+    g_ref = x64.t() @ (p - y)
+    assert (u.double() - u_ref).abs().max().item() <= 2e-4 * u_ref.abs().max().item()
+    assert (g.double() - g_ref).abs().max().item() <= 2e-4 * g_ref.abs().max().item()
+    assert K.counters.get("rowstream.smgrad", 0) > 0
