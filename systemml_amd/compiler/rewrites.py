@@ -149,6 +149,11 @@ class Rewriter:
             if (o == "*" and _is_lit(a, 1)) or (o == "+" and _is_lit(a, 0)):
                 self._count("identity")
                 return b
+        if o in ("*", "/") and self.fuse and a.dt == "M" and b.dt == "M":
+            q = _match_wquat_cell(o, a, b, h)
+            if q is not None:
+                self._count("wquat-" + q.p["kind"])
+                return q
         # remove unnecessary outer product with ones: A op (v %*% matrix(1,1,k))
         if o in CELLWISE:
             if b.op == "mm" and not b.p.get("transA") and _is_ones_matrix(b.inputs[1], rows1=True):
@@ -164,6 +169,11 @@ class Rewriter:
     def _rw_agg(self, h):
         x = h.inputs[0]
         o, d = h.p["o"], h.p["dir"]
+        if d == "all" and o in ("sum", "sumsq") and self.fuse:
+            q = _match_wquat_agg(o, x, h)
+            if q is not None:
+                self._count("wquat-" + q.p["kind"])
+                return q
         if o == "sum":
             if x.op == "b" and x.p["o"] == "^" and _is_lit(x.inputs[1], 2) and x.inputs[0].dt != "S":
                 self._count("sumsq")
@@ -205,6 +215,11 @@ class Rewriter:
         if not transA and b.op == "t" and b.inputs[0] is a:
             self._count("tsmm")
             return Hop("tsmm", [a], {"left": False}, dt="M", pos=h.pos)
+        if self.fuse:
+            q = _match_wdivmm(a, b, transA, h)
+            if q is not None:
+                self._count("wquat-wdivmm")
+                return q
         if transA and self.fuse:
             X = a
             m = self._match_mmchain(X, b)
@@ -300,6 +315,139 @@ class Rewriter:
                                 self._count("mmchain-row")
                                 return Hop("mmchain", [X, xv.inputs[1], P], {"type": "XtPSXv"}, dt="M")
         return None
+
+
+# ----------------------------------------------------------------------------
+# weighted quaternary operators (reference: hops/rewrite/RewriteAlgebraicSimplificationDynamic
+# #simplifyWeighted{SquaredLoss,Sigmoid,DivMM,CrossEntropy,UnaryMM}; executed by
+# ops/quaternary.py with sampled products at the non-zeros of sparse W / X)
+# ----------------------------------------------------------------------------
+_WUMM_UOPS = {"exp", "log", "abs", "sqrt", "sin", "cos", "tan", "tanh", "sign", "round", "floor", "ceil"}
+
+
+def _uv(h):
+    """(U, V) when h is U %*% t(V)."""
+    if h.op == "mm" and not h.p.get("transA") and h.inputs[1].op == "t" and h.inputs[0].dt == "M":
+        return h.inputs[0], h.inputs[1].inputs[0]
+    return None
+
+
+def _uv_eps(h):
+    """(U, V, eps) for U %*% t(V) [+ eps] (eps a scalar)."""
+    m = _uv(h)
+    if m is not None:
+        return m[0], m[1], None
+    if h.op == "b" and h.p["o"] == "+":
+        for x, e in ((h.inputs[0], h.inputs[1]), (h.inputs[1], h.inputs[0])):
+            m = _uv(x)
+            if m is not None and e.dt == "S":
+                return m[0], m[1], e
+    return None
+
+
+def _is_neg(h):
+    if h.op == "u" and h.p["o"] == "neg":
+        return h.inputs[0]
+    if h.op == "b" and h.p["o"] == "-" and _is_lit(h.inputs[0], 0):
+        return h.inputs[1]
+    return None
+
+
+def _wq(kind, ins, p, dt, h):
+    q = dict(p)
+    q["kind"] = kind
+    return Hop("wquat", ins, q, dt=dt, pos=h.pos)
+
+
+def _match_wquat_agg(o, x, h):
+    if o == "sumsq":
+        if x.op != "b" or x.p["o"] != "-":
+            return None
+        A, B = x.inputs
+        for X, R in ((A, B), (B, A)):
+            if X.dt != "M":
+                continue
+            m = _uv(R)
+            if m is not None:
+                return _wq("wsloss", [X, m[0], m[1]], {"type": "none"}, "S", h)
+            if X is A and R.op == "b" and R.p["o"] == "*":
+                for W, P in (R.inputs, R.inputs[::-1]):
+                    m = _uv(P)
+                    if m is not None and W.dt == "M":
+                        return _wq("wsloss", [X, m[0], m[1], W], {"type": "pre"}, "S", h)
+        return None
+    if x.op == "wquat" and x.p["kind"] == "wumm" and x.p["uop"] == "log" and x.p.get("op") == "*":
+        return _wq("wcemm", list(x.inputs), {}, "S", h)
+    if x.op != "b" or x.p["o"] != "*":
+        return None
+    for W, P in (x.inputs, x.inputs[::-1]):
+        if W.dt != "M":
+            continue
+        # sum(W * (X - U%*%t(V))^2)
+        if P.op == "b" and P.p["o"] == "^" and _is_lit(P.inputs[1], 2):
+            dd = P.inputs[0]
+            if dd.op == "b" and dd.p["o"] == "-":
+                for X, R in (dd.inputs, dd.inputs[::-1]):
+                    m = _uv(R)
+                    if m is None or X.dt != "M":
+                        continue
+                    if W.op == "b" and W.p["o"] == "!=" and W.inputs[0] is X and _is_lit(W.inputs[1], 0):
+                        return _wq("wsloss", [X, m[0], m[1]], {"type": "post_nz"}, "S", h)
+                    return _wq("wsloss", [X, m[0], m[1], W], {"type": "post"}, "S", h)
+        # sum(X * log(U%*%t(V) [+ eps]))
+        if P.op == "u" and P.p["o"] == "log":
+            m = _uv_eps(P.inputs[0])
+            if m is not None:
+                U, V, e = m
+                return _wq("wcemm", [W, U, V] + ([e] if e is not None else []), {"eps": e is not None}, "S", h)
+    return None
+
+
+def _match_wquat_cell(o, a, b, h):
+    if o == "*":
+        for W, P in ((a, b), (b, a)):
+            lg = False
+            s = P
+            if s.op == "u" and s.p["o"] == "log" and s.inputs[0].op == "u" and s.inputs[0].p["o"] == "sigmoid":
+                lg, s = True, s.inputs[0]
+            if s.op == "u" and s.p["o"] == "sigmoid":
+                z = s.inputs[0]
+                n = _is_neg(z)
+                m = _uv(n if n is not None else z)
+                if m is not None:
+                    return _wq("wsigmoid", [W, m[0], m[1]], {"minus": n is not None, "log": lg}, "M", h)
+    cands = [(a, b)] if o == "/" else [(a, b), (b, a)]
+    for X, P in cands:
+        if P.op == "u" and P.p["o"] in _WUMM_UOPS:
+            m = _uv(P.inputs[0])
+            if m is not None:
+                return _wq("wumm", [X, m[0], m[1]], {"uop": P.p["o"], "op": o}, "M", h)
+        if P.op == "b" and P.p["o"] == "^" and _is_lit(P.inputs[1], 2):
+            m = _uv(P.inputs[0])
+            if m is not None:
+                return _wq("wumm", [X, m[0], m[1]], {"uop": "^2", "op": o}, "M", h)
+    return None
+
+
+def _match_wdivmm(a, b, transA, h):
+    """(W / (U%*%t(V) [+eps])) %*% V,  t(U) %*% (W / (U%*%t(V) [+eps])), and the W * (U%*%t(V))
+    forms."""
+    q, other = (b, a) if transA else (a, b)
+    if q.op != "b" or q.p["o"] not in ("/", "*") or q.inputs[0].dt != "M":
+        return None
+    mult = q.p["o"] == "*"
+    cands = [(q.inputs[0], q.inputs[1])]
+    if mult:
+        cands.append((q.inputs[1], q.inputs[0]))
+    for W, R in cands:
+        m = _uv_eps(R) if not mult else (_uv(R) + (None,) if _uv(R) else None)
+        if m is None:
+            continue
+        U, V, e = m
+        if (transA and other is U) or (not transA and other is V):
+            return _wq("wdivmm", [W, U, V] + ([e] if e is not None else []),
+                       {"left": transA, "mult": mult, "eps": e is not None}, "M", h)
+    return None
 
 
 def cse(roots):

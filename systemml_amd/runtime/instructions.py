@@ -16,10 +16,10 @@ from ..ops import sparse as SP
 from . import builtins as B
 
 
-_SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak"}
+_SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
 # operators that compute on matrix operands (placement applies); the rest move values around
-_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "tak", "t", "rix", "lix", "bi"}
+_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "wquat", "tak", "t", "rix", "lix", "bi"}
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
 
@@ -138,6 +138,9 @@ def _make_impl(h):
         return (lambda ctx, a: C.mmchain(t, a[0], a[1], a[2] if len(a) > 2 else None)), "mmchain-" + t
     if op == "smgrad":
         return (lambda ctx, a: C.smgrad(a[0], a[1], a[2], a[3] if len(a) > 3 else None)), "smgrad"
+    if op == "wquat":
+        from ..ops import quaternary as Q
+        return (lambda ctx, a: Q.execute(p, a)), "wquat-" + p["kind"]
     if op == "tak":
         return (lambda ctx, a: C.tak(a[0], a[1])), "tak+*"
     if op == "t":

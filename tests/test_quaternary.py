@@ -1,0 +1,117 @@
+"""Weighted quaternary operators (wsloss / wsigmoid / wdivmm / wcemm / wumm): rewrite detection
+and numerics of the fused sparse (sampled-product) and dense paths against numpy fp64
+references of the unfused expressions (reference tests: test/integration/functions/quaternary/
+Weighted*Test.java, which compare the rewritten against the unrewritten script)."""
+import numpy as np
+import pytest
+import torch
+
+from systemml_amd.api.executor import run, compile_script, explain
+from systemml_amd.conf import DMLConfig
+from systemml_amd.ops import quaternary as Q
+
+CFG = DMLConfig(gpu=False)
+
+GEN = """
+X = rand(rows=300, cols=250, sparsity=%s, min=1, max=2, seed=1)
+W = rand(rows=300, cols=250, sparsity=%s, min=0.5, max=1, seed=2)
+U = rand(rows=300, cols=7, min=0.1, max=1, seed=3)
+V = rand(rows=250, cols=7, min=0.1, max=1, seed=4)
+"""
+
+CASES = {
+    "wsloss-post": ("r = sum(W * (X - U %*% t(V))^2)",
+                    lambda X, W, U, V: np.sum(W * (X - U @ V.T) ** 2)),
+    "wsloss-post_nz": ("r = sum((X != 0) * (X - U %*% t(V))^2)",
+                       lambda X, W, U, V: np.sum((X != 0) * (X - U @ V.T) ** 2)),
+    "wsloss-pre": ("r = sum((X - W * (U %*% t(V)))^2)",
+                   lambda X, W, U, V: np.sum((X - W * (U @ V.T)) ** 2)),
+    "wsloss-none": ("r = sum((X - U %*% t(V))^2)",
+                    lambda X, W, U, V: np.sum((X - U @ V.T) ** 2)),
+    "wsigmoid": ("r = W * sigmoid(U %*% t(V))",
+                 lambda X, W, U, V: W / (1 + np.exp(-(U @ V.T)))),
+    "wsigmoid-minus-log": ("r = W * log(sigmoid(-(U %*% t(V))))",
+                           lambda X, W, U, V: W * np.log(1 / (1 + np.exp(U @ V.T)))),
+    "wdivmm-right": ("r = (W / (U %*% t(V))) %*% V",
+                     lambda X, W, U, V: (W / (U @ V.T)) @ V),
+    "wdivmm-left-eps": ("r = t(U) %*% (W / (U %*% t(V) + 1e-6))",
+                        lambda X, W, U, V: U.T @ (W / (U @ V.T + 1e-6))),
+    "wdivmm-mult": ("r = (W * (U %*% t(V))) %*% V",
+                    lambda X, W, U, V: (W * (U @ V.T)) @ V),
+    "wcemm": ("r = sum(X * log(U %*% t(V)))",
+              lambda X, W, U, V: np.sum(X * np.log(U @ V.T))),
+    "wcemm-eps": ("r = sum(X * log(U %*% t(V) + 1e-15))",
+                  lambda X, W, U, V: np.sum(X * np.log(U @ V.T + 1e-15))),
+    "wumm": ("r = X * exp(U %*% t(V))",
+             lambda X, W, U, V: X * np.exp(U @ V.T)),
+    "wumm-div": ("r = X / (U %*% t(V))^2",
+                 lambda X, W, U, V: X / (U @ V.T) ** 2),
+}
+
+
+def _np(v):
+    if isinstance(v, torch.Tensor):
+        if v.layout != torch.strided:
+            v = v.to_dense()
+        return v.double().numpy()
+    return v
+
+
+@pytest.mark.parametrize("sp", ["0.05", "1.0"])
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_wquat_rewrite_and_numerics(case, sp):
+    body, ref = CASES[case]
+    src = GEN % (sp, sp) + body
+    cs = compile_script(src, inputs={}, outputs=["r", "X", "W", "U", "V"], config=CFG)
+    assert "wquat" in explain(cs.cp), explain(cs.cp)
+    res = run(src, inputs={}, outputs=["r", "X", "W", "U", "V"], config=CFG, out=lambda s: None)
+    X, W, U, V = (_np(res[k]) for k in "XWUV")
+    expect = ref(X, W, U, V)
+    np.testing.assert_allclose(_np(res["r"]), expect, rtol=1e-4, atol=1e-6)
+
+
+def test_wquat_disabled_without_fusion():
+    cfg = DMLConfig(gpu=False)
+    cfg.fusion = False
+    src = GEN % ("0.05", "0.05") + CASES["wsloss-post"][0]
+    cs = compile_script(src, inputs={}, outputs=["r"], config=cfg)
+    assert "wquat" not in explain(cs.cp)
+
+
+def test_sparse_paths_match_dense_direct():
+    g = torch.Generator().manual_seed(0)
+    m, n, r = 120, 90, 5
+    Wd = (torch.rand(m, n, generator=g) < 0.1).float() * torch.rand(m, n, generator=g)
+    Xd = (torch.rand(m, n, generator=g) < 0.1).float() * (1 + torch.rand(m, n, generator=g))
+    U = torch.rand(m, r, generator=g) + 0.1
+    V = torch.rand(n, r, generator=g) + 0.1
+    Ws, Xs = Wd.to_sparse_csr(), Xd.to_sparse_csr()
+    uv = U @ V.T
+    for kind in ("post", "pre", "none", "post_nz"):
+        fused = Q.wsloss(kind, Xs if kind in ("none", "post_nz") else Xd, U, V, Ws)
+        unfused = Q.wsloss(kind, Xd, U, V, Wd)
+        assert fused == pytest.approx(unfused, rel=1e-4)
+    np.testing.assert_allclose(Q.wsigmoid(Ws, U, V, True, False).to_dense(),
+                               Wd * torch.sigmoid(-uv), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(Q.wdivmm(Ws, U, V, True, False, 1e-6),
+                               U.T @ (Wd / (uv + 1e-6)), rtol=1e-4)
+    np.testing.assert_allclose(Q.wdivmm(Ws, U, V, False, True), (Wd * uv) @ V, rtol=1e-4)
+    assert Q.wcemm(Xs, U, V) == pytest.approx(float((Xd * torch.log(uv)).sum()), rel=1e-5)
+    np.testing.assert_allclose(Q.wumm(Xs, U, V, "exp").to_dense(), Xd * torch.exp(uv), rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_wquat_sparse_on_gpu():
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(1)
+    m, n, r = 4000, 3000, 16
+    Wd = (torch.rand(m, n, generator=g) < 0.01).float()
+    Xd = Wd * (1 + torch.rand(m, n, generator=g))
+    U = torch.rand(m, r, generator=g)
+    V = torch.rand(n, r, generator=g)
+    ref = float((Wd * (Xd - U @ V.T) ** 2).sum())
+    got = Q.wsloss("post_nz", Xd.to_sparse_csr().to(dev), U.to(dev), V.to(dev))
+    assert got == pytest.approx(ref, rel=1e-4)
+    ref2 = (Wd / (U @ V.T)) @ V
+    got2 = Q.wdivmm(Wd.to_sparse_csr().to(dev), U.to(dev), V.to(dev), False)
+    np.testing.assert_allclose(got2.cpu(), ref2, rtol=1e-4)
