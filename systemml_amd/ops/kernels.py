@@ -62,6 +62,9 @@ def load(required=False):
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                       ctypes.c_void_p]
+    L.sysml_sddmm.restype = ctypes.c_int
+    L.sysml_sddmm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     L.sysml_set_rows_per_iter.argtypes = [ctypes.c_int]
     L.sysml_set_rows_per_iter.restype = None
     L.sysml_mchain.restype = ctypes.c_int
@@ -413,4 +416,25 @@ def _chunked_tsmm_bf16(x, left):
         c = x[s:s + step].to(dt)
         part = c.t() @ c
         out = part if out is None else out + part
+    return out
+
+
+def sddmm(crow, col, U, V):
+    """<U[i_k], V[j_k]> at the non-zeros of a CSR pattern (ops/hip/sddmm.hip); None when the
+    shape is unsupported (r > 256).  U, V: fp32 contiguous on the GPU; crow/col int64."""
+    import torch
+    L = load(required=True)
+    m, r = U.shape
+    if r > 256 or col.numel() == 0:
+        return None
+    U = U.float().contiguous()
+    V = V.float().contiguous()
+    crow = crow.to(torch.int64).contiguous()
+    col = col.to(torch.int64).contiguous()
+    out = torch.empty(col.numel(), dtype=torch.float32, device=U.device)
+    st = torch.cuda.current_stream(U.device).cuda_stream
+    rc = L.sysml_sddmm(crow.data_ptr(), col.data_ptr(), U.data_ptr(), V.data_ptr(), m, r, out.data_ptr(), st)
+    if rc != 0:
+        raise RuntimeError(f"sysml_sddmm failed: {rc}")
+    _count("sddmm")
     return out

@@ -53,7 +53,14 @@ def _coo_idx(x):
 
 
 def sddmm(row, col, U, V):
-    """<U[row_k], V[col_k]> for every k (fp32 accumulate)."""
+    """<U[row_k], V[col_k]> for every k (fp32 accumulate); on the GPU the hand-written
+    wave-per-row kernel of ops/hip/sddmm.hip (row must be sorted, as CSR order gives)."""
+    if U.is_cuda and row.numel() > 0:
+        from . import kernels
+        crow = torch.searchsorted(row, torch.arange(U.shape[0] + 1, device=row.device))
+        out = kernels.sddmm(crow, col, U, V)
+        if out is not None:
+            return out
     U = U.float()
     V = V.float()
     out = torch.empty(row.numel(), dtype=torch.float32, device=U.device)

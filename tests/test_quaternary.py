@@ -115,3 +115,22 @@ def test_wquat_sparse_on_gpu():
     ref2 = (Wd / (U @ V.T)) @ V
     got2 = Q.wdivmm(Wd.to_sparse_csr().to(dev), U.to(dev), V.to(dev), False)
     np.testing.assert_allclose(got2.cpu(), ref2, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [16, 7, 200])
+def test_sddmm_hip_kernel_matches_fp32(r):
+    from systemml_amd.ops import kernels
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(r)
+    m, n = 5000, 3000
+    S = ((torch.rand(m, n, generator=g) < 0.005).float()).to_sparse_csr()
+    U = torch.randn(m, r, generator=g)
+    V = torch.randn(n, r, generator=g)
+    crow, col = S.crow_indices(), S.col_indices()
+    rows = torch.repeat_interleave(torch.arange(m), crow[1:] - crow[:-1])
+    ref = (U[rows] * V[col]).sum(1)
+    got = kernels.sddmm(crow.to(dev), col.to(dev), U.to(dev), V.to(dev))
+    assert got is not None
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(got.cpu(), ref, rtol=1e-4, atol=1e-4)
