@@ -324,6 +324,8 @@ def smgrad(X, V, Y):
 # dispatch helpers used by ops/core.py
 # ----------------------------------------------------------------------------
 def try_mm(a, b, transA):
+    """Dense GPU `%*%`: tall-skinny shapes on the row-streaming / MFMA-chain kernels, every
+    other shape on the MFMA GEMM (ops/gemm.py -> ops/hip/gemm.hip)."""
     if not isinstance(b, torch.Tensor) or SP.is_sparse(b):
         return None
     if not b.is_cuda:
@@ -332,12 +334,15 @@ def try_mm(a, b, transA):
         K = b.shape[1]
         if K <= 8:
             if transA and b.shape[0] == a.shape[0]:
-                return xtg(a, b)
+                r = xtg(a, b)
+                if r is not None:
+                    return r
             if not transA and b.shape[0] == a.shape[1]:
-                return xv(a, b)
-    if a.dtype == torch.bfloat16:
-        return _chunked_mm_bf16(a, b, transA)
-    return None
+                r = xv(a, b)
+                if r is not None:
+                    return r
+    from . import gemm
+    return _result(gemm.matmul(a.t() if transA else a, b))
 
 
 def try_mmchain(ctype, X, v, w):
@@ -349,9 +354,9 @@ def try_mmchain(ctype, X, v, w):
 
 
 def try_tsmm(x, left):
-    if x.dtype == torch.bfloat16:
-        return _chunked_tsmm_bf16(x, left)
-    return None
+    """t(X) %*% X / X %*% t(X) on the MFMA GEMM, upper block triangle only (ops/hip/gemm.hip)."""
+    from . import gemm
+    return _result(gemm.tsmm(x, left))
 
 
 def sumsq(x, d):
@@ -383,40 +388,6 @@ def sumsq(x, d):
         return tot
     xx = cvt(x)
     return torch.sum(xx * xx, dim=1 if d == "row" else 0, keepdim=True)
-
-
-def _chunk_rows(x, budget_cells=1 << 26):
-    return max(1, budget_cells // max(1, x.shape[1]))
-
-
-def _chunked_mm_bf16(a, b, transA):
-    """bf16-stored operand without a full-size fp32 copy: row chunks upcast on the fly."""
-    dt = backend.dtype
-    b = b.to(dt) if b.dtype != torch.bfloat16 else b.to(dt)
-    step = _chunk_rows(a)
-    if transA:
-        out = None
-        for s in range(0, a.shape[0], step):
-            c = a[s:s + step].to(dt)
-            part = c.t() @ b[s:s + step]
-            out = part if out is None else out + part
-        return out
-    outs = [a[s:s + step].to(dt) @ b for s in range(0, a.shape[0], step)]
-    return torch.cat(outs, 0)
-
-
-def _chunked_tsmm_bf16(x, left):
-    dt = backend.dtype
-    if not left:
-        xx = x.to(dt)
-        return xx @ xx.t()
-    step = _chunk_rows(x)
-    out = None
-    for s in range(0, x.shape[0], step):
-        c = x[s:s + step].to(dt)
-        part = c.t() @ c
-        out = part if out is None else out + part
-    return out
 
 
 def sddmm(crow, col, U, V):

@@ -1,0 +1,105 @@
+"""GPU numerics of the hand-written MFMA GEMM / tsmm kernels (ops/hip/gemm.hip) against an
+fp64 torch reference: ragged (non tile-multiple) shapes, every operand orientation
+(A %*% B, t(A) %*% B, A %*% t(B), t(A) %*% t(B)), K from 1 to 4096, split-K, and tsmm."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=[32, 64])
+def G(request):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from systemml_amd.ops import gemm
+    gemm.set_bk(request.param)
+    yield gemm
+    gemm.set_bk(0)
+
+
+def _mk(shape, dt, trans, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    r, c = shape
+    base = torch.rand((c, r) if trans else (r, c), generator=g, device="cuda", dtype=torch.float64) * 2 - 1
+    base = base.to(dt)
+    return base.t() if trans else base
+
+
+def _check(C, P, Q, tol):
+    ref = P.double() @ Q.double()
+    bound = P.double().abs() @ Q.double().abs()
+    err = (C.double() - ref).abs()
+    worst = (err - tol * bound - 1e-30).max().item()
+    assert worst <= 0, f"max err {err.max().item():.3e} (bound {tol:g} * |A||B|)"
+
+
+SHAPES = [(1, 1, 1), (7, 9, 5), (100, 9, 130), (257, 64, 255), (300, 100, 513), (256, 256, 256),
+          (512, 4096, 300), (64, 777, 1000), (1000, 33, 8)]
+TOL = {torch.bfloat16: 2e-6, torch.float32: 2e-6, torch.float64: 1e-14}
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32, torch.float64])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("M,K,N", SHAPES)
+def test_gemm_layouts(G, dt, ta, tb, M, K, N):
+    P = _mk((M, K), dt, ta, 1 + M + K)
+    Q = _mk((K, N), dt, tb, 2 + N)
+    C = G.matmul(P, Q)
+    assert C.shape == (M, N)
+    # bf16 products are exact in fp32; the error is fp32 accumulation (~K * 2^-24)
+    _check(C, P, Q, TOL[dt] * max(1, K) ** 0.5 * 8)
+
+
+def test_gemm_identity_asymmetric(G):
+    # A = I with an asymmetric B catches a transposed C/D write
+    for dt in (torch.bfloat16, torch.float32, torch.float64):
+        n = 300
+        I = torch.eye(n, dtype=dt, device="cuda")
+        B = torch.arange(n * 280, device="cuda", dtype=torch.float64).reshape(n, 280).remainder(97).to(dt)
+        assert torch.equal(G.matmul(I, B).double(), B.double())
+        assert torch.equal(G.matmul(B.t(), I).double(), B.t().double())
+
+
+def test_gemm_mixed_bf16_fp32(G):
+    P = _mk((3000, 512), torch.bfloat16, False, 3)
+    Q = _mk((512, 70), torch.float32, False, 4)
+    C = G.matmul(P, Q)
+    _check(C, P.float(), Q, 2e-5)
+    C2 = G.matmul(Q.t(), P.t())
+    _check(C2, Q.t(), P.t().float(), 2e-5)
+
+
+def test_gemm_splitk_tall(G):
+    # t(X) %*% Y with X 200000 x 96: few output tiles, long K -> split-K slabs
+    X = _mk((200_000, 96), torch.bfloat16, False, 5)
+    Y = _mk((200_000, 40), torch.bfloat16, False, 6)
+    C = G.matmul(X.t(), Y)
+    _check(C, X.t(), Y, 2e-6 * 450 * 8)
+    for dt in (torch.float32, torch.float64):
+        Xf, Yf = X.to(dt), Y.to(dt)
+        _check(G.matmul(Xf.t(), Yf), Xf.t(), Yf, TOL[dt] * 450 * 8)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32, torch.float64])
+@pytest.mark.parametrize("n,d", [(5000, 300), (100_000, 520), (37, 9)])
+@pytest.mark.parametrize("left", [True, False])
+def test_tsmm(G, dt, n, d, left):
+    if not left and n > 10000:
+        n = 3000
+    X = _mk((n, d), dt, False, 7 + d)
+    C = G.tsmm(X, left)
+    P, Q = (X.t(), X) if left else (X, X.t())
+    _check(C, P, Q, TOL[dt] * max(n if left else d, 1) ** 0.5 * 8)
+    assert torch.equal(C, C.t())
+
+
+def test_gemm_nonfinite_tail(G):
+    # K-tail masking must not turn a non-finite value past K into NaN: allocate the operand
+    # inside a bigger buffer with inf beyond column K
+    buf = torch.full((64, 72), float("inf"), dtype=torch.bfloat16, device="cuda")
+    P = buf[:, :65]
+    P.copy_(_mk((64, 65), torch.bfloat16, False, 9))
+    Q = _mk((65, 40), torch.bfloat16, False, 10)
+    C = G.matmul(P, Q)
+    assert torch.isfinite(C).all()
+    _check(C, P, Q, 1e-4)
