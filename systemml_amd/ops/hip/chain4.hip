@@ -1,0 +1,470 @@
+// Row-group fused chain kernels: t(X) %*% g(X %*% V) for tall X (N x D, D <= 1024) and skinny V
+// (D x K, K in {1, 2, 4}) in ONE pass over X, with the cross-lane work batched over groups of
+// four rows.
+//
+// Reference semantics: LibMatrixMult.matrixMultChain (XtXv, XtwXv, XtXvy) and the MultiLogReg
+// inner-loop chain t(X) %*% (P * (X %*% V) - P * rowSums(P * (X %*% V))) plus the fused
+// softmax gradient (U = X %*% V, t(X) %*% (softmax([U, 0])[, 1:K] - Y)) that
+// compiler/rewrites.py forms from MultiLogReg's line search (scripts/algorithms/MultiLogReg.dml).
+//
+// Why a second front end next to rowstream.hip's per-row RowOps: with one row at a time every
+// dot product needs its own 64-lane reduction (4 DPP steps + 4 readlanes each, a long dependent
+// chain), so the K = 4 chains were VALU-latency bound (149 VALU/row for XtPSXv, 290 for the
+// softmax gradient at one wave per SIMD; profiles/pmc_chain_r2.txt).  Here a wave takes four
+// rows, leaving 4K partial dot products per lane, and reduces all of them together with a
+// *transposing* butterfly: each step exchanges half of the remaining values with a partner
+// lane and adds (v_permlane32_swap / v_permlane16_swap for lane bits 5 / 4, DPP row_mirror /
+// row_half_mirror for bits 3 / 2), so the 16 sums of a K = 4 group cost ~35 VALU instead of
+// ~190, and each lane ends up owning one (row, k) value.  The row epilogue (Hessian weights,
+// softmax) then runs on 16 lanes at once, and its results reach the accumulate phase as
+// wave-uniform SGPR operands of v_pk_fma_f32.
+//
+// Streaming: X rows arrive by LDS-DMA (global_load_lds_dwordx4; the row-side operand by
+// global_load_lds_dword) into a per-wave ring of R = 8 row slots (two groups) retired with a
+// counted s_waitcnt vmcnt, exactly as rowstream_dma_kernel; the fused-softmax U output is one
+// store per group (lane-selected address, never skipped) and enters the vmcnt count.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <unordered_set>
+
+namespace sysml_c4 {
+
+enum Mode { XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5, XTSMG = 10 };   // = rowstream.hip
+constexpr int WAVES = 4;
+constexpr int BLOCK = 64 * WAVES;
+constexpr int G = 4;     // rows per group
+constexpr int R = 8;     // ring slots per wave (two groups)
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) char lds_char;
+
+__device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 16); }
+
+template <typename T> struct Pieces { static constexpr int P = (int)sizeof(T) / 2; };   // 16-B pieces / 8 elements
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int QP_X1 = 0xB1, QP_X2 = 0x4E, ROW_HALF_MIRROR = 0x141, ROW_MIRROR = 0x140;
+
+// partner value for butterfly step s: s = 0 lane ^ 32, 1 lane ^ 16, 2 lane ^ 15 (row_mirror),
+// 3 lane ^ 7 (row_half_mirror), 4 lane ^ 1, 5 lane ^ 2 (quad_perm)
+template <int S>
+__device__ __forceinline__ float partner(float v) {
+  if constexpr (S == 0) return __shfl_xor(v, 32, 64);
+  else if constexpr (S == 1) return __shfl_xor(v, 16, 64);
+  else if constexpr (S == 2) return dpp<ROW_MIRROR>(v);
+  else if constexpr (S == 3) return dpp<ROW_HALF_MIRROR>(v);
+  else if constexpr (S == 4) return dpp<QP_X1>(v);
+  else return dpp<QP_X2>(v);
+}
+
+// one halving step over the lane bit of step S: values [0, n/2) are kept by lanes whose bit
+// is 0, [n/2, n) by lanes whose bit is 1; the partner's copy of the kept half is added
+template <int S, int N>
+__device__ __forceinline__ void halve(float (&v)[16], int lane) {
+  constexpr int H = N / 2;
+  if constexpr (S == 0 || S == 1) {
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      // v_permlane{32,16}_swap: lanes with the bit clear get {own a, partner a}, lanes with
+      // it set get {partner b, own b}  (tools/probe/permlane_probe.hip)
+      uint32_t a = __float_as_uint(v[i]), b = __float_as_uint(v[i + H]);
+      if constexpr (S == 0) {
+        auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+        v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      } else {
+        auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+        v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      }
+    }
+  } else {
+    const bool hi = (lane >> (S == 2 ? 3 : 2)) & 1;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      const float keep = hi ? v[i + H] : v[i];
+      const float send = hi ? v[i] : v[i + H];
+      v[i] = keep + partner<S>(send);
+    }
+  }
+}
+
+// reduce NV = 4K per-lane partials over the wave; afterwards lane l owns value
+// (l >> (6 - log2 NV)) & (NV - 1), replicated on 64 / NV lanes.
+template <int NV>
+__device__ __forceinline__ float transpose_reduce(float (&v)[16], int lane) {
+  static_assert(NV == 4 || NV == 8 || NV == 16, "NV");
+  halve<0, NV>(v, lane);
+  halve<1, NV / 2>(v, lane);
+  if constexpr (NV >= 8) halve<2, NV / 4>(v, lane);
+  if constexpr (NV >= 16) halve<3, NV / 8>(v, lane);
+  float x = v[0];
+  if constexpr (NV < 8) x += partner<2>(x);
+  if constexpr (NV < 16) x += partner<3>(x);
+  x += partner<4>(x);
+  x += partner<5>(x);
+  return x;
+}
+
+template <int N> __device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// one X row of the ring slot -> 8J fp32 values of this lane.  All of the row's LDS reads and
+// their lgkmcnt wait sit in ONE asm statement: hipcc must not see an LDS read it would order
+// behind the pending LDS-DMA with vmcnt(0), and the wait must not be separable from the reads.
+__device__ __forceinline__ void unpack_bf16(uint4 r, float* o) {
+  o[0] = bf2f(r.x & 0xffffu); o[1] = bf2f(r.x >> 16);
+  o[2] = bf2f(r.y & 0xffffu); o[3] = bf2f(r.y >> 16);
+  o[4] = bf2f(r.z & 0xffffu); o[5] = bf2f(r.z >> 16);
+  o[6] = bf2f(r.w & 0xffffu); o[7] = bf2f(r.w >> 16);
+}
+__device__ __forceinline__ void unpack_f32(uint4 r, float* o) {
+  o[0] = __uint_as_float(r.x); o[1] = __uint_as_float(r.y);
+  o[2] = __uint_as_float(r.z); o[3] = __uint_as_float(r.w);
+}
+
+template <typename T, int J>
+__device__ __forceinline__ void lds_row(const lds_char* slot, int lane, float (&x)[J * 8]) {
+  const uint32_t a = (uint32_t)(uintptr_t)(slot + lane * 16);
+  if constexpr (sizeof(T) == 2 && J == 1) {
+    uint4 r0;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(r0) : "v"(a) : "memory");
+    unpack_bf16(r0, x);
+  } else if constexpr (sizeof(T) == 2 && J == 2) {
+    uint4 r0, r1;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(r0), "=&v"(r1) : "v"(a) : "memory");
+    unpack_bf16(r0, x);
+    unpack_bf16(r1, x + 8);
+  } else if constexpr (J == 1) {
+    uint4 r0, r1;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(r0), "=&v"(r1) : "v"(a) : "memory");
+    unpack_f32(r0, x);
+    unpack_f32(r1, x + 4);
+  } else {
+    uint4 r0, r1, r2, r3;
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\tds_read_b128 %2, %4 offset:2048\n\t"
+        "ds_read_b128 %3, %4 offset:3072\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : "v"(a) : "memory");
+    unpack_f32(r0, x);
+    unpack_f32(r1, x + 4);
+    unpack_f32(r2, x + 8);
+    unpack_f32(r3, x + 12);
+  }
+}
+
+__device__ __forceinline__ float lds_f32(const lds_char* p) {
+  uint32_t t;
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(t) : "v"(a) : "memory");
+  return __uint_as_float(t);
+}
+
+template <typename T, int K, int J>
+constexpr size_t lds_bytes() {
+  constexpr size_t ring = (size_t)WAVES * R * (J * Pieces<T>::P * 1024 + 256);
+  constexpr size_t red = (size_t)J * 512 * K * 4;
+  return ring > red ? ring : red;
+}
+
+template <typename T, int K, int J, int MODE>
+__global__ void __launch_bounds__(BLOCK, 2)
+chain4_kernel(const T* __restrict__ X, int64_t N, int D, const float* __restrict__ V, int ldv,
+              const float* __restrict__ S, int lds, int sbc, float* __restrict__ out,
+              float* __restrict__ U, int ldu, int64_t rows_per_block) {
+  constexpr int C = J * 8;
+  constexpr int K2 = (K + 1) / 2;
+  constexpr int NV = G * K;
+  constexpr int LSH = (NV == 16) ? 2 : (NV == 8) ? 3 : 4;   // lanes per value = 1 << LSH
+  constexpr int P = Pieces<T>::P;
+  constexpr int XB = J * P * 1024;
+  constexpr int SLOT = XB + 256;
+  constexpr int NPR = J * P + 1;                  // DMA instructions per row (X pieces + S)
+  constexpr bool SMG = (MODE == XTSMG);
+  constexpr int NSTG = SMG ? 1 : 0;               // stores per group
+  constexpr int NGR = R / G;                      // groups in the ring
+  constexpr int WAITN = (NGR - 1) * (G * NPR + NSTG);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  // ---- V slice in registers: vreg[c][kk] = V[d(c)][2kk .. 2kk+1], d(c) = (j*64 + lane)*8 + e
+  f2 vreg[C][K2];
+  {
+    float* sV = reinterpret_cast<float*>(smem);
+    constexpr int Dp = J * 512;
+    for (int i = threadIdx.x; i < Dp * K; i += BLOCK) {
+      const int d = i / K, k = i - d * K;
+      sV[i] = (d < D) ? V[(int64_t)d * ldv + k] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk) {
+          const float* p = sV + ((j * 64 + lane) * 8 + e) * K + 2 * kk;
+          vreg[j * 8 + e][kk] = f2{p[0], (2 * kk + 1 < K) ? p[1] : 0.f};
+        }
+    __syncthreads();   // the ring overlays the V staging area
+  }
+  f2 acc[C][K2];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int kk = 0; kk < K2; ++kk) acc[c][kk] = f2{0.f, 0.f};
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
+  const int64_t rlast = r1 - 1;
+  int coff[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c0 = (j * 64 + lane) * 8;
+    coff[j] = (c0 < D) ? c0 : D - 8;
+  }
+  int scol;
+  if constexpr (SMG) scol = lane < sbc ? lane : sbc - 1;
+  else if constexpr (MODE == XTWXV || MODE == XTXVY) scol = sbc ? 0 : (lane < K ? lane : K - 1);
+  else scol = lane < K ? lane : K - 1;
+
+  lds_char* ring = (lds_char*)smem + wave * (R * SLOT);
+  float* const upad = U + N * (int64_t)ldu;
+
+  auto fetch = [&](int slot, int64_t rr) {
+    rr = (rr < rlast) ? rr : rlast;
+    const T* row = X + rr * (int64_t)D;
+    lds_char* sb = ring + slot * SLOT;
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int h = 0; h < P; ++h)
+        __builtin_amdgcn_global_load_lds((const void*)(row + coff[j] + h * (8 / P)),
+                                         (void __attribute__((address_space(3)))*)(sb + (j * P + h) * 1024), 16, 0,
+                                         0);
+    __builtin_amdgcn_global_load_lds((const void*)(S + rr * (int64_t)lds + scol),
+                                     (void __attribute__((address_space(3)))*)(sb + XB), 4, 0, 0);
+  };
+
+  // rows of the wave: base + (slot) * WAVES; group q = slots [4q, 4q + 4)
+  constexpr int STEP = WAVES * R;
+  int64_t base = r0 + wave;
+#pragma unroll
+  for (int q = 0; q < NGR; ++q) {
+    // round-0 invariant of the counted wait: every group sees NGR-1 younger (store + refill)
+    // sets, so groups after the first are preceded by a dummy store
+    if constexpr (SMG) if (q > 0) *upad = 0.f;
+#pragma unroll
+    for (int s = 0; s < G; ++s) fetch(q * G + s, base + (q * G + s) * WAVES);
+  }
+
+  const int myv = (lane >> LSH) & (NV - 1);   // (row, k) value this lane owns after the reduce
+  const int myrho = myv / K, myk = myv - (myv / K) * K;
+
+  for (; base < r1; base += STEP) {
+#pragma unroll
+    for (int q = 0; q < NGR; ++q) {
+      wait_vmcnt<WAITN>();
+      // ---- phase 1: 4K partial dot products per lane
+      float pv[16];
+#pragma unroll
+      for (int rho = 0; rho < G; ++rho) {
+        float x[C];
+        lds_row<T, J>(ring + (q * G + rho) * SLOT, lane, x);
+        f2 u0[K2];
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk) u0[kk] = f2{0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int kk = 0; kk < K2; ++kk) u0[kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, vreg[c][kk], u0[kk]);
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk) {
+          const f2 u = u0[kk];
+          pv[rho * K + 2 * kk] = u.x;
+          if (2 * kk + 1 < K) pv[rho * K + 2 * kk + 1] = u.y;
+        }
+      }
+      // ---- transposing butterfly: lane owns u = (X V)[row myrho][myk]
+      const float u = transpose_reduce<NV>(pv, lane);
+      const int64_t myrow = base + (int64_t)(q * G + myrho) * WAVES;
+      const bool rvalid = myrow < r1;
+      const float sval = lds_f32(ring + (q * G + myrho) * SLOT + XB + 4 * myk);
+      // ---- row epilogue on the (row, k) lanes
+      float g;
+      if constexpr (MODE == XTXV) {
+        g = u;
+      } else if constexpr (MODE == XTWXV) {
+        g = sval * u;
+      } else if constexpr (MODE == XTXVY) {
+        g = u - sval;
+      } else if constexpr (MODE == XTPSXV) {
+        const float qv = sval * u;
+        float sq = qv;
+        if constexpr (K >= 2) sq += (K == 2) ? partner<2>(sq) : partner<3>(sq);
+        if constexpr (K >= 4) sq += partner<2>(sq);
+        g = qv - sval * sq;
+      } else {   // XTSMG: softmax over [u_1 .. u_kact, 0]
+        const bool act = myk < sbc;
+        float m = act ? u : 0.f;
+        if constexpr (K >= 2) m = fmaxf(m, (K == 2) ? partner<2>(m) : partner<3>(m));
+        if constexpr (K >= 4) m = fmaxf(m, partner<2>(m));
+        m = fmaxf(m, 0.f);
+        const float e = act ? __expf(u - m) : 0.f;
+        float s = e;
+        if constexpr (K >= 2) s += (K == 2) ? partner<2>(s) : partner<3>(s);
+        if constexpr (K >= 4) s += partner<2>(s);
+        s += __expf(-m);
+        g = act ? e / s - sval : 0.f;
+        // U output: one store per group (replica 0 of each valid cell, else the pad row)
+        const bool st = act && rvalid && ((lane & ((1 << LSH) - 1)) == 0);
+        float* dst = st ? U + myrow * (int64_t)ldu + myk : upad;
+        *dst = u;
+      }
+      g = rvalid ? g : 0.f;
+      // ---- phase 2: acc[c][k] += x[row][c] * g[row][k] (g wave-uniform from SGPRs)
+#pragma unroll
+      for (int rho = 0; rho < G; ++rho) {
+        f2 gk[K2];
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk) {
+          const int v0 = rho * K + 2 * kk;
+          const float ga = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), v0 << LSH));
+          const float gb = (2 * kk + 1 < K)
+                               ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), (v0 + 1) << LSH))
+                               : 0.f;
+          gk[kk] = f2{ga, gb};
+        }
+        float x[C];
+        lds_row<T, J>(ring + (q * G + rho) * SLOT, lane, x);
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int kk = 0; kk < K2; ++kk) acc[c][kk] = __builtin_elementwise_fma(f2{x[c], x[c]}, gk[kk], acc[c][kk]);
+      }
+      // ---- refill the group's slots (their LDS reads have retired)
+#pragma unroll
+      for (int s = 0; s < G; ++s) fetch(q * G + s, base + STEP + (q * G + s) * WAVES);
+    }
+  }
+  wait_vmcnt<0>();   // no LDS-DMA may outlive the ring
+
+  // ---- combine the 4 waves' accumulators through LDS, one partial per block
+  float* red = reinterpret_cast<float*>(smem);
+  __syncthreads();
+  for (int w = 0; w < WAVES; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+          for (int kk = 0; kk < K2; ++kk) {
+            const int idx = ((j * 64 + lane) * 8 + e) * K + 2 * kk;
+            const f2 a = acc[j * 8 + e][kk];
+            if (w == 0) {
+              red[idx] = a.x;
+              if (2 * kk + 1 < K) red[idx + 1] = a.y;
+            } else {
+              red[idx] += a.x;
+              if (2 * kk + 1 < K) red[idx + 1] += a.y;
+            }
+          }
+    }
+    __syncthreads();
+  }
+  float* dst = out + (int64_t)blockIdx.x * D * K;
+  for (int i = threadIdx.x; i < D * K; i += BLOCK) dst[i] = red[i];
+}
+
+static void allow_lds(const void* fn, size_t bytes) {
+  static std::unordered_set<const void*> done;
+  if (bytes <= 65536 || done.count(fn)) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  done.insert(fn);
+}
+
+template <typename T, int K, int J, int MODE>
+static int launch(bool occ, const void* X, int64_t N, int D, const float* V, int ldv, const float* S, int lds,
+                  int sbc, float* out, float* U, int ldu, int grid, int64_t rpb, hipStream_t st) {
+  auto kfn = chain4_kernel<T, K, J, MODE>;
+  const size_t sh = lds_bytes<T, K, J>();
+  allow_lds(reinterpret_cast<const void*>(kfn), sh);
+  if (occ) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, BLOCK, sh) != hipSuccess) return -1;
+    return nb;
+  }
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(BLOCK), sh, st, (const T*)X, N, D, V, ldv, S, lds, sbc, out, U, ldu,
+                     rpb);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <typename T, int MODE>
+static int route_kj(int K, int J, bool occ, const void* X, int64_t N, int D, const float* V, int ldv, const float* S,
+                    int lds, int sbc, float* out, float* U, int ldu, int grid, int64_t rpb, hipStream_t st) {
+#define C4_CASE(KV, JV)                                                                                    \
+  if (K == KV && J == JV) return launch<T, KV, JV, MODE>(occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st);
+  C4_CASE(1, 1) C4_CASE(1, 2) C4_CASE(2, 1) C4_CASE(2, 2) C4_CASE(4, 1) C4_CASE(4, 2)
+#undef C4_CASE
+  return -1;
+}
+
+template <typename T>
+static int route(int mode, int K, int J, bool occ, const void* X, int64_t N, int D, const float* V, int ldv,
+                 const float* S, int lds, int sbc, float* out, float* U, int ldu, int grid, int64_t rpb,
+                 hipStream_t st) {
+  switch (mode) {
+    case XTXV: return route_kj<T, XTXV>(K, J, occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st);
+    case XTWXV: return route_kj<T, XTWXV>(K, J, occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st);
+    case XTXVY: return route_kj<T, XTXVY>(K, J, occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st);
+    case XTPSXV: return route_kj<T, XTPSXV>(K, J, occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st);
+    case XTSMG: return route_kj<T, XTSMG>(K, J, occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st);
+    default: return -1;
+  }
+}
+
+}  // namespace sysml_c4
+
+extern "C" {
+
+// Blocks per CU of the kernel for (mode, xdtype, K, D) (the host sizes the grid from it).
+int sysml_chain4_occupancy(int mode, int xdtype, int K, int D) {
+  using namespace sysml_c4;
+  if (D <= 0 || D > 1024) return -1;
+  const int J = D <= 512 ? 1 : 2;
+  if (xdtype == 0)
+    return route<uint16_t>(mode, K, J, true, nullptr, 0, D, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, 0, 0, 0,
+                           nullptr);
+  if (xdtype == 1)
+    return route<float>(mode, K, J, true, nullptr, 0, D, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, 0, 0, 0,
+                        nullptr);
+  return -1;
+}
+
+// X: N x D (bf16 xdtype 0 / fp32 xdtype 1), D % 8 == 0, 16-B aligned; V: D x K fp32 (ldv);
+// S: row-side operand (N x ., leading dim lds; sbc: broadcast column for XtwXv/XtXvy, number
+// of real classes for the softmax gradient); out: grid x (D*K) fp32 partials; U (softmax
+// gradient only): (N + 1) x ldu fp32, row N is a scratch pad.  K in {1, 2, 4}.
+int sysml_chain4(int mode, int xdtype, const void* X, int64_t N, int D, const float* V, int ldv, const float* S,
+                 int lds, int sbc, float* out, float* U, int ldu, int K, int grid, int64_t rows_per_block,
+                 void* stream) {
+  using namespace sysml_c4;
+  if (D <= 0 || D > 1024 || (D & 7) || N <= 0 || grid <= 0 || (((uintptr_t)X) & 15)) return -1;
+  if (mode == XTSMG && (U == nullptr || sbc < 1 || sbc > K)) return -1;
+  const int J = D <= 512 ? 1 : 2;
+  hipStream_t st = (hipStream_t)stream;
+  if (xdtype == 0)
+    return route<uint16_t>(mode, K, J, false, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rows_per_block, st);
+  if (xdtype == 1)
+    return route<float>(mode, K, J, false, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rows_per_block, st);
+  return -1;
+}
+
+}  // extern "C"

@@ -31,6 +31,7 @@
 // written (reduced over blocks by the host wrapper).  Accumulation is fp32 for
 // bf16/fp32 X and fp64 for fp64 X.
 #include <hip/hip_runtime.h>
+#include <unordered_set>
 #include <stdint.h>
 
 namespace sysml {
@@ -211,6 +212,9 @@ rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
     if (ri < r1) {
 #pragma unroll
       for (int j = 0; j < J; ++j) load_raw<T>(nxt[i][j], X + ri * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+    } else {
+#pragma unroll
+      for (int j = 0; j < J; ++j) nxt[i][j] = Raw8<T>{};   // rows past the block: zeros, never garbage
     }
   }
   for (; r < r1; r += STEP) {
@@ -226,6 +230,9 @@ rowstream_kernel(const T* __restrict__ X, int64_t N, int D, int vec,
       if (rn < r1) {
 #pragma unroll
         for (int j = 0; j < J; ++j) load_raw<T>(nxt[i][j], X + rn * (int64_t)D, (j * 64 + lane) * 8, D, vec);
+      } else {
+#pragma unroll
+        for (int j = 0; j < J; ++j) nxt[i][j] = Raw8<T>{};
       }
     }
     bool valid[R];
@@ -385,6 +392,7 @@ struct RowOps {
 
   f2 vreg[VREG ? C : 1][VREG ? K2 : 1];
   f2 acc[MI::accum ? C : 1][MI::accum ? K2 : 1];
+  float ulast[MODE == XTSMG ? K : 1];   // XTSMG: U row of the last processed row (wave-uniform)
   const float* sV;
   int lane;
 
@@ -493,11 +501,10 @@ struct RowOps {
           const float inv = 1.f / s;
 #pragma unroll
           for (int k = 0; k < K; ++k) gs[k] = (k < kact) ? e[k] * inv - sv[k] : 0.f;
-          if (valid) {
+          // U is not stored here: the DMA front end batches the row outputs of a whole ring
+          // round into one store (a per-row store would share vmcnt with the LDS-DMA ring)
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-              if (lane == k && k < kact) out[r * (int64_t)ldo + k] = us[k];
-          }
+          for (int k = 0; k < K; ++k) ulast[k] = us[k];
         }
 #pragma unroll
         for (int kk = 0; kk < K2; ++kk)
@@ -712,11 +719,21 @@ rowstream_dma_kernel(const T* __restrict__ X, int64_t N, int D,
 #pragma unroll
   for (int p = 0; p < R; ++p) fetch(p, base + p * WAVES);
 
+  // XTSMG: lane p*K + k collects U[row of slot p][k] over a ring round; one store per round
+  // (to U's pad row N for lanes without a valid cell, so it is never skipped).  Invariant for
+  // the counted wait: exactly one store is younger than the loads of the slot being waited
+  // on, hence the dummy store after the prologue.
+  constexpr bool SMG = (MODE == XTSMG);
+  constexpr int NST = SMG ? 1 : 0;
+  float ureg = 0.f;
+  float* const upad = uout + N * (int64_t)ldu;
+  if constexpr (SMG) *upad = 0.f;
+
   for (; base < r1; base += STEP) {
 #pragma unroll
     for (int p = 0; p < R; ++p) {
       const int64_t r = base + p * WAVES;   // wave-uniform
-      wait_vmcnt<(R - 1) * NPR>();          // slot p landed; R-1 rows stay in flight
+      wait_vmcnt<(R - 1) * NPR + NST>();    // slot p landed; R-1 rows stay in flight
       Raw8<T> cur[J];
       float sl;
       const uint32_t xa = ring_addr + p * SLOT + lane * 16;
@@ -729,6 +746,17 @@ rowstream_dma_kernel(const T* __restrict__ X, int64_t N, int D,
       if constexpr (!OPS::NEEDS) sl = 0.f;
       fetch(p, r + STEP);                   // refill the slot (its LDS reads have retired)
       ops.process(cur, sl, r, r < r1, uout, ldu, sbc);
+      if constexpr (SMG) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) ureg = (lane == p * K + k) ? ops.ulast[k] : ureg;
+      }
+    }
+    if constexpr (SMG) {
+      const int sl_ = lane / K, kl = lane - (lane / K) * K;
+      const int64_t row = base + (int64_t)sl_ * WAVES;
+      const bool ok = (lane < R * K) && (kl < sbc) && (row < r1);
+      float* dst = ok ? uout + row * (int64_t)ldu + kl : upad;
+      *dst = ureg;
     }
   }
   wait_vmcnt<0>();                          // no LDS-DMA may outlive the block's LDS
@@ -746,6 +774,14 @@ static int g_rows_per_iter = 0;   // 0 = auto, else rows per iteration (generic)
 static int g_variant = 0;         // 0 = auto (packed fp32 where applicable), 1 = generic scalar kernel
 static float* g_uout = nullptr;   // XTSMG: row output U (set by sysml_rowstream_smg around the launch)
 static int g_ldu = 0;
+
+// dynamic LDS above 64 KiB must be allowed per kernel (once)
+static void allow_lds(const void* fn, size_t bytes) {
+  static std::unordered_set<const void*> done;
+  if (bytes <= 65536 || done.count(fn)) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  done.insert(fn);
+}
 
 template <typename T, typename A, int K, int J, int MODE>
 static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int ldv, const void* S,
@@ -774,10 +810,32 @@ static int launch_t(const void* X, int64_t N, int D, int vec, const void* V, int
         if (deep) SYSML_PK(4); else SYSML_PK(2);
 #undef SYSML_PK
       } else {
-        const size_t shd = deep ? dma_lds_bytes<T, K, J, 4>() : dma_lds_bytes<T, K, J, 2>();
-#define SYSML_DMA(PF) hipLaunchKernelGGL((rowstream_dma_kernel<T, K, J, MODE, PF>), dim3(grid), dim3(BLOCK), shd, st, \
-          (const T*)X, N, D, (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, rpb, g_uout, g_ldu)
-        if (deep) SYSML_DMA(4); else SYSML_DMA(2);
+        // LDS-DMA ring depth R (rows in flight per wave).  The ring is LDS, so R costs no
+        // VGPRs; what bounds it is the LDS of the co-resident blocks.  The K >= 4 kernels run 2
+        // waves/SIMD (XTSMG 1) by VGPRs, so they get deeper rings to keep ~96 KiB of X in
+        // flight per CU (profiles/rowstream_ring_depth_r2.txt); narrower modes are LDS-limited
+        // at R = 4 (bf16) / 2 (fp32) with 3 blocks per CU.
+        int R = deep ? 4 : 2;
+        if (!knob) {
+          if (MODE == XTSMG) R = sizeof(T) == 2 ? 12 : 6;
+          else if (K >= 4) R = sizeof(T) == 2 ? 6 : 3;
+        }
+#define SYSML_DMA(PF) do { \
+          auto kfn = rowstream_dma_kernel<T, K, J, MODE, PF>; \
+          const size_t shb = dma_lds_bytes<T, K, J, PF>(); \
+          allow_lds(reinterpret_cast<const void*>(kfn), shb); \
+          hipLaunchKernelGGL(kfn, dim3(grid), dim3(BLOCK), shb, st, (const T*)X, N, D, \
+                             (const float*)V, ldv, (const float*)S, lds, sbc, (float*)out, rpb, g_uout, g_ldu); \
+        } while (0)
+        if constexpr (MODE == XTSMG) {
+          if constexpr (sizeof(T) == 2) { if (R == 12) SYSML_DMA(12); else if (R == 4) SYSML_DMA(4); else SYSML_DMA(2); }
+          else { if (R == 6) SYSML_DMA(6); else if (R == 4) SYSML_DMA(4); else SYSML_DMA(2); }
+        } else if constexpr (K >= 4) {
+          if constexpr (sizeof(T) == 2) { if (R == 6) SYSML_DMA(6); else if (R == 4) SYSML_DMA(4); else SYSML_DMA(2); }
+          else { if (R == 3) SYSML_DMA(3); else if (R == 4) SYSML_DMA(4); else SYSML_DMA(2); }
+        } else {
+          if (R == 4) SYSML_DMA(4); else SYSML_DMA(2);
+        }
 #undef SYSML_DMA
       }
       return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -866,7 +924,8 @@ int sysml_rowstream(int mode, int xdtype, const void* X, int64_t N, int D, const
   return -1;
 }
 
-// Fused multinomial-logreg candidate evaluation (mode XTSMG): U = X %*% V (N x kact, written
+// Fused multinomial-logreg candidate evaluation (mode XTSMG): U = X %*% V (N x kact, written; U
+// must have N + 1 rows: row N is a scratch pad the kernel stores into
 // to U with leading dimension ldu) and partial[grid][D x K] of t(X) %*% (softmax([U,0])[,1:kact]
 // - Y[,1:kact]) in one pass over X.  V is D x K (K = kact padded to 2 or 4, zero columns),
 // Y is N x >= kact (leading dimension ldy).  bf16 / fp32 X only.  Returns 0 on success.

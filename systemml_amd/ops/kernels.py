@@ -73,6 +73,13 @@ def load(required=False):
                                ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     L.sysml_mchain_occupancy.restype = ctypes.c_int
     L.sysml_mchain_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.sysml_chain4.restype = ctypes.c_int
+    L.sysml_chain4.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_int64, ctypes.c_void_p]
+    L.sysml_chain4_occupancy.restype = ctypes.c_int
+    L.sysml_chain4_occupancy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     _lib = L
     return L
 
@@ -256,6 +263,54 @@ def xtg(X, G):
     return _result(R if kp == K else R[:, :K].contiguous())
 
 
+# ----------------------------------------------------------------------------
+# Row-group chain kernels (ops/hip/chain4.hip): batched transposing reductions over 4 rows.
+# SYSML_CHAIN4=0 routes the chains back to the per-row rowstream kernels (A/B switch).
+# ----------------------------------------------------------------------------
+CHAIN4 = os.environ.get("SYSML_CHAIN4", "1") != "0"
+_c4occ = {}
+
+
+def _c4_ok(X, mode, kp):
+    # K = 1 chains (LinregCG's XtXv) stay on the per-row kernel: one dot product per row has
+    # nothing to batch and rowstream streams it 4-7 % faster (profiles/chain4_kbench_r2.txt)
+    if not (CHAIN4 and X.dtype in (torch.bfloat16, torch.float32) and kp in ((1, 2, 4) if mode == XTSMG else (2, 4))):
+        return False
+    if X.shape[1] % 8 or X.data_ptr() % 16 or not X.is_contiguous():
+        return False
+    # the K = 4, D > 512 bf16 XtXv instantiation spills (hipcc register allocation): rowstream
+    return not (mode == XTXV and kp == 4 and X.dtype == torch.bfloat16 and X.shape[1] > 512)
+
+
+def _c4_grid(L, mode, X, kp):
+    code = 0 if X.dtype == torch.bfloat16 else 1
+    key = (mode, code, kp, X.shape[1] > 512, X.device.index)
+    if key not in _c4occ:
+        occ = L.sysml_chain4_occupancy(mode, code, kp, X.shape[1])
+        cus = torch.cuda.get_device_properties(X.device).multi_processor_count
+        _c4occ[key] = max(1, occ) * cus
+    return _c4occ[key]
+
+
+def _chain4(mode, X, kp, V, S, lds, sbc, U=None, ldu=0):
+    """Launch chain4; returns the D x kp fp32 result (sum of the per-block partials)."""
+    L = load(required=True)
+    N, D = X.shape
+    code = 0 if X.dtype == torch.bfloat16 else 1
+    grid = min(_c4_grid(L, mode, X, kp), (N + 63) // 64)
+    rpb = (N + grid - 1) // grid
+    grid = (N + rpb - 1) // rpb
+    part = torch.empty((grid, D * kp), dtype=torch.float32, device=X.device)
+    if S is None:
+        S, lds = V, 0      # the kernel streams a row-side operand in every mode: any valid memory
+    rc = L.sysml_chain4(mode, code, ctypes.c_void_p(X.data_ptr()), N, D, ctypes.c_void_p(V.data_ptr()), kp,
+                        ctypes.c_void_p(S.data_ptr()), lds, sbc, ctypes.c_void_p(part.data_ptr()),
+                        ctypes.c_void_p(U.data_ptr() if U is not None else 0), ldu, kp, grid, rpb, _stream())
+    if rc != 0:
+        return None
+    return part.sum(0).reshape(D, kp)
+
+
 def mmchain(ctype, X, V, W=None):
     mode = _CHAIN[ctype]
     K = V.shape[1]
@@ -274,6 +329,13 @@ def mmchain(ctype, X, V, W=None):
             S = _pad_cols(W, kp, adt, X.device).contiguous()
         else:
             return None
+    if _c4_ok(X, mode, kp):
+        Vf = _pad_cols(V, kp, torch.float32, X.device).contiguous()
+        Sf = S.to(torch.float32).contiguous() if S is not None else None
+        R = _chain4(mode, X, kp, Vf, Sf, Sf.shape[1] if Sf is not None else 0, sbc)
+        if R is not None:
+            _count("chain4.mmchain." + ctype)
+            return _result(R if kp == K else R[:, :K].contiguous())
     if _mfma_ok(X, kp, mode):
         R = _mchain(mode, X, kp, V=V, S=S, sbc=sbc)
         if R is not None:
@@ -299,19 +361,28 @@ def smgrad(X, V, Y):
     if K > 4 or Y.shape != (X.shape[0], K) or V.shape[0] != X.shape[1]:
         return None
     kp = _kpad(K)
+    N, D = X.shape
+    if _c4_ok(X, XTSMG, kp):
+        Vf = _pad_cols(V, kp, torch.float32, X.device).contiguous()
+        Yc = Y.to(device=X.device, dtype=torch.float32).contiguous()
+        Upad = torch.empty((N + 1, K), dtype=torch.float32, device=X.device)   # row N: kernel's pad row
+        G = _chain4(XTSMG, X, kp, Vf, Yc, K, K, U=Upad, ldu=K)
+        if G is not None:
+            _count("chain4.smgrad")
+            return _result(Upad[:N]), _result(G if kp == K else G[:, :K].contiguous())
     kp = max(kp, 2)
     L = load(required=True)
     code, adt = _xcode(X)
-    N, D = X.shape
     Vp = _pad_cols(V, kp, torch.float32, X.device).contiguous()
     Yc = Y.to(device=X.device, dtype=torch.float32).contiguous()
-    U = torch.empty((N, K), dtype=torch.float32, device=X.device)
+    Upad = torch.empty((N + 1, K), dtype=torch.float32, device=X.device)   # row N: kernel's pad row
+    U = Upad[:N]
     grid = _grid(N)
     rpb = (N + grid - 1) // grid
     grid = (N + rpb - 1) // rpb
     part = torch.empty((grid, D * kp), dtype=torch.float32, device=X.device)
     rc = L.sysml_rowstream_smg(code, ctypes.c_void_p(X.data_ptr()), N, D, ctypes.c_void_p(Vp.data_ptr()), kp,
-                               ctypes.c_void_p(Yc.data_ptr()), K, K, ctypes.c_void_p(U.data_ptr()), K,
+                               ctypes.c_void_p(Yc.data_ptr()), K, K, ctypes.c_void_p(Upad.data_ptr()), K,
                                ctypes.c_void_p(part.data_ptr()), kp, grid, rpb, _stream())
     if rc != 0:
         return None

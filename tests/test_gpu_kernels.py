@@ -111,8 +111,10 @@ def test_dml_uses_fused_kernels(gpu_config):
 def mfma_all(K):
     """Route every eligible op (incl. the fused chains) through the MFMA kernel."""
     K.MFMA_ALL = True
+    K.CHAIN4 = False
     yield
     K.MFMA_ALL = False
+    K.CHAIN4 = True
 
 
 def _ints(shape, lo, hi, seed):
@@ -201,4 +203,51 @@ def test_smgrad_fused_softmax_gradient(K, dt, d, k):
     g_ref = x64.t() @ (p - y)
     assert (u.double() - u_ref).abs().max().item() <= 2e-4 * u_ref.abs().max().item()
     assert (g.double() - g_ref).abs().max().item() <= 2e-4 * g_ref.abs().max().item()
-    assert K.counters.get("rowstream.smgrad", 0) > 0
+    assert K.counters.get("rowstream.smgrad", 0) + K.counters.get("chain4.smgrad", 0) > 0
+
+
+# ---------------------------------------------------------------------------
+# Row-group chain kernels (ops/hip/chain4.hip): exact small-integer data through every mode,
+# ragged row counts (partial groups / blocks) and D not a multiple of 64.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 15, 17, 4099, 50001])
+@pytest.mark.parametrize("d", [8, 136, 512, 520, 1000])
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_chain4_exact_integer(K, n, d, k, dt):
+    x = _ints((n, d), -3, 3, 11 + d).to(dt)
+    x64 = x.double()
+    v = _ints((d, k), -2, 2, 21 + k)
+    g = _ints((n, k), -2, 2, 31 + n)
+    w = _ints((n, 1), 0, 3, 41 + n)
+    u64 = x64 @ v
+    c0 = dict(K.counters)
+    torch.testing.assert_close(K.mmchain("XtXv", x, v).double(), x64.t() @ u64, rtol=0, atol=0)
+    torch.testing.assert_close(K.mmchain("XtXvy", x, v, g).double(), x64.t() @ (u64 - g), rtol=0, atol=0)
+    torch.testing.assert_close(K.mmchain("XtwXv", x, v, w).double(), x64.t() @ (w * u64), rtol=0, atol=0)
+    q = g * u64
+    ref = x64.t() @ (q - g * q.sum(1, keepdim=True))
+    torch.testing.assert_close(K.mmchain("XtPSXv", x, v, g).double(), ref, rtol=0, atol=0)
+    used = sum(v_ - c0.get(k_, 0) for k_, v_ in K.counters.items() if k_.startswith("chain4."))
+    if k > 1:
+        assert used >= 3
+
+
+@pytest.mark.parametrize("n", [17, 4099, 300001])
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+def test_chain4_softmax_gradient(K, n, k):
+    d = 1000
+    x = _mk(n, d, torch.bfloat16, seed=5)
+    x64 = x.double()
+    g0 = torch.Generator(device="cuda").manual_seed(3)
+    v = torch.randn((d, k), generator=g0, device="cuda", dtype=torch.float64) * 0.05
+    y = (torch.rand((n, k), generator=g0, device="cuda") < 0.3).double()
+    c0 = K.counters.get("chain4.smgrad", 0)
+    U, G = K.smgrad(x, v.float(), y.float())
+    assert K.counters.get("chain4.smgrad", 0) == c0 + 1
+    u64 = x64 @ v
+    lt = torch.cat([u64, torch.zeros((n, 1), device="cuda", dtype=torch.float64)], 1)
+    p = torch.softmax(lt, 1)[:, :k]
+    G64 = x64.t() @ (p - y)
+    torch.testing.assert_close(U.double(), u64, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(G.double(), G64, rtol=2e-4, atol=2e-3 * G64.abs().max().item())

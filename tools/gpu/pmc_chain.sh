@@ -1,0 +1,13 @@
+#!/bin/bash
+# PMC counter passes over the fused chain kernels (tools/bench_chain.py); one pass per run
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+mkdir -p $R/gpurun_out/pmc
+P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD"
+P2="FETCH_SIZE GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_INST_LEVEL_VMEM SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"
+i=0
+for P in "$P1" "$P2"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $P -d $R/gpurun_out/pmc/p$i -o p --output-format csv -- python3 $R/tools/bench_chain.py --reps 2 "$@" > $R/gpurun_out/pmc/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+done
+python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc > $R/gpurun_out/pmc/summary.txt
