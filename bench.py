@@ -102,6 +102,11 @@ def main():
     ap.add_argument("--stats", action="store_true")
     ap.add_argument("--gpu-min-cells", type=int, default=None,
                     help="host-placement threshold for small matrices (default: config default)")
+    ap.add_argument("--lazy", action="store_true",
+                    help="HBM-resident lazy scalars (all matrices in HBM) instead of host scalars + hybrid "
+                         "placement (measured slower on this benchmark: 511 vs 486 ms)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="compile MultiLogReg after LinregCG ran instead of overlapping the two")
     a = ap.parse_args()
 
     from systemml_amd.parallel import dist as D
@@ -119,7 +124,7 @@ def main():
     if ctx is None:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
 
-    cfg = DMLConfig(precision="single", dist_min_rows=100_000)
+    cfg = DMLConfig(precision="single", dist_min_rows=100_000, lazy_scalars=a.lazy)
     if a.gpu_min_cells is not None:
         cfg.gpu_min_cells = a.gpu_min_cells
     from systemml_amd.ops.backend import backend
@@ -143,10 +148,20 @@ def main():
     log = []
     out = (lambda s: log.append(s)) if not a.verbose else (lambda s: print(s, file=sys.stderr))
 
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(1)
+
+    def compile_mlr():
+        return EX.compile_script(src_mlr, args_mlr, inputs={"X": X2, "Y_vec": lab}, outputs=["B_out"], config=cfg)
+
     def step(stats=None):
+        # both scripts are parsed + compiled inside every step; MultiLogReg's compilation runs on
+        # a host thread while LinregCG executes (the GPU-bound execution releases the GIL at
+        # each device wait), as a pipelined driver would
         cs1 = EX.compile_script(src_lr, args_lr, inputs={"X": X1, "y": y1}, outputs=["B_out"], config=cfg)
+        fut = None if a.no_overlap else pool.submit(compile_mlr)
         r1, _ = EX.execute(cs1, {"X": X1, "y": y1}, out=out, dist=ctx, stats=stats)
-        cs2 = EX.compile_script(src_mlr, args_mlr, inputs={"X": X2, "Y_vec": lab}, outputs=["B_out"], config=cfg)
+        cs2 = compile_mlr() if fut is None else fut.result()
         r2, _ = EX.execute(cs2, {"X": X2, "Y_vec": lab}, out=out, dist=ctx, stats=stats)
         return r1["B_out"], r2["B_out"]
 

@@ -155,12 +155,13 @@ def execute(cs: CompiledScript, inputs=None, out=None, stats=None, dist=None):
                     if isinstance(v_, int) and v_:
                         stats.counters["bufferpool." + k_] = v_
     from ..runtime.bufferpool import Evicted
+    from ..runtime import scalars as S_
     res = {}
     for k in cs.outputs:
         v = ctx.vars.get(k)
         if isinstance(v, Evicted):
             v = ctx.pool.restore(ctx.vars, k, v)
-        res[k] = v
+        res[k] = S_.materialize(v)
     return res, ctx
 
 

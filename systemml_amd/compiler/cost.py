@@ -296,7 +296,7 @@ def _chain_block(bb, env, stats):
 # program-level pass
 # ----------------------------------------------------------------------------
 def _shape_of(v):
-    if isinstance(v, (bool, int, float, str)):
+    if isinstance(v, (bool, int, float, str)) or getattr(v, "is_dev_scalar", False):
         return SCALAR
     sh = getattr(v, "shape", None)
     if sh is not None and len(sh) == 2:

@@ -22,6 +22,8 @@ class DMLConfig:
     bf16_storage_min_cells: int = 0     # >0: large read-only inputs stored bf16 (fp32 accumulate)
     dist_min_rows: int = 100_000        # row-partition matrices with >= rows across ranks (SPMD)
     gpu_min_cells: int = 16384          # GPU backend: smaller matrices (and their operators) stay on host
+    lazy_scalars: bool = False          # GPU backend: aggregates return HBM-resident scalars (runtime/scalars.DevScalar);
+                                        # implies every matrix lives in HBM (gpu_min_cells ignored)
     parallelism: int = 8                # parfor local workers
     # compiler
     rewrites: bool = True
@@ -50,6 +52,7 @@ class DMLConfig:
         "sysml.gpu.storage.bf16.mincells": ("bf16_storage_min_cells", int),
         "sysml.dist.minrows": ("dist_min_rows", int),
         "sysml.gpu.mincells": ("gpu_min_cells", int),
+        "sysml.gpu.lazy.scalars": ("lazy_scalars", lambda v: str(v).lower() == "true"),
         "sysml.parallel.ops": ("parallelism", lambda v: 8 if str(v).lower() == "true" else 1),
         "sysml.localtmpdir": ("scratch", str),
         "sysml.scratch": ("scratch", str),

@@ -19,6 +19,7 @@ class Backend:
         self.bf16_min_cells = 0
         self.stream_sync = False
         self.small_cells = 0        # GPU backend: matrices below this many cells live on the host
+        self.lazy = False           # GPU backend: HBM-resident scalars (runtime/scalars.DevScalar)
 
     @property
     def on_gpu(self):
@@ -36,6 +37,9 @@ class Backend:
             self.dtype = torch.float32 if prec in ("single", "float", "fp32", "bf16") else torch.float64
             self.bf16_min_cells = 0 if config is None else config.bf16_storage_min_cells
             self.small_cells = 16384 if config is None else int(config.gpu_min_cells)
+            self.lazy = bool(config is not None and getattr(config, "lazy_scalars", False))
+            if self.lazy:
+                self.small_cells = 0
             want_k = True if config is None else config.hip_kernels
             if want_k:
                 from . import kernels
@@ -49,6 +53,7 @@ class Backend:
             self.use_kernels = False
             self.bf16_min_cells = 0
             self.small_cells = 0
+            self.lazy = False
         return self
 
 

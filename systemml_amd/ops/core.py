@@ -16,6 +16,7 @@ import torch
 
 from ..parser.errors import DMLRuntimeError
 from ..runtime import scalars as S
+from ..runtime.scalars import DevScalar
 from .backend import backend
 from . import sparse as SP
 from . import compress as CMP
@@ -185,11 +186,106 @@ _PYNUM = (int, float, bool)
 _STRIDED = torch.strided
 
 
+# ----------------------------------------------------------------------------
+# HBM-resident scalars (runtime/scalars.DevScalar): scalar algebra queued on the device
+# ----------------------------------------------------------------------------
+_DEV_ARITH = {"+", "-", "*", "/", "^", "min", "max"}
+_DEV_CMP = {"==": torch.eq, "!=": torch.ne, "<": torch.lt, "<=": torch.le, ">": torch.gt, ">=": torch.ge}
+
+
+def _lazy_out(r):
+    """A 0-d (or 1x1) device aggregate -> DevScalar on a lazy backend, else a Python float."""
+    if backend.lazy and isinstance(r, Tensor) and r.is_cuda:
+        return DevScalar(r.reshape(()).to(torch.float64))
+    return float(r.item()) if isinstance(r, Tensor) else float(r)
+
+
+def _dev_bool(x):
+    """(x != 0) as a 0-d bool tensor (x DevScalar) or a Python bool."""
+    if type(x) is DevScalar:
+        return x.t != 0
+    return S.as_bool(x)
+
+
+def _dev_binary(op, a, b):
+    da, db = type(a) is DevScalar, type(b) is DevScalar
+    other = b if da else a
+    if isinstance(other, Tensor) and not (da and db):
+        if other.is_cuda and other.layout is _STRIDED and op in BIN and op not in ("log",) \
+                and not op.startswith("bitw"):
+            m = cvt(other)
+            s = (a if da else b).t.to(m.dtype)
+            return BIN[op](s, m) if da else BIN[op](m, s)
+        return binary(op, S.materialize(a), S.materialize(b))
+    if isinstance(other, (str,)) or not (da and db or isinstance(other, (int, float, bool))):
+        return binary(op, S.materialize(a), S.materialize(b))
+    x = a.t if da else float(S._num(a))
+    y = b.t if db else float(S._num(b))
+    if op in _DEV_ARITH:
+        if op == "+":
+            r = x + y
+        elif op == "-":
+            r = x - y
+        elif op == "*":
+            r = x * y
+        elif op == "/":
+            r = x / y
+        elif op == "^":
+            r = torch.pow(x, y)
+        else:
+            xt = x if da else torch.full_like(y, x)
+            yt = y if db else torch.full_like(x, y)
+            r = torch.minimum(xt, yt) if op == "min" else torch.maximum(xt, yt)
+        return DevScalar(r)
+    if op in _DEV_CMP:
+        r = _DEV_CMP[op](x, y) if da else _DEV_CMP[op](torch.full_like(y, x), y)
+        return DevScalar(r.to(torch.float64), "b")
+    if op in ("&", "|", "xor"):
+        p, q = _dev_bool(a), _dev_bool(b)
+        if not isinstance(p, Tensor):
+            p, q = q, p                      # p is the device side
+        if not isinstance(q, Tensor):        # fold the host boolean
+            if op == "&":
+                return DevScalar(p.to(torch.float64), "b") if q else False
+            if op == "|":
+                return True if q else DevScalar(p.to(torch.float64), "b")
+            return DevScalar((~p if q else p).to(torch.float64), "b")
+        r = torch.logical_and(p, q) if op == "&" else torch.logical_or(p, q) if op == "|" else torch.logical_xor(p, q)
+        return DevScalar(r.to(torch.float64), "b")
+    return S.binary(op, S.materialize(a), S.materialize(b))
+
+
+_DEV_UN = {"neg": torch.neg, "abs": torch.abs, "exp": torch.exp, "log": torch.log, "sqrt": torch.sqrt,
+           "floor": torch.floor, "ceil": torch.ceil, "sign": torch.sign, "sin": torch.sin, "cos": torch.cos,
+           "tan": torch.tan, "asin": torch.asin, "acos": torch.acos, "atan": torch.atan, "sinh": torch.sinh,
+           "cosh": torch.cosh, "tanh": torch.tanh, "sigmoid": torch.sigmoid,
+           "round": lambda t: torch.floor(t + 0.5)}
+
+
+def _dev_unary(op, x):
+    f = _DEV_UN.get(op)
+    if f is not None and x.vt == "d":
+        return DevScalar(f(x.t))
+    if op == "not":
+        return DevScalar((x.t == 0).to(torch.float64), "b")
+    if op in ("ident", "cast_scalar"):
+        return x
+    if op == "cast_double":
+        return DevScalar(x.t) if x.vt == "d" else DevScalar(x.t.clone())
+    if op == "cast_bool":
+        return DevScalar((x.t != 0).to(torch.float64), "b")
+    if op == "cast_matrix":
+        return x.t.reshape(1, 1).to(backend.dtype)
+    return unary(op, x.value())
+
+
 def binary(op, a, b):
     # fast paths: two Python scalars; dense same-device same-dtype tensors (or tensor-scalar)
     ta_, tb_ = type(a), type(b)
     if ta_ in _PYNUM and tb_ in _PYNUM:
         return S.binary(op, a, b)
+    if ta_ is DevScalar or tb_ is DevScalar:
+        return _dev_binary(op, a, b)
     if ta_ is Tensor and a.layout is _STRIDED and a.dtype is not torch.bfloat16:
         fn = BIN.get(op)
         if fn is not None:
@@ -276,6 +372,8 @@ UN = {
 
 
 def unary(op, x):
+    if type(x) is DevScalar:
+        return _dev_unary(op, x)
     if CMP.is_compressed(x):
         if op in ("nrow", "ncol", "length"):
             r, c = x.shape
@@ -288,6 +386,8 @@ def unary(op, x):
         if op == "cast_scalar" or op in ("cast_double", "cast_int", "cast_bool"):
             if x.numel() != 1:
                 raise DMLRuntimeError(f"cannot cast {x.shape[0]}x{x.shape[1]} matrix to scalar")
+            if backend.lazy and x.is_cuda and op in ("cast_scalar", "cast_double"):
+                return DevScalar(cvt(x).reshape(()).to(torch.float64))
             v = float(x.reshape(-1)[0].item())
             return S.unary(op, v) if op != "cast_scalar" else v
         if op == "cast_matrix":
@@ -366,6 +466,8 @@ def agg(o, d, x):
     if not isinstance(x, Tensor):
         if is_dist(x):
             return _dist().agg(o, d, x)
+        if type(x) is DevScalar:
+            x = x.value()
         if isinstance(x, (int, float, bool)):
             v = _num(x)
             if o in ("sum", "mean", "min", "max", "prod", "trace"):
@@ -406,7 +508,7 @@ def agg(o, d, x):
             r = torch.trace(x)
         else:
             raise DMLRuntimeError(f"unknown aggregate {o}")
-        return float(r.item())
+        return _lazy_out(r)
     dim = 1 if d == "row" else 0
     if o == "sum":
         return torch.sum(x, dim=dim, keepdim=True)
@@ -445,7 +547,9 @@ def tak(a, b):
     a, b = cvt(a), cvt(b)
     if b.dtype != a.dtype:
         b = b.to(a.dtype)
-    return float(torch.dot(a.reshape(-1), b.reshape(-1)).item())
+    if a.device != b.device:
+        b = b.to(a.device)
+    return _lazy_out(torch.dot(a.reshape(-1), b.reshape(-1)))
 
 
 # ----------------------------------------------------------------------------

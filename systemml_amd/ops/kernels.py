@@ -292,6 +292,19 @@ def _c4_grid(L, mode, X, kp):
     return _c4occ[key]
 
 
+def _rows_f32(S, kp, sbc, device):
+    """Row-side operand for chain4 as (fp32 tensor, leading dimension) without a copy when it is
+    already an fp32 row-major view (e.g. P[, 1:K] of a wider P): the kernel reads S[r*lds + k]."""
+    if S.device != device:
+        S = S.to(device)
+    if S.dtype != torch.float32:
+        S = S.float()
+    if S.stride(1) == 1 and S.stride(0) >= S.shape[1] and S.data_ptr() % 4 == 0:
+        return S, S.stride(0)
+    S = S.contiguous()
+    return S, S.shape[1]
+
+
 def _chain4(mode, X, kp, V, S, lds, sbc, U=None, ldu=0):
     """Launch chain4; returns the D x kp fp32 result (sum of the per-block partials)."""
     L = load(required=True)
@@ -331,8 +344,11 @@ def mmchain(ctype, X, V, W=None):
             return None
     if _c4_ok(X, mode, kp):
         Vf = _pad_cols(V, kp, torch.float32, X.device).contiguous()
-        Sf = S.to(torch.float32).contiguous() if S is not None else None
-        R = _chain4(mode, X, kp, Vf, Sf, Sf.shape[1] if Sf is not None else 0, sbc)
+        # W as is (strided views included) when the kernel reads no column past it: sbc broadcast
+        # or W already kp wide; otherwise the zero-padded copy S
+        src = W if (W is not None and (sbc or W.shape[1] == kp)) else S
+        Sf, lds = _rows_f32(src, kp, sbc, X.device) if src is not None else (None, 0)
+        R = _chain4(mode, X, kp, Vf, Sf, lds, sbc)
         if R is not None:
             _count("chain4.mmchain." + ctype)
             return _result(R if kp == K else R[:, :K].contiguous())
@@ -364,9 +380,9 @@ def smgrad(X, V, Y):
     N, D = X.shape
     if _c4_ok(X, XTSMG, kp):
         Vf = _pad_cols(V, kp, torch.float32, X.device).contiguous()
-        Yc = Y.to(device=X.device, dtype=torch.float32).contiguous()
+        Yc, ldy = _rows_f32(Y, K, 1, X.device)
         Upad = torch.empty((N + 1, K), dtype=torch.float32, device=X.device)   # row N: kernel's pad row
-        G = _chain4(XTSMG, X, kp, Vf, Yc, K, K, U=Upad, ldu=K)
+        G = _chain4(XTSMG, X, kp, Vf, Yc, ldy, K, U=Upad, ldu=K)
         if G is not None:
             _count("chain4.smgrad")
             return _result(Upad[:N]), _result(G if kp == K else G[:, :K].contiguous())
@@ -447,7 +463,8 @@ def sumsq(x, d):
                 _count("rowstream.colsumsq")
                 c = part[:g].sum(0).reshape(1, -1)
                 if d == "all":
-                    return float(c.sum().item())
+                    from .core import _lazy_out
+                    return _lazy_out(c.sum())
                 return _result(c)
     # generic: chunked to bound temporaries
     from .core import cvt

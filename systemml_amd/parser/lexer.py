@@ -9,6 +9,7 @@ ids, `ns::name` namespaced ids, and the R-style operators `%*%`, `%/%`,
 """
 from __future__ import annotations
 
+import re
 from dataclasses import dataclass
 
 from .errors import ParseError
@@ -47,7 +48,99 @@ def _is_id_char(c):
     return c.isalnum() or c == "_" or c == "."
 
 
+_NUM = r"(?:\d+\.(?!\.)\d*|\.\d+|\d+)(?:[eE][+-]?\d+)?"
+_DML_RE = re.compile(
+    r"(?P<ws>[ \t\r]+)|(?P<nl>\n)|(?P<com>#[^\n]*)|(?P<bcom>/\*)|"
+    r"(?P<num>" + _NUM + r")(?P<lsuf>[lL])?|"
+    r"(?P<id>[^\W\d][\w.]*(?:::[^\W\d][\w.]*)?)|"
+    r"(?P<cmd>\$\w*)|(?P<str>[\"'])|"
+    r"(?P<op>" + "|".join(re.escape(o) for o in _DML_OPS) + r")")
+
+
+def _tokenize_dml(src: str, filename: str):
+    """DML tokens via one compiled master regex (same rules as the character loop below,
+    which is kept for PyDML's indentation handling); ~10x faster on the algorithm scripts."""
+    toks = []
+    append = toks.append
+    i, n = 0, len(src)
+    line, col0 = 1, 0
+    match = _DML_RE.match
+
+    def err(msg):
+        raise ParseError(f"{filename or '<script>'} line {line}: {msg}")
+
+    while i < n:
+        m = match(src, i)
+        if m is None:
+            err(f"unexpected character {src[i]!r}")
+        kind = m.lastgroup
+        if kind == "lsuf":
+            kind = "num"
+        j = m.end()
+        if kind == "ws" or kind == "com":
+            i = j
+            continue
+        if kind == "nl":
+            line += 1
+            i = j
+            col0 = i
+            continue
+        col = i - col0
+        if kind == "id":
+            word = m.group("id")
+            if "::" not in word:
+                while word.endswith("."):
+                    word = word[:-1]
+                    j -= 1
+            append(Token("ID", word, line, col))
+        elif kind == "num":
+            text = m.group("num")
+            if "." in text or "e" in text or "E" in text:
+                append(Token("DOUBLE", float(text), line, col))
+            else:
+                append(Token("INT", int(text), line, col))
+        elif kind == "op":
+            append(Token("OP", m.group("op"), line, col))
+        elif kind == "cmd":
+            if j == i + 1:
+                err("invalid command-line parameter")
+            append(Token("CMD", src[i + 1:j], line, col))
+        elif kind == "bcom":
+            k = src.find("*/", i + 2)
+            if k < 0:
+                err("unterminated block comment")
+            nl = src.count("\n", i, k + 2)
+            if nl:
+                line += nl
+                col0 = src.rfind("\n", i, k + 2) + 1
+            j = k + 2
+        else:   # string literal
+            c = src[i]
+            j = i + 1
+            buf = []
+            while j < n and src[j] != c:
+                if src[j] == "\\" and j + 1 < n:
+                    e = src[j + 1]
+                    buf.append(_ESC.get(e, "\\" + e))
+                    j += 2
+                    continue
+                if src[j] == "\n":
+                    line += 1
+                    col0 = j + 1
+                buf.append(src[j])
+                j += 1
+            if j >= n:
+                err("unterminated string literal")
+            append(Token("STRING", "".join(buf), line, col))
+            j += 1
+        i = j
+    append(Token("EOF", None, line, 0))
+    return toks
+
+
 def tokenize(src: str, pydml: bool = False, filename: str = ""):
+    if not pydml:
+        return _tokenize_dml(src, filename)
     ops = _PYDML_OPS if pydml else _DML_OPS
     toks = []
     i, n = 0, len(src)
@@ -108,8 +201,8 @@ def tokenize(src: str, pydml: bool = False, filename: str = ""):
             col0 = i
             continue
         if c == "#":
-            while i < n and src[i] != "\n":
-                i += 1
+            j = src.find("\n", i)
+            i = n if j < 0 else j
             continue
         if c == "/" and i + 1 < n and src[i + 1] == "*":
             j = src.find("*/", i + 2)

@@ -25,8 +25,23 @@ import time
 import torch
 
 
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """One copy stream per device: evictions / restores overlap the compute stream."""
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
 class Evicted:
-    __slots__ = ("cpu", "path", "device", "dtype", "shape", "nbytes")
+    """Handle of an evicted device tensor.  Host tier: pinned buffer filled by an async D2H copy
+    on the device's side stream (ordered after the producing stream by an event; the device
+    block is released to the caching allocator only after the copy, via record_stream).
+    Disk tier: a synchronous torch.save of our own spill file."""
+    __slots__ = ("cpu", "path", "device", "dtype", "shape", "nbytes", "done")
 
     def __init__(self, t: torch.Tensor, spill_dir=None):
         self.device = t.device
@@ -35,14 +50,23 @@ class Evicted:
         self.nbytes = t.numel() * t.element_size()
         self.path = None
         self.cpu = None
+        self.done = None
         if spill_dir is not None:
             fd, self.path = tempfile.mkstemp(prefix="sysml_spill_", suffix=".pt", dir=spill_dir)
             os.close(fd)
             torch.save(t.detach().cpu(), self.path)
-        else:
-            host = torch.empty(t.shape, dtype=t.dtype, pin_memory=t.is_cuda)
-            host.copy_(t, non_blocking=False)
+        elif t.is_cuda:
+            host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            side = _side_stream(t.device)
+            side.wait_stream(torch.cuda.current_stream(t.device))
+            with torch.cuda.stream(side):
+                host.copy_(t, non_blocking=True)
+                t.record_stream(side)
+                self.done = torch.cuda.Event()
+                self.done.record(side)
             self.cpu = host
+        else:
+            self.cpu = t.clone()
 
     def restore(self) -> torch.Tensor:
         if self.path is not None:
@@ -51,9 +75,21 @@ class Evicted:
                 os.remove(self.path)
             except OSError:
                 pass
-        else:
-            t = self.cpu
-        return t.to(self.device, non_blocking=True)
+            return t.to(self.device, non_blocking=True)
+        if self.device.type != "cuda":
+            return self.cpu
+        cur = torch.cuda.current_stream(self.device)
+        side = _side_stream(self.device)
+        with torch.cuda.stream(side):
+            if self.done is not None:
+                side.wait_event(self.done)
+            d = torch.empty(self.shape, dtype=self.dtype, device=self.device)
+            d.copy_(self.cpu, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        cur.wait_event(ev)
+        d.record_stream(cur)
+        return d
 
     def __repr__(self):
         where = "disk" if self.path else "host"
@@ -74,6 +110,8 @@ class BufferPool:
         self.min_bytes = 1 << 20          # smaller variables are never worth evicting
         self.host_tensors = False         # tests: treat host tensors as the "device" tier
         self._total = None
+        self._next_check = 0.0
+        self.check_interval = 0.005       # s between proactive HBM-usage checks (the query is not free)
 
     # ------------------------------------------------------------------ access
     def touch(self, frame, name):
@@ -130,7 +168,14 @@ class BufferPool:
         return freed
 
     def maybe_evict(self, frames, keep=()):
-        if not self.enabled or not torch.cuda.is_available():
+        if not self.enabled:
+            return 0
+        now = time.perf_counter()
+        if now < self._next_check and self.frac > 0:
+            return 0
+        self._next_check = now + self.check_interval
+        if not torch.cuda.is_available():
+            self._next_check = float("inf")
             return 0
         dev = torch.cuda.current_device()
         if self._total is None:

@@ -14,10 +14,14 @@ from ..parser.errors import DMLRuntimeError
 from ..ops import core as C
 from ..ops import sparse as SP
 from . import builtins as B
+from .scalars import DevScalar
 
 
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
+# operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
+# receive materialised Python values (one device sync)
+_LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "t", "tak"}
 # operators that compute on matrix operands (placement applies); the rest move values around
 _COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "wquat", "tak", "t", "rix", "lix", "bi"}
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
@@ -31,15 +35,28 @@ def make_impl(h):
     fn, code = _make_impl(h)
     if h.op in _COMPUTE_OPS and not (h.op == "bi" and h.p.get("name") in _NO_PLACE_BI):
         fn = _placed(fn)
-    if h.op in _SPARSE_OK_OPS or (h.op == "u" and h.p.get("o") in _SPARSE_OK_UNARY):
+    sparse_ok = h.op in _SPARSE_OK_OPS or (h.op == "u" and h.p.get("o") in _SPARSE_OK_UNARY)
+    lazy_ok = h.op in _LAZY_OK_OPS
+    if sparse_ok and lazy_ok:
         return fn, code
     is_sp = SP.is_special
     dense = SP.densify
+    DS = DevScalar
+
+    if sparse_ok:
+        def mat(ctx, a):
+            # operators that need Python scalars: device-resident scalars are materialised here
+            for x in a:
+                if type(x) is DS:
+                    return fn(ctx, [y.value() if type(y) is DS else y for y in a])
+            return fn(ctx, a)
+        return mat, code
 
     def wrapped(ctx, a):
         for x in a:
-            if is_sp(x):
-                return fn(ctx, [dense(y) for y in a])
+            if is_sp(x) or type(x) is DS:
+                a = [dense(y) if is_sp(y) else (y.value() if type(y) is DS and not lazy_ok else y) for y in a]
+                break
         return fn(ctx, a)
     return wrapped, code
 

@@ -50,6 +50,8 @@ class ExecutionContext:
 
 # ----------------------------------------------------------------------------
 def _to_bool(v):
+    if type(v) is S.DevScalar:
+        return bool(v.value())
     if isinstance(v, torch.Tensor):
         if v.numel() != 1:
             raise DMLRuntimeError("predicate must evaluate to a scalar")
@@ -58,6 +60,8 @@ def _to_bool(v):
 
 
 def _to_num(v):
+    if type(v) is S.DevScalar:
+        return v.value()
     if isinstance(v, torch.Tensor):
         if v.numel() != 1:
             raise DMLRuntimeError("loop bound must be a scalar")

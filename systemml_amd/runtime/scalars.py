@@ -16,6 +16,59 @@ from ..parser.errors import DMLRuntimeError
 INF = float("inf")
 
 
+class DevScalar:
+    """A DML double/boolean scalar that stays resident in HBM as a 0-d fp64 tensor.
+
+    Aggregates over HBM matrices (sum, tak+*, as.scalar, ...) return one instead of a Python
+    float when the backend runs with lazy scalars, so an iterative script's scalar algebra
+    (alphas, norms, convergence tests) is queued on the device behind the kernels that
+    produce it; the host only synchronises where it must branch (a loop or if predicate), or
+    where a value leaves the engine (print, casts, indexing, results).  Reference analogue:
+    the CP ScalarObject (runtime/instructions/cp/DoubleObject.java), which is always on the
+    JVM heap — on the GPU backend that costs a device round trip per scalar.
+    """
+    __slots__ = ("t", "vt", "_v")
+    is_dev_scalar = True
+
+    def __init__(self, t, vt="d"):
+        self.t = t          # 0-d float64 tensor on the device
+        self.vt = vt        # 'd' (DOUBLE) | 'b' (BOOLEAN)
+        self._v = None
+
+    def value(self):
+        """Materialise (one device sync, cached)."""
+        if self._v is None:
+            x = float(self.t.item())
+            self._v = (x != 0.0) if self.vt == "b" else x
+        return self._v
+
+    def __float__(self):
+        return float(self.value())
+
+    def __int__(self):
+        return int(self.value())
+
+    def __bool__(self):
+        return bool(self.value())
+
+    def __index__(self):
+        return int(self.value())
+
+    def __str__(self):
+        return to_str(self.value())
+
+    def __format__(self, spec):
+        return format(self.value(), spec)
+
+    def __repr__(self):
+        return f"DevScalar({self.t!r}, {self.vt})"
+
+
+def materialize(v):
+    """Python value of a possibly device-resident scalar."""
+    return v.value() if type(v) is DevScalar else v
+
+
 def java_double_str(d: float) -> str:
     """Emulates java.lang.Double.toString."""
     if d != d:
@@ -45,6 +98,8 @@ def java_double_str(d: float) -> str:
 
 
 def to_str(v) -> str:
+    if type(v) is DevScalar:
+        v = v.value()
     if isinstance(v, bool):
         return "TRUE" if v else "FALSE"
     if isinstance(v, int):
@@ -57,6 +112,8 @@ def to_str(v) -> str:
 
 
 def vtype_of(v):
+    if type(v) is DevScalar:
+        return "BOOLEAN" if v.vt == "b" else "DOUBLE"
     if isinstance(v, bool):
         return "BOOLEAN"
     if isinstance(v, int):
