@@ -29,6 +29,9 @@ UNK = (-1, -1)
 SCALAR = (0, 0)
 
 
+_ABSENT = object()
+
+
 def _lv(h):
     return h.value if h.op == "lit" else None
 
@@ -89,15 +92,17 @@ def infer(h, dims, env):
         return ins[0]
     if op == "rix":
         r, c = ins[0]
-        rl, ru, cl, cu = (_lv(x) for x in h.inputs[1:5])
+        # a bound is absent (literal None: whole range), a literal, or an expression (unknown)
+        rl, ru, cl, cu = ((_ABSENT if (x.op == "lit" and x.value is None) else _lv(x)) for x in h.inputs[1:5])
 
         def span(lo, hi, n):
-            if lo is None and hi is None:
+            if lo is _ABSENT and hi is _ABSENT:
                 return n
-            lo_, hi_ = _int_or(lo, 1 if lo is None else -1), _int_or(hi, n if hi is None else -1)
+            lo_ = 1 if lo is _ABSENT else _int_or(lo)
+            hi_ = n if hi is _ABSENT else _int_or(hi)
             return hi_ - lo_ + 1 if lo_ >= 0 and hi_ >= 0 else -1
         lists = h.p.get("list", False)
-        return (span(rl, ru, r), c if lists and cl is None else span(cl, cu, c))
+        return (span(rl, ru, r), c if lists and cl is _ABSENT else span(cl, cu, c))
     if op == "bi":
         return _infer_bi(h, ins)
     return UNK
@@ -367,6 +372,51 @@ def reorder_chains(cp, inputs=None):
     return stats
 
 
+def _check_dims(roots, dims):
+    """Known-dimension validation of unconditional code (reference BinaryExpression /
+    AggBinaryOp validate): %*% inner dimensions, cellwise operand shapes."""
+    from ..parser.errors import LanguageError
+    exact = {}
+    ok_bi = ("matrix", "rand", "seq", "cbind", "rbind", "append", "diag")
+    for h in H.walk(roots):
+        # dims that are certain within this block: literal-sized constructors and exact
+        # shape-preserving / shape-computing operators over them (reads of variables from other
+        # blocks are not trusted: their shape may depend on control flow)
+        ins = [exact.get(c.id, UNK) for c in h.inputs]
+        if h.op == "lit" or h.dt == "S":
+            d = SCALAR
+        elif h.op in ("b", "u", "t", "mm", "agg", "rix") or (h.op == "bi" and h.p.get("name") in ok_bi):
+            if h.op == "u" and h.p.get("o", "").startswith("cast"):
+                d = UNK
+            elif h.op != "bi" and any(x == UNK for x in ins[:2]):
+                d = UNK
+            else:
+                d = infer(h, exact, {})
+        else:
+            d = UNK
+        exact[h.id] = d
+    for h in H.walk(roots):
+        if h.op not in ("mm", "b") or len(h.inputs) != 2:
+            continue
+        a, b = (exact.get(c.id, UNK) for c in h.inputs)
+        if not (_known(a) and _known(b)) or a == SCALAR or b == SCALAR:
+            continue
+        if h.op == "mm":
+            inner = a[0] if h.p.get("transA") else a[1]
+            if inner != b[0]:
+                ra, ca = (a[1], a[0]) if h.p.get("transA") else a
+                raise LanguageError(f"{h.pos}: matrix multiplication dimension mismatch: "
+                                    f"{ra}x{ca} %*% {b[0]}x{b[1]} (inner dimensions must match)")
+        else:
+            (ra, ca), (rb, cb) = a, b
+            ok = (a == b or (ra == rb and (ca == 1 or cb == 1)) or (ca == cb and (ra == 1 or rb == 1))
+                  or (ra == 1 and ca == 1) or (rb == 1 and cb == 1) or (ca == 1 and rb == 1)
+                  or (ra == 1 and cb == 1))
+            if not ok:
+                raise LanguageError(f"{h.pos}: mismatch in dimensions for cellwise operator "
+                                    f"'{h.p.get('o')}': {ra}x{ca} vs {rb}x{cb}")
+
+
 def annotate(cp, inputs=None, config=None):
     """After instruction generation: dims, memory estimates and exec types of the final
     (rewritten) HOP DAGs, for -explain and the cost statistics."""
@@ -375,6 +425,8 @@ def annotate(cp, inputs=None, config=None):
 
     def visit(bb, env):
         dims = annotate_dag(list(bb.roots) + list(bb.env_out.values()), env, config)
+        if not getattr(bb, "cond", True):
+            _check_dims(list(bb.roots) + list(bb.env_out.values()), dims)
         for h in H.walk(list(bb.roots) + list(bb.env_out.values())):
             if h.exec_type and h.op not in ("lit", "tread"):
                 counts[h.exec_type] = counts.get(h.exec_type, 0) + 1

@@ -71,9 +71,23 @@ class Translator:
         self.args = dict(args or {})
         self.config = config
         self.base_dir = base_dir or os.getcwd()
+        # validation (reference StatementBlock.validate / Expression.raiseValidateError): reads
+        # of never-defined variables and known-dimension mismatches are errors in unconditional
+        # code, warnings inside if / loop bodies
+        self.cond_depth = 0
+        self.warnings = []
+        self.inputs = set()
         self.functions = {}       # (nskey, name) -> FunctionBlock
         self.func_defs = {}       # (nskey, name) -> (FunctionDef, FileCtx)
         self.loaded_files = {}    # abs path -> FileCtx
+
+    def validate_error(self, msg):
+        """reference Statement.raiseValidateError: error if unconditional, else a warning."""
+        if self.cond_depth > 0:
+            if msg not in self.warnings:
+                self.warnings.append(msg)
+            return
+        raise LanguageError(msg)
 
     # ------------------------------------------------------------------ imports
     def _register_file(self, prog: A.Program, key, path):
@@ -179,8 +193,12 @@ class Translator:
                     pred = Predicate(pb.expr(st.pred), pb.reads)
                     c1, c2 = dict(consts), dict(consts)
                     t1, t2 = dict(types), dict(types)
-                    tb = self.build_stmts(st.then_body, ctx, c1, types=t1)
-                    eb = self.build_stmts(st.else_body, ctx, c2, types=t2)
+                    self.cond_depth += 1
+                    try:
+                        tb = self.build_stmts(st.then_body, ctx, c1, types=t1)
+                        eb = self.build_stmts(st.else_body, ctx, c2, types=t2)
+                    finally:
+                        self.cond_depth -= 1
                     blocks.append(IfBlock(pred, tb, eb, pos=st.pos))
                     merged = {k: v for k, v in c1.items() if k in c2 and _same(c2[k], v)}
                     consts.clear()
@@ -196,7 +214,11 @@ class Translator:
                     self._loop_types(st.body, ctx, consts, types)
                     pb = _BBuilder(self, ctx, consts, types)
                     pred = Predicate(pb.expr(st.pred), pb.reads)
-                    body = self.build_stmts(st.body, ctx, dict(consts), types=dict(types))
+                    self.cond_depth += 1
+                    try:
+                        body = self.build_stmts(st.body, ctx, dict(consts), types=dict(types))
+                    finally:
+                        self.cond_depth -= 1
                     blocks.append(WhileBlock(pred, body, pos=st.pos))
                     cur = _BBuilder(self, ctx, consts, types)
                 elif isinstance(st, A.For):
@@ -221,7 +243,11 @@ class Translator:
                         consts.pop(v, None)
                     types[st.var] = "S"
                     self._loop_types(st.body, ctx, consts, types)
-                    body = self.build_stmts(st.body, ctx, dict(consts), types=dict(types))
+                    self.cond_depth += 1
+                    try:
+                        body = self.build_stmts(st.body, ctx, dict(consts), types=dict(types))
+                    finally:
+                        self.cond_depth -= 1
                     fb = ForBlock(st.var, p_from, p_to, p_incr, body, parfor=st.parfor, params=params, pos=st.pos)
                     blocks.append(fb)
                     cur = _BBuilder(self, ctx, consts, types)
@@ -236,7 +262,11 @@ class Translator:
         """Fixpoint of data types over a loop body (types assigned in the body that differ
         from the entry types become unknown)."""
         t = dict(types)
-        self.build_stmts(body, ctx, dict(consts), types=t)
+        self.cond_depth += 1
+        try:
+            self.build_stmts(body, ctx, dict(consts), types=t)
+        finally:
+            self.cond_depth -= 1
         for k, v in t.items():
             if k in types and types[k] != v:
                 types[k] = "U"
@@ -425,6 +455,7 @@ class _BBuilder:
     def finish(self) -> BasicBlock:
         bb = BasicBlock()
         bb.pos = self.pos
+        bb.cond = self.tr.cond_depth > 0
         bb.roots = list(self.roots)
         bb.env_out = dict(self.env)
         bb.reads = set(self.reads)
@@ -439,6 +470,9 @@ class _BBuilder:
             return self.lit(self.consts[name], pos)
         h = self.treads.get(name)
         if h is None:
+            if name not in self.types and name not in self.tr.inputs:
+                self.tr.validate_error(f"{pos}: Undefined Variable ({name}) used in statement" if pos else
+                                       f"Undefined Variable ({name}) used in statement")
             h = Hop("tread", p={"name": name}, pos=pos, dt=self.types.get(name, "U"))
             self.treads[name] = h
         self.reads.add(name)
@@ -541,10 +575,21 @@ class _BBuilder:
                 raise LanguageError(f"{call.pos}: unknown parameter '{k}' for function {call.name}")
             bound[k] = v
         inputs, given = [], []
-        for n in names:
+        for prm in fb.inputs:
+            n = prm.name
             if n in bound:
+                # data-type check of the argument against the declared parameter (reference
+                # FunctionCallIdentifier.validateExpression)
+                want = prm.dtype[0] if prm.dtype in ("MATRIX", "SCALAR", "FRAME", "LIST") else None
+                got = bound[n].dt
+                if want in ("M", "S") and got in ("M", "S") and want != got:
+                    raise LanguageError(f"{call.pos}: data type mismatch for parameter '{n}' of function "
+                                        f"{call.name}: expected {prm.dtype.lower()}, got "
+                                        f"{'matrix' if got == 'M' else 'scalar'}")
                 inputs.append(bound[n])
                 given.append(n)
+            elif prm.default is None:
+                raise LanguageError(f"{call.pos}: missing argument '{n}' in call to function {call.name}")
         return self.mk("fcall", inputs, p={"fkey": (fb.namespace, fb.name), "given": tuple(given)},
                        pos=call.pos, cse=False)
 
@@ -729,7 +774,9 @@ def _live_block(b, live_after):
         for _ in range(10):
             lin = _live_list(b.body, end)
             new_end = set(live_after) | preds | lin
-            if isinstance(b, ForBlock):
+            if isinstance(b, ForBlock) and b.var not in live_after:
+                # the iteration variable keeps its last value after the loop
+                # (reference ForProgramBlock.java:126), so it stays live when read later
                 new_end.discard(b.var)
             if new_end == end:
                 break

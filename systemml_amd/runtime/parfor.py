@@ -24,6 +24,14 @@ import torch
 from ..parser.errors import DMLRuntimeError
 
 
+def parfor_iterations(start, end, incr, as_int):
+    """Iteration values of a parfor: ceil((to - from + 1) / incr) of them starting at `from`
+    (reference ParForProgramBlock.computeNumIterations, ParForProgramBlock.java:1756) -- so a
+    parfor over 1:0 runs zero times, where a plain for loop counts down."""
+    n = int(math.ceil((float(end) - float(start) + 1.0) / float(incr)))
+    return [int(start + k * incr) if as_int else float(start + k * incr) for k in range(max(0, n))]
+
+
 def _iterations(start, end, incr, as_int):
     out = []
     i = start
@@ -88,7 +96,7 @@ def _eq(a, b):
 
 def exec_parfor(ctx, b, start, end, incr, as_int):
     from .program import exec_blocks, ExecutionContext
-    iters = _iterations(start, end, incr, as_int)
+    iters = parfor_iterations(start, end, incr, as_int)
     if not iters:
         return
     par = b.params.get("par")

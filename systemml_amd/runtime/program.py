@@ -179,9 +179,14 @@ def exec_block(ctx, b):
             raise DMLRuntimeError("for loop increment must not be zero")
         as_int = all(isinstance(x, int) or (isinstance(x, float) and x.is_integer()) for x in (start, end, incr)) \
             and not any(isinstance(x, float) and not x.is_integer() for x in (start, incr))
-        if b.parfor and ctx.config.parallelism > 1:
-            from .parfor import exec_parfor
-            exec_parfor(ctx, b, start, end, incr, as_int)
+        if b.parfor:
+            from .parfor import exec_parfor, parfor_iterations
+            if ctx.config.parallelism > 1:
+                exec_parfor(ctx, b, start, end, incr, as_int)
+                return
+            for it in parfor_iterations(start, end, incr, as_int):
+                ctx.vars[b.var] = it
+                exec_blocks(ctx, b.body)
             return
         i = start
         cnt = 0

@@ -544,9 +544,10 @@ def test_cox_regression_and_predict():
     np.testing.assert_allclose(M[:, 2], np.sqrt(np.diag(np.linalg.inv(I))), rtol=1e-8)
     l0, g0, I0 = _cox_ref(t, e, Zk, np.zeros(5))
     np.testing.assert_allclose(St.ravel()[:4], [n, e.sum(), l, -2 * l + 10], rtol=1e-10)
-    np.testing.assert_allclose(Tst[:, 0], [2 * (l - l0), M[:, 0] @ I @ M[:, 0],
+    # rows in the reference's order (Cox.dml:423-440): Wald, likelihood ratio, score
+    np.testing.assert_allclose(Tst[:, 0], [M[:, 0] @ I @ M[:, 0], 2 * (l - l0),
                                            g0 @ np.linalg.solve(I0, g0)], rtol=1e-8)
-    np.testing.assert_allclose(Tst[0, 2], chi2.sf(2 * (l - l0), 5), rtol=1e-8)
+    np.testing.assert_allclose(Tst[1, 2], chi2.sf(2 * (l - l0), 5), rtol=1e-8)
 
     # prediction on new records (original column layout)
     Y = X[:7].copy()

@@ -229,9 +229,41 @@ def test_constant_branch_removal_and_merge():
 
 
 def test_undefined_variable_error():
-    from systemml_amd.parser.errors import DMLRuntimeError
-    with pytest.raises(DMLRuntimeError, match="not defined"):
+    # unconditional read of a never-defined variable: compile-time error with its position
+    # (reference StatementBlock.validate -> Statement.raiseValidateError)
+    from systemml_amd.parser.errors import LanguageError
+    with pytest.raises(LanguageError, match=r"line 1:6: Undefined Variable \(undefined_var\)"):
         R("print(undefined_var)")
+
+
+def test_validation_conditional_is_warning_and_runtime_error():
+    from systemml_amd.parser.errors import DMLRuntimeError, LanguageError
+    # inside a branch: only a warning at compile time; executing it fails at run time
+    R("x = sum(rand(rows=1, cols=1, min=3, max=3))\nif (x > 5) { print(y) }")
+    with pytest.raises(DMLRuntimeError, match="not defined"):
+        R("x = sum(rand(rows=1, cols=1, min=7, max=7))\nif (x > 5) { print(y) }")
+    # defined on one path only: fine at compile time (conditionally defined)
+    R("x = sum(rand(rows=1, cols=1, min=7, max=7))\nif (x > 5) { y = 1 }\nprint(y)")
+
+
+def test_validation_known_dimension_mismatch():
+    from systemml_amd.parser.errors import LanguageError
+    with pytest.raises(LanguageError, match="line 3.*dimension"):
+        R("A = matrix(1, rows=3, cols=4)\nB = matrix(1, rows=5, cols=2)\nC = A %*% B\nprint(sum(C))")
+    with pytest.raises(LanguageError, match="line 3.*dimension"):
+        R("A = matrix(1, rows=3, cols=4)\nB = matrix(1, rows=5, cols=4)\nC = A + B\nprint(sum(C))")
+    R("A = matrix(1, rows=3, cols=4)\nv = matrix(1, rows=1, cols=4)\nC = A + v\nprint(sum(C))")
+
+
+def test_validation_function_calls():
+    from systemml_amd.parser.errors import LanguageError
+    f = "f = function(matrix[double] M, double s) return (double r) { r = sum(M) * s }\n"
+    with pytest.raises(LanguageError, match="too many arguments"):
+        R(f + "x = f(matrix(1, rows=2, cols=2), 2, 3)\nprint(x)")
+    with pytest.raises(LanguageError, match="missing argument 's'"):
+        R(f + "x = f(matrix(1, rows=2, cols=2))\nprint(x)")
+    with pytest.raises(LanguageError, match="type"):
+        R(f + "x = f(3, 2)\nprint(x)")
 
 
 def test_stop():

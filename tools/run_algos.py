@@ -42,6 +42,8 @@ def make_data(d, n=200, m=8, seed=3):
     write(f"{d}/y", y)
     write(f"{d}/ybin", ybin)
     write(f"{d}/ycls", ycls)
+    write(f"{d}/ydummy", np.eye(3)[ycls[:, 0] - 1])        # recoded + dummy-coded labels (tree scripts)
+    write(f"{d}/y01", ((X @ beta + 1.5 * rng.standard_normal((n, 1))) > 0) * 1.0)   # noisy: finite MLE
     write(f"{d}/counts", counts)
     write(f"{d}/Xpos", Xpos + 0.1)
     write(f"{d}/Xint", Xint)
@@ -60,8 +62,12 @@ def make_data(d, n=200, m=8, seed=3):
     write(f"{d}/gi", np.array([[3]]))
     write(f"{d}/si", np.array([[3]]))
     write(f"{d}/F", np.array([[4], [5], [6]]))
-    write(f"{d}/Xcs", np.sort(rng.random((30, 1)) * 10, 0))
-    write(f"{d}/ycs", np.sin(np.sort(rng.random((30, 1)) * 10, 0)))
+    # unit-spaced knots: the reference Cspline scripts build the right-hand side with dy * h^2
+    # where the spline equations need dy / h^2 (CsplineCG.dml calcKnotsDerivKs); the two agree
+    # for h = 1, so their outputs are comparable with ours there
+    xk = np.arange(1.0, 31.0).reshape(-1, 1)
+    write(f"{d}/Xcs", xk)
+    write(f"{d}/ycs", np.sin(xk * 0.3))
 
 
 def cases(d):
@@ -94,23 +100,52 @@ def cases(d):
                             types2=f"{d}/K2", OUTDIR=f"{o}/bivar"),
         "ALS-CG": dict(X=f"{d}/R", U=f"{o}/U", V=f"{o}/V", rank=4, reg="L2", lambda_=0.01, maxi=10),
         "ALS-DS": dict(V=f"{d}/R", L=f"{o}/L", R=f"{o}/Rf", rank=4, reg="L2", lambda_=0.01, maxi=10),
-        "decision-tree": dict(X=f"{d}/X", Y=f"{d}/ycls", M=f"{o}/tree", bins=5, depth=4, num_leaf=5),
+        "decision-tree": dict(X=f"{d}/X", Y=f"{d}/ydummy", M=f"{o}/tree", bins=5, depth=4, num_leaf=5),
         "decision-tree-predict": dict(X=f"{d}/X", Y=f"{d}/ycls", M=f"{o}/tree", P=f"{o}/treeP",
                                       A=f"{o}/treeA", CM=f"{o}/treeCM"),
-        "random-forest": dict(X=f"{d}/X", Y=f"{d}/ycls", M=f"{o}/rf", bins=5, depth=4, num_leaf=5, num_trees=3),
+        "random-forest": dict(X=f"{d}/X", Y=f"{d}/ydummy", M=f"{o}/rf", bins=5, depth=4, num_leaf=5, num_trees=3),
         "random-forest-predict": dict(X=f"{d}/X", Y=f"{d}/ycls", M=f"{o}/rf", P=f"{o}/rfP", A=f"{o}/rfA",
                                       CM=f"{o}/rfCM"),
         "KM": dict(X=f"{d}/surv", TE=f"{d}/te", GI=f"{d}/gi", SI=f"{d}/si", O=f"{o}/km", M=f"{o}/kmM",
                    T=f"{o}/kmT"),
         "Cox": dict(X=f"{d}/surv", TE=f"{d}/te", F=f"{d}/F", M=f"{o}/coxM", S=f"{o}/coxS", T=f"{o}/coxT",
                     COV=f"{o}/coxCOV", RT=f"{o}/coxRT", XO=f"{o}/coxXO", MF=f"{o}/coxMF"),
-        "CsplineCG": dict(X=f"{d}/Xcs", Y=f"{d}/ycs", K=f"{o}/csK", O=f"{o}/csO", inp_x=4.5),
+        "CsplineCG": dict(X=f"{d}/Xcs", Y=f"{d}/ycs", K=f"{o}/csK", O=f"{o}/csO", inp_x=4.5, maxi=100,
+                          tol=1e-12),
         "CsplineDS": dict(X=f"{d}/Xcs", Y=f"{d}/ycs", K=f"{o}/csK2", O=f"{o}/csO2", inp_x=4.5),
-        "StepLinearRegDS": dict(X=f"{d}/X", Y=f"{d}/y", B=f"{o}/stepB", S=f"{o}/stepS"),
-        "StepGLM": dict(X=f"{d}/X", Y=f"{d}/counts", B=f"{o}/sglmB", S=f"{o}/sglmS", dfam=1, vpow=1.0, link=1,
-                        lpow=0.0),
-        "stratstats": dict(X=f"{d}/Xint", Xcid=f"{d}/S1", Ycid=f"{d}/S2", S=f"{d}/gi", O=f"{o}/strat"),
+        "StepLinearRegDS": dict(X=f"{d}/X", Y=f"{d}/y", B=f"{o}/stepB", S=f"{o}/stepS", icpt=1, thr=0.01),
+        "StepGLM": dict(X=f"{d}/X", Y=f"{d}/y01", B=f"{o}/sglmB", S=f"{o}/sglmS", link=2, yneg=0.0, icpt=1,
+                        thr=0.01, tol=1e-9),
+        "stratstats": dict(X=f"{d}/Xint", Xcid=f"{d}/S1", Ycid=f"{d}/S2", Scid=3, O=f"{o}/strat"),
     }
+
+
+def run_suite(script_dir, d, out_dir=None, only=None, out_lines=None):
+    """Run every case whose script exists in `script_dir` on the data in `d` (make_data); the
+    scripts' output files go to `out_dir` (default d/out).  Returns {name: None | exception}."""
+    from systemml_amd.api import executor as EX
+    from systemml_amd.conf import DMLConfig
+    cfg = DMLConfig(gpu=False)
+    o = out_dir or f"{d}/out"
+    os.makedirs(o, exist_ok=True)
+    res = {}
+    for name, args in cases(d).items():
+        if only and name not in only:
+            continue
+        path = os.path.join(script_dir, name + ".dml")
+        if not os.path.exists(path):
+            continue
+        args = {k.rstrip("_"): (str(v).replace(f"{d}/out", o)) for k, v in args.items()}
+        out = [] if out_lines is None else out_lines.setdefault(name, [])
+        try:
+            with open(path) as f:
+                src = f.read()
+            cs = EX.compile_script(src, args, config=cfg, filename=path)
+            EX.execute(cs, {}, out=out.append)
+            res[name] = None
+        except Exception as e:  # noqa: BLE001
+            res[name] = e
+    return res
 
 
 def main():
@@ -120,37 +155,29 @@ def main():
     ap.add_argument("--only", nargs="*")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
-    from systemml_amd.api import executor as EX
-    from systemml_amd.conf import DMLConfig
     d = tempfile.mkdtemp()
     os.makedirs(d + "/out", exist_ok=True)
     make_data(d)
-    cfg = DMLConfig(gpu=False)
     ok = fail = 0
-    for name, args in cases(d).items():
+    for name in cases(d):
         if a.only and name not in a.only:
             continue
-        path = os.path.join(a.dir, name + ".dml")
-        if not os.path.exists(path):
+        if not os.path.exists(os.path.join(a.dir, name + ".dml")):
             print(f"SKIP {name} (no script)")
             continue
-        args = {k.rstrip("_"): v for k, v in args.items()}
         t = time.time()
-        out = []
-        try:
-            with open(path) as f:
-                src = f.read()
-            cs = EX.compile_script(src, {k: str(v) for k, v in args.items()}, config=cfg, filename=path)
-            EX.execute(cs, {}, out=out.append)
+        lines = {}
+        r = run_suite(a.dir, d, only=[name], out_lines=lines)[name]
+        if r is None:
             print(f"OK   {name:24s} {time.time() - t:6.2f}s")
             ok += 1
-        except Exception as e:  # noqa: BLE001
-            print(f"FAIL {name:24s} {type(e).__name__}: {str(e)[:300]}")
+        else:
+            print(f"FAIL {name:24s} {type(r).__name__}: {str(r)[:300]}")
             if a.verbose:
-                traceback.print_exc()
+                traceback.print_exception(type(r), r, r.__traceback__)
             fail += 1
         if a.verbose:
-            print("\n".join(out[-5:]))
+            print("\n".join(lines.get(name, [])[-int(os.environ.get("RUN_ALGOS_TAIL", "5")):]))
     print(f"{ok} ok, {fail} failed")
     return 0 if fail == 0 else 1
 
