@@ -74,6 +74,7 @@ class Rewriter:
         self.enabled = True if config is None else getattr(config, "rewrites", True)
         self.fuse = True if config is None else getattr(config, "fusion", True)
         self.stats = {}
+        self.multi = set()       # ids of hops with more than one consumer (see count_consumers)
 
     def _count(self, name):
         self.stats[name] = self.stats.get(name, 0) + 1
@@ -91,6 +92,8 @@ class Rewriter:
                 n = h
         else:
             n = h
+        if h.id in self.multi:
+            self.multi.add(n.id)
         if self.enabled:
             for _ in range(8):
                 m = self.apply_rules(n)
@@ -150,7 +153,7 @@ class Rewriter:
                 self._count("identity")
                 return b
         if o in ("*", "/") and self.fuse and a.dt == "M" and b.dt == "M":
-            q = _match_wquat_cell(o, a, b, h)
+            q = _wquat_guard(_match_wquat_cell(o, a, b, h), self.multi)
             if q is not None:
                 self._count("wquat-" + q.p["kind"])
                 return q
@@ -170,7 +173,7 @@ class Rewriter:
         x = h.inputs[0]
         o, d = h.p["o"], h.p["dir"]
         if d == "all" and o in ("sum", "sumsq") and self.fuse:
-            q = _match_wquat_agg(o, x, h)
+            q = _wquat_guard(_match_wquat_agg(o, x, h), self.multi)
             if q is not None:
                 self._count("wquat-" + q.p["kind"])
                 return q
@@ -216,7 +219,7 @@ class Rewriter:
             self._count("tsmm")
             return Hop("tsmm", [a], {"left": False}, dt="M", pos=h.pos)
         if self.fuse:
-            q = _match_wdivmm(a, b, transA, h)
+            q = _wquat_guard(_match_wdivmm(a, b, transA, h), self.multi)
             if q is not None:
                 self._count("wquat-wdivmm")
                 return q
@@ -353,10 +356,57 @@ def _is_neg(h):
     return None
 
 
-def _wq(kind, ins, p, dt, h):
+def _wq(kind, ins, p, dt, h, uv=None):
     q = dict(p)
     q["kind"] = kind
+    if uv is not None:
+        q["_uvid"] = uv.id          # consumed by _wquat_guard
     return Hop("wquat", ins, q, dt=dt, pos=h.pos)
+
+
+def _known(d):
+    return d is not None and d >= 0
+
+
+def _wquat_guard(q, multi):
+    """The reference's applicability checks for the weighted quaternary rewrites
+    (hops/rewrite/RewriteAlgebraicSimplificationDynamic#simplifyWeighted*): W / X, U and V
+    must have matching sizes where known (a broadcast vector W is not a weight matrix), and
+    the U %*% t(V) product must have no other consumer -- otherwise the dense product is
+    needed anyway and fusing would compute it twice."""
+    if q is None:
+        return None
+    uvid = q.p.pop("_uvid", None)
+    if uvid is not None and uvid in multi:
+        return None
+    W, U, V = q.inputs[0], q.inputs[1], q.inputs[2]
+    if _known(W.dim1) and _known(U.dim1) and W.dim1 != U.dim1:
+        return None
+    if _known(W.dim2) and _known(V.dim1) and W.dim2 != V.dim1:
+        return None
+    if len(q.inputs) > 3 and q.p["kind"] == "wsloss" and q.inputs[3].dt == "M":
+        W2 = q.inputs[3]
+        if (_known(W2.dim1) and _known(W.dim1) and W2.dim1 != W.dim1) or \
+                (_known(W2.dim2) and _known(W.dim2) and W2.dim2 != W.dim2):
+            return None
+    return q
+
+
+def count_consumers(roots):
+    """Ids of hops referenced by more than one parent (or by a root list more than once)."""
+    seen, cnt = set(), {}
+    stack = list(roots)
+    for r in roots:
+        cnt[r.id] = cnt.get(r.id, 0) + 1
+    while stack:
+        h = stack.pop()
+        if h.id in seen:
+            continue
+        seen.add(h.id)
+        for c in h.inputs:
+            cnt[c.id] = cnt.get(c.id, 0) + 1
+            stack.append(c)
+    return {k for k, v in cnt.items() if v > 1}
 
 
 def _match_wquat_agg(o, x, h):
@@ -369,12 +419,12 @@ def _match_wquat_agg(o, x, h):
                 continue
             m = _uv(R)
             if m is not None:
-                return _wq("wsloss", [X, m[0], m[1]], {"type": "none"}, "S", h)
+                return _wq("wsloss", [X, m[0], m[1]], {"type": "none"}, "S", h, R)
             if X is A and R.op == "b" and R.p["o"] == "*":
                 for W, P in (R.inputs, R.inputs[::-1]):
                     m = _uv(P)
                     if m is not None and W.dt == "M":
-                        return _wq("wsloss", [X, m[0], m[1], W], {"type": "pre"}, "S", h)
+                        return _wq("wsloss", [X, m[0], m[1], W], {"type": "pre"}, "S", h, P)
         return None
     if x.op == "wquat" and x.p["kind"] == "wumm" and x.p["uop"] == "log" and x.p.get("op") == "*":
         return _wq("wcemm", list(x.inputs), {}, "S", h)
@@ -392,14 +442,14 @@ def _match_wquat_agg(o, x, h):
                     if m is None or X.dt != "M":
                         continue
                     if W.op == "b" and W.p["o"] == "!=" and W.inputs[0] is X and _is_lit(W.inputs[1], 0):
-                        return _wq("wsloss", [X, m[0], m[1]], {"type": "post_nz"}, "S", h)
-                    return _wq("wsloss", [X, m[0], m[1], W], {"type": "post"}, "S", h)
+                        return _wq("wsloss", [X, m[0], m[1]], {"type": "post_nz"}, "S", h, R)
+                    return _wq("wsloss", [X, m[0], m[1], W], {"type": "post"}, "S", h, R)
         # sum(X * log(U%*%t(V) [+ eps]))
         if P.op == "u" and P.p["o"] == "log":
             m = _uv_eps(P.inputs[0])
             if m is not None:
                 U, V, e = m
-                return _wq("wcemm", [W, U, V] + ([e] if e is not None else []), {"eps": e is not None}, "S", h)
+                return _wq("wcemm", [W, U, V] + ([e] if e is not None else []), {"eps": e is not None}, "S", h, P.inputs[0])
     return None
 
 
@@ -415,17 +465,18 @@ def _match_wquat_cell(o, a, b, h):
                 n = _is_neg(z)
                 m = _uv(n if n is not None else z)
                 if m is not None:
-                    return _wq("wsigmoid", [W, m[0], m[1]], {"minus": n is not None, "log": lg}, "M", h)
+                    return _wq("wsigmoid", [W, m[0], m[1]], {"minus": n is not None, "log": lg}, "M", h,
+                               n if n is not None else z)
     cands = [(a, b)] if o == "/" else [(a, b), (b, a)]
     for X, P in cands:
         if P.op == "u" and P.p["o"] in _WUMM_UOPS:
             m = _uv(P.inputs[0])
             if m is not None:
-                return _wq("wumm", [X, m[0], m[1]], {"uop": P.p["o"], "op": o}, "M", h)
+                return _wq("wumm", [X, m[0], m[1]], {"uop": P.p["o"], "op": o}, "M", h, P.inputs[0])
         if P.op == "b" and P.p["o"] == "^" and _is_lit(P.inputs[1], 2):
             m = _uv(P.inputs[0])
             if m is not None:
-                return _wq("wumm", [X, m[0], m[1]], {"uop": "^2", "op": o}, "M", h)
+                return _wq("wumm", [X, m[0], m[1]], {"uop": "^2", "op": o}, "M", h, P.inputs[0])
     return None
 
 
@@ -446,7 +497,7 @@ def _match_wdivmm(a, b, transA, h):
         U, V, e = m
         if (transA and other is U) or (not transA and other is V):
             return _wq("wdivmm", [W, U, V] + ([e] if e is not None else []),
-                       {"left": transA, "mult": mult, "eps": e is not None}, "M", h)
+                       {"left": transA, "mult": mult, "eps": e is not None}, "M", h, R)
     return None
 
 
@@ -484,6 +535,7 @@ def cse(roots):
 def rewrite_block(bb, config=None):
     """Rewrite a BasicBlock's DAG in place (roots + env_out)."""
     rw = Rewriter(config)
+    rw.multi = count_consumers(list(bb.roots) + list(bb.env_out.values()))
     bb.roots = [rw.rewrite(r) for r in bb.roots]
     bb.env_out = {k: rw.rewrite(v) for k, v in bb.env_out.items()}
     roots, visit = cse(bb.roots)

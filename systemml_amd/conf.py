@@ -35,7 +35,7 @@ class DMLConfig:
     explain: str = ""                   # '' | hops | runtime | recompile_hops
     print_rank0_only: bool = True
     scratch: str = "scratch_space"
-    seed: int = -1
+    seed: int = -1                      # >= 0: rand/sample without a seed draw a repeatable sequence
     hip_kernels: bool = True            # use in-tree HIP kernels for the hot ops on GPU
     hip_graphs: bool = False
     # compressed linear algebra (ops/compress.py): "false" | "true" | "auto" (auto: ratio >= 3)
@@ -54,6 +54,7 @@ class DMLConfig:
         "sysml.gpu.mincells": ("gpu_min_cells", int),
         "sysml.gpu.lazy.scalars": ("lazy_scalars", lambda v: str(v).lower() == "true"),
         "sysml.parallel.ops": ("parallelism", lambda v: 8 if str(v).lower() == "true" else 1),
+        "sysml.random.seed": ("seed", int),
         "sysml.localtmpdir": ("scratch", str),
         "sysml.scratch": ("scratch", str),
         "sysml.stats.maxHeavyHitters": ("stats_count", int),

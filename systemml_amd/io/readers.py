@@ -63,6 +63,10 @@ def read(ctx, fname, **kw):
         return float(txt)
     if dtype == "frame":
         return read_frame(fname, fmt, rows, cols, md, **kw)
+    if ctx is not None and ctx.dist is not None:
+        part = _read_partitioned(ctx, fname, fmt, rows, cols, md, kw)
+        if part is not None:
+            return part
     if fmt == "csv":
         header = _b(kw.get("header", md.get("header", False)))
         sep = kw.get("sep", md.get("sep", ","))
@@ -86,6 +90,66 @@ def read(ctx, fname, **kw):
         else:
             raise DMLRuntimeError(f"read: dimensions {arr.shape} do not match metadata {rows}x{cols}")
     return _post(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64)), ctx)
+
+
+def _read_partitioned(ctx, fname, fmt, rows, cols, md, kw):
+    """SPMD read: each rank parses / maps only its own row block (reference analogue: the
+    per-partition HDFS splits a Spark job reads).  Binary files are memory-mapped and
+    sliced; single-file CSVs go through the native row-range parser.  Returns None when the
+    matrix stays replicated (fewer than `sysml.dist.minrows` rows) or the format has no
+    partitioned reader."""
+    from ..parallel import dist as D
+    from ..ops import native
+    dctx = ctx.dist
+    minr = ctx.config.dist_min_rows
+    files = _files(fname)
+    if fmt == "binary":
+        with open(fname, "rb") as f:
+            head = f.read(32)
+        r, c = (int(v) for v in np.frombuffer(head[8:24], dtype=np.int64))
+        if r < minr:
+            return None
+        code = int(np.frombuffer(head[24:28], dtype=np.int32)[0])
+        dt = {0: np.float64, 1: np.float32, 2: np.uint16}[code]
+        s, e = dctx.partition(r)
+        arr = np.memmap(fname, dtype=dt, mode="r", offset=32 + s * c * np.dtype(dt).itemsize, shape=(e - s, c))
+        loc = torch.from_numpy(np.array(arr)).view(torch.bfloat16) if code == 2 else \
+            torch.from_numpy(np.array(arr, dtype=np.float64))
+        return D.local_block(dctx, loc, r, c)
+    if fmt != "csv" or len(files) != 1 or native.lib() is None:
+        return None
+    header = _b(kw.get("header", md.get("header", False)))
+    sep = kw.get("sep", md.get("sep", ","))
+    if kw.get("naStrings", md.get("naStrings")) is not None or not _b(kw.get("fill", md.get("fill", True))) \
+            or float(kw.get("default", md.get("default", 0.0))) != 0.0 or len(sep) != 1:
+        return None
+    thr = os.cpu_count() or 8
+    if rows <= 0:
+        got = native.parse_csv_rows(files[0], 0, 0, sep, header, thr)
+        if got is None:
+            return None
+        rows = got[1]
+    if rows < minr:
+        return None
+    s, e = dctx.partition(rows)
+    got = native.parse_csv_rows(files[0], s, e, sep, header, thr)
+    if got is None:
+        return None
+    arr, total = got
+    if total != rows:
+        raise DMLRuntimeError(f"read: {fname} has {total} rows, metadata says {rows}")
+    if cols > 0 and arr.shape[1] != cols:
+        if arr.shape[1] > cols:
+            raise DMLRuntimeError(f"read: dimensions do not match metadata {rows}x{cols}")
+        arr = np.hstack([arr, np.zeros((arr.shape[0], cols - arr.shape[1]))])
+    ncols = arr.shape[1] if cols <= 0 else cols
+    if arr.shape[0] == 0:
+        arr = np.zeros((0, ncols))
+    # column count of an empty local block: agree on the global maximum
+    ncols = int(dctx.allreduce_scalar(float(ncols), "max"))
+    if arr.shape[1] != ncols:
+        arr = np.zeros((arr.shape[0], ncols)) if arr.shape[0] == 0 else arr
+    return D.local_block(dctx, torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64)), rows, ncols)
 
 
 def _post(t, ctx):

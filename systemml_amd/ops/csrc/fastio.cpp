@@ -115,9 +115,13 @@ extern "C" {
 
 void sysml_free(void* p) { std::free(p); }
 
-// CSV of doubles -> row-major buffer.  Returns rows*cols or -1 on error.
-int64_t sysml_parse_csv(const char* path, char sep, int header, int64_t* rows_out, int64_t* cols_out,
-                        double** out, int threads) {
+// CSV of doubles -> row-major buffer of data rows [row_lo, row_hi) (all rows: 0, INT64_MAX).
+// Every thread counts the rows of its byte range (memchr only), then only the ranges that
+// overlap the requested rows are parsed -- a rank of an SPMD run parses just its own row
+// block.  *total_out receives the file's row count.  Returns rows*cols or -1 on error.
+int64_t sysml_parse_csv_rows(const char* path, char sep, int header, int64_t row_lo, int64_t row_hi,
+                             int64_t* rows_out, int64_t* cols_out, int64_t* total_out, double** out,
+                             int threads) {
   Mapped f;
   if (!f.open(path)) return -1;
   const char* p = f.p;
@@ -151,7 +155,11 @@ int64_t sysml_parse_csv(const char* path, char sep, int header, int64_t* rows_ou
   }
   std::vector<size_t> roff(threads + 1, 0);
   for (int t = 0; t < threads; ++t) roff[t + 1] = roff[t] + rcount[t];
-  int64_t rows = (int64_t)roff[threads];
+  int64_t total = (int64_t)roff[threads];
+  if (row_lo < 0) row_lo = 0;
+  if (row_hi > total) row_hi = total;
+  if (row_lo > row_hi) row_lo = row_hi;
+  int64_t rows = row_hi - row_lo;
   double* buf = (double*)std::malloc(sizeof(double) * (size_t)std::max<int64_t>(rows * cols, 1));
   if (!buf) return -1;
   bool bad = false;
@@ -159,15 +167,22 @@ int64_t sysml_parse_csv(const char* path, char sep, int header, int64_t* rows_ou
     std::vector<std::thread> ts;
     for (int t = 0; t < threads; ++t)
       ts.emplace_back([&, t] {
+        int64_t r = (int64_t)roff[t];
+        if (r >= row_hi || (int64_t)roff[t + 1] <= row_lo) return;
         size_t i = b[t], z = b[t + 1];
-        double* o = buf + roff[t] * cols;
-        while (i < z) {
+        while (i < z && r < row_hi) {
           const char* nl = (const char*)memchr(p + i, '\n', z - i);
           size_t end = nl ? (size_t)(nl - p) : z;
           const char* s = p + i;
           const char* e = p + end;
           const char* q = skip_ws(s, e);
           if (q < e) {
+            const int64_t row = r++;            // data row index in the file
+            if (row < row_lo) {
+              i = end + 1;
+              continue;
+            }
+            double* o = buf + (row - row_lo) * cols;
             int64_t c = 0;
             while (c < cols) {
               double v;
@@ -178,7 +193,6 @@ int64_t sysml_parse_csv(const char* path, char sep, int header, int64_t* rows_ou
               else break;
             }
             for (; c < cols; ++c) o[c] = 0.0;   // short line: fill
-            o += cols;
           }
           i = end + 1;
         }
@@ -188,8 +202,15 @@ int64_t sysml_parse_csv(const char* path, char sep, int header, int64_t* rows_ou
   }
   *rows_out = rows;
   *cols_out = cols;
+  *total_out = total;
   *out = buf;
   return rows * cols;
+}
+
+int64_t sysml_parse_csv(const char* path, char sep, int header, int64_t* rows_out, int64_t* cols_out,
+                        double** out, int threads) {
+  int64_t total;
+  return sysml_parse_csv_rows(path, sep, header, 0, INT64_MAX, rows_out, cols_out, &total, out, threads);
 }
 
 // "i j v" text cell format -> n x 3 row-major buffer; returns n or -1.

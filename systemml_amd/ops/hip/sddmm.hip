@@ -2,72 +2,132 @@
 // reference: LibMatrixMult.java#matrixMultWSLossSparseDense / wdivmm / wcemm, which loop over
 // the non-zeros of W and compute dotProduct(U[i], V[j]) per non-zero).
 //
-// out[k] = <U[i_k], V[j_k]> for every non-zero k of a CSR pattern (crow/col int64).
-// CDNA4 mapping: one 64-lane wavefront per CSR row (grid-stride over rows).  The wave stages
-// U[i] (r <= 256 fp32) in its LDS slice once; then each lane owns one non-zero of the row
-// and reads V[j] with 16-byte loads (r % 4 == 0) while the U values come from LDS as
-// broadcast reads (every lane reads the same address -> no bank conflicts).  The kernel is a
-// gather: its bound is HBM/L2 traffic of the V rows (r*4 bytes per non-zero), so U is read
-// once per row instead of once per non-zero.
+// out[k] = <U[i_k], V[j_k]> for every non-zero k of a CSR pattern (crow/col int64), in fp32 or
+// fp64 (the engine's default precision is fp64; the result is accumulated in the operand type).
+//
+// CDNA4 mapping: one 64-lane wavefront per CSR row (grid-stride over rows).  The wave is split
+// into groups of G lanes; a group owns one non-zero at a time and reads the whole V[j] row with
+// one 16-byte load per lane (G * 16 B = r * sizeof(T): r=64 fp32 -> G=16, 4 non-zeros per wave
+// instruction, each a fully coalesced 256 B segment), multiplies with the matching slice of
+// U[i] that the lane keeps in registers for the whole row, and reduces over the group with
+// xor-shuffles.  V traffic is exactly r*sizeof(T) per non-zero in whole cache lines; U[i] is
+// read once per row.  Rows that need more than 64 lanes (r*sizeof(T) > 1 KiB) loop over chunks.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 namespace sysml_sd {
 
 constexpr int WAVES = 4;
-constexpr int RMAX = 256;
 
-template <bool VEC4>
+template <typename T, int NV>
+__device__ __forceinline__ void load_vec(const T* p, T (&v)[NV]) {
+  if constexpr (NV == 4) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else if constexpr (NV == 2) {
+    const double2 x = *reinterpret_cast<const double2*>(p);
+    v[0] = x.x; v[1] = x.y;
+  } else {
+    v[0] = *p;
+  }
+}
+
+// G lanes per non-zero, NV elements per lane per chunk (16 B when vectorised), NCH chunks
+template <typename T, int G, int NV, int NCH>
 __global__ __launch_bounds__(WAVES * 64) void sddmm_kernel(const int64_t* __restrict__ crow,
                                                            const int64_t* __restrict__ col,
-                                                           const float* __restrict__ U,
-                                                           const float* __restrict__ V, int64_t m, int r,
-                                                           float* __restrict__ out) {
-  __shared__ float su[WAVES][RMAX];
+                                                           const T* __restrict__ U, const T* __restrict__ V,
+                                                           int64_t m, int r, T* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
+  const int gl = lane & (G - 1);          // lane within its group
+  const int grp = lane / G;               // group within the wave
+  constexpr int NG = 64 / G;
   for (int64_t i = (int64_t)blockIdx.x * WAVES + w; i < m; i += (int64_t)gridDim.x * WAVES) {
     const int64_t b = crow[i], e = crow[i + 1];
-    if (b == e) continue;                       // wave-uniform: whole wave skips empty rows
-    for (int k = lane; k < r; k += 64) su[w][k] = U[i * r + k];
-    __builtin_amdgcn_wave_barrier();            // LDS ops of one wave complete in order
-    for (int64_t p = b + lane; p < e; p += 64) {
-      const float* vr = V + col[p] * (int64_t)r;
-      float acc = 0.f;
-      if (VEC4) {
-        for (int k = 0; k < r; k += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(vr + k);
-          acc += su[w][k] * v.x + su[w][k + 1] * v.y + su[w][k + 2] * v.z + su[w][k + 3] * v.w;
-        }
-      } else {
-        for (int k = 0; k < r; ++k) acc += su[w][k] * vr[k];
-      }
-      out[p] = acc;
+    if (b == e) continue;                 // wave-uniform
+    T u[NCH][NV];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int k = (c * G + gl) * NV;
+      if (k < r) load_vec<T, NV>(U + i * r + k, u[c]);
+      else
+#pragma unroll
+        for (int j = 0; j < NV; ++j) u[c][j] = T(0);
     }
-    __builtin_amdgcn_wave_barrier();            // LDS slice reused by this wave's next row
+    for (int64_t p0 = b; p0 < e; p0 += NG) {
+      const int64_t p = p0 + grp;
+      T acc = T(0);
+      if (p < e) {
+        const T* vr = V + col[p] * (int64_t)r;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int k = (c * G + gl) * NV;
+          if (k < r) {
+            T v[NV];
+            load_vec<T, NV>(vr + k, v);
+#pragma unroll
+            for (int j = 0; j < NV; ++j) acc += u[c][j] * v[j];
+          }
+        }
+      }
+#pragma unroll
+      for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (gl == 0 && p < e) out[p] = acc;
+    }
   }
+}
+
+template <typename T, int NV>
+int launch(const int64_t* crow, const int64_t* col, const T* U, const T* V, int64_t m, int r, T* out,
+           hipStream_t s) {
+  int64_t blocks = (m + WAVES - 1) / WAVES;
+  if (blocks > 256 * 64) blocks = 256 * 64;     // 8 XCDs x 32 CUs x 64: grid-stride beyond that
+  const int lanes = (r + NV - 1) / NV;          // lanes needed to cover one row once
+  dim3 g((unsigned)blocks), t(WAVES * 64);
+#define SD_CASE(G_, NCH_) hipLaunchKernelGGL((sddmm_kernel<T, G_, NV, NCH_>), g, t, 0, s, crow, col, U, V, m, r, out)
+  if (lanes <= 1) SD_CASE(1, 1);
+  else if (lanes <= 2) SD_CASE(2, 1);
+  else if (lanes <= 4) SD_CASE(4, 1);
+  else if (lanes <= 8) SD_CASE(8, 1);
+  else if (lanes <= 16) SD_CASE(16, 1);
+  else if (lanes <= 32) SD_CASE(32, 1);
+  else if (lanes <= 64) SD_CASE(64, 1);
+  else if (lanes <= 128) SD_CASE(64, 2);
+  else if (lanes <= 256) SD_CASE(64, 4);
+  else return -1;
+#undef SD_CASE
+  return (int)hipGetLastError();
 }
 
 }  // namespace sysml_sd
 
 extern "C" {
 
-// Returns 0 on success, -1 on unsupported shape, otherwise a hipError_t.
-int sysml_sddmm(const void* crow, const void* col, const float* U, const float* V, int64_t m, int r,
-                float* out, void* stream) {
+// dtype 0 = fp32, 1 = fp64.  Returns 0 on success, -1 on unsupported shape, else a hipError_t.
+int sysml_sddmm(int dtype, const void* crow, const void* col, const void* U, const void* V, int64_t m, int r,
+                void* out, void* stream) {
   using namespace sysml_sd;
-  if (r <= 0 || r > RMAX || m <= 0) return -1;
-  int64_t blocks = (m + WAVES - 1) / WAVES;
-  if (blocks > 256 * 64) blocks = 256 * 64;     // 8 XCDs x 32 CUs x 64: grid-stride beyond that
+  if (r <= 0 || m <= 0) return -1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool vec = (r % 4) == 0 && (reinterpret_cast<uintptr_t>(V) % 16) == 0;
-  if (vec)
-    hipLaunchKernelGGL(sddmm_kernel<true>, dim3((unsigned)blocks), dim3(WAVES * 64), 0, s,
-                       (const int64_t*)crow, (const int64_t*)col, U, V, m, r, out);
-  else
-    hipLaunchKernelGGL(sddmm_kernel<false>, dim3((unsigned)blocks), dim3(WAVES * 64), 0, s,
-                       (const int64_t*)crow, (const int64_t*)col, U, V, m, r, out);
-  return (int)hipGetLastError();
+  const auto* cr = static_cast<const int64_t*>(crow);
+  const auto* cl = static_cast<const int64_t*>(col);
+  const bool aligned = (reinterpret_cast<uintptr_t>(U) % 16) == 0 && (reinterpret_cast<uintptr_t>(V) % 16) == 0;
+  if (dtype == 0) {
+    const auto* u = static_cast<const float*>(U);
+    const auto* v = static_cast<const float*>(V);
+    auto* o = static_cast<float*>(out);
+    if (aligned && r % 4 == 0) return launch<float, 4>(cr, cl, u, v, m, r, o, s);
+    return launch<float, 1>(cr, cl, u, v, m, r, o, s);
+  }
+  if (dtype == 1) {
+    const auto* u = static_cast<const double*>(U);
+    const auto* v = static_cast<const double*>(V);
+    auto* o = static_cast<double*>(out);
+    if (aligned && r % 2 == 0) return launch<double, 2>(cr, cl, u, v, m, r, o, s);
+    return launch<double, 1>(cr, cl, u, v, m, r, o, s);
+  }
+  return -1;
 }
 
 }  // extern "C"

@@ -63,8 +63,8 @@ def load(required=False):
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                       ctypes.c_void_p]
     L.sysml_sddmm.restype = ctypes.c_int
-    L.sysml_sddmm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
-                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    L.sysml_sddmm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     L.sysml_set_rows_per_iter.argtypes = [ctypes.c_int]
     L.sysml_set_rows_per_iter.restype = None
     L.sysml_mchain.restype = ctypes.c_int
@@ -478,21 +478,27 @@ def sumsq(x, d):
     return torch.sum(xx * xx, dim=1 if d == "row" else 0, keepdim=True)
 
 
-def sddmm(crow, col, U, V):
-    """<U[i_k], V[j_k]> at the non-zeros of a CSR pattern (ops/hip/sddmm.hip); None when the
-    shape is unsupported (r > 256).  U, V: fp32 contiguous on the GPU; crow/col int64."""
+def sddmm(crow, col, U, V, dtype=None):
+    """<U[i_k], V[j_k]> at the non-zeros of a CSR pattern (ops/hip/sddmm.hip), computed and
+    returned in `dtype` (fp32 or fp64; default: fp64 if either factor is fp64, else fp32 --
+    bf16 factors are widened); None when the shape is unsupported."""
     import torch
     L = load(required=True)
     m, r = U.shape
-    if r > 256 or col.numel() == 0:
+    if dtype is None:
+        dtype = torch.float64 if torch.float64 in (U.dtype, V.dtype) else torch.float32
+    if col.numel() == 0 or r > (1024 if dtype == torch.float32 else 512):
         return None
-    U = U.float().contiguous()
-    V = V.float().contiguous()
+    U = U.to(dtype).contiguous()
+    V = V.to(dtype).contiguous()
     crow = crow.to(torch.int64).contiguous()
     col = col.to(torch.int64).contiguous()
-    out = torch.empty(col.numel(), dtype=torch.float32, device=U.device)
+    out = torch.empty(col.numel(), dtype=dtype, device=U.device)
     st = torch.cuda.current_stream(U.device).cuda_stream
-    rc = L.sysml_sddmm(crow.data_ptr(), col.data_ptr(), U.data_ptr(), V.data_ptr(), m, r, out.data_ptr(), st)
+    rc = L.sysml_sddmm(0 if dtype == torch.float32 else 1, crow.data_ptr(), col.data_ptr(), U.data_ptr(),
+                       V.data_ptr(), m, r, out.data_ptr(), st)
+    if rc == -1:
+        return None
     if rc != 0:
         raise RuntimeError(f"sysml_sddmm failed: {rc}")
     _count("sddmm")

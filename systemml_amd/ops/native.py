@@ -27,6 +27,11 @@ def lib():
             L.sysml_parse_csv.argtypes = [ctypes.c_char_p, ctypes.c_char, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_double)), ctypes.c_int]
+            L.sysml_parse_csv_rows.restype = ctypes.c_int64
+            L.sysml_parse_csv_rows.argtypes = [ctypes.c_char_p, ctypes.c_char, ctypes.c_int, ctypes.c_int64,
+                                               ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                               ctypes.POINTER(ctypes.POINTER(ctypes.c_double)), ctypes.c_int]
             L.sysml_parse_ijv.restype = ctypes.c_int64
             L.sysml_parse_ijv.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_double)),
                                           ctypes.c_int]
@@ -52,6 +57,25 @@ def parse_csv(path, sep=",", header=False, threads=8):
     arr = np.ctypeslib.as_array(buf, shape=(max(n, 1),))[:n].copy().reshape(rows.value, cols.value)
     L.sysml_free(buf)
     return arr
+
+
+def parse_csv_rows(path, row_lo, row_hi, sep=",", header=False, threads=8):
+    """Data rows [row_lo, row_hi) of a CSV file and the file's total row count (only the
+    byte ranges holding those rows are parsed)."""
+    L = lib()
+    if L is None or len(sep) != 1:
+        return None
+    rows, cols, total = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    buf = ctypes.POINTER(ctypes.c_double)()
+    rc = L.sysml_parse_csv_rows(path.encode(), sep.encode(), int(bool(header)), int(row_lo), int(row_hi),
+                                ctypes.byref(rows), ctypes.byref(cols), ctypes.byref(total), ctypes.byref(buf),
+                                threads)
+    if rc < 0:
+        return None
+    n = rows.value * cols.value
+    arr = np.ctypeslib.as_array(buf, shape=(max(n, 1),))[:n].copy().reshape(rows.value, cols.value)
+    L.sysml_free(buf)
+    return arr, total.value
 
 
 def parse_ijv(path, threads=8):

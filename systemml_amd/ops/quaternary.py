@@ -20,8 +20,12 @@ gathers of U and V in nnz chunks, an r-wide dot per non-zero; both gathers hit H
 streaming bandwidth because r is small) and the result is either reduced to a scalar, kept
 as a CSR with W's pattern, or multiplied by V / U through the sparse product.  wsloss "none"
 over a sparse X uses sum(X^2) - 2 sum(U .* (X V)) + sum((U'U) .* (V'V)), which reads X once.
-Dense operands (or row-partitioned / compressed ones) run the equivalent unfused operator
-sequence of ops/core.py, so results never depend on the representation.
+Dense operands (or compressed ones) run the equivalent unfused operator sequence of
+ops/core.py, so results never depend on the representation: the operators are sparse-safe
+as in the reference (cells where W / X is zero contribute 0, even where f(U V') is +-inf or
+NaN), and everything computes in the engine precision (fp64 by default; the SDDMM kernel has
+fp32 and fp64 variants).  Row-partitioned operands run the same code per rank
+(parallel/dist.wquat).
 """
 from __future__ import annotations
 
@@ -52,22 +56,42 @@ def _coo_idx(x):
     return row, col, val
 
 
-def sddmm(row, col, U, V):
-    """<U[row_k], V[col_k]> for every k (fp32 accumulate); on the GPU the hand-written
-    wave-per-row kernel of ops/hip/sddmm.hip (row must be sorted, as CSR order gives)."""
-    if U.is_cuda and row.numel() > 0:
+def _cdt(*xs):
+    """Compute dtype: the engine's precision (fp64 unless `precision=single`); bf16-stored
+    factors compute in fp32 (reference: the weighted operators compute in double)."""
+    from .backend import backend
+    dts = {x.dtype for x in xs if isinstance(x, torch.Tensor)}
+    if torch.float64 in dts or backend.dtype == torch.float64:
+        return torch.float64
+    return torch.float32
+
+
+def sddmm(row, col, U, V, crow=None, dtype=None):
+    """<U[row_k], V[col_k]> for every k in `dtype`; on the GPU the hand-written grouped-lane
+    kernel of ops/hip/sddmm.hip (row must be sorted, as CSR order gives)."""
+    from .backend import backend
+    dt = dtype or _cdt(U, V)
+    if U.is_cuda and row.numel() > 0 and backend.use_kernels:
         from . import kernels
-        crow = torch.searchsorted(row, torch.arange(U.shape[0] + 1, device=row.device))
-        out = kernels.sddmm(crow, col, U, V)
+        if crow is None:
+            crow = torch.searchsorted(row, torch.arange(U.shape[0] + 1, device=row.device))
+        out = kernels.sddmm(crow, col, U, V, dt)
         if out is not None:
             return out
-    U = U.float()
-    V = V.float()
-    out = torch.empty(row.numel(), dtype=torch.float32, device=U.device)
+    U = U.to(dt)
+    V = V.to(dt)
+    out = torch.empty(row.numel(), dtype=dt, device=U.device)
     for s in range(0, row.numel(), _CHUNK):
         e = min(s + _CHUNK, row.numel())
         out[s:e] = (U.index_select(0, row[s:e]) * V.index_select(0, col[s:e])).sum(1)
     return out
+
+
+def _sd(x, U, V, dt):
+    """(row, col, values as dt, sampled U V' as dt) at the non-zeros of CSR x."""
+    x = _csr(x)
+    r, c, v = _coo_idx(x)
+    return r, c, v.to(dt), sddmm(r, c, U, V, crow=x.crow_indices(), dtype=dt)
 
 
 def _plain(x):
@@ -85,8 +109,7 @@ def _uvt(U, V):
 
 def _sparse_like(pattern, vals):
     p = _csr(pattern)
-    return torch.sparse_csr_tensor(p.crow_indices(), p.col_indices(), vals.to(torch.float32),
-                                   size=p.shape, device=p.device)
+    return torch.sparse_csr_tensor(p.crow_indices(), p.col_indices(), vals, size=p.shape, device=p.device)
 
 
 def _check(U, V, m, n):
@@ -96,32 +119,56 @@ def _check(U, V, m, n):
                               f"V{tuple(V.shape)} for a {m} x {n} matrix")
 
 
+def _values_at(X, W, r, c, dt):
+    """X's values at W's non-zero positions (r, c in CSR order).  A sparse X is looked up by
+    sorted linear index (same pattern: its values directly) -- never densified."""
+    if SP.is_sparse(X):
+        xs, ws = _csr(X), _csr(W)
+        if xs.col_indices().numel() == ws.col_indices().numel() and \
+                torch.equal(xs.crow_indices(), ws.crow_indices()) and torch.equal(xs.col_indices(), ws.col_indices()):
+            return xs.values().to(dt)
+        xr, xc, xv = _coo_idx(xs)
+        n = X.shape[1]
+        kx = xr * n + xc                              # sorted (CSR order)
+        kw = r * n + c
+        pos = torch.searchsorted(kx, kw).clamp_(max=max(kx.numel() - 1, 0))
+        hit = (kx.numel() > 0) & (kx[pos] == kw) if kx.numel() else torch.zeros_like(kw, dtype=torch.bool)
+        return torch.where(hit, xv[pos].to(dt), torch.zeros((), dtype=dt, device=xv.device)) if kx.numel() \
+            else torch.zeros(kw.numel(), dtype=dt, device=kw.device)
+    return X[r, c].to(dt)
+
+
 # ----------------------------------------------------------------------------- wsloss
 def wsloss(kind, X, U, V, W=None):
     C = _C()
     if _dense_ok(X, U, V) and (W is None or _dense_ok(W)) and _plain(U) and _plain(V):
         _check(U, V, X.shape[0], X.shape[1])
+        dt = _cdt(X, U, V, W)
         if kind == "post_nz" and SP.is_sparse(X):
-            r, c, xv = _coo_idx(X)
-            d = xv.float() - sddmm(r, c, U, V)
+            _, _, xv, uv = _sd(X, U, V, dt)
+            d = xv - uv
             return float((d * d).sum().item())
         if kind == "post" and W is not None and SP.is_sparse(W):
-            r, c, wv = _coo_idx(W)
-            xd = SP.densify(X).float()
-            d = xd[r, c] - sddmm(r, c, U, V)
-            return float((wv.float() * d * d).sum().item())
+            r, c, wv, uv = _sd(W, U, V, dt)
+            d = _values_at(X, W, r, c, dt) - uv
+            return float((wv * d * d).sum().item())
         if kind == "pre" and W is not None and SP.is_sparse(W) and _plain(X):
-            r, c, wv = _coo_idx(W)
-            wuv = wv.float() * sddmm(r, c, U, V)
-            xf = X.float()
-            return float(((xf * xf).sum() - 2.0 * (xf[r, c] * wuv).sum() + (wuv * wuv).sum()).item())
+            # sum((X - W*UV')^2): residual at W's non-zeros plus X^2 where W is zero -- both
+            # sums of squares, no cancelling subtraction
+            r, c, wv, uv = _sd(W, U, V, dt)
+            xrc = X[r, c].to(dt)
+            d = xrc - wv * uv
+            xz = X.to(dt).clone()
+            xz[r, c] = 0
+            return float(((d * d).sum() + (xz * xz).sum()).item())
         if kind == "none" and SP.is_sparse(X):
-            Uf, Vf = U.float(), V.float()
-            xs = _csr(X).float() if X.dtype != torch.float32 else _csr(X)
-            xv = xs.values()
-            xvu = (torch.sparse.mm(xs, Vf) * Uf).sum()          # sum(X .* U V')
-            uv2 = ((Uf.t() @ Uf) * (Vf.t() @ Vf)).sum()          # sum((U V')^2)
-            return float(((xv * xv).sum() - 2.0 * xvu + uv2).item())
+            # sum((X - UV')^2) = sum_nz (x - uv)^2 + sum_zero uv^2, the second term as
+            # sum((U'U) .* (V'V)) - sum_nz uv^2 (a sum over cells X does not hold, fp64)
+            _, _, xv, uv = _sd(X, U, V, dt)
+            Uf, Vf = U.to(dt), V.to(dt)
+            d = xv - uv
+            zero_part = ((Uf.t() @ Uf) * (Vf.t() @ Vf)).sum() - (uv * uv).sum()
+            return float(((d * d).sum() + zero_part).item())
     # unfused (dense, row-partitioned or compressed operands)
     X = SP.densify(X)
     uv = _uvt(U, V)
@@ -141,19 +188,31 @@ def _sig(uv, minus, log):
     return torch.log(s) if log else s
 
 
+def _sparse_safe(W, f):
+    """W * f with f only where W != 0: the operators are sparse-safe in the reference (they
+    iterate over W's non-zeros), so zeros of W stay 0 even where f is +-inf or NaN."""
+    C = _C()
+    Wd = SP.densify(W)
+    prod = C.binary("*", Wd, f)
+    if isinstance(prod, torch.Tensor) and isinstance(Wd, torch.Tensor):
+        return torch.where(Wd != 0, prod, torch.zeros((), dtype=prod.dtype, device=prod.device))
+    return prod
+
+
 def wsigmoid(W, U, V, minus=False, log=False):
     C = _C()
     if SP.is_sparse(W) and _plain(U) and _plain(V):
         _check(U, V, W.shape[0], W.shape[1])
-        r, c, wv = _coo_idx(W)
-        return _sparse_like(W, wv.float() * _sig(sddmm(r, c, U, V), minus, log))
+        dt = _cdt(W, U, V)
+        _, _, wv, uv = _sd(W, U, V, dt)
+        return _sparse_like(W, wv * _sig(uv, minus, log))
     uv = _uvt(U, V)
     if minus:
         uv = C.unary("neg", uv)
     s = C.unary("sigmoid", uv)
     if log:
         s = C.unary("log", s)
-    return C.binary("*", SP.densify(W), s)
+    return _sparse_safe(W, s)
 
 
 # ------------------------------------------------------------------------------ wdivmm
@@ -162,20 +221,20 @@ def wdivmm(W, U, V, left, mult=False, eps=None):
     C = _C()
     if SP.is_sparse(W) and _plain(U) and _plain(V):
         _check(U, V, W.shape[0], W.shape[1])
-        r, c, wv = _coo_idx(W)
-        uv = sddmm(r, c, U, V)
+        dt = _cdt(W, U, V)
+        _, _, wv, uv = _sd(W, U, V, dt)
         if mult:
-            q = wv.float() * uv
+            q = wv * uv
         else:
-            q = wv.float() / (uv + eps if eps is not None else uv)
+            q = wv / (uv + eps if eps is not None else uv)
         S = _sparse_like(W, q)
         if left:
-            return torch.sparse.mm(S.t().to_sparse_csr(), U.float()).t().contiguous()
-        return torch.sparse.mm(S, V.float())
+            return torch.sparse.mm(S.t().to_sparse_csr(), U.to(dt)).t().contiguous()
+        return torch.sparse.mm(S, V.to(dt))
     uv = _uvt(U, V)
     if eps is not None:
         uv = C.binary("+", uv, eps)
-    q = C.binary("*" if mult else "/", SP.densify(W), uv)
+    q = C.binary("*", SP.densify(W), uv) if mult else _sparse_safe(W, C.binary("/", 1.0, uv))
     return C.mm(U, q, True) if left else C.mm(q, V)
 
 
@@ -184,15 +243,15 @@ def wcemm(X, U, V, eps=None):
     C = _C()
     if SP.is_sparse(X) and _plain(U) and _plain(V):
         _check(U, V, X.shape[0], X.shape[1])
-        r, c, xv = _coo_idx(X)
-        uv = sddmm(r, c, U, V)
+        dt = _cdt(X, U, V)
+        _, _, xv, uv = _sd(X, U, V, dt)
         if eps is not None:
             uv = uv + eps
-        return float((xv.float() * torch.log(uv)).sum().item())
+        return float((xv * torch.log(uv)).sum().item())
     uv = _uvt(U, V)
     if eps is not None:
         uv = C.binary("+", uv, eps)
-    return C.tak(SP.densify(X), C.unary("log", uv))
+    return C.agg("sum", "all", _sparse_safe(X, C.unary("log", uv)))
 
 
 # -------------------------------------------------------------------------------- wumm
@@ -201,16 +260,22 @@ def wumm(X, U, V, uop, op="*"):
     C = _C()
     if SP.is_sparse(X) and op == "*" and _plain(U) and _plain(V):
         _check(U, V, X.shape[0], X.shape[1])
-        r, c, xv = _coo_idx(X)
-        f = C.unary(uop, sddmm(r, c, U, V)) if uop != "^2" else sddmm(r, c, U, V) ** 2
-        return _sparse_like(X, xv.float() * f)
+        dt = _cdt(X, U, V)
+        _, _, xv, uv = _sd(X, U, V, dt)
+        f = C.unary(uop, uv) if uop != "^2" else uv * uv
+        return _sparse_like(X, xv * f)
     uv = _uvt(U, V)
     f = C.binary("^", uv, 2.0) if uop == "^2" else C.unary(uop, uv)
+    if op == "*":
+        return _sparse_safe(X, f)
     return C.binary(op, SP.densify(X), f)
 
 
 def execute(p, a):
     """Dispatch of a `wquat` hop (compiler/rewrites.py#_match_wquat)."""
+    C = _C()
+    if any(C.is_dist(x) for x in a):
+        return C._dist().wquat(p, a)
     k = p["kind"]
     eps = a[3] if p.get("eps") else None
     if k == "wsloss":

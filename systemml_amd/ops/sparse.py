@@ -91,6 +91,28 @@ def rand_csr(rows, cols, sparsity, lo, hi, pdf, gen, dtype, device, chunk_cells=
     return torch.sparse_csr_tensor(crow_t, col_t, val_t, (rows, cols), device=device)
 
 
+def csr_rows(x, r0, r1):
+    """Rows [r0, r1) of a CSR matrix, still CSR (no densification)."""
+    crow = x.crow_indices()
+    a, b = int(crow[r0].item()), int(crow[r1].item())
+    return torch.sparse_csr_tensor((crow[r0:r1 + 1] - a).contiguous(), x.col_indices()[a:b].contiguous(),
+                                   x.values()[a:b].contiguous(), (r1 - r0, x.shape[1]), device=x.device)
+
+
+def csr_vstack(parts):
+    """rbind of CSR matrices with equal column counts, still CSR."""
+    crows, cols, vals, base, rows = [], [], [], 0, 0
+    for i, p in enumerate(parts):
+        cr = p.crow_indices()
+        crows.append(cr[(0 if i == 0 else 1):] + base)
+        cols.append(p.col_indices())
+        vals.append(p.values())
+        base += int(cr[-1].item())
+        rows += p.shape[0]
+    return torch.sparse_csr_tensor(torch.cat(crows), torch.cat(cols), torch.cat(vals), (rows, parts[0].shape[1]),
+                                   device=parts[0].device)
+
+
 # ----------------------------------------------------------------------------
 # sparse-aware operators (dense operands pass through untouched)
 # ----------------------------------------------------------------------------

@@ -50,7 +50,8 @@ def _mat(x, what="argument"):
     if isinstance(x, Tensor):
         return C.cvt(x)
     if C.is_dist(x):
-        return C._dist().gather(x)
+        import sys
+        return C._dist()._fallback(x, "builtin:" + sys._getframe(1).f_code.co_name)
     if isinstance(x, FrameBlock):
         return place(x.to_matrix())
     if isinstance(x, (int, float, bool)):
@@ -187,6 +188,16 @@ def _fmt_dec(v, d):
 # ============================================================================
 # data generation (reference: LibMatrixDatagen.java, DataGenCPInstruction.java)
 # ============================================================================
+def _seed(ctx, seed):
+    """Resolve `seed = -1` (draw a fresh one).  In an SPMD run every rank must draw the same
+    value for a replicated result, and a fixed `sysml.random.seed` makes runs repeatable:
+    both come from the execution context's SeedSource (runtime/program.py)."""
+    seed = _int(seed) if seed is not None else -1
+    if seed != -1 or ctx is None or getattr(ctx, "seeds", None) is None:
+        return seed
+    return ctx.seeds.next()
+
+
 def _gen(seed):
     seed = _int(seed) if seed is not None else -1
     g = torch.Generator(device="cpu")
@@ -218,24 +229,58 @@ def b_rand(ctx, rows=None, cols=None, min=0.0, max=1.0, sparsity=1.0, pdf="unifo
     lo, hi = _float(min), _float(max)
     sp = _float(sparsity)
     pdf = str(pdf).lower()
+    seed = _seed(ctx, seed)
     if ctx is not None and ctx.dist is not None and r >= ctx.config.dist_min_rows:
-        return C._dist().rand(ctx, r, c, lo, hi, sp, pdf, _int(seed), _float(lam))
-    return _rand_local(r, c, lo, hi, sp, pdf, _int(seed), _float(lam))
+        return C._dist().rand(ctx, r, c, lo, hi, sp, pdf, seed, _float(lam))
+    return _rand_local(r, c, lo, hi, sp, pdf, seed, _float(lam))
 
 
-def _rand_local(r, c, lo, hi, sp, pdf, seed, lam, device=None, row_offset=0):
+RAND_CHUNK_CELLS = 1 << 22
+
+
+def rand_chunk_rows(c):
+    """Rows per generator chunk: a seeded rand is produced in chunks of whole rows, chunk k
+    from its own seed, so any row range of it can be generated alone and a row-partitioned
+    rand equals the single-process one (reference: LibMatrixDatagen seeds per block)."""
+    return max(1, RAND_CHUNK_CELLS // max(c, 1))
+
+
+def _chunk_seed(seed, k):
+    return seed if k == 0 else (seed + k * 1000003) % (1 << 62)
+
+
+def _rand_local(r, c, lo, hi, sp, pdf, seed, lam, device=None, row_offset=0, total_rows=None):
+    """Rows [row_offset, row_offset + r) of a (total_rows x c) rand matrix."""
     device = device or _dev()
     dt = _dt()
-    g = torch.Generator(device=device)
-    if seed == -1:
-        g.seed()
-    else:
-        g.manual_seed(seed + row_offset * 1000003)
+    total = r + row_offset if total_rows is None else total_rows
     if r == 0 or c == 0:
         return torch.zeros((r, c), dtype=dt, device=device)
+    if seed == -1:
+        seed = int(torch.randint(0, 1 << 62, (1,)).item())
+    ch = rand_chunk_rows(c)
+    k0, k1 = row_offset // ch, (row_offset + r - 1) // ch
     from ..ops import sparse as SP
-    if sp < SP.SPARSITY_TURN_POINT and r * c >= SP.MIN_CELLS and pdf in ("uniform", "normal") \
-            and not (pdf == "uniform" and lo == hi == 0):
+    sparse = sp < SP.SPARSITY_TURN_POINT and total * c >= SP.MIN_CELLS and pdf in ("uniform", "normal") \
+        and not (pdf == "uniform" and lo == hi == 0)
+    parts = []
+    for k in range(k0, k1 + 1):
+        a, b = k * ch, min(total, (k + 1) * ch)
+        g = torch.Generator(device=device)
+        g.manual_seed(_chunk_seed(seed, k))
+        blk = _rand_block(b - a, c, lo, hi, sp, pdf, lam, g, dt, device, sparse)
+        lo_r, hi_r = max(a, row_offset) - a, min(b, row_offset + r) - a
+        if lo_r != 0 or hi_r != b - a:
+            blk = SP.csr_rows(blk, lo_r, hi_r) if sparse else blk[lo_r:hi_r]
+        parts.append(blk)
+    if len(parts) == 1:
+        return parts[0] if sparse or parts[0].is_contiguous() else parts[0].contiguous()
+    return SP.csr_vstack(parts) if sparse else torch.cat(parts, 0)
+
+
+def _rand_block(r, c, lo, hi, sp, pdf, lam, g, dt, device, sparse):
+    from ..ops import sparse as SP
+    if sparse:
         # sparse rand: CSR generated directly (reference: sparse MatrixBlocks below the turn point)
         return SP.rand_csr(r, c, sp, lo, hi, pdf, g, dt, device)
     if pdf == "uniform":
@@ -329,7 +374,7 @@ def b_sample(ctx, range_=None, size=None, replace=False, seed=-1, **kw):
     if isinstance(replace, (int, float)) and not isinstance(replace, bool) and seed == -1:
         seed = replace
         rep = False
-    g = _gen(seed)
+    g = _gen(_seed(ctx, seed))
     if rep:
         v = torch.randint(1, rng + 1, (n,), generator=g, dtype=torch.int64)
     else:
@@ -434,6 +479,9 @@ def b_order(ctx, target=None, by=1, decreasing=False, **kw):
 
 @builtin("removeEmpty")
 def b_removeEmpty(ctx, target=None, margin="rows", select=None, **kw):
+    if C.is_dist(target) and margin == "rows" and (select is None or C.is_dist(select)
+                                                   or isinstance(select, Tensor)):
+        return C._dist().remove_empty_rows(target, select)
     m = _mat(target)
     empty_return = _bool(kw.get("empty.return", True))
     if margin == "rows":

@@ -117,6 +117,7 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
     def worker():
         wctx = ExecutionContext(ctx.program, ctx.config, stats=ctx.stats, out=ctx._out, dist=None)
         wctx.vars = dict(ctx.vars)
+        wctx.seeds = ctx.seeds
         while True:
             with lock:
                 if not queue:

@@ -31,6 +31,9 @@ class ExecutionContext:
         self.frame_stack = []        # callers' variable frames (buffer-pool eviction candidates)
         self.debugger = None         # utils/debugger.Debugger when run with -debug
         self.pool = None
+        self.seeds = SeedSource(config, dist)
+        if dist is not None and config is not None:
+            dist.min_rows = config.dist_min_rows
         if config is not None and getattr(config, "bufferpool", False) and torch.cuda.is_available():
             from .bufferpool import BufferPool
             self.pool = BufferPool(config)
@@ -46,6 +49,31 @@ class ExecutionContext:
         else:
             sys.stdout.write(s + "\n")
             sys.stdout.flush()
+
+
+class SeedSource:
+    """Seeds for rand/sample calls without an explicit seed.  With `sysml.random.seed` set
+    (config.seed >= 0) they are a deterministic sequence; in an SPMD run rank 0's random
+    base seed is broadcast so every rank draws the same replicated values (ranks execute
+    the same program, so their call sequences agree)."""
+
+    def __init__(self, config, dist=None):
+        import threading
+        self.lock = threading.Lock()
+        self.count = 0
+        base = getattr(config, "seed", -1) if config is not None else -1
+        if (base is None or base < 0) and dist is not None:
+            import random
+            v = float(random.getrandbits(40)) if dist.rank == 0 else 0.0
+            base = int(dist.allreduce_scalar(v, "sum"))
+        self.base = base if base is not None and base >= 0 else None
+
+    def next(self):
+        if self.base is None:
+            return -1
+        with self.lock:
+            self.count += 1
+            return (self.base * 7919 + self.count * 104729) % (1 << 62)
 
 
 # ----------------------------------------------------------------------------

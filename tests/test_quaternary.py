@@ -67,7 +67,7 @@ def test_wquat_rewrite_and_numerics(case, sp):
     res = run(src, inputs={}, outputs=["r", "X", "W", "U", "V"], config=CFG, out=lambda s: None)
     X, W, U, V = (_np(res[k]) for k in "XWUV")
     expect = ref(X, W, U, V)
-    np.testing.assert_allclose(_np(res["r"]), expect, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(_np(res["r"]), expect, rtol=1e-9, atol=1e-9)
 
 
 def test_wquat_disabled_without_fusion():
@@ -98,6 +98,112 @@ def test_sparse_paths_match_dense_direct():
     np.testing.assert_allclose(Q.wdivmm(Ws, U, V, False, True), (Wd * uv) @ V, rtol=1e-4)
     assert Q.wcemm(Xs, U, V) == pytest.approx(float((Xd * torch.log(uv)).sum()), rel=1e-5)
     np.testing.assert_allclose(Q.wumm(Xs, U, V, "exp").to_dense(), Xd * torch.exp(uv), rtol=1e-5)
+
+
+def _near_converged(dtype=torch.float64, m=300, n=200, r=6, seed=0):
+    """Large-magnitude sparse X that U V' reproduces up to a tiny residual: the regime in which
+    sum(X^2) - 2 sum(X .* UV') + sum(UV'^2) cancels catastrophically."""
+    g = torch.Generator().manual_seed(seed)
+    U = (torch.rand(m, r, generator=g, dtype=torch.float64) + 0.5) * 100
+    V = (torch.rand(n, r, generator=g, dtype=torch.float64) + 0.5) * 100
+    mask = torch.rand(m, n, generator=g, dtype=torch.float64) < 0.05
+    Xd = torch.where(mask, U @ V.T + 1e-3 * torch.randn(m, n, generator=g, dtype=torch.float64),
+                     torch.zeros((), dtype=torch.float64))
+    return Xd.to(dtype), U.to(dtype), V.to(dtype), mask
+
+
+def test_wsloss_fp64_no_cancellation():
+    """(advisor finding) the fused sparse paths compute in the engine precision (fp64) with
+    the residual summed directly: near convergence on a large-magnitude X they agree with the
+    fp64 unfused expression to ~1e-9 relative."""
+    Xd, U, V, mask = _near_converged()
+    Xs = Xd.to_sparse_csr()
+    W = mask.double()
+    Ws = W.to_sparse_csr()
+    uv = U @ V.T
+    exact = {
+        "post_nz": float(((Xd - uv) ** 2 * mask).sum()),
+        "post": float((W * (Xd - uv) ** 2).sum()),
+        "none": float(((Xd - uv) ** 2).sum()),
+        "pre": float(((Xd - W * uv) ** 2).sum()),
+    }
+    assert exact["post_nz"] < 1e-3 * float((Xd ** 2).sum()) * 1e-9      # residual is tiny
+    got = {
+        "post_nz": Q.wsloss("post_nz", Xs, U, V),
+        "post": Q.wsloss("post", Xs, U, V, Ws),           # sparse X gathered at W's pattern
+        "none": Q.wsloss("none", Xs, U, V),
+        "pre": Q.wsloss("pre", Xd, U, V, Ws),
+    }
+    for k in exact:
+        assert got[k] == pytest.approx(exact[k], rel=1e-9), (k, got[k], exact[k])
+    # sparse X with a pattern different from W: looked up, not densified
+    W2 = (torch.rand(Xd.shape, generator=torch.Generator().manual_seed(9), dtype=torch.float64) < 0.05).double()
+    e2 = float((W2 * (Xd - uv) ** 2).sum())
+    assert Q.wsloss("post", Xs, U, V, W2.to_sparse_csr()) == pytest.approx(e2, rel=1e-9)
+
+
+def test_wquat_sparse_safe_semantics():
+    """(advisor finding) zeros of X / W contribute 0 even where f(U V') overflows: dense and
+    sparse representations give the same result (reference: the operators iterate over the
+    non-zeros)."""
+    g = torch.Generator().manual_seed(2)
+    m, n, r = 40, 30, 3
+    U = torch.rand(m, r, generator=g, dtype=torch.float64) * 400     # exp(U V') overflows to inf
+    V = torch.rand(n, r, generator=g, dtype=torch.float64) * 400
+    Xd = (torch.rand(m, n, generator=g, dtype=torch.float64) < 0.2).double() * 1e-300
+    dense = Q.wumm(Xd, U, V, "exp")
+    sparse = Q.wumm(Xd.to_sparse_csr(), U, V, "exp").to_dense()
+    assert not torch.isnan(dense).any() and torch.equal(torch.isinf(dense), torch.isinf(sparse))
+    assert bool((dense[Xd == 0] == 0).all())
+    # log(sigmoid(-uv)) = -inf where uv is huge: zero weights stay 0
+    ws = Q.wsigmoid(Xd, U, V, True, True)
+    assert bool((ws[Xd == 0] == 0).all())
+
+
+def test_wquat_rewrite_guards():
+    """(advisor finding) like the reference: no rewrite when W is a broadcast vector (sizes
+    differ) or when U %*% t(V) has another consumer."""
+    src_vec = """
+U = rand(rows=300, cols=4, seed=1)
+V = rand(rows=250, cols=4, seed=2)
+w = rand(rows=300, cols=1, seed=3)
+r = w * exp(U %*% t(V))
+"""
+    cs = compile_script(src_vec, inputs={}, outputs=["r"], config=CFG)
+    assert "wquat" not in explain(cs.cp)
+    res = run(src_vec, inputs={}, outputs=["r", "U", "V"], config=CFG, out=lambda s: None)
+    assert res["r"].shape == (300, 250)
+    src_shared = GEN % ("0.05", "0.05") + """
+UV = U %*% t(V)
+r = sum(W * (X - UV)^2)
+s = sum(UV)
+"""
+    cs = compile_script(src_shared, inputs={}, outputs=["r", "s"], config=CFG)
+    assert "wquat" not in explain(cs.cp)
+
+
+@pytest.mark.gpu
+def test_sddmm_fp64_kernel_and_near_converged_wsloss_on_gpu():
+    """fp64 SDDMM kernel (grouped-lane variant) against the host fp64 expression."""
+    from systemml_amd.ops import kernels
+    dev = torch.device("cuda:0")
+    Xd, U, V, mask = _near_converged(m=2000, n=1500, r=8)
+    Xs = Xd.to_sparse_csr()
+    exact = float(((Xd - U @ V.T) ** 2 * mask).sum())
+    before = kernels.counters.get("sddmm", 0)
+    got = Q.wsloss("post_nz", Xs.to(dev), U.to(dev), V.to(dev))
+    assert kernels.counters.get("sddmm", 0) > before
+    assert got == pytest.approx(exact, rel=1e-9)
+    for r in (1, 5, 64, 100, 300):
+        g = torch.Generator().manual_seed(r)
+        S = (torch.rand(700, 500, generator=g) < 0.02).double().to_sparse_csr()
+        Uh = torch.randn(700, r, generator=g, dtype=torch.float64)
+        Vh = torch.randn(500, r, generator=g, dtype=torch.float64)
+        crow, col = S.crow_indices(), S.col_indices()
+        rows = torch.repeat_interleave(torch.arange(700), crow[1:] - crow[:-1])
+        ref = (Uh[rows] * Vh[col]).sum(1)
+        out = kernels.sddmm(crow.to(dev), col.to(dev), Uh.to(dev), Vh.to(dev), torch.float64)
+        np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=1e-12, atol=1e-12)
 
 
 @pytest.mark.gpu
