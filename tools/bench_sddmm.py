@@ -1,9 +1,13 @@
 """SDDMM (ops/hip/sddmm.hip) vs. the torch gather formulation on an ALS-shaped sampled product:
 m=n=1M, nnz=50M (0.005%), rank r in {16, 64}, fp32 and fp64.  Prints one JSON line per rank."""
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from systemml_amd.ops import kernels
 
