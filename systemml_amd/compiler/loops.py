@@ -168,3 +168,175 @@ def hoist_program(cp):
         if fb.body is not None:
             hoist_loop_invariants(fb.body, stats)
     return stats
+
+
+# ----------------------------------------------------------------------------
+# update-in-place (reference: hops/rewrite/RewriteMarkLoopVariablesUpdateInPlace.java)
+# ----------------------------------------------------------------------------
+_SHAPE = ("nrow", "ncol", "length")
+_FRESH = ("agg", "tak", "mm", "tsmm", "mmchain")
+
+
+def _dag(bb):
+    """All hops of a basic block and their consumers: id -> [(consumer hop | 'ENV:<name>', input index)]."""
+    tops = list(bb.roots) + list(bb.env_out.values())
+    hops = H.walk(tops)
+    cons = {}
+    for h in hops:
+        for i, c in enumerate(h.inputs):
+            cons.setdefault(c.id, []).append((h, i))
+    for name, h in bb.env_out.items():
+        cons.setdefault(h.id, []).append(("ENV:" + name, -1))
+    for r in bb.roots:
+        cons.setdefault(r.id, []).append(("ROOT", -1))
+    return hops, cons
+
+
+def _closure(hs):
+    out = {}
+    for h in H.walk(hs):
+        out[h.id] = h
+    return out
+
+
+def _bb_update_in_place_ok(bb, v):
+    """True when, in this block, matrix variable v is only (a) the target of a left-indexing
+    chain whose final result is v's new value, (b) an input of nrow/ncol/length, or (c) read
+    inside the index/value inputs of that chain and nowhere else -- so modifying v's buffer in
+    place can neither be observed through another reference nor race an unordered read."""
+    if v not in bb.reads and v not in bb.writes:
+        return True
+    hops, cons = _dag(bb)
+    final = bb.env_out.get(v)
+    chain = []
+    if final is not None and not (final.op == "tread" and final.p.get("name") == v):
+        h = final
+        while h.op == "lix":
+            chain.append(h)
+            h = h.inputs[0]
+        if not (h.op == "tread" and h.p.get("name") == v) or not chain:
+            return False
+    elif final is not None:
+        return True
+    chain_ids = {h.id for h in chain}
+    # hops allowed to consume (values derived from) v: inside the non-target inputs of the chain
+    inner = _closure([x for lx in chain for x in lx.inputs[1:]])
+    treads = [h for h in hops if h.op == "tread" and h.p.get("name") == v]
+    sources = treads + chain[:-1] if chain else treads
+    if not chain:
+        # v only read in this block: by operators that produce a fresh value (never a view
+        # or the same buffer), so no reference to v's buffer survives the block
+        for t in treads:
+            for c, i in cons.get(t.id, []):
+                if isinstance(c, str) or not (c.op in _FRESH or (c.op == "u" and c.p.get("o") in _SHAPE)):
+                    return False
+        return True
+    for s in sources:
+        for c, i in cons.get(s.id, []):
+            if isinstance(c, str):
+                return False                      # aliased into another variable / root
+            if c.id in chain_ids and i == 0:
+                continue                          # next left-indexing of the chain
+            if c.op == "u" and c.p.get("o") in _SHAPE:
+                continue
+            if c.id in inner:
+                continue
+            return False
+    # everything computed inside the chain's inputs must be consumed only there (no escaping views)
+    for hid, h in inner.items():
+        if h.op == "tread":
+            continue
+        for c, i in cons.get(hid, []):
+            if isinstance(c, str) or not (c.id in inner or c.id in chain_ids):
+                return False
+    for h in inner.values():
+        if h.op == "rix" and h.inputs[0].id in {s.id for s in sources}:
+            h.p["copy"] = True                    # a view of v must not alias the updated buffer
+    return True
+
+
+def _uip_ok(blocks, v):
+    """Predicates only produce scalars (evaluated before the blocks they guard), so reads
+    there are safe; nested loops that touch v must have marked it themselves."""
+    for b in blocks:
+        if isinstance(b, BasicBlock):
+            if not _bb_update_in_place_ok(b, v):
+                return False
+        elif isinstance(b, IfBlock):
+            if not (_uip_ok(b.then_blocks, v) and _uip_ok(b.else_blocks, v)):
+                return False
+        elif isinstance(b, (WhileBlock, ForBlock)):
+            if v in assigned_in(b.body):
+                if v not in getattr(b, "inplace_vars", ()):
+                    return False
+            elif not _uip_ok(b.body, v):
+                return False
+    return True
+
+
+def _reads_in(blocks, v):
+    for b in blocks:
+        if isinstance(b, BasicBlock):
+            if v in b.reads:
+                return True
+        elif isinstance(b, IfBlock):
+            if v in b.pred.reads or _reads_in(b.then_blocks, v) or _reads_in(b.else_blocks, v):
+                return True
+        elif isinstance(b, WhileBlock):
+            if v in b.pred.reads or _reads_in(b.body, v):
+                return True
+        elif isinstance(b, ForBlock):
+            preds = [b.start, b.end] + ([b.incr] if b.incr is not None else [])
+            if any(v in p.reads for p in preds) or _reads_in(b.body, v):
+                return True
+    return False
+
+
+def _lix_in(blocks, v, out):
+    for b in blocks:
+        if isinstance(b, BasicBlock):
+            h = b.env_out.get(v)
+            while h is not None and h.op == "lix":
+                out.append(h)
+                h = h.inputs[0]
+        elif isinstance(b, IfBlock):
+            _lix_in(b.then_blocks, v, out)
+            _lix_in(b.else_blocks, v, out)
+        elif isinstance(b, (WhileBlock, ForBlock)):
+            _lix_in(b.body, v, out)
+    return out
+
+
+def mark_update_in_place(blocks, stats=None):
+    """Mark loop variables that are only modified by left indexing (and otherwise only queried
+    for their shape) as update-in-place: the runtime then copies the matrix once on loop entry
+    and applies every `X[i, ] = ...` to that private buffer instead of cloning the whole matrix
+    per assignment (O(rows) instead of O(rows^2) bytes for a row-by-row loop).  parfor bodies
+    are excluded (workers share the pre-loop value)."""
+    stats = {} if stats is None else stats
+    for b in blocks:
+        if isinstance(b, IfBlock):
+            mark_update_in_place(b.then_blocks, stats)
+            mark_update_in_place(b.else_blocks, stats)
+        elif isinstance(b, (WhileBlock, ForBlock)):
+            mark_update_in_place(b.body, stats)           # inner loops first
+            b.inplace_vars = []
+            if isinstance(b, ForBlock) and b.parfor:
+                continue
+            cand = sorted(assigned_in(b.body) - ({b.var} if isinstance(b, ForBlock) else set()))
+            for v in cand:
+                lixes = _lix_in(b.body, v, [])
+                if lixes and all(h.dt == "M" for h in lixes) and _uip_ok(b.body, v):
+                    b.inplace_vars.append(v)
+                    for h in lixes:
+                        h.p["inplace"] = True
+                    stats["update-in-place"] = stats.get("update-in-place", 0) + 1
+    return stats
+
+
+def mark_program(cp):
+    stats = mark_update_in_place(cp.blocks)
+    for fb in cp.functions.values():
+        if fb.body is not None:
+            mark_update_in_place(fb.body, stats)
+    return stats

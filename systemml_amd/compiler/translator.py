@@ -145,6 +145,8 @@ class Translator:
             ipa.run(cp, self.config)                # inter-procedural analysis (inlining, ...)
             from .loops import hoist_program
             cp.licm_stats = hoist_program(cp)      # before liveness: adds blocks / variables
+            from .loops import mark_program
+            cp.licm_stats.update(mark_program(cp))
         # liveness
         for fb in self.functions.values():
             if fb.body is not None:

@@ -730,7 +730,10 @@ def _check_range(r0, r1, c0, c1, nr, nc):
                               f"must be within matrix dimensions [{nr},{nc}]")
 
 
-def lix(x, y, rl, ru, cl, cu, list_mode=False):
+def lix(x, y, rl, ru, cl, cu, list_mode=False, owned=None):
+    """X[rl:ru, cl:cu] = y.  `owned` (update-in-place loops, compiler/loops.py): a WeakSet of
+    buffers this loop execution already copied; those are modified in place, anything else is
+    copied once and registered."""
     from ..runtime.data import ListObject
     if isinstance(x, ListObject):
         i = _bound(rl, 1)
@@ -761,7 +764,13 @@ def lix(x, y, rl, ru, cl, cu, list_mode=False):
     r0, r1 = _bound(rl, 1), _bound(ru, nr)
     c0, c1 = _bound(cl, 1), _bound(cu, nc)
     _check_range(r0, r1, c0, c1, nr, nc)
-    out = cvt(x).clone()
+    if owned is not None and type(x) is Tensor and x.layout == torch.strided and x in owned \
+            and cvt(x) is x:
+        out = x
+    else:
+        out = cvt(x).clone()
+        if owned is not None and type(out) is Tensor:
+            owned.add(out)
     if isinstance(y, Tensor):
         y = cvt(y)
         if tuple(y.shape) != (r1 - r0 + 1, c1 - c0 + 1):

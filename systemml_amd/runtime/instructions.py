@@ -8,6 +8,8 @@ live, so the same instruction stream runs on every backend.
 """
 from __future__ import annotations
 
+import torch
+
 from .bufferpool import Evicted
 
 from ..parser.errors import DMLRuntimeError
@@ -164,9 +166,17 @@ def _make_impl(h):
         return (lambda ctx, a: C.transpose(a[0])), "r'"
     if op == "rix":
         lm = p.get("list", False)
+        if p.get("copy"):
+            # slice of an update-in-place variable: must not stay a view of its buffer
+            def rix_copy(ctx, a):
+                r = C.rix(a[0], a[1], a[2], a[3], a[4], lm)
+                return r.clone() if type(r) is torch.Tensor else r
+            return rix_copy, "rix"
         return (lambda ctx, a: C.rix(a[0], a[1], a[2], a[3], a[4], lm)), "rix"
     if op == "lix":
         lm = p.get("list", False)
+        if p.get("inplace"):
+            return (lambda ctx, a: C.lix(a[0], a[1], a[2], a[3], a[4], a[5], lm, owned=ctx.owned)), "lix-inplace"
         return (lambda ctx, a: C.lix(a[0], a[1], a[2], a[3], a[4], a[5], lm)), "lix"
     if op == "fout":
         i = p["i"]

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import sys
 import time
+import weakref
 
 import torch
 
@@ -32,6 +33,7 @@ class ExecutionContext:
         self.debugger = None         # utils/debugger.Debugger when run with -debug
         self.pool = None
         self.seeds = SeedSource(config, dist)
+        self.owned = OwnedBuffers()      # buffers owned by update-in-place loops (compiler/loops.py)
         if dist is not None and config is not None:
             dist.min_rows = config.dist_min_rows
         if config is not None and getattr(config, "bufferpool", False) and torch.cuda.is_available():
@@ -49,6 +51,27 @@ class ExecutionContext:
         else:
             sys.stdout.write(s + "\n")
             sys.stdout.flush()
+
+
+class OwnedBuffers:
+    """Identity set of tensors held weakly (a WeakSet would compare tensors with their
+    elementwise ==)."""
+
+    def __init__(self):
+        self._d = {}
+
+    def __contains__(self, t):
+        r = self._d.get(id(t))
+        return r is not None and r() is t
+
+    def add(self, t):
+        k = id(t)
+        d = self._d
+        d[k] = weakref.ref(t, lambda _r, k=k: d.pop(k, None) if d.get(k) is _r else None)
+
+    def discard(self, t):
+        if t in self:
+            del self._d[id(t)]
 
 
 class SeedSource:
@@ -192,6 +215,14 @@ def exec_block(ctx, b):
         else:
             exec_blocks(ctx, b.else_blocks)
         return
+    uip = getattr(b, "inplace_vars", None)
+    if uip:
+        # loop entry: buffers of update-in-place variables may be aliased by now (e.g. `Y = X`
+        # after a previous run of this loop), so the first left-indexing copies again
+        for v in uip:
+            x = ctx.vars.get(v)
+            if isinstance(x, torch.Tensor):
+                ctx.owned.discard(x)
     if isinstance(b, WhileBlock):
         while _to_bool(eval_pred(ctx, b.pred)):
             exec_blocks(ctx, b.body)

@@ -315,3 +315,54 @@ def test_buffer_pool_evicts_lru_and_restores(tmp_path):
     assert isinstance(main["B"], Evicted) and main["B"].path is not None
     assert torch.equal(pool.restore(main, "B", main["B"]), torch.ones(2, 2))
     assert pool.stats["evict_disk"] >= 1 and "Buffer pool" in pool.report()
+
+
+def test_update_in_place_loop_is_linear_time():
+    """A row-by-row left-indexing loop over a 1M x 10 matrix: marked update-in-place
+    (reference RewriteMarkLoopVariablesUpdateInPlace), so each iteration writes one row
+    instead of cloning the whole matrix -- time grows linearly with the row count."""
+    import time
+    from systemml_amd.api.executor import compile_script
+    def src(n, m):
+        return f"""
+X = matrix(0, rows={n}, cols=10)
+for (i in 1:{m}) {{
+  X[i, ] = matrix(i, rows=1, cols=10)
+}}
+s = sum(X)
+"""
+    cs = compile_script(src(1000000, 10), outputs=["s"], config=CFG)
+    assert cs.cp.licm_stats.get("update-in-place") == 1
+    times = {}
+    for m in (2000, 4000):
+        t = time.perf_counter()
+        res, _ = R(src(1000000, m), outputs=["s"])
+        times[m] = time.perf_counter() - t
+        assert res["s"] == 10 * m * (m + 1) / 2
+    # cloning 80 MB per iteration would make 4000 iterations take minutes
+    assert times[4000] < 2.5 * times[2000] + 1.0, times
+
+
+def test_update_in_place_preserves_value_semantics():
+    res, _ = R("""
+      X = matrix(0, rows=5, cols=3)
+      Y = X
+      for (i in 1:5) { X[i, ] = matrix(i, rows=1, cols=3) }
+      Z = X
+      for (i in 1:5) { X[i, 1] = -i }
+      for (i in 2:5) { X[i, 2] = as.scalar(X[i - 1, 2]) + 10 }
+      W = matrix(0, rows=4, cols=2)
+      for (i in 1:4) { r = W[1, ]; W[i, ] = r + i; W[1, 1] = 7 }
+    """, outputs=["X", "Y", "Z", "W", "r"])
+    Y, Z, X, W, r = (M(res, k) for k in ("Y", "Z", "X", "W", "r"))
+    assert (Y == 0).all()                                    # alias taken before the loop
+    np.testing.assert_array_equal(Z, np.repeat(np.arange(1, 6)[:, None], 3, 1))   # alias taken between loops
+    np.testing.assert_array_equal(X[:, 0], -np.arange(1, 6))
+    np.testing.assert_array_equal(X[:, 1], [1, 11, 21, 31, 41])
+    w = np.zeros((4, 2))
+    for i in range(1, 5):
+        rr = w[0].copy()
+        w[i - 1] = rr + i
+        w[0, 0] = 7
+    np.testing.assert_array_equal(W, w)
+    np.testing.assert_array_equal(r.ravel(), rr)
