@@ -94,38 +94,71 @@ def _eq(a, b):
         return False
 
 
+def _body_reads(blocks, out=None):
+    from ..compiler.blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
+    out = set() if out is None else out
+    for x in blocks:
+        if isinstance(x, BasicBlock):
+            out |= set(x.reads)
+        elif isinstance(x, IfBlock):
+            out |= x.pred.reads
+            _body_reads(x.then_blocks, out)
+            _body_reads(x.else_blocks, out)
+        elif isinstance(x, WhileBlock):
+            out |= x.pred.reads
+            _body_reads(x.body, out)
+        elif isinstance(x, ForBlock):
+            for p in (x.start, x.end, x.incr):
+                if p is not None:
+                    out |= p.reads
+            _body_reads(x.body, out)
+    return out
+
+
+def _run_iters(wctx, b, iters, idx, fork):
+    from .program import exec_blocks, SeedSource
+    for k, it in zip(idx, iters):
+        wctx.seeds = SeedSource.iteration_source(fork, k)
+        wctx.vars[b.var] = it
+        exec_blocks(wctx, b.body)
+
+
 def exec_parfor(ctx, b, start, end, incr, as_int):
-    from .program import exec_blocks, ExecutionContext
+    from .program import ExecutionContext
     iters = parfor_iterations(start, end, incr, as_int)
     if not iters:
         return
+    fork = ctx.seeds.fork()
     par = b.params.get("par")
     k = int(par) if isinstance(par, (int, float)) and par else ctx.config.parallelism
     k = max(1, min(k, len(iters)))
-    sequential = k == 1 or ctx.dist is not None or (torch.cuda.is_available() and _on_gpu())
     result_vars = list(b.result_vars)
     base = {v: ctx.vars.get(v) for v in result_vars}
-    if sequential:
-        for it in iters:
-            ctx.vars[b.var] = it
-            exec_blocks(ctx, b.body)
+    if ctx.dist is not None and ctx.dist.world > 1 and _spmd_ok(ctx, b):
+        exec_parfor_spmd(ctx, b, iters, fork, result_vars, base)
         return
-    tasks = partition_tasks(iters, k, b.params.get("taskpartitioner", "factoring"), b.params.get("tasksize"))
+    sequential = k == 1 or ctx.dist is not None or (torch.cuda.is_available() and _on_gpu())
+    if sequential:
+        saved = ctx.seeds
+        try:
+            _run_iters(ctx, b, iters, range(len(iters)), fork)
+        finally:
+            ctx.seeds = saved
+        return
+    tasks = partition_tasks(list(enumerate(iters)), k, b.params.get("taskpartitioner", "factoring"),
+                            b.params.get("tasksize"))
     lock = threading.Lock()
     queue = list(tasks)
 
     def worker():
         wctx = ExecutionContext(ctx.program, ctx.config, stats=ctx.stats, out=ctx._out, dist=None)
         wctx.vars = dict(ctx.vars)
-        wctx.seeds = ctx.seeds
         while True:
             with lock:
                 if not queue:
                     break
                 task = queue.pop(0)
-            for it in task:
-                wctx.vars[b.var] = it
-                exec_blocks(wctx, b.body)
+            _run_iters(wctx, b, [it for _, it in task], [i for i, _ in task], fork)
         return {v: wctx.vars.get(v) for v in result_vars}
 
     with ThreadPoolExecutor(max_workers=k) as ex:
@@ -134,6 +167,71 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
     for v in result_vars:
         ctx.vars[v] = _merge(base[v], [r[v] for r in results])
     ctx.vars[b.var] = iters[-1]
+
+
+# ----------------------------------------------------------------------------
+# SPMD ("remote") parfor across GPU ranks
+# ----------------------------------------------------------------------------
+def _spmd_ok(ctx, b):
+    """Iterations can run rank-locally when the body reads no row-partitioned matrix (a
+    body touching one would issue collectives a different number of times per rank).
+    mode=LOCAL keeps every rank executing every iteration."""
+    from ..ops import core as C
+    if str(b.params.get("mode", "")).upper() == "LOCAL":
+        return False
+    for v in _body_reads(b.body):
+        if C.is_dist(ctx.vars.get(v)):
+            return False
+    return True
+
+
+def exec_parfor_spmd(ctx, b, iters, fork, result_vars, base):
+    """Remote parfor over the ranks of an SPMD run (reference: RemoteParForSpark -- there
+    each task runs on a Spark executor; here each rank runs a contiguous range of iterations
+    on its own GPU with rank-local operators), then the result variables are merged like
+    ResultMergeLocalMemory with compare, across ranks: every rank all-reduces the cells its
+    iterations changed (values and a change mask), so each rank ends with the merged
+    matrix.  Scalars take the value of the last iteration that changed them."""
+    from .program import ExecutionContext
+    dist = ctx.dist
+    parts = dist.all_partitions(len(iters))
+    lo, hi = parts[dist.rank]
+    wctx = ExecutionContext(ctx.program, ctx.config, stats=ctx.stats,
+                            out=ctx._out if dist.rank == 0 else (lambda s: None), dist=None)
+    wctx.vars = dict(ctx.vars)
+    _run_iters(wctx, b, iters[lo:hi], range(lo, hi), fork)
+    from ..parallel import dist as D
+    D.stats["parfor_remote"] = D.stats.get("parfor_remote", 0) + 1
+    for v in result_vars:
+        ctx.vars[v] = _merge_spmd(dist, base[v], wctx.vars.get(v), lo < hi, hi)
+    ctx.vars[b.var] = iters[-1]
+
+
+def _merge_spmd(dist, base, mine, ran, last_idx):
+    import torch.distributed as tdist
+    if isinstance(base, torch.Tensor) and base.layout == torch.strided:
+        dev = dist.device if tdist.get_backend(dist.group) != "gloo" else torch.device("cpu")
+        b = base.to(dev)
+        if isinstance(mine, torch.Tensor) and mine is not base and ran:
+            if mine.shape != base.shape:
+                raise DMLRuntimeError("parfor result merge: dimension change of a result variable")
+            m = mine.to(device=dev, dtype=b.dtype)
+            changed = ~((m == b) | (torch.isnan(m) & torch.isnan(b)))
+        else:
+            m = b
+            changed = torch.zeros(b.shape, dtype=torch.bool, device=dev)
+        buf = torch.stack([torch.where(changed, m, torch.zeros((), dtype=b.dtype, device=dev)).double(),
+                           changed.double()])
+        dist.allreduce_(buf, "sum")
+        any_changed = buf[1] > 0
+        out = torch.where(any_changed, buf[0].to(b.dtype), b)
+        return out.to(base.device)
+    # scalars / other values: the rank that ran the highest-numbered iteration changing it wins
+    changed = ran and not _eq(mine, base)
+    objs = [None] * dist.world
+    tdist.all_gather_object(objs, (last_idx if changed else -1, mine if changed else None), group=dist.group)
+    best = max(objs, key=lambda o: o[0])
+    return base if best[0] < 0 else best[1]
 
 
 def _on_gpu():

@@ -98,6 +98,21 @@ class SeedSource:
             self.count += 1
             return (self.base * 7919 + self.count * 104729) % (1 << 62)
 
+    def fork(self):
+        """One draw of this stream for a parfor loop: every iteration derives its own stream
+        from it (iteration_source), so an iteration sees the same random numbers whichever
+        worker, thread or rank runs it, and this stream advances the same on every rank."""
+        return None if self.base is None else self.next()
+
+    @staticmethod
+    def iteration_source(fork, key):
+        import threading
+        c = SeedSource.__new__(SeedSource)
+        c.lock = threading.Lock()
+        c.count = 0
+        c.base = None if fork is None else (fork * 31 + int(key) * 1000003 + 17) % (1 << 62)
+        return c
+
 
 # ----------------------------------------------------------------------------
 def _to_bool(v):
@@ -239,13 +254,8 @@ def exec_block(ctx, b):
         as_int = all(isinstance(x, int) or (isinstance(x, float) and x.is_integer()) for x in (start, end, incr)) \
             and not any(isinstance(x, float) and not x.is_integer() for x in (start, incr))
         if b.parfor:
-            from .parfor import exec_parfor, parfor_iterations
-            if ctx.config.parallelism > 1:
-                exec_parfor(ctx, b, start, end, incr, as_int)
-                return
-            for it in parfor_iterations(start, end, incr, as_int):
-                ctx.vars[b.var] = it
-                exec_blocks(ctx, b.body)
+            from .parfor import exec_parfor
+            exec_parfor(ctx, b, start, end, incr, as_int)
             return
         i = start
         cnt = 0
