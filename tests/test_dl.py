@@ -86,3 +86,124 @@ def test_caffe2dml_load_converted_caffemodel(tmp_path):
     np.testing.assert_allclose(m.init_weights_["W_conv1"], w["conv1_weight"])
     m.load(str(d))
     assert set(m.init_weights_) == {"W_conv1", "b_conv1", "W_ip1", "b_ip1"}
+
+
+RESNET = """
+name: "res"
+layer { name: "data" type: "Data" top: "data" top: "label" }
+layer { name: "c1" type: "Convolution" bottom: "data" top: "c1" convolution_param { num_output: 4 kernel_size: 3 pad: 1 } }
+layer { name: "bn1" type: "BatchNorm" bottom: "c1" top: "c1" }
+layer { name: "sc1" type: "Scale" bottom: "c1" top: "c1" }
+layer { name: "r1" type: "ReLU" bottom: "c1" top: "c1" }
+layer { name: "c2" type: "Convolution" bottom: "c1" top: "c2" convolution_param { num_output: 4 kernel_size: 3 pad: 1 } }
+layer { name: "c3" type: "Convolution" bottom: "c1" top: "c3" convolution_param { num_output: 2 kernel_size: 1 } }
+layer { name: "sum" type: "Eltwise" bottom: "c1" bottom: "c2" top: "sum" eltwise_param { operation: SUM coeff: 1 coeff: 0.5 } }
+layer { name: "cat" type: "Concat" bottom: "sum" bottom: "c3" top: "cat" }
+layer { name: "pool" type: "Pooling" bottom: "cat" top: "pool" pooling_param { pool: AVE kernel_size: 2 stride: 2 } }
+layer { name: "ip" type: "InnerProduct" bottom: "pool" top: "ip" inner_product_param { num_output: 3 } }
+layer { name: "loss" type: "SoftmaxWithLoss" bottom: "ip" bottom: "label" top: "loss" }
+"""
+
+
+def _grad_script(layers, input_shape):
+    """Forward + loss + backward of a generated network on fixed inputs (no update)."""
+    from systemml_amd.models import dl
+    gen = dl._Gen(layers, input_shape)
+    lines = gen.sources() + ["Xb = X", "Yb = Y"] + gen.forward(train=True) + [f"loss = {gen.loss_expr()}"] + \
+        gen.backward()
+    grads = {t: gen.grad_of(t) for t in dl.trainable(gen.layers)}
+    return "\n".join(lines), grads, dl.state_vars(gen.layers)
+
+
+def test_dag_network_gradients_match_finite_differences():
+    """Residual add with coefficients, channel concat of two branches, one activation
+    consumed by three layers (gradient accumulation), BatchNorm + Scale: the generated
+    backward pass agrees with central differences of the generated forward pass."""
+    import os
+    from systemml_amd.api.executor import run
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.conf import DMLConfig
+    from systemml_amd.models import dl
+    layers = dl.caffe_layers(parse_prototxt(RESNET))
+    src, grads, state = _grad_script(layers, (1, 4, 4))
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((6, 16))
+    Y = np.eye(3)[rng.integers(0, 3, 6)]
+    init = dl._Gen(layers, (1, 4, 4)).init()
+    w = run("\n".join(dl._Gen(layers, (1, 4, 4)).sources() + init), outputs=state, config=DMLConfig(gpu=False),
+            out=lambda s: None, filename=os.path.join(SCRIPTS_DIR, "g.dml"))
+    w = {k: np.asarray(v.double().numpy() if hasattr(v, "numpy") else v) for k, v in w.items()}
+    cfg = DMLConfig(gpu=False)
+
+    def ev(ws, outs):
+        return run(src, inputs=dict(ws, X=X, Y=Y), outputs=outs, config=cfg, out=lambda s: None,
+                   filename=os.path.join(SCRIPTS_DIR, "g.dml"))
+    res = ev(w, ["loss"] + list(grads.values()))
+    checked = 0
+    for t, g in grads.items():
+        G = res[g].double().numpy().reshape(w[t].shape)
+        for idx in [(0, 0), tuple(np.array(w[t].shape) - 1)]:
+            wp = {k: v.copy() for k, v in w.items()}
+            wm = {k: v.copy() for k, v in w.items()}
+            h = 1e-5
+            wp[t][idx] += h
+            wm[t][idx] -= h
+            num = (ev(wp, ["loss"])["loss"] - ev(wm, ["loss"])["loss"]) / (2 * h)
+            assert abs(num - G[idx]) < 1e-6 + 1e-4 * abs(num), (t, idx, num, G[idx])
+            checked += 1
+    assert checked == 2 * len(grads) and {"g_sc1", "be_sc1", "W_c2", "W_c3", "W_ip"} <= set(grads)
+
+
+def test_caffe_residual_network_trains_all_algorithms(tmp_path):
+    X, y = _images(n=240, seed=4)
+    (tmp_path / "net.prototxt").write_text(RESNET)
+    (tmp_path / "solver.prototxt").write_text('net: "net.prototxt"\nbase_lr: 0.05\nmomentum: 0.9\nlr_policy: "fixed"\n'
+                                              'max_iter: 60\ntype: "SGD"\n')
+    for algo in ("minibatch", "allreduce_parallel_batches"):
+        m = Caffe2DML(solver=str(tmp_path / "solver.prototxt"), input_shape=(1, 8, 8))
+        m.set(batch_size=16, train_algo=algo, parallel_batches=3, test_algo="allreduce")
+        m.fit(X, y)
+        assert m.score(X, y) > 0.9, algo
+        assert {"em_bn1", "ev_bn1", "g_sc1", "be_sc1"} <= set(m.model_)
+        if algo != "minibatch":
+            assert "parfor (j in 1:ntask)" in m.train_script_
+        assert "parfor (i in 1:iters)" in m.predict_script_
+    with pytest.raises(ValueError):
+        m.set(train_algo="nonsense")
+
+
+def test_keras_functional_and_lstm():
+    X, y = _images(n=240, seed=5)
+    cfg = {"class_name": "Model", "config": {"layers": [
+        {"class_name": "InputLayer", "name": "in", "config": {"name": "in"}, "inbound_nodes": []},
+        {"class_name": "Conv2D", "name": "a", "config": {"name": "a", "filters": 3, "kernel_size": [3, 3],
+                                                          "padding": "same", "activation": "relu"},
+         "inbound_nodes": [[["in", 0, 0, {}]]]},
+        {"class_name": "Conv2D", "name": "b", "config": {"name": "b", "filters": 3, "kernel_size": [1, 1],
+                                                          "activation": "linear"},
+         "inbound_nodes": [[["in", 0, 0, {}]]]},
+        {"class_name": "Add", "name": "add", "config": {"name": "add"}, "inbound_nodes": [[["a", 0, 0, {}], ["b", 0, 0, {}]]]},
+        {"class_name": "Concatenate", "name": "cat", "config": {"name": "cat", "axis": -3},
+         "inbound_nodes": [[["add", 0, 0, {}], ["a", 0, 0, {}]]]},
+        {"class_name": "Flatten", "name": "f", "config": {"name": "f"}, "inbound_nodes": [[["cat", 0, 0, {}]]]},
+        {"class_name": "Dense", "name": "d", "config": {"name": "d", "units": 3, "activation": "softmax"},
+         "inbound_nodes": [[["f", 0, 0, {}]]]}]}}
+    m = Keras2DML(keras_model=json.dumps(cfg), input_shape=(1, 8, 8), batch_size=32, max_iter=120,
+                  optimizer="adam", lr=0.01, lr_policy="fixed", weight_decay=0.0)
+    m.fit(X, y)
+    assert m.score(X, y) > 0.9
+    # sequence classification with an LSTM: the class is which third of the sequence is bright
+    rng = np.random.default_rng(6)
+    n, T, D = 240, 6, 3
+    ys = rng.integers(0, 3, n)
+    S = rng.random((n, T, D)) * 0.2
+    for k in range(3):
+        S[ys == k, 2 * k:2 * k + 2, :] += 1.0
+    seq = {"class_name": "Sequential", "config": {"layers": [
+        {"class_name": "LSTM", "config": {"name": "lstm", "units": 8, "return_sequences": False}},
+        {"class_name": "Dense", "config": {"name": "out", "units": 3, "activation": "softmax"}}]}}
+    m2 = Keras2DML(keras_model=json.dumps(seq), input_shape=(T, D), batch_size=24, max_iter=150,
+                   optimizer="adam", lr=0.02, lr_policy="fixed", weight_decay=0.0)
+    m2.fit(S.reshape(n, -1), ys)
+    assert m2.score(S.reshape(n, -1), ys) > 0.9
+    assert "lstm::backward" in m2.train_script_
