@@ -62,6 +62,17 @@ def load(required=False):
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                       ctypes.c_void_p]
+    L.sysml_conv2d.restype = ctypes.c_int
+    L.sysml_conv2d.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 6 + [ctypes.c_int] * 13 + \
+        [ctypes.c_void_p]
+    L.sysml_pool2d.restype = ctypes.c_int
+    L.sysml_pool2d.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 10 + [ctypes.c_void_p]
+    L.sysml_bias_op.restype = ctypes.c_int
+    L.sysml_bias_op.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.sysml_relu_backward.restype = ctypes.c_int
+    L.sysml_relu_backward.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int64, ctypes.c_void_p]
     L.sysml_sddmm.restype = ctypes.c_int
     L.sysml_sddmm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
@@ -502,4 +513,120 @@ def sddmm(crow, col, U, V, dtype=None):
     if rc != 0:
         raise RuntimeError(f"sysml_sddmm failed: {rc}")
     _count("sddmm")
+    return out
+
+
+# ----------------------------------------------------------------------------
+# DNN (ops/hip/dnn.hip)
+# ----------------------------------------------------------------------------
+CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) instead of exact fp32 MFMA
+
+
+def _conv_code(dt):
+    if dt == torch.bfloat16:
+        return 0
+    if dt == torch.float32:
+        return 3 if CONV_BF16_FP32 else 1
+    if dt == torch.float64:
+        return 2
+    return None
+
+
+def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, relu=False):
+    """Implicit-GEMM convolution (mode 0 forward, 1 backward data, 2 backward filter).  X / W /
+    D are the DML 2-D matrices (NCHW rows); returns the DML 2-D result.  bf16 operands compute
+    on bf16 MFMA with an fp32 result; fp32 / fp64 on exact MFMA."""
+    L = load(required=True)
+    ref = X if X is not None else D
+    dt = ref.dtype
+    code = _conv_code(dt)
+    if code is None:
+        return None
+    odt = torch.float32 if dt == torch.bfloat16 else dt
+    dev = ref.device
+
+    def prep(t):
+        return None if t is None else t.to(device=dev, dtype=dt).contiguous()
+    X, W, D = prep(X), prep(W), prep(D)
+    Ho = (H + 2 * ph - KH) // sh + 1
+    Wo = (Wd + 2 * pw - KW) // sw + 1
+    if mode == 0:
+        shape = (N, F * Ho * Wo)
+    elif mode == 1:
+        shape = (N, C * H * Wd)
+    else:
+        shape = (F, C * KH * KW)
+    out = torch.empty(shape, dtype=odt, device=dev)
+    ws = None
+    ksplit = 1
+    if mode == 2:
+        tiles = ((F + 63) // 64) * ((C * KH * KW + 63) // 64)
+        K = N * Ho * Wo
+        ksplit = max(1, min(4096 // max(tiles, 1), K // 512))
+        if ksplit > 1:
+            ws = torch.empty((ksplit, F, C * KH * KW), dtype=odt, device=dev)
+    b = None if bias is None else bias.to(device=dev, dtype=odt).contiguous().reshape(-1)
+    rc = L.sysml_conv2d(code, mode, _ptr(X), _ptr(W), _ptr(D), _ptr(b), out.data_ptr(), _ptr(ws), ksplit,
+                        N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, int(bool(relu)), _stream())
+    if rc == -1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"sysml_conv2d failed: {rc}")
+    _count(("conv2d", "conv2d_bwd_data", "conv2d_bwd_filter")[mode])
+    return out
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def pool2d(backward, avg, X, D, N, C, H, W, KH, KW, sh, sw, ph, pw):
+    L = load(required=True)
+    dt = X.dtype if X.dtype in (torch.float32, torch.float64) else torch.float32
+    code = 1 if dt == torch.float32 else 2
+    X = X.to(dt).contiguous()
+    D = None if D is None else D.to(device=X.device, dtype=dt).contiguous()
+    Ho = (H + 2 * ph - KH) // sh + 1
+    Wo = (W + 2 * pw - KW) // sw + 1
+    out = torch.empty((N, C * (H * W if backward else Ho * Wo)), dtype=dt, device=X.device)
+    rc = L.sysml_pool2d(code, int(bool(backward)), int(bool(avg)), X.data_ptr(), _ptr(D), out.data_ptr(),
+                        N, C, H, W, KH, KW, sh, sw, ph, pw, _stream())
+    if rc == -1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"sysml_pool2d failed: {rc}")
+    _count("pool_bwd" if backward else "pool")
+    return out
+
+
+def bias_op(X, b, mult=False, relu=False):
+    L = load(required=True)
+    dt = X.dtype if X.dtype in (torch.float32, torch.float64) else torch.float32
+    X = X.to(dt).contiguous()
+    b = b.to(device=X.device, dtype=dt).contiguous().reshape(-1)
+    C = b.numel()
+    if X.shape[1] % C:
+        return None
+    out = torch.empty_like(X)
+    rc = L.sysml_bias_op(1 if dt == torch.float32 else 2, X.data_ptr(), b.data_ptr(), out.data_ptr(), X.numel(),
+                         C, X.shape[1] // C, int(bool(mult)), int(bool(relu)), _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_bias_op failed: {rc}")
+    _count("bias_mult" if mult else "bias_add")
+    return out
+
+
+def relu_backward(X, D):
+    L = load(required=True)
+    dt = torch.promote_types(X.dtype, D.dtype)
+    if dt not in (torch.float32, torch.float64):
+        dt = torch.float32
+    X = X.to(dt).contiguous()
+    D = D.to(device=X.device, dtype=dt).contiguous()
+    out = torch.empty_like(X)
+    rc = L.sysml_relu_backward(1 if dt == torch.float32 else 2, X.data_ptr(), D.data_ptr(), out.data_ptr(),
+                               X.numel(), _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_relu_backward failed: {rc}")
+    _count("relu_backward")
     return out

@@ -1025,18 +1025,14 @@ REGISTRY["avg_pool_backward"] = _pool_factory("avg", True)
 
 @builtin("bias_add")
 def b_bias_add(ctx, input, bias):
-    x = _mat(input)
-    b = _mat(bias).reshape(-1)
-    C_ = b.numel()
-    return (x.reshape(x.shape[0], C_, -1) + b.reshape(1, C_, 1)).reshape(x.shape[0], -1)
+    from ..ops import dnn
+    return dnn.bias_op(_mat(input), _mat(bias), mult=False)
 
 
 @builtin("bias_multiply")
 def b_bias_mult(ctx, input, bias):
-    x = _mat(input)
-    b = _mat(bias).reshape(-1)
-    C_ = b.numel()
-    return (x.reshape(x.shape[0], C_, -1) * b.reshape(1, C_, 1)).reshape(x.shape[0], -1)
+    from ..ops import dnn
+    return dnn.bias_op(_mat(input), _mat(bias), mult=True)
 
 
 # ============================================================================

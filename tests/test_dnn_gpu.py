@@ -1,0 +1,134 @@
+"""Hand-written CDNA4 DNN kernels (ops/hip/dnn.hip) against fp64 PyTorch references of the
+same operators: implicit-GEMM conv2d forward / backward-data / backward-filter (exact fp32 and
+fp64 MFMA, bf16 MFMA for bf16 operands), max / avg pooling and their backward passes, bias
+add / multiply and relu backward.  Reference tests: test/integration/functions/tensor/
+{Conv2DTest, Conv2DBackwardTest, Conv2DBackwardDataTest, PoolTest, PoolBackwardTest}."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # N, C, H, W, F, K, stride, pad
+    (3, 5, 11, 9, 7, 3, 1, 1),
+    (2, 3, 16, 16, 16, 5, 2, 2),
+    (4, 8, 7, 7, 6, 1, 1, 0),
+    (2, 2, 9, 13, 3, 3, 2, 0),
+    (1, 64, 14, 14, 96, 3, 1, 1),
+]
+
+
+def _ref_conv(X, W, N, C, H, Wd, F_, K, s, p):
+    x = X.double().cpu().reshape(N, C, H, Wd).requires_grad_(True)
+    w = W.double().cpu().reshape(F_, C, K, K).requires_grad_(True)
+    out = F.conv2d(x, w, stride=s, padding=p)
+    g = torch.randn(out.shape, dtype=torch.float64, generator=torch.Generator().manual_seed(7))
+    out.backward(g)
+    return out.reshape(N, -1).detach(), g.reshape(N, -1), x.grad.reshape(N, -1), w.grad.reshape(F_, -1)
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float64, 1e-12), (torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv2d_kernels(shape, dt, tol):
+    from systemml_amd.ops import kernels as Kn
+    N, C, H, Wd, F_, K, s, p = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    X = torch.randn(N, C * H * Wd, generator=g, dtype=torch.float64)
+    W = torch.randn(F_, C * K * K, generator=g, dtype=torch.float64)
+    if dt == torch.bfloat16:       # reference on the bf16-rounded operands
+        X, W = X.to(dt).double(), W.to(dt).double()
+    out, G, dX, dW = _ref_conv(X, W, N, C, H, Wd, F_, K, s, p)
+    if dt == torch.bfloat16:
+        G = G.to(dt).double()
+    dev = torch.device("cuda:0")
+    Xd, Wdv, Gd = X.to(dev, dt), W.to(dev, dt), G.to(dev, dt)
+    c0 = dict(Kn.counters)
+    got = Kn.conv2d(0, Xd, Wdv, None, N, C, H, Wd, F_, K, K, s, s, p, p)
+    gx = Kn.conv2d(1, None, Wdv, Gd, N, C, H, Wd, F_, K, K, s, s, p, p)
+    gw = Kn.conv2d(2, Xd, None, Gd, N, C, H, Wd, F_, K, K, s, s, p, p)
+    torch.cuda.synchronize()
+    for name, a, b in (("fwd", got, out), ("bwd_data", gx, dX), ("bwd_filter", gw, dW)):
+        a = a.double().cpu()
+        scale = b.abs().max().item() + 1e-30
+        err = (a - b).abs().max().item() / scale
+        assert err < tol, (name, err)
+    assert Kn.counters["conv2d"] > c0.get("conv2d", 0)
+    assert Kn.counters["conv2d_bwd_filter"] > c0.get("conv2d_bwd_filter", 0)
+
+
+def test_conv2d_bias_relu_epilogue():
+    from systemml_amd.ops import kernels as Kn
+    N, C, H, Wd, F_, K = 2, 3, 8, 8, 5, 3
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(N, C * H * Wd, generator=g)
+    W = torch.randn(F_, C * K * K, generator=g)
+    b = torch.randn(F_, 1, generator=g)
+    ref = torch.relu(F.conv2d(X.reshape(N, C, H, Wd), W.reshape(F_, C, K, K), padding=1) + b.reshape(1, -1, 1, 1))
+    dev = torch.device("cuda:0")
+    got = Kn.conv2d(0, X.to(dev), W.to(dev), None, N, C, H, Wd, F_, K, K, 1, 1, 1, 1, bias=b.to(dev), relu=True)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.reshape(N, -1).numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("cfg", [(2, 3, 8, 8, 2, 2, 0), (3, 4, 9, 7, 3, 2, 1), (1, 2, 6, 6, 3, 1, 1)])
+def test_pooling_kernels(cfg, dt):
+    from systemml_amd.ops import kernels as Kn
+    N, C, H, W, k, s, p = cfg
+    g = torch.Generator().manual_seed(k * 10 + s)
+    X = torch.randn(N, C * H * W, generator=g, dtype=torch.float64)
+    dev = torch.device("cuda:0")
+    for avg in (False, True):
+        x = X.reshape(N, C, H, W).clone().requires_grad_(True)
+        if avg:
+            o = F.avg_pool2d(x, k, s, p, count_include_pad=True)
+        else:
+            o = F.max_pool2d(F.pad(x, (p, p, p, p), value=-float("inf")), k, s)
+        G = torch.randn(o.shape, generator=g, dtype=torch.float64)
+        o.backward(G)
+        got = Kn.pool2d(False, avg, X.to(dev, dt), None, N, C, H, W, k, k, s, s, p, p)
+        gx = Kn.pool2d(True, avg, X.to(dev, dt), G.reshape(N, -1).to(dev, dt), N, C, H, W, k, k, s, s, p, p)
+        tol = 1e-12 if dt == torch.float64 else 1e-5
+        np.testing.assert_allclose(got.double().cpu().numpy(), o.detach().reshape(N, -1).numpy(), rtol=tol, atol=tol)
+        np.testing.assert_allclose(gx.double().cpu().numpy(), x.grad.reshape(N, -1).numpy(), rtol=tol, atol=tol)
+
+
+def test_bias_and_relu_backward_kernels():
+    from systemml_amd.ops import kernels as Kn
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(6, 4 * 10, generator=g, dtype=torch.float64)
+    b = torch.randn(4, 1, generator=g, dtype=torch.float64)
+    D = torch.randn(6, 40, generator=g, dtype=torch.float64)
+    dev = torch.device("cuda:0")
+    xr = X.reshape(6, 4, 10)
+    np.testing.assert_allclose(Kn.bias_op(X.to(dev), b.to(dev)).cpu().numpy(),
+                               (xr + b.reshape(1, 4, 1)).reshape(6, -1).numpy())
+    np.testing.assert_allclose(Kn.bias_op(X.to(dev), b.to(dev), mult=True).cpu().numpy(),
+                               (xr * b.reshape(1, 4, 1)).reshape(6, -1).numpy())
+    np.testing.assert_allclose(Kn.relu_backward(X.to(dev), D.to(dev)).cpu().numpy(), (D * (X > 0)).numpy())
+
+
+def test_lenet_builtins_use_hip_kernels_end_to_end():
+    """The nn library's conv / pool layers on the GPU backend run the dnn.hip kernels and
+    match the CPU backend."""
+    from systemml_amd.api.executor import run
+    from systemml_amd.conf import DMLConfig
+    from systemml_amd.ops import kernels as Kn
+    src = """
+o = conv2d(X, W, input_shape=[8,1,12,12], filter_shape=[4,1,3,3], stride=[1,1], padding=[1,1])
+o = bias_add(o, b)
+p = max_pool(o, input_shape=[8,4,12,12], pool_size=[2,2], stride=[2,2], padding=[0,0])
+dp = max_pool_backward(o, p, input_shape=[8,4,12,12], pool_size=[2,2], stride=[2,2], padding=[0,0])
+dw = conv2d_backward_filter(X, dp, input_shape=[8,1,12,12], filter_shape=[4,1,3,3], stride=[1,1], padding=[1,1])
+dx = conv2d_backward_data(W, dp, input_shape=[8,1,12,12], filter_shape=[4,1,3,3], stride=[1,1], padding=[1,1])
+s = sum(p) + sum(dw) + sum(dx)
+"""
+    rng = np.random.default_rng(1)
+    ins = {"X": rng.random((8, 144)), "W": rng.random((4, 9)) - 0.5, "b": rng.random((4, 1))}
+    c0 = dict(Kn.counters)
+    gpu = run(src, inputs=ins, outputs=["s", "dw", "dx"], config=DMLConfig(gpu=True, gpu_min_cells=0),
+              out=lambda s: None)
+    cpu = run(src, inputs=ins, outputs=["s", "dw", "dx"], config=DMLConfig(gpu=False), out=lambda s: None)
+    assert abs(float(gpu["s"]) - float(cpu["s"])) < 1e-9 * abs(float(cpu["s"]))
+    for k in ("conv2d", "conv2d_bwd_filter", "conv2d_bwd_data", "pool", "pool_bwd", "bias_add"):
+        assert Kn.counters.get(k, 0) > c0.get(k, 0), k
