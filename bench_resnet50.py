@@ -1,0 +1,136 @@
+"""ResNet-50 training throughput through the DML nn library (BASELINE.json config 5:
+"Keras2DML / scripts/nn ResNet-50 training bf16"), on synthetic data and random-init weights.
+
+The network is built as a Caffe2DML layer DAG (models/dl.py: Convolution + BatchNorm + Scale +
+ReLU bottlenecks with Eltwise residual sums, 3x3/2 max pool, 7x7 average pool, InnerProduct,
+SoftmaxWithLoss), the generated forward / backward / SGD-momentum DML runs on the MI355X
+backend: every conv2d / conv2d_backward_* / pooling / bias op is a hand-written kernel of
+ops/hip/dnn.hip; convolutions compute on bf16 MFMA with fp32 accumulation (activations and
+the other layers stay fp32).
+
+    python bench_resnet50.py [--batch 32] [--steps 3] [--warmup 1] [--image 224]
+Prints one JSON line (images/s over the timed steps).
+"""
+import argparse
+import json
+import os
+import re
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import numpy as np  # noqa: E402
+
+
+def resnet50_layers(classes=1000, stages=(3, 4, 6, 3), image=224):
+    """Layer DAG of ResNet-50 (torchvision layout: stride on the 3x3 conv of a bottleneck)."""
+    from systemml_amd.models.dl import Layer, INPUT
+    L = []
+
+    def conv(name, bottom, F, k, s, p):
+        L.append(Layer("conv", name, [bottom], [name], F=F, kh=k, kw=k, sh=s, sw=s, ph=p, pw=p))
+        return name
+
+    def bn_relu(name, bottom, relu=True):
+        L.append(Layer("batchnorm", "bn_" + name, [bottom], ["bn_" + name], affine=False, mu=0.9, eps=1e-5))
+        L.append(Layer("scale", "sc_" + name, ["bn_" + name], ["sc_" + name]))
+        top = "sc_" + name
+        if relu:
+            L.append(Layer("relu", "relu_" + name, [top], ["relu_" + name]))
+            top = "relu_" + name
+        return top
+
+    x = bn_relu("conv1", conv("conv1", INPUT, 64, 7, 2, 3))
+    L.append(Layer("pool", "pool1", [x], ["pool1"], mode="MAX", kh=3, kw=3, sh=2, sw=2, ph=1, pw=1))
+    x = "pool1"
+    width = 64
+    for si, nblk in enumerate(stages):
+        for b in range(nblk):
+            s = 2 if (b == 0 and si > 0) else 1
+            nm = f"s{si + 1}b{b + 1}"
+            y = bn_relu(nm + "a", conv(nm + "a", x, width, 1, 1, 0))
+            y = bn_relu(nm + "b", conv(nm + "b", y, width, 3, s, 1))
+            y = bn_relu(nm + "c", conv(nm + "c", y, width * 4, 1, 1, 0), relu=False)
+            sc = x
+            if b == 0:
+                sc = bn_relu(nm + "p", conv(nm + "p", x, width * 4, 1, s, 0), relu=False)
+            L.append(Layer("eltwise", nm + "sum", [y, sc], [nm + "sum"], op="SUM", coeff=[1.0, 1.0]))
+            L.append(Layer("relu", nm + "out", [nm + "sum"], [nm + "out"]))
+            x = nm + "out"
+        width *= 2
+    g = -(-image // 32)                       # final feature map side (7 at 224)
+    L.append(Layer("pool", "gap", [x], ["gap"], mode="AVE", kh=g, kw=g, sh=1, sw=1, ph=0, pw=0))
+    L.append(Layer("dense", "fc", ["gap"], ["fc"], M=classes))
+    L.append(Layer("softmax_loss", "loss", ["fc"], ["prob"]))
+    return L
+
+
+def build_script(layers, input_shape, steps, batch):
+    from systemml_amd.models import dl
+    gen = dl._Gen(layers, input_shape)
+    params = dl.trainable(gen.layers)
+    sc = dl._solver_consts({"type": "momentum", "base_lr": 0.01, "momentum": 0.9, "weight_decay": 1e-4})
+    lines = gen.sources("momentum") + ["X = read($X)", "Y = read($Y)", "N = nrow(X)", f"bs = {batch}",
+                                       "lr0 = 0.01", "lr = lr0", "it = 0"]
+    lines += gen.init()
+    lines += dl._opt_init("momentum", params)
+    lines += [f"for (i in 1:{steps}) {{", "  t0 = time()", "  beg = ((i - 1) * bs) %% N + 1",
+              "  end = min(N, beg + bs - 1)", "  Xb = X[beg:end, ]", "  Yb = Y[beg:end, ]"]
+    lines += ["  " + c for c in gen.forward(train=True)]
+    lines.append(f"  loss = {gen.loss_expr()}")
+    lines += ["  " + c for c in gen.backward()]
+    lines += [f"  {a} = {b}" for a, b in gen.bn_updates()]
+    lines += dl._opt_update(sc, gen, params, "  ")
+    lines += ['  print("STEP " + i + " loss " + loss + " ns " + (time() - t0))', "}"]
+    return "\n".join(lines)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--exact-fp32", action="store_true", help="convolutions on exact fp32 MFMA instead of bf16")
+    a = ap.parse_args()
+    import torch
+    from systemml_amd.api.executor import compile_script, execute
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.conf import DMLConfig
+    from systemml_amd.ops import kernels as K
+    K.CONV_BF16_FP32 = not a.exact_fp32
+    layers = resnet50_layers(image=a.image)
+    shape = (3, a.image, a.image)
+    total = a.steps + a.warmup
+    src = build_script(layers, shape, total, a.batch)
+    rng = np.random.default_rng(0)
+    n = a.batch * min(total, 2)
+    X = rng.standard_normal((n, 3 * a.image * a.image)).astype(np.float32)
+    Y = np.eye(1000, dtype=np.float32)[rng.integers(0, 1000, n)]
+    cfg = DMLConfig(precision="single", gpu_min_cells=0)
+    cs = compile_script(src, {"X": "X", "Y": "Y"}, inputs={"X": X, "Y": Y}, config=cfg,
+                        filename=os.path.join(SCRIPTS_DIR, "resnet50_bench.dml"))
+    out = []
+    t = time.perf_counter()
+    execute(cs, {"X": X, "Y": Y}, out=out.append)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    wall = time.perf_counter() - t
+    steps = [(int(m.group(1)), float(m.group(2)), int(m.group(3))) for m in
+             (re.match(r"STEP (\d+) loss (\S+) ns (\d+)", s) for s in out) if m]
+    timed = [ns for i, _, ns in steps if i > a.warmup]
+    ms = sum(timed) / len(timed) / 1e6
+    print(json.dumps({"metric": "ResNet-50 training images/s (scripts/nn via Caffe2DML layer DAG)",
+                      "value": round(a.batch / (ms / 1e3), 2), "unit": "images/s", "n_gpus": 1,
+                      "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2),
+                      "higher_is_better": True, "dtype": "fp32-exact" if a.exact_fp32 else "bf16 conv MFMA / fp32",
+                      "data": "synthetic N(0,1) images, random labels, random-init weights",
+                      "losses": [round(l, 4) for _, l, _ in steps], "wall_s": round(wall, 1),
+                      "kernel_counters": {k: v for k, v in K.counters.items() if k.startswith(("conv", "pool", "bias"))},
+                      "config": {"model": "ResNet-50", "batch": a.batch, "image": a.image, "classes": 1000}}))
+
+
+if __name__ == "__main__":
+    main()

@@ -662,7 +662,11 @@ class _BBuilder:
         if name == "ifelse" and all(h.op == "lit" for h in pos_args) and len(pos_args) == 3:
             return pos_args[1] if S.as_bool(pos_args[0].value) else pos_args[2]
         if name == "time":
-            return self.mk("bi", [], p={"name": "time"}, dt="S", pos=pos, cse=False)
+            # evaluated where its statement stands: a pure hop would be emitted lazily at its
+            # first use (e.g. after a later time() call)
+            h = self.mk("bi", [], p={"name": "time"}, dt="S", pos=pos, cse=False)
+            self.roots.append(h)
+            return h
         if name == "eval":
             # dynamic function call: resolve at runtime in this file context
             return self._eval_call(pos_args, named, pos)

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace sysml_dnn {
 
@@ -41,101 +42,13 @@ struct Conv {
   int tm, tn;        // tiles along M, Ncol
   int ksplit, kper;  // BWD_FILTER split-K (kper: K elements per split, multiple of BK)
   int relu;          // FWD epilogue: max(0, .)
+  int avec;          // FWD: filter rows 16-B aligned (vector loads of W)
 };
-
-template <typename T> __device__ __forceinline__ float tof(T v) { return (float)v; }
-template <> __device__ __forceinline__ float tof<__bf16>(__bf16 v) { return (float)v; }
 
 // bijective XCD-aware remap (dispatch is round-robin over the 8 XCDs)
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
-// ---- operand gathers ------------------------------------------------------------------
-// Column side ("B"): a thread owns GEMM column n and 8 consecutive k starting at k0.
-template <int MODE, typename TI, int KV>
-__device__ __forceinline__ void gather_b(const Conv& c, int n, int k0, float (&v)[KV]) {
-  const TI* __restrict__ X = (const TI*)c.X;
-  const TI* __restrict__ Dp = (const TI*)c.D;
-  const int KK = c.KH * c.KW;
-  if constexpr (MODE == FWD) {
-    // n -> (img, oh, ow);  k -> (ci, kh, kw)
-    const int P = c.Ho * c.Wo;
-    const bool nv = n < c.Ncol;
-    const int img = nv ? n / P : 0, p = n - img * P, oh = p / c.Wo, ow = p - oh * c.Wo;
-    int ci = k0 / KK, r = k0 - ci * KK, kh = r / c.KW, kw = r - kh * c.KW;
-    const int64_t ibase = (int64_t)img * c.C * c.H * c.Wd;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      const int ih = oh * c.sh - c.ph + kh, iw = ow * c.sw - c.pw + kw;
-      const bool ok = nv && (k0 + j) < c.K && ih >= 0 && ih < c.H && iw >= 0 && iw < c.Wd;
-      v[j] = ok ? tof<TI>(X[ibase + ((int64_t)ci * c.H + ih) * c.Wd + iw]) : 0.f;
-      if (++kw == c.KW) { kw = 0; if (++kh == c.KH) { kh = 0; ++ci; } }
-    }
-  } else if constexpr (MODE == BWD_DATA) {
-    // n -> (img, ih, iw);  k -> (f, kh, kw);  value dout[img, f, (ih+ph-kh)/sh, (iw+pw-kw)/sw]
-    const int HW = c.H * c.Wd, P = c.Ho * c.Wo;
-    const bool nv = n < c.Ncol;
-    const int img = nv ? n / HW : 0, q = n - img * HW, ih = q / c.Wd, iw = q - ih * c.Wd;
-    int f = k0 / KK, r = k0 - f * KK, kh = r / c.KW, kw = r - kh * c.KW;
-    const int64_t dbase = (int64_t)img * c.F * P;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      const int th = ih + c.ph - kh, tw = iw + c.pw - kw;
-      const int oh = th / c.sh, ow = tw / c.sw;
-      const bool ok = nv && (k0 + j) < c.K && th >= 0 && tw >= 0 && oh * c.sh == th && ow * c.sw == tw &&
-                      oh < c.Ho && ow < c.Wo;
-      v[j] = ok ? tof<TI>(Dp[dbase + (int64_t)f * P + oh * c.Wo + ow]) : 0.f;
-      if (++kw == c.KW) { kw = 0; if (++kh == c.KH) { kh = 0; ++f; } }
-    }
-  } else {
-    // BWD_FILTER: n -> (ci, kh, kw);  k -> (img, p): im2col value
-    const int P = c.Ho * c.Wo;
-    const bool nv = n < c.Ncol;
-    const int ci = nv ? n / KK : 0, r = n - ci * KK, kh = r / c.KW, kw = r - kh * c.KW;
-    int img = k0 / P, p = k0 - img * P, oh = p / c.Wo, ow = p - oh * c.Wo;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      const int ih = oh * c.sh - c.ph + kh, iw = ow * c.sw - c.pw + kw;
-      const bool ok = nv && (k0 + j) < c.K && ih >= 0 && ih < c.H && iw >= 0 && iw < c.Wd;
-      v[j] = ok ? tof<TI>(X[((int64_t)img * c.C + ci) * c.H * c.Wd + (int64_t)ih * c.Wd + iw]) : 0.f;
-      if (++ow == c.Wo) { ow = 0; if (++oh == c.Ho) { oh = 0; ++img; } }
-    }
-  }
-}
-
-// Row side ("A"): a thread owns GEMM row m and 8 consecutive k starting at k0.
-template <int MODE, typename TI, int KV>
-__device__ __forceinline__ void gather_a(const Conv& c, int m, int k0, float (&v)[KV]) {
-  const int KK = c.KH * c.KW;
-  const bool mv = m < c.M;
-  if constexpr (MODE == FWD) {
-    const TI* __restrict__ W = (const TI*)c.W;
-    const int64_t base = (int64_t)(mv ? m : 0) * c.K;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) v[j] = (mv && k0 + j < c.K) ? tof<TI>(W[base + k0 + j]) : 0.f;
-  } else if constexpr (MODE == BWD_DATA) {
-    // A(c, (f,kh,kw)) = W[f, c*KK + kh*KW + kw]
-    const TI* __restrict__ W = (const TI*)c.W;
-    int f = k0 / KK, r = k0 - f * KK;
-    const int64_t CKK = (int64_t)c.C * KK;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      v[j] = (mv && k0 + j < c.K) ? tof<TI>(W[f * CKK + (int64_t)m * KK + r]) : 0.f;
-      if (++r == KK) { r = 0; ++f; }
-    }
-  } else {
-    // A(f, (img,p)) = dout[img, f, p]
-    const TI* __restrict__ Dp = (const TI*)c.D;
-    const int P = c.Ho * c.Wo;
-    int img = k0 / P, p = k0 - img * P;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      v[j] = (mv && k0 + j < c.K) ? tof<TI>(Dp[((int64_t)img * c.F + m) * P + p]) : 0.f;
-      if (++p == P) { p = 0; ++img; }
-    }
-  }
 }
 
 // output index of GEMM element (m, n)
@@ -154,14 +67,67 @@ __device__ __forceinline__ int64_t out_index(const Conv& c, int m, int n) {
   }
 }
 
+// ---- implicit-GEMM convolution ----------------------------------------------------------
+// Per K-tile, BK threads decode the tile's k indices once into an LDS table (int4 per k):
+//   FWD        k = (ci, kh, kw):     x = ci*H*W + kh*W + kw, y = kh, z = kw,            w = k
+//   BWD_DATA   k = (f, kh, kw):      x = f*P,                y = kh, z = kw,            w = f*C*KK + kh*KW + kw
+//   BWD_FILTER k = (img, oh, ow):    x = img*CHW + hs*W + ws, y = hs = oh*sh-ph, z = ws, w = img*F*P + p
+// and every thread decodes its fixed GEMM column / row once per block, so gathering one
+// element is two adds, two unsigned compares and a masked load (no divisions in the loop).
+// Element (row side):    A[ra + w]                     (W for FWD / BWD_DATA, dout for BWD_FILTER)
+// Element (column side): FWD / BWD_FILTER: X[cb + x] if (ch + y, cw + z) inside the image
+//                        BWD_DATA: dout[cb + x + th*Wo + tw], th = ch - y, tw = cw - z on the stride grid
 constexpr int TM = 64, TN = 64, NT = 256;
 
-// ---- bf16 MFMA kernel (fp32 accumulate) ---------------------------------------------------
-template <int MODE, typename TI, typename TO>
-__global__ void __launch_bounds__(NT) conv_bf16_kernel(Conv c) {
-  constexpr int BK = 32, LDK = BK + 8;           // 80-B rows: conflict-free 16-B fragment reads
-  __shared__ __attribute__((aligned(16))) __bf16 As[TM][LDK];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[TN][LDK];
+template <int PATH> struct PathCfg;                       // 0: bf16 MFMA, 1: f32, 2: f64
+template <> struct PathCfg<0> { static constexpr int BK = 32; typedef f4 acc_t; };
+template <> struct PathCfg<1> { static constexpr int BK = 16; typedef f4 acc_t; };
+template <> struct PathCfg<2> { static constexpr int BK = 16; typedef d4 acc_t; };
+
+template <int MODE>
+__device__ __forceinline__ int4 decode_k(const Conv& c, int k) {
+  const int KK = c.KH * c.KW;
+  if (MODE == FWD) {
+    const int ci = k / KK, r = k - ci * KK, kh = r / c.KW, kw = r - kh * c.KW;
+    return int4{ci * c.H * c.Wd + kh * c.Wd + kw, kh, kw, k};
+  } else if (MODE == BWD_DATA) {
+    const int f = k / KK, r = k - f * KK, kh = r / c.KW, kw = r - kh * c.KW;
+    return int4{f * c.Ho * c.Wo, kh, kw, f * c.C * KK + r};
+  } else {
+    const int P = c.Ho * c.Wo;
+    const int img = k / P, p = k - img * P, oh = p / c.Wo, ow = p - oh * c.Wo;
+    const int hs = oh * c.sh - c.ph, ws = ow * c.sw - c.pw;
+    return int4{img * c.C * c.H * c.Wd + hs * c.Wd + ws, hs, ws, img * c.F * P + p};
+  }
+}
+
+template <int PATH, typename TI> struct Store;
+template <typename TI> struct Store<0, TI> {
+  template <int KV>
+  static __device__ __forceinline__ void put(__bf16* row, const TI (&v)[KV]) {
+    bf8 p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = (__bf16)v[j];
+    *(bf8*)row = p;
+  }
+};
+template <int PATH, typename TI> struct Store {
+  template <int KV, typename S>
+  static __device__ __forceinline__ void put(S* row, const TI (&v)[KV]) {
+#pragma unroll
+    for (int j = 0; j < KV; ++j) row[j] = (S)v[j];
+  }
+};
+
+template <int MODE, typename TI, int PATH, typename TO>
+__global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
+  typedef PathCfg<PATH> Cfg;
+  constexpr int BK = Cfg::BK, KV = BK / 4;
+  typedef typename std::conditional<PATH == 0, __bf16, typename std::conditional<PATH == 1, float, double>::type>::type S;
+  constexpr int LDK = PATH == 0 ? BK + 8 : BK + 1;       // bf16: 80-B rows; exact: odd stride
+  __shared__ __attribute__((aligned(16))) S As[TM][LDK];
+  __shared__ __attribute__((aligned(16))) S Bs[TN][LDK];
+  __shared__ int4 tab[2][BK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -171,46 +137,174 @@ __global__ void __launch_bounds__(NT) conv_bf16_kernel(Conv c) {
   const int m0 = bm * TM, n0 = bn * TN;
   const int kbeg = split * c.kper;
   const int kend = min(c.K, kbeg + c.kper);
-  // loader roles: A -> row tid/4, k (tid%4)*8;  B -> col tid/4, k (tid%4)*8
-  const int ar = tid >> 2, ak = (tid & 3) * 8;
-  f4 acc[2][2];
+  const TI* __restrict__ Ap = (const TI*)(MODE == BWD_FILTER ? c.D : c.W);
+  const TI* __restrict__ Bp = (const TI*)(MODE == BWD_DATA ? c.D : c.X);
+  // Load mappings (which thread fetches which tile elements), chosen so that the lanes of one
+  // load instruction touch consecutive addresses:
+  //   FWD / BWD_DATA  A: row tid/4, k (tid%4)*KV..+KV  (W rows are contiguous in k: 16-B loads)
+  //                   B: column tid%64, k (tid/64)*KV..  (lanes = consecutive output / input pixels)
+  //   BWD_FILTER      A, B: k = tid%BK (lanes = consecutive output pixels), RPT rows / columns each
+  constexpr bool KL = MODE == BWD_FILTER;
+  constexpr int RPT = KL ? (TM * BK) / NT : 1;          // rows per thread in the k-lane mapping
+  const int ar = KL ? (tid / BK) * RPT : tid >> 2;
+  const int ak = KL ? tid % BK : (tid & 3) * KV;
+  const int bc = KL ? (tid / BK) * RPT : tid & 63;
+  const int bk = KL ? tid % BK : (tid >> 6) * KV;
+  constexpr int NA = KL ? RPT : KV;                      // elements per thread per operand
+  // fixed per-thread row / column decode
+  int ra[KL ? RPT : 1];
+  bool mv[KL ? RPT : 1];
+#pragma unroll
+  for (int q = 0; q < (KL ? RPT : 1); ++q) {
+    const int m = m0 + ar + q;
+    mv[q] = m < c.M;
+    ra[q] = MODE == FWD ? m * c.K : (MODE == BWD_DATA ? m * c.KH * c.KW : m * c.Ho * c.Wo);
+  }
+  int cb[KL ? RPT : 1], ch[KL ? RPT : 1], cw[KL ? RPT : 1];
+#pragma unroll
+  for (int q = 0; q < (KL ? RPT : 1); ++q) {
+    const int n = n0 + bc + q;
+    cb[q] = 0; ch[q] = -(1 << 29); cw[q] = 0;
+    if (n < c.Ncol) {
+      if (MODE == FWD) {
+        const int P = c.Ho * c.Wo, img = n / P, p = n - img * P, oh = p / c.Wo, ow = p - oh * c.Wo;
+        ch[q] = oh * c.sh - c.ph;
+        cw[q] = ow * c.sw - c.pw;
+        cb[q] = img * c.C * c.H * c.Wd + ch[q] * c.Wd + cw[q];   // + x = image cell (ci, ch + kh, cw + kw)
+      } else if (MODE == BWD_DATA) {
+        const int HW = c.H * c.Wd, img = n / HW, qq = n - img * HW, ih = qq / c.Wd, iw = qq - ih * c.Wd;
+        ch[q] = ih + c.ph;
+        cw[q] = iw + c.pw;
+        cb[q] = img * c.F * c.Ho * c.Wo;
+      } else {
+        const int KK = c.KH * c.KW, ci = n / KK, r = n - ci * KK, kh = r / c.KW, kw = r - kh * c.KW;
+        ch[q] = kh;
+        cw[q] = kw;
+        cb[q] = ci * c.H * c.Wd + kh * c.Wd + kw;
+      }
+    }
+  }
+  const bool s1 = c.sh == 1 && c.sw == 1;
+  TI va[NA], vb[NA];
+  auto build = [&](int buf, int k0) {
+    if (tid < BK) {
+      const int k = k0 + tid;
+      tab[buf][tid] = k < kend ? decode_k<MODE>(c, k) : int4{0, -(1 << 29), -(1 << 29), -1};
+    }
+  };
+  auto bval = [&](const int4& e, int q) -> TI {
+    if (MODE != BWD_DATA) {
+      const int ih = ch[q] + e.y, iw = cw[q] + e.z;
+      return ((unsigned)ih < (unsigned)c.H && (unsigned)iw < (unsigned)c.Wd) ? Bp[cb[q] + e.x] : TI(0);
+    } else {
+      const int th = ch[q] - e.y, tw = cw[q] - e.z;
+      bool ok;
+      int oh, ow;
+      if (s1) {
+        oh = th; ow = tw;
+        ok = (unsigned)th < (unsigned)c.Ho && (unsigned)tw < (unsigned)c.Wo;
+      } else {
+        oh = th / c.sh; ow = tw / c.sw;
+        ok = th >= 0 && tw >= 0 && oh * c.sh == th && ow * c.sw == tw && oh < c.Ho && ow < c.Wo;
+      }
+      return ok ? Bp[cb[q] + e.x + oh * c.Wo + ow] : TI(0);
+    }
+  };
+  auto gather = [&](int buf, int k0) {
+    if constexpr (KL) {
+      const int4 e = tab[buf][ak];
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        va[q] = (mv[q] && e.w >= 0) ? Ap[ra[q] + e.w] : TI(0);
+        vb[q] = bval(e, q);
+      }
+    } else {
+      // A: FWD rows are contiguous in k -> one 16-B load when the KV-run is in range and aligned
+      bool vec = false;
+      if constexpr (MODE == FWD && sizeof(TI) * KV == 16) vec = c.avec && mv[0] && (k0 + ak + KV) <= kend;
+      if (vec) {
+        typedef TI vt __attribute__((ext_vector_type(KV)));
+        const vt x = *(const vt*)(Ap + ra[0] + k0 + ak);
+#pragma unroll
+        for (int j = 0; j < KV; ++j) va[j] = x[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < KV; ++j) {
+          const int4 e = tab[buf][ak + j];
+          va[j] = (mv[0] && e.w >= 0) ? Ap[ra[0] + e.w] : TI(0);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < KV; ++j) vb[j] = bval(tab[buf][bk + j], 0);
+    }
+  };
+  auto store = [&]() {
+    if constexpr (KL) {
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        As[ar + q][ak] = (S)va[q];
+        Bs[bc + q][bk] = (S)vb[q];
+      }
+    } else {
+      Store<PATH, TI>::template put<KV>(&As[ar][ak], va);
+      Store<PATH, TI>::template put<KV>(&Bs[bc][bk], vb);
+    }
+  };
+  typename Cfg::acc_t acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  float va[8], vb[8];
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0;
   if (kbeg < kend) {
-    gather_a<MODE, TI, 8>(c, m0 + ar, kbeg + ak, va);
-    gather_b<MODE, TI, 8>(c, n0 + ar, kbeg + ak, vb);
-  }
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    bf8 pa, pb;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      pa[j] = (__bf16)((k0 + ak + j) < kend ? va[j] : 0.f);
-      pb[j] = (__bf16)((k0 + ak + j) < kend ? vb[j] : 0.f);
-    }
-    __syncthreads();                             // previous tile's fragment reads done
-    *(bf8*)&As[ar][ak] = pa;
-    *(bf8*)&Bs[ar][ak] = pb;
+    build(0, kbeg);
     __syncthreads();
-    if (k0 + BK < kend) {                         // next tile's gathers overlap this tile's MFMAs
-      gather_a<MODE, TI, 8>(c, m0 + ar, k0 + BK + ak, va);
-      gather_b<MODE, TI, 8>(c, n0 + ar, k0 + BK + ak, vb);
-    }
-    const int kc = (lane >> 4) * 8;
-    bf8 fa[2], fb[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) fa[i] = *(const bf8*)&As[wr * 32 + i * 16 + (lane & 15)][kc];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) fb[j] = *(const bf8*)&Bs[wc * 32 + j * 16 + (lane & 15)][kc];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    gather(0, kbeg);
   }
-  // epilogue: 16x16 C/D map col = lane & 15, row = (lane >> 4) * 4 + reg
-  TO* out = (TO*)c.out + (MODE == BWD_FILTER ? (int64_t)split * c.M * c.Ncol : 0);
+  int buf = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += BK, buf ^= 1) {
+    __syncthreads();                                     // fragment reads of the previous tile done
+    store();
+    const bool more = k0 + BK < kend;
+    if (more) build(buf ^ 1, k0 + BK);
+    __syncthreads();
+    if (more) gather(buf ^ 1, k0 + BK);                  // next tile's loads overlap this tile's MFMAs
+    if constexpr (PATH == 0) {
+      const int kc = (lane >> 4) * 8;
+      bf8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = *(const bf8*)&As[wr * 32 + i * 16 + (lane & 15)][kc];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = *(const bf8*)&Bs[wc * 32 + j * 16 + (lane & 15)][kc];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK; ks += 4) {
+        const int k = ks + (lane >> 4);
+        S fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[i] = As[wr * 32 + i * 16 + (lane & 15)][k];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = Bs[wc * 32 + j * 16 + (lane & 15)][k];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if constexpr (PATH == 1) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            else acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          }
+      }
+    }
+  }
+  // epilogue.  C/D maps: f32 16x16: row = (lane >> 4) * 4 + reg;  f64 16x16: row = (lane >> 4) + 4 * reg
+  // split-K: partial sums are added atomically into the zero-initialised output (vector
+  // global atomics, fp32 / fp64); bias / relu then run as a separate pass (host)
+  const bool atomic = c.ksplit > 1;
+  TO* out = (TO*)c.out;
   const TO* bias = (const TO*)c.bias;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -218,193 +312,19 @@ __global__ void __launch_bounds__(NT) conv_bf16_kernel(Conv c) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
-        const int n = n0 + wc * 32 + j * 16 + (lane & 15);
-        if (m < c.M && n < c.Ncol) {
-          float v = acc[i][j][r];
-          if (MODE == FWD && bias) v += (float)bias[m];
-          if (MODE == FWD && c.relu) v = v > 0.f ? v : 0.f;
-          out[out_index<MODE>(c, m, n)] = (TO)v;
+        const int mo = m0 + wr * 32 + i * 16 + (PATH == 2 ? (lane >> 4) + 4 * r : (lane >> 4) * 4 + r);
+        const int no = n0 + wc * 32 + j * 16 + (lane & 15);
+        if (mo < c.M && no < c.Ncol) {
+          TO v = (TO)acc[i][j][r];
+          if (atomic) {
+            atomicAdd(out + out_index<MODE>(c, mo, no), v);
+            continue;
+          }
+          if (MODE == FWD && bias) v += bias[mo];
+          if (MODE == FWD && c.relu) v = v > TO(0) ? v : TO(0);
+          out[out_index<MODE>(c, mo, no)] = v;
         }
       }
-}
-
-// ---- exact fp32 / fp64 MFMA kernel --------------------------------------------------------
-template <typename T> struct Exact;
-template <> struct Exact<float> {
-  typedef f4 acc_t;
-  static __device__ __forceinline__ acc_t mfma(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) * 4 + r; }
-};
-template <> struct Exact<double> {
-  typedef d4 acc_t;
-  static __device__ __forceinline__ acc_t mfma(double a, double b, acc_t c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }
-};
-
-// exact path: gathers produce the storage type directly (no fp32 rounding for fp64)
-template <int MODE, typename T, int KV>
-__device__ __forceinline__ void gather_b_x(const Conv& c, int n, int k0, T (&v)[KV]) {
-  const T* __restrict__ X = (const T*)c.X;
-  const T* __restrict__ Dp = (const T*)c.D;
-  const int KK = c.KH * c.KW;
-  const bool nv = n < c.Ncol;
-  if constexpr (MODE == FWD) {
-    const int P = c.Ho * c.Wo;
-    const int img = nv ? n / P : 0, p = n - img * P, oh = p / c.Wo, ow = p - oh * c.Wo;
-    int ci = k0 / KK, r = k0 - ci * KK, kh = r / c.KW, kw = r - kh * c.KW;
-    const int64_t ibase = (int64_t)img * c.C * c.H * c.Wd;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      const int ih = oh * c.sh - c.ph + kh, iw = ow * c.sw - c.pw + kw;
-      const bool ok = nv && (k0 + j) < c.K && ih >= 0 && ih < c.H && iw >= 0 && iw < c.Wd;
-      v[j] = ok ? X[ibase + ((int64_t)ci * c.H + ih) * c.Wd + iw] : T(0);
-      if (++kw == c.KW) { kw = 0; if (++kh == c.KH) { kh = 0; ++ci; } }
-    }
-  } else if constexpr (MODE == BWD_DATA) {
-    const int HW = c.H * c.Wd, P = c.Ho * c.Wo;
-    const int img = nv ? n / HW : 0, q = n - img * HW, ih = q / c.Wd, iw = q - ih * c.Wd;
-    int f = k0 / KK, r = k0 - f * KK, kh = r / c.KW, kw = r - kh * c.KW;
-    const int64_t dbase = (int64_t)img * c.F * P;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      const int th = ih + c.ph - kh, tw = iw + c.pw - kw;
-      const int oh = th / c.sh, ow = tw / c.sw;
-      const bool ok = nv && (k0 + j) < c.K && th >= 0 && tw >= 0 && oh * c.sh == th && ow * c.sw == tw &&
-                      oh < c.Ho && ow < c.Wo;
-      v[j] = ok ? Dp[dbase + (int64_t)f * P + oh * c.Wo + ow] : T(0);
-      if (++kw == c.KW) { kw = 0; if (++kh == c.KH) { kh = 0; ++f; } }
-    }
-  } else {
-    const int P = c.Ho * c.Wo;
-    const int ci = nv ? n / KK : 0, r = n - ci * KK, kh = r / c.KW, kw = r - kh * c.KW;
-    int img = k0 / P, p = k0 - img * P, oh = p / c.Wo, ow = p - oh * c.Wo;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      const int ih = oh * c.sh - c.ph + kh, iw = ow * c.sw - c.pw + kw;
-      const bool ok = nv && (k0 + j) < c.K && ih >= 0 && ih < c.H && iw >= 0 && iw < c.Wd;
-      v[j] = ok ? X[((int64_t)img * c.C + ci) * c.H * c.Wd + (int64_t)ih * c.Wd + iw] : T(0);
-      if (++ow == c.Wo) { ow = 0; if (++oh == c.Ho) { oh = 0; ++img; } }
-    }
-  }
-}
-
-template <int MODE, typename T, int KV>
-__device__ __forceinline__ void gather_a_x(const Conv& c, int m, int k0, T (&v)[KV]) {
-  const int KK = c.KH * c.KW;
-  const bool mv = m < c.M;
-  if constexpr (MODE == FWD) {
-    const T* __restrict__ W = (const T*)c.W;
-    const int64_t base = (int64_t)(mv ? m : 0) * c.K;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) v[j] = (mv && k0 + j < c.K) ? W[base + k0 + j] : T(0);
-  } else if constexpr (MODE == BWD_DATA) {
-    const T* __restrict__ W = (const T*)c.W;
-    int f = k0 / KK, r = k0 - f * KK;
-    const int64_t CKK = (int64_t)c.C * KK;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      v[j] = (mv && k0 + j < c.K) ? W[f * CKK + (int64_t)m * KK + r] : T(0);
-      if (++r == KK) { r = 0; ++f; }
-    }
-  } else {
-    const T* __restrict__ Dp = (const T*)c.D;
-    const int P = c.Ho * c.Wo;
-    int img = k0 / P, p = k0 - img * P;
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      v[j] = (mv && k0 + j < c.K) ? Dp[((int64_t)img * c.F + m) * P + p] : T(0);
-      if (++p == P) { p = 0; ++img; }
-    }
-  }
-}
-
-template <int MODE, typename T>
-__global__ void __launch_bounds__(NT) conv_exact_kernel(Conv c) {
-  constexpr int BK = 16, LDK = BK + 1;           // odd row stride: conflict-free column reads
-  __shared__ T As[TM][LDK];
-  __shared__ T Bs[TN][LDK];
-  typedef Exact<T> E;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntile = c.tm * c.tn;
-  const int tile = wg % ntile, split = wg / ntile;
-  const int bm = tile % c.tm, bn = tile / c.tm;
-  const int m0 = bm * TM, n0 = bn * TN;
-  const int kbeg = split * c.kper;
-  const int kend = min(c.K, kbeg + c.kper);
-  const int ar = tid >> 2, ak = (tid & 3) * 4;   // 64 rows x 4 groups of 4 k
-  typename E::acc_t acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] = T(0);
-  T va[4], vb[4];
-  if (kbeg < kend) {
-    gather_a_x<MODE, T, 4>(c, m0 + ar, kbeg + ak, va);
-    gather_b_x<MODE, T, 4>(c, n0 + ar, kbeg + ak, vb);
-  }
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool in = (k0 + ak + j) < kend;
-      As[ar][ak + j] = in ? va[j] : T(0);
-      Bs[ar][ak + j] = in ? vb[j] : T(0);
-    }
-    __syncthreads();
-    if (k0 + BK < kend) {
-      gather_a_x<MODE, T, 4>(c, m0 + ar, k0 + BK + ak, va);
-      gather_b_x<MODE, T, 4>(c, n0 + ar, k0 + BK + ak, vb);
-    }
-#pragma unroll
-    for (int ks = 0; ks < BK; ks += 4) {
-      const int k = ks + (lane >> 4);
-      T fa[2], fb[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = As[wr * 32 + i * 16 + (lane & 15)][k];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = Bs[wc * 32 + j * 16 + (lane & 15)][k];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = E::mfma(fa[i], fb[j], acc[i][j]);
-    }
-  }
-  T* out = (T*)c.out + (MODE == BWD_FILTER ? (int64_t)split * c.M * c.Ncol : 0);
-  const T* bias = (const T*)c.bias;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * 32 + i * 16 + E::row(lane, r);
-        const int n = n0 + wc * 32 + j * 16 + (lane & 15);
-        if (m < c.M && n < c.Ncol) {
-          T v = acc[i][j][r];
-          if (MODE == FWD && bias) v += bias[m];
-          if (MODE == FWD && c.relu) v = v > T(0) ? v : T(0);
-          out[out_index<MODE>(c, m, n)] = v;
-        }
-      }
-}
-
-// split-K slabs -> output
-template <typename T>
-__global__ void __launch_bounds__(256) slab_sum(const T* __restrict__ s, int ks, int64_t n, T* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    T a = 0;
-    for (int k = 0; k < ks; ++k) a += s[(int64_t)k * n + i];
-    out[i] = a;
-  }
 }
 
 // ---- pooling ----------------------------------------------------------------------------
@@ -495,7 +415,7 @@ __global__ void __launch_bounds__(256) bias_op(const T* __restrict__ X, const T*
                                                 int64_t total, int C, int P, int mult, int relu) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int ch = (int)((i / P) % C);
-    T v = mult ? X[i] * b[ch] : X[i] + b[ch];
+    T v = b ? (mult ? X[i] * b[ch] : X[i] + b[ch]) : X[i];
     if (relu) v = v > T(0) ? v : T(0);
     O[i] = v;
   }
@@ -518,8 +438,8 @@ inline unsigned grid_for(int64_t n) {
 extern "C" {
 
 // dtype: 0 bf16 in (fp32 out), 1 fp32 exact, 2 fp64 exact, 3 fp32 in / bf16 MFMA / fp32 out.
-// mode: 0 forward, 1 backward data, 2 backward filter.  ws: fp32/fp64 workspace for the
-// backward-filter split-K slabs (ksplit * F * C*KH*KW elements), may be null when ksplit = 1.
+// mode: 0 forward, 1 backward data, 2 backward filter.  ksplit > 1 splits the GEMM depth over
+// blocks that accumulate atomically (ws unused).
 // Returns 0, -1 (unsupported) or a hipError_t.
 int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* D, const void* bias, void* out,
                  void* ws, int ksplit, int N, int C, int H, int Wd, int F, int KH, int KW, int sh, int sw, int ph,
@@ -531,31 +451,37 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   c.Ho = (H + 2 * ph - KH) / sh + 1;
   c.Wo = (Wd + 2 * pw - KW) / sw + 1;
   c.relu = relu;
+  {
+    const int es = dtype == 2 ? 8 : (dtype == 0 ? 2 : 4);
+    const int64_t rowb = (int64_t)C * KH * KW * es;
+    c.avec = (rowb % 16 == 0) && (reinterpret_cast<uintptr_t>(W) % 16 == 0);
+  }
   if (c.Ho <= 0 || c.Wo <= 0 || N <= 0) return -1;
   const int64_t P = (int64_t)c.Ho * c.Wo, KK = (int64_t)KH * KW;
   int64_t M, Nc, K;
   if (mode == FWD) { M = F; Nc = (int64_t)N * P; K = C * KK; }
   else if (mode == BWD_DATA) { M = C; Nc = (int64_t)N * H * Wd; K = F * KK; }
   else { M = F; Nc = C * KK; K = (int64_t)N * P; }
+  // 32-bit element offsets inside the kernels
   if (M >= (1LL << 31) || Nc >= (1LL << 31) || K >= (1LL << 31)) return -1;
+  if ((int64_t)N * C * H * Wd >= (1LL << 31) || (int64_t)N * F * P >= (1LL << 31) || (int64_t)F * C * KK >= (1LL << 31))
+    return -1;
   c.M = (int)M; c.Ncol = (int)Nc; c.K = (int)K;
   c.tm = (int)((M + TM - 1) / TM);
   c.tn = (int)((Nc + TN - 1) / TN);
   const bool bfmma = dtype == 0 || dtype == 3;
   const int BK = bfmma ? 32 : 16;
-  if (mode != BWD_FILTER) ksplit = 1;
   if (ksplit < 1) ksplit = 1;
   int64_t kper = (K + ksplit - 1) / ksplit;
   kper = (kper + BK - 1) / BK * BK;
   ksplit = (int)((K + kper - 1) / kper);
   c.ksplit = ksplit;
   c.kper = (int)kper;
-  void* final_out = out;
-  if (ksplit > 1) {
-    if (!ws) return -1;
-    c.out = ws;
-  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (ksplit > 1) {
+    const int64_t n = M * Nc;
+    if (hipMemsetAsync(out, 0, n * (dtype == 2 ? 8 : 4), s) != hipSuccess) return (int)hipGetLastError();
+  }
   const int64_t nwg = (int64_t)c.tm * c.tn * ksplit;
   if (nwg >= (1LL << 31)) return -1;
   dim3 g((unsigned)nwg), t(NT);
@@ -566,25 +492,25 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
     else hipLaunchKernelGGL((KERN<BWD_FILTER, __VA_ARGS__>), g, t, 0, s, c);                 \
   } while (0)
   if (dtype == 0) {
-    LAUNCH(conv_bf16_kernel, __bf16, float);
+    LAUNCH(conv_kernel, __bf16, 0, float);
   } else if (dtype == 3) {
-    LAUNCH(conv_bf16_kernel, float, float);
+    LAUNCH(conv_kernel, float, 0, float);
   } else if (dtype == 1) {
-    LAUNCH(conv_exact_kernel, float);
+    LAUNCH(conv_kernel, float, 1, float);
   } else if (dtype == 2) {
-    LAUNCH(conv_exact_kernel, double);
+    LAUNCH(conv_kernel, double, 2, double);
   } else {
     return -1;
   }
 #undef LAUNCH
-  if (ksplit > 1) {
+  if (ksplit > 1 && mode == FWD && (bias || relu)) {
     const int64_t n = M * Nc;
     if (dtype == 2)
-      hipLaunchKernelGGL(slab_sum<double>, dim3(grid_for(n)), dim3(256), 0, s, (const double*)ws, ksplit, n,
-                         (double*)final_out);
+      hipLaunchKernelGGL(bias_op<double>, dim3(grid_for(n)), dim3(256), 0, s, (const double*)out,
+                         bias ? (const double*)bias : nullptr, (double*)out, n, F, (int)P, 0, relu);
     else
-      hipLaunchKernelGGL(slab_sum<float>, dim3(grid_for(n)), dim3(256), 0, s, (const float*)ws, ksplit, n,
-                         (float*)final_out);
+      hipLaunchKernelGGL(bias_op<float>, dim3(grid_for(n)), dim3(256), 0, s, (const float*)out,
+                         bias ? (const float*)bias : nullptr, (float*)out, n, F, (int)P, 0, relu);
   }
   return (int)hipGetLastError();
 }

@@ -557,14 +557,15 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
     else:
         shape = (F, C * KH * KW)
     out = torch.empty(shape, dtype=odt, device=dev)
-    ws = None
+    # GEMM view (M x Ncol, depth K); split K when the output tiles alone cannot fill the chip:
+    # ~2k blocks in flight, each reducing >= 512 products per output (slab traffic stays small)
+    M, Nc, K = {0: (F, N * Ho * Wo, C * KH * KW), 1: (C, N * H * Wd, F * KH * KW),
+                2: (F, C * KH * KW, N * Ho * Wo)}[mode]
+    tiles = ((M + 63) // 64) * ((Nc + 63) // 64)
     ksplit = 1
-    if mode == 2:
-        tiles = ((F + 63) // 64) * ((C * KH * KW + 63) // 64)
-        K = N * Ho * Wo
-        ksplit = max(1, min(4096 // max(tiles, 1), K // 512))
-        if ksplit > 1:
-            ws = torch.empty((ksplit, F, C * KH * KW), dtype=odt, device=dev)
+    if tiles < 2048:
+        ksplit = max(1, min(256, 2048 // max(tiles, 1), K // 512))
+    ws = None
     b = None if bias is None else bias.to(device=dev, dtype=odt).contiguous().reshape(-1)
     rc = L.sysml_conv2d(code, mode, _ptr(X), _ptr(W), _ptr(D), _ptr(b), out.data_ptr(), _ptr(ws), ksplit,
                         N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, int(bool(relu)), _stream())
