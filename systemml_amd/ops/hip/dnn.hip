@@ -410,15 +410,27 @@ __global__ void __launch_bounds__(256) pool_bwd(Pool p) {
 }
 
 // ---- elementwise: bias add / multiply (channel-wise), relu backward --------------------------
+// one block row per (image, channel): blockIdx.x = n*C + c, threads stride over its P cells --
+// the channel is known per block, no per-element index division
 template <typename T>
 __global__ void __launch_bounds__(256) bias_op(const T* __restrict__ X, const T* __restrict__ b, T* __restrict__ O,
-                                                int64_t total, int C, int P, int mult, int relu) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int ch = (int)((i / P) % C);
-    T v = b ? (mult ? X[i] * b[ch] : X[i] + b[ch]) : X[i];
+                                                int C, int P, int mult, int relu) {
+  const int64_t rc = blockIdx.x;
+  const int ch = (int)(rc % C);
+  const T bv = b ? b[ch] : (mult ? T(1) : T(0));
+  const T* x = X + rc * P;
+  T* o = O + rc * P;
+  for (int p = blockIdx.y * 256 + threadIdx.x; p < P; p += gridDim.y * 256) {
+    T v = mult ? x[p] * bv : x[p] + bv;
     if (relu) v = v > T(0) ? v : T(0);
-    O[i] = v;
+    o[p] = v;
   }
+}
+
+inline dim3 bias_grid(int64_t rows_ch, int P) {
+  int64_t gy = (P + 255) / 256;
+  if (gy > 1024) gy = 1024;
+  return dim3((unsigned)rows_ch, (unsigned)(gy < 1 ? 1 : gy));
 }
 
 template <typename T>
@@ -505,12 +517,13 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
 #undef LAUNCH
   if (ksplit > 1 && mode == FWD && (bias || relu)) {
     const int64_t n = M * Nc;
+    const dim3 bg = bias_grid(n / P, (int)P);
     if (dtype == 2)
-      hipLaunchKernelGGL(bias_op<double>, dim3(grid_for(n)), dim3(256), 0, s, (const double*)out,
-                         bias ? (const double*)bias : nullptr, (double*)out, n, F, (int)P, 0, relu);
+      hipLaunchKernelGGL(bias_op<double>, bg, dim3(256), 0, s, (const double*)out,
+                         bias ? (const double*)bias : nullptr, (double*)out, F, (int)P, 0, relu);
     else
-      hipLaunchKernelGGL(bias_op<float>, dim3(grid_for(n)), dim3(256), 0, s, (const float*)out,
-                         bias ? (const float*)bias : nullptr, (float*)out, n, F, (int)P, 0, relu);
+      hipLaunchKernelGGL(bias_op<float>, bg, dim3(256), 0, s, (const float*)out,
+                         bias ? (const float*)bias : nullptr, (float*)out, F, (int)P, 0, relu);
   }
   return (int)hipGetLastError();
 }
@@ -543,12 +556,14 @@ int sysml_bias_op(int dtype, const void* X, const void* b, void* out, int64_t to
                   void* stream) {
   using namespace sysml_dnn;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (P <= 0 || total % P) return -1;
+  const dim3 bg = bias_grid(total / P, P);
   if (dtype == 1)
-    hipLaunchKernelGGL(bias_op<float>, dim3(grid_for(total)), dim3(256), 0, s, (const float*)X, (const float*)b,
-                       (float*)out, total, C, P, mult, relu);
+    hipLaunchKernelGGL(bias_op<float>, bg, dim3(256), 0, s, (const float*)X, (const float*)b, (float*)out, C, P, mult,
+                       relu);
   else if (dtype == 2)
-    hipLaunchKernelGGL(bias_op<double>, dim3(grid_for(total)), dim3(256), 0, s, (const double*)X, (const double*)b,
-                       (double*)out, total, C, P, mult, relu);
+    hipLaunchKernelGGL(bias_op<double>, bg, dim3(256), 0, s, (const double*)X, (const double*)b, (double*)out, C, P,
+                       mult, relu);
   else
     return -1;
   return (int)hipGetLastError();

@@ -73,6 +73,10 @@ def load(required=False):
     L.sysml_relu_backward.restype = ctypes.c_int
     L.sysml_relu_backward.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_int64, ctypes.c_void_p]
+    L.sysml_spmm.restype = ctypes.c_int
+    L.sysml_spmm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                             ctypes.c_int, ctypes.c_void_p]
     L.sysml_sddmm.restype = ctypes.c_int
     L.sysml_sddmm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
@@ -631,3 +635,37 @@ def relu_backward(X, D):
         raise RuntimeError(f"sysml_relu_backward failed: {rc}")
     _count("relu_backward")
     return out
+
+
+# ----------------------------------------------------------------------------
+# CSR sparse x dense (ops/hip/spmm.hip)
+# ----------------------------------------------------------------------------
+def spmm(A, B, transA=False):
+    """A (CSR, m x n) %*% B (dense n x K), or t(A) %*% B (B: m x K) without transposing A.
+    Computed in the wider of the two dtypes (fp32 / fp64); None if unsupported."""
+    L = load(required=True)
+    if A.layout != torch.sparse_csr or B.dim() != 2:
+        return None
+    dt = torch.promote_types(A.dtype, B.dtype)
+    if dt not in (torch.float32, torch.float64):
+        dt = torch.float32
+    m, n = A.shape
+    K = B.shape[1]
+    if B.shape[0] != (m if transA else n):
+        return None
+    crow = A.crow_indices().to(torch.int64).contiguous()
+    col = A.col_indices().to(torch.int64).contiguous()
+    val = A.values().to(dt).contiguous()
+    B = B.to(device=val.device, dtype=dt).contiguous()
+    if transA:
+        C = torch.zeros((n, K), dtype=dt, device=val.device)
+    else:
+        C = torch.empty((m, K), dtype=dt, device=val.device)
+    rc = L.sysml_spmm(1 if dt == torch.float32 else 2, int(bool(transA)), crow.data_ptr(), col.data_ptr(),
+                      val.data_ptr(), B.data_ptr(), K, C.data_ptr(), K, m, K, _stream())
+    if rc == -1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"sysml_spmm failed: {rc}")
+    _count("spmm_t" if transA else "spmm")
+    return C

@@ -3,8 +3,9 @@ and the sparse paths of LibMatrixMult / LibMatrixAgg; MatrixBlock.evalSparseForm
 decides dense vs sparse with a 0.4 sparsity turn point).
 
 Representation: a torch CSR tensor (`torch.sparse_csr`) on the backend device; on the
-MI355X the products run on hipSPARSE/rocSPARSE through torch.  Only the operations that
-benefit from sparsity keep the CSR form (matrix products incl. tsmm / mmchain, sum-type
+MI355X sparse x dense products (and row / column sums) run the in-tree SpMM / SpMV kernel
+(ops/hip/spmm.hip) and the sampled products of the weighted quaternary operators the SDDMM
+kernel (ops/hip/sddmm.hip).  Only the operations that benefit from sparsity keep the CSR form (matrix products incl. tsmm / mmchain, sum-type
 aggregates, transpose, scaling by a scalar, shape queries, write); every other operator
 receives a densified operand (instructions.make_impl), so semantics never depend on the
 format.
@@ -122,7 +123,16 @@ def _dense_rhs(b, dtype):
 
 
 def mm(a, b, transA=False):
-    """a %*% b (or t(a) %*% b) with a and/or b sparse."""
+    """a %*% b (or t(a) %*% b) with a and/or b sparse.  On the MI355X a CSR left operand with
+    a dense right operand runs the hand-written SpMM / SpMV kernel of ops/hip/spmm.hip (t(A)
+    as a scatter with atomics, no transposed copy of A)."""
+    if is_sparse(a) and a.layout == torch.sparse_csr and a.is_cuda and not is_sparse(b):
+        from .backend import backend
+        if backend.use_kernels:
+            from . import kernels
+            r = kernels.spmm(a, densify(b), transA)
+            if r is not None:
+                return r
     if is_sparse(a):
         if transA:
             a = a.t()                                  # CSR^T = CSC, consumed by spmm
@@ -156,9 +166,9 @@ def agg(o, d, x):
         s = float(vals.sum().item())
         return s / (r * c) if o == "mean" else s
     if d == "row":
-        out = x @ torch.ones((c, 1), dtype=vals.dtype, device=vals.device)
+        out = mm(x, torch.ones((c, 1), dtype=vals.dtype, device=vals.device))
         return out / c if o == "mean" else out
-    out = (x.t() @ torch.ones((r, 1), dtype=vals.dtype, device=vals.device)).t().contiguous()
+    out = mm(x, torch.ones((r, 1), dtype=vals.dtype, device=vals.device), transA=True).t().contiguous()
     return out / r if o == "mean" else out
 
 

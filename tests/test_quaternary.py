@@ -186,6 +186,8 @@ s = sum(UV)
 def test_sddmm_fp64_kernel_and_near_converged_wsloss_on_gpu():
     """fp64 SDDMM kernel (grouped-lane variant) against the host fp64 expression."""
     from systemml_amd.ops import kernels
+    from systemml_amd.ops.backend import backend
+    backend.configure(DMLConfig(gpu=True))          # kernels on (fp64 engine precision)
     dev = torch.device("cuda:0")
     Xd, U, V, mask = _near_converged(m=2000, n=1500, r=8)
     Xs = Xd.to_sparse_csr()

@@ -65,3 +65,28 @@ def test_sparse_read_text_cell(tmp_path):
     r = run(f'X = read("{f}")\ns = sum(X %*% matrix(1, rows=300, cols=1))', outputs=["X", "s"], config=CFG)
     assert SP.is_sparse(r["X"])
     np.testing.assert_allclose(r["s"], A.sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 3, 16, 64, 100])
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_spmm_hip_kernel(K, dt):
+    """CSR x dense (and t(CSR) x dense) HIP kernel against an fp64 dense reference."""
+    from systemml_amd.ops import kernels
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(K)
+    m, n = 700, 500
+    D = (torch.rand(m, n, generator=g) < 0.03).double() * torch.randn(m, n, generator=g, dtype=torch.float64)
+    D[5] = 0                                   # empty rows
+    A = D.to(dt).to_sparse_csr().to(dev)
+    B = torch.randn(n, K, generator=g, dtype=torch.float64)
+    Bt = torch.randn(m, K, generator=g, dtype=torch.float64)
+    tol = 1e-12 if dt == torch.float64 else 1e-4
+    c0 = kernels.counters.get("spmm", 0)
+    got = kernels.spmm(A, B.to(dev, dt))
+    gott = kernels.spmm(A, Bt.to(dev, dt), transA=True)
+    np.testing.assert_allclose(got.double().cpu().numpy(), (D.to(dt).double() @ B.to(dt).double()).numpy(),
+                               rtol=tol, atol=tol)
+    np.testing.assert_allclose(gott.double().cpu().numpy(), (D.to(dt).double().T @ Bt.to(dt).double()).numpy(),
+                               rtol=tol * 10, atol=tol * 10)
+    assert kernels.counters["spmm"] > c0
