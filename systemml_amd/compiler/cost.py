@@ -48,6 +48,32 @@ def _int_or(v, default=-1):
     return default
 
 
+def _sval(h, dims, depth=0):
+    """Compile-time value of a scalar hop when it follows from literals and known matrix
+    sizes (nrow / ncol / length of a matrix whose dims are known, arithmetic on those) --
+    reference: the size-expression evaluation of Hop.computeSizeInformation."""
+    if h is None or depth > 8:
+        return None
+    if h.op == "lit":
+        return h.value
+    if h.op == "u" and h.p.get("o") in ("nrow", "ncol", "length") and h.inputs:
+        d = dims.get(h.inputs[0].id, UNK)
+        if _known(d):
+            return {"nrow": d[0], "ncol": d[1], "length": d[0] * d[1]}[h.p["o"]]
+        return None
+    if h.op == "u" and h.p.get("o") in ("cast_int", "cast_double", "cast_scalar") and h.inputs:
+        return _sval(h.inputs[0], dims, depth + 1)
+    if h.op == "b" and h.p.get("o") in ("+", "-", "*", "/", "%/%") and len(h.inputs) == 2:
+        a, b = _sval(h.inputs[0], dims, depth + 1), _sval(h.inputs[1], dims, depth + 1)
+        if isinstance(a, (int, float)) and isinstance(b, (int, float)) and not isinstance(a, bool) \
+                and not isinstance(b, bool):
+            o = h.p["o"]
+            if o in ("/", "%/%") and b == 0:
+                return None
+            return {"+": a + b, "-": a - b, "*": a * b, "/": a / b if o == "/" else a, "%/%": a // b if b else a}[o]
+    return None
+
+
 def infer(h, dims, env):
     """Output (rows, cols) of hop h given input dims; (0, 0) for scalars, -1 unknown."""
     op = h.op
@@ -104,7 +130,7 @@ def infer(h, dims, env):
         lists = h.p.get("list", False)
         return (span(rl, ru, r), c if lists and cl is _ABSENT else span(cl, cu, c))
     if op == "bi":
-        return _infer_bi(h, ins)
+        return _infer_bi(h, ins, dims)
     return UNK
 
 
@@ -117,16 +143,17 @@ def _bi_arg(h, i, name):
     return None
 
 
-def _infer_bi(h, ins):
+def _infer_bi(h, ins, dims=None):
     name = h.p.get("name")
+    dims = dims or {}
     if name in ("matrix", "rand"):
         if name == "matrix":
             data = _bi_arg(h, 0, "data")
             r, c = _bi_arg(h, 1, "rows"), _bi_arg(h, 2, "cols")
         else:
             r, c = _bi_arg(h, 99, "rows"), _bi_arg(h, 99, "cols")
-        rv = _int_or(_lv(r)) if r is not None else -1
-        cv = _int_or(_lv(c)) if c is not None else -1
+        rv = _int_or(_sval(r, dims)) if r is not None else -1
+        cv = _int_or(_sval(c, dims)) if c is not None else -1
         return (rv, cv)
     if name == "seq":
         a, b = (_lv(x) for x in h.inputs[:2]) if len(h.inputs) >= 2 else (None, None)
@@ -169,19 +196,62 @@ def mem_estimate(d, bytes_per_cell=8):
     return d[0] * d[1] * bytes_per_cell
 
 
+def _world(config):
+    w = getattr(config, "_world", None) if config is not None else None
+    if w is None:
+        from ..parallel import dist as D
+        ctx = D.get_context()
+        w = ctx.world if ctx is not None else 1
+    return w
+
+
 def exec_type(h, d, in_dims, config):
-    if h.dt == "S" or d == SCALAR:
-        return "CP"
-    cells = [x[0] * x[1] for x in [d] + list(in_dims) if _known(x)]
-    unknown = not _known(d) or any(not _known(x) for x in in_dims if x != SCALAR)
+    """Execution type of a HOP (reference Hop.findExecTypeByMemEstimate): None when a matrix
+    operand or the output has unknown dimensions -- decided at run time by dynamic
+    recompilation (recompile_exec_types) from the actual shapes."""
+    mats = [x for x in in_dims if x != SCALAR]
+    if h.op == "sink" or ((h.dt == "S" or d == SCALAR) and not mats):
+        return "CP"                          # scalar operations
+    if d == SCALAR:
+        d = (1, 1)                           # aggregate of matrices: placed by its operands
+    if not _known(d) or any(not _known(x) for x in mats):
+        return None
     gpu = config is not None and getattr(config, "gpu", False)
-    if config is not None and _known(d) and getattr(config, "dist_min_rows", 0) and \
-            d[0] >= config.dist_min_rows and getattr(config, "_world", 1) > 1:
-        return "DIST"
+    world = _world(config) if config is not None else 1
+    if config is not None and world > 1:
+        if getattr(config, "dist_min_rows", 0) and d[0] >= config.dist_min_rows:
+            return "DIST"
+        budget = getattr(config, "gpu_mem_budget", 0)
+        if budget and sum(x[0] * x[1] * 8 for x in [d] + list(in_dims) if _known(x)) > budget:
+            return "DIST"
+    cells = [x[0] * x[1] for x in [d] + list(in_dims) if _known(x)]
     small = getattr(config, "gpu_min_cells", 16384) if config is not None else 16384
-    if gpu and (unknown or max(cells or [0]) >= small):
+    if gpu and max(cells or [0]) >= small:
         return "GPU"
     return "CP"
+
+
+def physical_op(h, d, in_dims, et, config):
+    """Physical operator of a matrix multiplication (reference AggBinaryOp.optFindMMultMethod*):
+    DIST: mapmm (row-partitioned left, broadcast right), cpmm (co-partitioned t(X) %*% Y with
+    an all-reduce), rmm (both row-partitioned: ring of the right operand's blocks), tsmm /
+    mapmmchain (local fused kernel + all-reduce); GPU: MFMA GEMM, or a row-streaming kernel when
+    the product is skinny (<= 8 columns) over a tall operand; CP: host GEMM."""
+    if et is None or h.op not in ("mm", "tsmm", "mmchain", "smgrad"):
+        return None
+    if h.op == "tsmm":
+        return {"DIST": "tsmm+allreduce", "GPU": "mfma-tsmm", "CP": "cp-tsmm"}[et]
+    if h.op in ("mmchain", "smgrad"):
+        return {"DIST": "mapmmchain+allreduce", "GPU": "rowstream-chain", "CP": "cp-chain"}[et]
+    a, b = in_dims[0], in_dims[1]
+    if et == "DIST":
+        rows = getattr(config, "dist_min_rows", 1 << 62)
+        if h.p.get("transA"):
+            return "cpmm+allreduce"
+        return "rmm-ring" if _known(b) and b[0] >= rows else "mapmm"
+    if et == "GPU":
+        return "rowstream-skinny" if _known(d) and d[1] <= 8 and a[0] >= 2048 else "mfma-gemm"
+    return "cp-gemm"
 
 
 def annotate_dag(roots, env, config=None):
@@ -193,7 +263,9 @@ def annotate_dag(roots, env, config=None):
             d = (h.dim1, h.dim2)
         dims[h.id] = d
         h.dim1, h.dim2 = d
-        h.exec_type = exec_type(h, d, [dims.get(c.id, UNK) for c in h.inputs], config)
+        ind = [dims.get(c.id, UNK) for c in h.inputs]
+        h.exec_type = exec_type(h, d, ind, config)
+        h.phys = physical_op(h, d, ind, h.exec_type, config)
     return dims
 
 
@@ -427,9 +499,18 @@ def annotate(cp, inputs=None, config=None):
         dims = annotate_dag(list(bb.roots) + list(bb.env_out.values()), env, config)
         if not getattr(bb, "cond", True):
             _check_dims(list(bb.roots) + list(bb.env_out.values()), dims)
+        unknown = False
         for h in H.walk(list(bb.roots) + list(bb.env_out.values())):
-            if h.exec_type and h.op not in ("lit", "tread"):
+            if h.op in ("lit", "tread"):
+                continue
+            if h.exec_type:
                 counts[h.exec_type] = counts.get(h.exec_type, 0) + 1
+            elif h.dt == "M":
+                unknown = True
+        # exec types left open (unknown sizes) are decided when the block runs
+        bb.exec_recompile = unknown
+        if unknown:
+            counts["deferred"] = counts.get("deferred", 0) + 1
         return dims
 
     _walk_program(cp, env, visit)
@@ -463,3 +544,34 @@ def recompile_block(bb, vars_, make_impl, config):
         cache[sig] = plan
     bb.instrs, bb.writes_slots, bb.nslots, bb.debug_slots = plan
     return plan is not bb._orig_plan
+
+
+def recompile_exec_types(bb, vars_, config):
+    """Dynamic recompilation of execution types (reference Recompiler.recompileHopsDag +
+    Hop.refreshSizeInformation): re-infer the block's sizes from the actual shapes of its
+    live-in variables and re-select every operator's exec type / physical operator.  Cached on
+    the shape signature; returns True when the plan changed."""
+    names = getattr(bb, "_et_names", None)
+    if names is None:
+        names = bb._et_names = tuple(sorted(bb.reads))
+    get = vars_.get
+    sig = tuple(_shape_of(get(n)) for n in names)
+    if getattr(bb, "_et_sig", None) == sig:
+        return False
+    bb._et_sig = sig
+    tops = list(bb.roots) + list(bb.env_out.values())
+    annotate_dag(tops, dict(zip(names, sig)), config)
+    return True
+
+
+def runtime_plan(bb, indent=""):
+    """-explain recompile_runtime: the block's instructions with their exec types and
+    physical operators after dynamic recompilation."""
+    lines = []
+    for ins in bb.instrs or []:
+        h = ins.hop
+        et = getattr(h, "exec_type", None) or "?"
+        ph = getattr(h, "phys", None)
+        dims = f" [{h.dim1}x{h.dim2}]" if h.dt == "M" else ""
+        lines.append(f"{indent}{et:4s} {ins.opcode}{dims}" + (f" ({ph})" if ph else ""))
+    return "\n".join(lines)

@@ -37,7 +37,7 @@ SIDE_EFFECT = {"print", "write", "stop", "assert", "printf"}
 
 class Hop:
     __slots__ = ("id", "op", "inputs", "p", "dim1", "dim2", "dt", "parents", "slot",
-                 "named", "pos", "exec_type")
+                 "named", "pos", "exec_type", "phys")
 
     def __init__(self, op, inputs=(), p=None, named=None, dt="U", dim1=-1, dim2=-1, pos=None):
         self.id = next(_ids)
@@ -51,7 +51,8 @@ class Hop:
         self.parents = []
         self.slot = -1
         self.pos = pos
-        self.exec_type = None
+        self.exec_type = None         # CP | GPU | DIST (compiler/cost.py); None: decided at run time
+        self.phys = None              # physical operator of matrix products (cost.physical_op)
 
     # convenience
     @property
@@ -125,7 +126,10 @@ def walk(roots):
 def explain_dag(roots, indent=""):
     lines = []
     for h in walk(roots):
-        et = f" {h.exec_type}" if h.exec_type else ""
+        et = f" {h.exec_type}" if h.exec_type else (" (exec type at run time)" if h.dt == "M" and
+                                                     h.op not in ("lit", "tread") else "")
+        if getattr(h, "phys", None):
+            et += f" {h.phys}"
         if h.dt == "M" and h.dim1 >= 0 and h.dim2 >= 0:
             mb = h.dim1 * h.dim2 * 8 / 1e6
             et += f" [{mb:.3g}MB]"

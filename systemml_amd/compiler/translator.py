@@ -183,6 +183,11 @@ class Translator:
             for st in lst:
                 if isinstance(st, (A.Assign, A.MultiAssign, A.ExprStmt)):
                     cur.add(st)
+                    if isinstance(st, A.Assign) and _reads_unknown_size(st.value):
+                        # reference RewriteSplitDagUnknownCSVRead: end the block after a read
+                        # of unknown size so the operators using it are recompiled (exec types,
+                        # mm-chain order) with the actual dimensions
+                        flush()
                 elif isinstance(st, (A.Import, A.SetWd)):
                     continue
                 elif isinstance(st, A.If):
@@ -695,6 +700,20 @@ class _BBuilder:
         return self.mk("bi", inputs, p={"name": "eval", "npos": len(pos_args), "nskey": self.ctx.key,
                                         "imports": tuple(sorted(self.ctx.imports.items()))},
                        named=[n for n, _ in named], pos=pos, cse=False)
+
+
+def _reads_unknown_size(e):
+    """True if the expression reads a matrix without literal rows / cols arguments."""
+    if isinstance(e, A.Call):
+        if e.name == "read" and not e.namespace:
+            named = {a.name for a in e.args if getattr(a, "name", None)}
+            return not {"rows", "cols"} <= named
+        return any(_reads_unknown_size(a.value) for a in e.args)
+    for attr in ("left", "right", "operand", "target"):
+        x = getattr(e, attr, None)
+        if isinstance(x, A.Expr) and _reads_unknown_size(x):
+            return True
+    return False
 
 
 _M_BUILTINS = ("matrix rand seq sample cbind rbind table ctable diag rev removeEmpty replace order solve inv "

@@ -36,7 +36,7 @@ def make_impl(h):
     hybrid host/HBM placement of `_placed` on a GPU backend."""
     fn, code = _make_impl(h)
     if h.op in _COMPUTE_OPS and not (h.op == "bi" and h.p.get("name") in _NO_PLACE_BI):
-        fn = _placed(fn)
+        fn = _placed(fn, h)
     sparse_ok = h.op in _SPARSE_OK_OPS or (h.op == "u" and h.p.get("o") in _SPARSE_OK_UNARY)
     lazy_ok = h.op in _LAZY_OK_OPS
     if sparse_ok and lazy_ok:
@@ -63,22 +63,34 @@ def make_impl(h):
     return wrapped, code
 
 
-def _placed(fn):
-    """Hybrid CP / GPU execution (reference: the per-operator CP vs GPU exec-type choice of
-    hops/Hop.java#findExecTypeByMemEstimate with the GPU operator threshold): matrices below
-    `sysml.gpu.mincells` cells live in host memory and their operators run on the CPU, where a
-    small op costs a few microseconds and its scalars are available without a device sync;
-    larger matrices stay resident in HBM.  An operator that mixes the two runs where its
-    largest operand lives (small operands are copied over), and a small result produced in HBM
-    (e.g. the D x K output of a fused t(X) %*% f(X %*% V) pass) is moved to host memory."""
+def _placed(fn, h):
+    """CP / GPU execution of one operator by its compiler-chosen exec type (reference:
+    hops/Hop.java#findExecTypeByMemEstimate with the GPU operator threshold, re-selected by
+    dynamic recompilation when sizes were unknown at compile time -- compiler/cost.py):
+      CP   operands in host memory, the operator runs on the CPU (a small op costs a few
+           microseconds and its scalar results are available without a device sync);
+      GPU  operands in HBM (host operands are copied over), HIP kernels;
+      DIST row-partitioned operands, operators of parallel/dist.py (placement untouched).
+    A small result computed in HBM (e.g. the D x K output of a fused t(X) %*% f(X %*% V)
+    pass) is moved to host memory, where its consumers run."""
     import torch
     from ..ops.backend import backend
     Tensor = torch.Tensor
 
     def run(ctx, a):
         small = backend.small_cells
-        if small <= 0:
+        if small <= 0 or not backend.on_gpu:
             return fn(ctx, a)
+        et = h.exec_type
+        if et == "CP":
+            a = [x.to("cpu") if (type(x) is Tensor and x.is_cuda and x.layout == torch.strided) else x for x in a]
+            return fn(ctx, a)
+        if et == "GPU":
+            gpu = backend.device
+            a = [x.to(gpu, non_blocking=True) if (type(x) is Tensor and not x.is_cuda) else x for x in a]
+            return demote(fn(ctx, a))
+        # not decided (e.g. DIST operands or a block never recompiled): run where the largest
+        # operand lives
         dev = None
         mixed = False
         for x in a:
@@ -96,12 +108,11 @@ def _placed(fn):
             gpu = backend.device
             a = [x.to(gpu, non_blocking=True) if (type(x) is Tensor and x.device.type != "cuda") else x
                  for x in a]
-        r = fn(ctx, a)
-        if type(r) is tuple:                 # multi-output fused operators
-            return tuple(demote(x) for x in r)
-        return demote(r)
+        return demote(fn(ctx, a))
 
     def demote(r):
+        if type(r) is tuple:                 # multi-output fused operators
+            return tuple(demote(x) for x in r)
         if type(r) is Tensor and r.is_cuda and r.numel() < backend.small_cells and r.dtype != torch.bfloat16 \
                 and not r.is_sparse and r.layout == torch.strided:
             return r.to("cpu")

@@ -215,6 +215,14 @@ def exec_block(ctx, b):
             from .instructions import make_impl
             if recompile_block(b, ctx.vars, make_impl, ctx.config) and ctx.stats is not None:
                 ctx.stats.count("recompiled blocks")
+        if getattr(b, "exec_recompile", False):
+            from ..compiler.cost import recompile_exec_types, runtime_plan
+            if recompile_exec_types(b, ctx.vars, ctx.config):
+                if ctx.stats is not None:
+                    ctx.stats.count("recompiled exec types")
+                if ctx.config is not None and ctx.config.explain == "recompile_runtime":
+                    ctx.print(f"# EXPLAIN (recompile_runtime): block at line "
+                              f"{b.pos.line if b.pos else '?'}\n" + runtime_plan(b, "  "))
         slots = exec_instrs(ctx, b.instrs, b.nslots)
         vars_ = ctx.vars
         for name, s in b.writes_slots:

@@ -366,3 +366,32 @@ def test_update_in_place_preserves_value_semantics():
         w[0, 0] = 7
     np.testing.assert_array_equal(W, w)
     np.testing.assert_array_equal(r.ravel(), rr)
+
+
+def test_exec_types_decided_by_size_and_recompiled_at_runtime():
+    """Exec types come from the compiler's size / memory estimates (reference
+    Hop.findExecTypeByMemEstimate); sizes unknown at compile time (a matrix read from a file)
+    are resolved by dynamic recompilation when the block runs, and the choice flips when the
+    input crosses the GPU operator threshold.  -explain recompile_runtime prints the plan."""
+    import os
+    import tempfile
+    import torch
+    from systemml_amd.api.executor import compile_script, execute, explain
+    from systemml_amd.io import writers
+    cfg = DMLConfig(gpu=True, gpu_min_cells=10000, explain="recompile_runtime")
+    d = tempfile.mkdtemp()
+    src = f'X = read("{d}/X")\nv = matrix(1, rows=ncol(X), cols=1)\ny = X %*% v\nG = t(X) %*% X\nprint(sum(y) + sum(G))'
+    plans = {}
+    for n in (20, 400):
+        writers.write(None, torch.ones((n, 30), dtype=torch.float64), f"{d}/X", format="csv")
+        cs = compile_script(src, config=cfg)
+        assert "exec type at run time" in explain(cs.cp, "hops")
+        out = []
+        execute(cs, {}, out=out.append)
+        plans[n] = "\n".join(o for o in out if o.startswith("# EXPLAIN (recompile_runtime)"))
+    small, large = plans[20], plans[400]
+    assert "CP   ba+*" in small and "(cp-gemm)" in small and "CP   tsmm" in small, small
+    assert "GPU  ba+*" in large and "(mfma-gemm)" in large and "(mfma-tsmm)" in large, large
+    # known sizes at compile time: chosen statically, nothing deferred
+    cs = compile_script("A = rand(rows=400, cols=30)\nB = A %*% t(A)\nprint(sum(B))", config=cfg)
+    assert cs.cp.exec_types.get("deferred", 0) == 0 and cs.cp.exec_types.get("GPU", 0) > 0
