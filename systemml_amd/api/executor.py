@@ -154,6 +154,12 @@ def execute(cs: CompiledScript, inputs=None, out=None, stats=None, dist=None):
                 for k_, v_ in ctx.pool.stats.items():
                     if isinstance(v_, int) and v_:
                         stats.counters["bufferpool." + k_] = v_
+            for k_, v_ in (getattr(cs.cp, "exec_types", None) or {}).items():
+                stats.counters[f"compiled exec type {k_}"] = v_
+            for k_, v_ in (getattr(cs.cp, "licm_stats", None) or {}).items():
+                stats.counters[f"rewrite {k_}"] = v_
+            for k_, v_ in (getattr(cs.cp, "chain_stats", None) or {}).items():
+                stats.counters[f"mm-chain {k_}"] = v_
     from ..runtime.bufferpool import Evicted
     from ..runtime import scalars as S_
     res = {}

@@ -26,6 +26,7 @@ _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
 _LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "t", "tak"}
 # operators that compute on matrix operands (placement applies); the rest move values around
 _COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "wquat", "tak", "t", "rix", "lix", "bi"}
+transfer_stats = {"h2d": 0, "d2h": 0, "h2d_bytes": 0, "d2h_bytes": 0}   # -stats (utils/stats.gpu_report)
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
 
@@ -83,11 +84,10 @@ def _placed(fn, h):
             return fn(ctx, a)
         et = h.exec_type
         if et == "CP":
-            a = [x.to("cpu") if (type(x) is Tensor and x.is_cuda and x.layout == torch.strided) else x for x in a]
+            a = [d2h(x) if (type(x) is Tensor and x.is_cuda and x.layout == torch.strided) else x for x in a]
             return fn(ctx, a)
         if et == "GPU":
-            gpu = backend.device
-            a = [x.to(gpu, non_blocking=True) if (type(x) is Tensor and not x.is_cuda) else x for x in a]
+            a = [h2d(x) if (type(x) is Tensor and not x.is_cuda) else x for x in a]
             return demote(fn(ctx, a))
         # not decided (e.g. DIST operands or a block never recompiled): run where the largest
         # operand lives
@@ -105,17 +105,27 @@ def _placed(fn, h):
             elif d != dev:
                 mixed = True
         if mixed:
-            gpu = backend.device
-            a = [x.to(gpu, non_blocking=True) if (type(x) is Tensor and x.device.type != "cuda") else x
-                 for x in a]
+            a = [h2d(x) if (type(x) is Tensor and x.device.type != "cuda") else x for x in a]
         return demote(fn(ctx, a))
+
+    ts = transfer_stats
+
+    def h2d(x):
+        ts["h2d"] += 1
+        ts["h2d_bytes"] += x.numel() * x.element_size()
+        return x.to(backend.device, non_blocking=True)
+
+    def d2h(x):
+        ts["d2h"] += 1
+        ts["d2h_bytes"] += x.numel() * x.element_size()
+        return x.to("cpu")
 
     def demote(r):
         if type(r) is tuple:                 # multi-output fused operators
             return tuple(demote(x) for x in r)
         if type(r) is Tensor and r.is_cuda and r.numel() < backend.small_cells and r.dtype != torch.bfloat16 \
                 and not r.is_sparse and r.layout == torch.strided:
-            return r.to("cpu")
+            return d2h(r)
         return r
     return run
 

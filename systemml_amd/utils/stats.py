@@ -1,15 +1,21 @@
 """Runtime statistics (`-stats`), reference: utils/Statistics.java + GPUStatistics.java.
 
-Records per-opcode counts and wall time (heavy hitters), compile/execute time,
-and GPU kernel-library usage counters."""
+Records per-opcode counts and wall time (heavy hitters; on a GPU backend every instruction
+is synchronised before it is timed, so the times are execution and not launch times unless
+sync=False is requested), compile / execute time, dynamic-recompilation and buffer-pool
+counters, host<->HBM transfers made by the CP/GPU placement (count, bytes, time), the
+caching allocator's HBM statistics and the invocation counts of the in-tree HIP kernels."""
 from __future__ import annotations
 
 import time
 
 
 class Statistics:
-    def __init__(self, enabled=False, sync=False):
+    def __init__(self, enabled=False, sync=None):
         self.enabled = enabled
+        if sync is None:                       # default: time executions, not launches, on a GPU
+            import torch
+            sync = torch.cuda.is_available()
         self.sync = sync
         self.ops = {}
         self.t_start = time.perf_counter()
@@ -37,6 +43,7 @@ class Statistics:
         if self.counters:
             for k_, v in sorted(self.counters.items()):
                 lines.append(f"{k_}:\t{v}")
+        lines += gpu_report()
         if self.ops:
             lines.append(f"Heavy hitter instructions:")
             lines.append("  #  Instruction        Time(s)   Count")
@@ -44,3 +51,25 @@ class Statistics:
             for i, (op, (n, t)) in enumerate(top, 1):
                 lines.append(f"{i:3d}  {op:<18s} {t:8.3f} {n:7d}")
         return "\n".join(lines)
+
+
+def gpu_report():
+    """GPUStatistics-style section: transfers made by the placement, HBM allocator state and
+    HIP kernel invocations (empty without a GPU)."""
+    import torch
+    out = []
+    from ..runtime import instructions as I
+    t = I.transfer_stats
+    if t["h2d"] or t["d2h"]:
+        out.append(f"Host->HBM transfers (count/MB):\t{t['h2d']}/{t['h2d_bytes'] / 1e6:.1f}")
+        out.append(f"HBM->host transfers (count/MB):\t{t['d2h']}/{t['d2h_bytes'] / 1e6:.1f}")
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        ms = torch.cuda.memory_stats()
+        out.append(f"HBM allocated / peak / reserved (GB):\t{ms.get('allocated_bytes.all.current', 0) / 1e9:.2f} / "
+                   f"{ms.get('allocated_bytes.all.peak', 0) / 1e9:.2f} / {ms.get('reserved_bytes.all.current', 0) / 1e9:.2f}")
+        out.append(f"HBM allocations / frees / alloc retries:\t{ms.get('allocation.all.allocated', 0)} / "
+                   f"{ms.get('allocation.all.freed', 0)} / {ms.get('num_alloc_retries', 0)}")
+    from ..ops import kernels as K
+    if K.counters:
+        out.append("HIP kernel invocations:\t" + ", ".join(f"{k}={v}" for k, v in sorted(K.counters.items())))
+    return out
