@@ -78,8 +78,14 @@ def read(ctx, fname, **kw):
         arr = read_text_cell(fname, rows, cols)
     elif fmt == "mm":
         arr = read_matrix_market(fname)
-    elif fmt == "binary":
-        return _post(read_binary(fname), ctx)
+    elif fmt in ("binary", "native"):
+        from . import binaryblock as BB
+        if BB.is_sequence_file(fname):
+            brlen = int(kw.get("rows_in_block", md.get("rows_in_block", 1000)))
+            bclen = int(kw.get("cols_in_block", md.get("cols_in_block", brlen)))
+            arr = BB.read_binary_block(fname, rows, cols, brlen, bclen)
+        else:
+            return _post(read_binary(fname), ctx)
     else:
         raise DMLRuntimeError(f"read: unsupported format '{fmt}'")
     if rows > 0 and cols > 0 and arr.shape != (rows, cols):
@@ -103,7 +109,16 @@ def _read_partitioned(ctx, fname, fmt, rows, cols, md, kw):
     dctx = ctx.dist
     minr = ctx.config.dist_min_rows
     files = _files(fname)
-    if fmt == "binary":
+    if fmt in ("binary", "native"):
+        from . import binaryblock as BB
+        if BB.is_sequence_file(fname):
+            if rows <= 0 or cols <= 0 or rows < minr:
+                return None
+            brlen = int(kw.get("rows_in_block", md.get("rows_in_block", 1000)))
+            bclen = int(kw.get("cols_in_block", md.get("cols_in_block", brlen)))
+            s, e = dctx.partition(rows)
+            loc = BB.read_binary_block(fname, rows, cols, brlen, bclen, row_range=(s, e))
+            return D.local_block(dctx, torch.from_numpy(loc), rows, cols)
         with open(fname, "rb") as f:
             head = f.read(32)
         r, c = (int(v) for v in np.frombuffer(head[8:24], dtype=np.int64))
@@ -190,7 +205,7 @@ def _sniff(fname):
     f = _files(fname)[0]
     with open(f, "rb") as fh:
         head = fh.read(64)
-    if head.startswith(BIN_MAGIC):
+    if head.startswith(BIN_MAGIC) or head.startswith(b"SEQ"):
         return "binary"
     if head.startswith(b"%%MatrixMarket"):
         return "mm"

@@ -48,9 +48,10 @@ def write(ctx, x, fname, format="text", **kw):
         return write_frame(x, fname, fmt, **kw)
     if isinstance(x, ListObject):
         raise DMLRuntimeError("write of lists is not supported")
-    if fmt == "binary" and isinstance(x, torch.Tensor) and x.dtype == torch.bfloat16:
+    if fmt in ("binary", "native") and isinstance(x, torch.Tensor) and x.dtype == torch.bfloat16:
+        # bf16 storage has no binary-block encoding: this framework's raw format (mmap-able)
         _write_binary_raw(x, fname, 2)
-        M.write_mtd(fname, "matrix", "double", x.shape[0], x.shape[1], fmt="binary")
+        M.write_mtd(fname, "matrix", "double", x.shape[0], x.shape[1], fmt=fmt)
         return
     a = _np(x)
     r, c = a.shape
@@ -78,6 +79,13 @@ def write(ctx, x, fname, format="text", **kw):
             for ii, jj in zip(i, j):
                 f.write(f"{ii + 1} {jj + 1} {S.java_double_str(float(a[ii, jj]))}\n")
     elif fmt == "binary":
+        # the reference's binary-block SequenceFile (io/binaryblock.py): loads in SystemML
+        from .binaryblock import write_binary_block
+        brlen = int(kw.get("rows_in_block", 1000))
+        write_binary_block(fname, a, brlen, brlen)
+        M.write_mtd(fname, "matrix", "double", r, c, nnz, fmt=fmt, rows_in_block=brlen, cols_in_block=brlen)
+        return
+    elif fmt == "native":
         _write_binary_raw(torch.from_numpy(a), fname, 0)
     else:
         raise DMLRuntimeError(f"write: unsupported format '{fmt}'")

@@ -141,6 +141,7 @@ def test_partitioned_reads(tmp_path):
     X = rng.standard_normal((101, 7))
     writers.write(None, torch.from_numpy(X), str(tmp_path / "X.csv"), format="csv")
     writers.write(None, torch.from_numpy(X), str(tmp_path / "X.bin"), format="binary")
+    writers.write(None, torch.from_numpy(X), str(tmp_path / "X.nat"), format="native")
     from systemml_amd.ops import native
     if native.lib() is None:
         pytest.skip("native IO library not built")
@@ -166,7 +167,7 @@ def _read_worker(rank, world, port, d, q):
         ctx = D.init(backend="gloo")
         ectx = ExecutionContext(None, DMLConfig(gpu=False, dist_min_rows=50), dist=ctx)
         blocks = {}
-        for f in ("X.csv", "X.bin"):
+        for f in ("X.csv", "X.bin", "X.nat"):
             m = readers.read(ectx, os.path.join(d, f))
             assert isinstance(m, D.DistMatrix), type(m)
             blocks[f] = (m.start, m.local.double().numpy(), D.gather(m).double().numpy())
