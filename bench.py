@@ -98,6 +98,8 @@ def main():
     ap.add_argument("--maxi", type=int, default=20)
     ap.add_argument("--moi", type=int, default=20)
     ap.add_argument("--mii", type=int, default=5)
+    ap.add_argument("--icpt", type=int, default=0, choices=[0, 1, 2],
+                    help="intercept mode of both scripts (perftest runs 0, 1 and 2; the headline is 0)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--stats", action="store_true")
     ap.add_argument("--gpu-min-cells", type=int, default=None,
@@ -143,8 +145,8 @@ def main():
         src_lr = f.read()
     with open(os.path.join(SCRIPTS_DIR, "algorithms", "MultiLogReg.dml")) as f:
         src_mlr = f.read()
-    args_lr = dict(X="X", Y="y", B="B", icpt=0, maxi=a.maxi, tol=0.0001, reg=0.01, fmt="csv")
-    args_mlr = dict(X="X", Y="Y", B="B", icpt=0, reg=0.01, tol=0.0001, moi=a.moi, mii=a.mii)
+    args_lr = dict(X="X", Y="y", B="B", icpt=a.icpt, maxi=a.maxi, tol=0.0001, reg=0.01, fmt="csv")
+    args_mlr = dict(X="X", Y="Y", B="B", icpt=a.icpt, reg=0.01, tol=0.0001, moi=a.moi, mii=a.mii)
     log = []
     out = (lambda s: log.append(s)) if not a.verbose else (lambda s: print(s, file=sys.stderr))
 
@@ -192,8 +194,8 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if a.xdtype == "bf16" else a.xdtype,
             "data": "synthetic (perftest generators genRandData4LogisticRegression / genRandData4Multinomial, "
                     "sparsity 0.9, generated in HBM)",
-            "config": {"model": "LinregCG+MultiLogReg (perftest: maxi=%d; k=%d moi=%d mii=%d)"
-                                % (a.maxi, a.classes, a.moi, a.mii),
+            "config": {"model": "LinregCG+MultiLogReg (perftest: maxi=%d; k=%d moi=%d mii=%d%s)"
+                                % (a.maxi, a.classes, a.moi, a.mii, "" if a.icpt == 0 else f"; icpt={a.icpt}"),
                        "global_batch": a.rows, "seq_len": a.cols, "rows": a.rows, "cols": a.cols,
                        "parallelism": f"dp{world}", "x_storage": a.xdtype, "accumulate": "fp32"},
         }

@@ -162,6 +162,9 @@ def _infer_bi(h, ins, dims=None):
             inc = inc if isinstance(inc, (int, float)) and inc else (1 if b >= a else -1)
             return (int((b - a) / inc) + 1, 1)
         return (-1, 1)
+    if name == "_cbind_const":
+        r, c = ins[0]
+        return (r, c + 1 if c >= 0 else -1)
     if name in ("cbind", "append"):
         if all(_known(d) for d in ins):
             return (ins[0][0], sum(d[1] for d in ins))

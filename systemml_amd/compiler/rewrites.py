@@ -133,7 +133,25 @@ class Rewriter:
             return self._rw_mm(h)
         if op == "bi" and h.p.get("name") in ("table", "ctable"):
             return self._match_onehot(h)
+        if op == "bi" and h.p.get("name") in ("cbind", "append"):
+            return self._match_cbind_const(h)
         return h
+
+    def _match_cbind_const(self, h):
+        """cbind(X, matrix(1, rows=n, cols=1)) -> _cbind_const(X, 1, n): the intercept column
+        of the regression scripts becomes a constant-column view (ops/augmented.py) instead
+        of an N x (D+1) copy; the builtin checks n == nrow(X) at run time."""
+        if len(h.inputs) != 2 or h.named or h.p.get("npos", 2) != 2:
+            return h
+        X, Mx = h.inputs
+        if X.dt != "M" or Mx.op != "bi" or Mx.p.get("name") != "matrix" or not _is_lit(Mx.inputs[0], 1):
+            return h
+        args = _bi_args(Mx)
+        rows, cols = args.get("rows"), args.get("cols")
+        if rows is None or cols is None or not _is_lit(cols, 1) or set(args) - {"data", "rows", "cols"}:
+            return h
+        self._count("cbind-const")
+        return Hop("bi", [X, Mx.inputs[0], rows], {"name": "_cbind_const", "npos": 3}, dt="M", pos=h.pos)
 
     def _rw_binary(self, h):
         a, b = h.inputs

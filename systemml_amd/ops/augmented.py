@@ -1,0 +1,194 @@
+"""Matrices with an implicit constant last column: cbind(X, c) without the copy.
+
+The intercept handling of the regression scripts (icpt = 1 | 2: `X = cbind(X, matrix(1, N, 1))`)
+would materialise a second N x (D+1) copy of the data -- 20 GB for the 10M x 1K perftest
+matrix -- and break the 16-byte row alignment the streaming kernels rely on.  The compiler
+rewrites `cbind(X, matrix(c, rows=nrow(X), cols=1))` into `_cbind_const(X, c)`
+(compiler/rewrites.py); at run time that is a `ConstCol` view and every operator the
+algorithms apply to it is computed from X and c:
+    A %*% v          = X %*% v[1:D] + c v[D+1]
+    t(A) %*% y       = rbind(t(X) %*% y, c colSums(y))
+    t(A) %*% f(A v)  (mmchain / smgrad) = the same with the fused kernels on X
+    t(A) %*% A       = [[t(X) X, c t(colSums(X))], [c colSums(X), N c^2]]
+    f(A), A op s     = ConstCol(f(X), f(c)),  ConstCol(X op s, c op s)
+    row / col / full aggregates from those of X
+Any other operator materialises the matrix (SP.densify), so semantics never change.
+(Reference analogue: none -- SystemML materialises the cbind; this is an MI355X-side layout
+choice.)
+"""
+from __future__ import annotations
+
+import torch
+
+from ..runtime import scalars as S
+
+
+class ConstCol:
+    __slots__ = ("X", "c")
+
+    def __init__(self, X, c):
+        self.X = X
+        self.c = float(c)
+
+    @property
+    def shape(self):
+        return (self.X.shape[0], self.X.shape[1] + 1)
+
+    @property
+    def dtype(self):
+        return self.X.dtype
+
+    @property
+    def device(self):
+        return self.X.device
+
+    @property
+    def is_cuda(self):
+        return self.X.is_cuda
+
+    def materialize(self):
+        X = _C().cvt(self.X)
+        col = torch.full((X.shape[0], 1), self.c, dtype=X.dtype, device=X.device)
+        return torch.cat([X, col], 1)
+
+    def __repr__(self):
+        return f"ConstCol({tuple(self.X.shape)} + const {self.c})"
+
+
+def is_cc(x):
+    return type(x) is ConstCol
+
+
+def _C():
+    from . import core
+    return core
+
+
+def make(X, c):
+    """cbind(X, c * ones(nrow(X), 1)); small matrices are simply concatenated."""
+    from . import sparse as SP
+    C = _C()
+    c = float(S.as_double(c))
+    if C.is_dist(X):
+        loc = C.cvt(SP.densify(X.local))
+        return X.like(torch.cat([loc, torch.full((loc.shape[0], 1), c, dtype=loc.dtype, device=loc.device)], 1))
+    if isinstance(X, torch.Tensor) and X.layout == torch.strided and X.numel() >= (1 << 20):
+        return ConstCol(X, c)
+    X = C.cvt(SP.densify(X))
+    return torch.cat([X, torch.full((X.shape[0], 1), c, dtype=X.dtype, device=X.device)], 1)
+
+
+def _split(v):
+    """v (D+1 x K) -> (v[1:D], v[D+1] as 1 x K)."""
+    return v[:-1], v[-1:]
+
+
+def mm(a, b, transA=False):
+    C = _C()
+    if is_cc(b):
+        b = b.materialize()
+        return C.mm(a, b, transA)
+    if transA:                                      # t(A) %*% y
+        y = C.cvt(b) if isinstance(b, torch.Tensor) else b
+        top = C.mm(a.X, y, True)
+        bot = a.c * C.agg("sum", "col", y)
+        return torch.cat([C.cvt(top), C.cvt(bot).to(C.cvt(top).device)], 0)
+    v = C.cvt(b)
+    vx, vc = _split(v)
+    u = C.mm(a.X, vx)
+    return C.binary("+", u, a.c * vc.to(u.device if isinstance(u, torch.Tensor) else vc.device))
+
+
+def tsmm(a, left=True):
+    C = _C()
+    if not left:
+        return C.tsmm(a.materialize(), False)
+    G = C.cvt(C.tsmm(a.X, True))
+    cs = C.cvt(C.agg("sum", "col", a.X)).to(G.device)
+    n = a.X.shape[0]
+    top = torch.cat([G, a.c * cs.t()], 1)
+    bot = torch.cat([a.c * cs, torch.full((1, 1), n * a.c * a.c, dtype=G.dtype, device=G.device)], 1)
+    return torch.cat([top, bot], 0)
+
+
+def mmchain(ctype, X, v, w=None):
+    """t(A) %*% g(A %*% v) for A = ConstCol: the product A v and the final t(A) g each run on
+    X with the streaming kernels, the constant column is added / reduced on the side."""
+    C = _C()
+    u = mm(X, v)
+    if ctype == "XtXv":
+        g = u
+    elif ctype == "XtwXv":
+        g = C.binary("*", w, u)
+    elif ctype == "XtXvy":
+        g = C.binary("-", u, w)
+    elif ctype == "XtPSXv":
+        q = C.binary("*", w, u)
+        g = C.binary("-", q, C.binary("*", w, C.agg("sum", "row", q)))
+    else:
+        raise ValueError(ctype)
+    return mm(X, g, transA=True)
+
+
+def smgrad(X, V, Y, kc):
+    C = _C()
+    u = C.cvt(mm(X, V))
+    lt = torch.cat([u, torch.zeros((u.shape[0], 1), dtype=u.dtype, device=u.device)], dim=1)
+    lt = lt - lt.max(dim=1, keepdim=True).values
+    e = torch.exp(lt)
+    p = e / e.sum(dim=1, keepdim=True)
+    g = C.binary("-", p[:, :kc], Y)
+    return u, mm(X, g, transA=True)
+
+
+def unary(op, a):
+    C = _C()
+    if op in ("nrow", "ncol", "length"):
+        r, c = a.shape
+        return {"nrow": r, "ncol": c, "length": r * c}[op]
+    if op.startswith("cast_") or op in ("cumsum", "cumprod", "cummin", "cummax"):
+        return C.unary(op, a.materialize())
+    fx = C.unary(op, a.X)
+    return ConstCol(fx, float(S.as_double(C.unary(op, a.c))))
+
+
+def binary(op, a, b):
+    C = _C()
+    if is_cc(a) and not isinstance(b, (torch.Tensor, ConstCol)) and not C.is_dist(b):
+        return ConstCol(C.binary(op, a.X, b), float(S.as_double(S.binary(op, a.c, S.as_double(b)))))
+    if is_cc(b) and not isinstance(a, (torch.Tensor, ConstCol)) and not C.is_dist(a):
+        return ConstCol(C.binary(op, a, b.X), float(S.as_double(S.binary(op, S.as_double(a), b.c))))
+    a = a.materialize() if is_cc(a) else a
+    b = b.materialize() if is_cc(b) else b
+    return C.binary(op, a, b)
+
+
+def agg(o, d, a):
+    C = _C()
+    n = a.X.shape[0]
+    if o in ("sum", "sumsq", "mean") :
+        cc = a.c * a.c if o == "sumsq" else a.c
+        base = "sumsq" if o == "sumsq" else "sum"
+        if d == "all":
+            s = float(S.as_double(C.agg(base, "all", a.X))) + n * cc
+            return s / (n * (a.X.shape[1] + 1)) if o == "mean" else s
+        if d == "row":
+            r = C.binary("+", C.agg(base, "row", a.X), cc)
+            return C.binary("/", r, a.X.shape[1] + 1) if o == "mean" else r
+        cs = C.cvt(C.agg(base, "col", a.X))
+        out = torch.cat([cs, torch.full((1, 1), n * cc, dtype=cs.dtype, device=cs.device)], 1)
+        return out / n if o == "mean" else out
+    return C.agg(o, d, a.materialize())
+
+
+def rix(a, rl, ru, cl, cu):
+    """A[rows, cols]: column ranges inside X stay views of X."""
+    C = _C()
+    D = a.X.shape[1]
+    c0 = C._bound(cl, 1)
+    c1 = C._bound(cu, D + 1)
+    if c1 <= D:
+        return C.rix(a.X, rl, ru, cl, c1)
+    if c0 == 1 and c1 == D + 1 and rl is None and ru is None:
+        return a
+    return C.rix(a.materialize(), rl, ru, cl, cu)

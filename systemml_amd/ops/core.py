@@ -279,7 +279,13 @@ def _dev_unary(op, x):
     return unary(op, x.value())
 
 
+from . import augmented as AUG   # noqa: E402  (cbind(X, const) views)
+_CC = AUG.ConstCol
+
+
 def binary(op, a, b):
+    if type(a) is _CC or type(b) is _CC:
+        return AUG.binary(op, a, b)
     # fast paths: two Python scalars; dense same-device same-dtype tensors (or tensor-scalar)
     ta_, tb_ = type(a), type(b)
     if ta_ in _PYNUM and tb_ in _PYNUM:
@@ -372,6 +378,8 @@ UN = {
 
 
 def unary(op, x):
+    if type(x) is _CC:
+        return AUG.unary(op, x)
     if type(x) is DevScalar:
         return _dev_unary(op, x)
     if CMP.is_compressed(x):
@@ -448,6 +456,8 @@ def _var(x, dim=None):
 
 
 def agg(o, d, x):
+    if type(x) is _CC:
+        return AUG.agg(o, d, x)
     if CMP.is_compressed(x):
         if o in ("sum", "sumsq", "mean"):
             sq = o == "sumsq"
@@ -564,6 +574,10 @@ def _need_mat(x, what):
 
 
 def mm(a, b, transA=False):
+    if type(a) is _CC or type(b) is _CC:
+        if type(a) is _CC:
+            return AUG.mm(a, b, transA)
+        b = b.materialize()
     if is_dist(a) or is_dist(b):
         return _dist().mm(a, b, transA)
     if CMP.is_compressed(a):
@@ -602,6 +616,8 @@ def mm(a, b, transA=False):
 
 
 def tsmm(x, left=True):
+    if type(x) is _CC:
+        return AUG.tsmm(x, left)
     if is_dist(x):
         return _dist().tsmm(x, left)
     if CMP.is_compressed(x):
@@ -620,6 +636,8 @@ def tsmm(x, left=True):
 
 def mmchain(ctype, X, v, w=None):
     """t(X) %*% f(X %*% v) fused chains (MapMultChain + codegen row template)."""
+    if type(X) is _CC:
+        return AUG.mmchain(ctype, X, v, w)
     if is_dist(X):
         return _dist().mmchain(ctype, X, v, w)
     if backend.use_kernels and isinstance(X, Tensor) and X.is_cuda and not SP.is_sparse(X):
@@ -634,6 +652,9 @@ def smgrad(X, V, Y, cu=None):
     """Fused multinomial-logreg candidate evaluation: returns (U, G) with U = X %*% V and
     G = t(X) %*% (P[, 1:cu] - Y), P = row-softmax of cbind(U, 0)  (the row template the
     compiler forms from MultiLogReg's line-search step, see rewrites.fuse_softmax_grad)."""
+    if type(X) is _CC:
+        K = V.shape[1]
+        return AUG.smgrad(X, V, Y, K if cu is None else int(S.as_double(cu)))
     if is_dist(X):
         return _dist().smgrad(X, V, Y, cu)
     K = V.shape[1] if hasattr(V, "shape") else None
@@ -678,6 +699,8 @@ def mmchain_ref(ctype, X, v, w=None):
 # reorg / indexing
 # ----------------------------------------------------------------------------
 def transpose(x):
+    if type(x) is _CC:
+        x = x.materialize()
     if is_dist(x):
         return _dist().transpose(x)
     if CMP.is_compressed(x):
@@ -706,6 +729,8 @@ def rix(x, rl, ru, cl, cu, list_mode=False):
         if lo == hi and (ru is rl or ru is None or list_mode):
             return x.get(lo)
         return x.slice(lo, hi)
+    if type(x) is _CC:
+        return AUG.rix(x, rl, ru, cl, cu)
     if is_dist(x):
         return _dist().rix(x, rl, ru, cl, cu)
     if isinstance(x, FrameBlock):
@@ -750,6 +775,10 @@ def lix(x, y, rl, ru, cl, cu, list_mode=False, owned=None):
                 data.append(None)
             data[i - 1] = y
         return ListObject(data, names)
+    if type(x) is _CC:
+        x = x.materialize()
+    if type(y) is _CC:
+        y = y.materialize()
     if is_dist(x) or is_dist(y):
         return _dist().lix(x, y, rl, ru, cl, cu)
     if hasattr(x, "columns") and hasattr(x, "set_slice"):   # frame target

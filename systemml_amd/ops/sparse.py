@@ -26,14 +26,18 @@ def densify(x):
     """Dense tensor of a sparse (CSR) or compressed (ops/compress.py) matrix."""
     if is_sparse(x):
         return x.to_dense()
-    if type(x).__name__ == "CompressedMatrix":
+    n = type(x).__name__
+    if n == "CompressedMatrix":
         return x.decompress()
+    if n == "ConstCol":
+        return x.materialize()
     return x
 
 
 def is_special(x) -> bool:
-    """Sparse or compressed representation (operators without a native path densify it)."""
-    return is_sparse(x) or type(x).__name__ == "CompressedMatrix"
+    """Sparse, compressed or constant-column (ops/augmented.py) representation: operators
+    without a native path densify it."""
+    return is_sparse(x) or type(x).__name__ in ("CompressedMatrix", "ConstCol")
 
 
 def nnz(x) -> int:

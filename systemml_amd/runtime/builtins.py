@@ -411,6 +411,16 @@ def b_cbind(ctx, *args, **kw):
     return torch.cat(ms, dim=1)
 
 
+@builtin("_cbind_const")
+def b_cbind_const(ctx, X, c, rows=None):
+    """cbind(X, matrix(c, rows=nrow(X), cols=1)) as a constant-column view (ops/augmented.py)."""
+    from ..ops import augmented as AUG
+    n = X.shape[0] if hasattr(X, "shape") else None
+    if rows is not None and n is not None and _int(rows) != n:
+        return b_cbind(ctx, X, b_matrix(ctx, c, rows, 1))     # shapes differ: the cbind's own error
+    return AUG.make(X, c)
+
+
 @builtin("rbind")
 def b_rbind(ctx, *args, **kw):
     if any(C.is_dist(a) for a in args):

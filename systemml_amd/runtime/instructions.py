@@ -20,6 +20,8 @@ from .scalars import DevScalar
 
 
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat"}
+# operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
+_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "rix", "t"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
@@ -42,7 +44,12 @@ def make_impl(h):
     lazy_ok = h.op in _LAZY_OK_OPS
     if sparse_ok and lazy_ok:
         return fn, code
-    is_sp = SP.is_special
+    if h.op in _CC_OK_OPS:
+        # constant-column views (ops/augmented.py) are handled by these operators themselves
+        def is_sp(x, _s=SP.is_special):
+            return _s(x) and type(x).__name__ != "ConstCol"
+    else:
+        is_sp = SP.is_special
     dense = SP.densify
     DS = DevScalar
 

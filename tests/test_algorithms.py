@@ -612,3 +612,31 @@ def test_step_glm_bernoulli(link, icpt):
     np.testing.assert_allclose(got, ref.x, atol=2e-4)
     np.testing.assert_allclose(r["dev"], 2 * ref.fun, rtol=1e-6)
     assert np.all(B[[c for c in range(m) if c not in cols], 0] == 0)
+
+
+@pytest.mark.parametrize("icpt", [1, 2])
+def test_intercept_column_is_a_view_and_matches_materialised(icpt):
+    """icpt = 1 | 2 append a ones column; the compiler turns it into a constant-column view
+    (ops/augmented.py) so X is never copied.  LinearRegCG and MultiLogReg produce the same
+    coefficients as with the materialised cbind (rewrites off)."""
+    import os
+    from systemml_amd.api.executor import compile_script, execute, explain
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.conf import DMLConfig
+    rng = np.random.default_rng(icpt)
+    X = rng.standard_normal((20000, 60)) + 0.5
+    y = X @ rng.standard_normal((60, 1)) + 1.0 + 0.1 * rng.standard_normal((20000, 1))
+    lab = (np.argmax(X[:, :3], 1) + 1).reshape(-1, 1).astype(float)
+    cases = [("LinearRegCG", {"X": X, "y": y}, dict(X="X", Y="y", B="B", icpt=icpt, maxi=20, tol=1e-12, reg=1e-3)),
+             ("MultiLogReg", {"X": X, "Y_vec": lab}, dict(X="X", Y="Y", B="B", icpt=icpt, moi=5, mii=5, reg=0.01))]
+    for name, ins, args in cases:
+        src = open(os.path.join(SCRIPTS_DIR, "algorithms", name + ".dml")).read()
+        outs = {}
+        for rw in (True, False):
+            cfg = DMLConfig(gpu=False, rewrites=rw)
+            cs = compile_script(src, args, inputs=ins, outputs=["B_out"], config=cfg)
+            if rw:
+                assert "_cbind_const" in explain(cs.cp, "hops"), name
+            res, _ = execute(cs, ins, out=lambda s: None)
+            outs[rw] = np.asarray(res["B_out"].double().numpy() if hasattr(res["B_out"], "numpy") else res["B_out"])
+        np.testing.assert_allclose(outs[True], outs[False], rtol=1e-7, atol=1e-9, err_msg=name)
