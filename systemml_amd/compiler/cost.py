@@ -98,6 +98,20 @@ def infer(h, dims, env):
         if o == "cast_matrix":
             return (1, 1) if ins[0] == SCALAR else ins[0]
         return ins[0]
+    if op == "cell":
+        mats = [x for x in ins if x != SCALAR]
+        if not mats or not all(_known(x) for x in mats):
+            d = UNK
+        else:
+            d = (max(x[0] for x in mats), max(x[1] for x in mats))
+        agg = h.p["prog"].agg
+        if not agg:
+            return d
+        if agg[1] == "all":
+            return SCALAR
+        if d == UNK:
+            return UNK
+        return (d[0], 1) if agg[1] == "row" else (1, d[1])
     if op == "agg":
         r, c = ins[0]
         d = h.p["dir"]

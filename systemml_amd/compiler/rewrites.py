@@ -563,6 +563,10 @@ def rewrite_block(bb, config=None):
         n = fuse_softmax_grad(bb)
         if n:
             rw.stats["softmax-grad"] = n
+        from .codegen import fuse_cells
+        n = fuse_cells(bb)
+        if n:
+            rw.stats["cell-fused-ops"] = n
     return rw.stats
 
 

@@ -55,7 +55,8 @@ def build_hip(force=False, verbose=True):
     bad = [c for c, p in zip(cmds, procs) if p.wait() != 0]
     if bad:
         raise subprocess.CalledProcessError(1, bad[0])
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs
+    # librtc: the run-time compiler of the generated fused kernels (ops/hip/rtc.hip)
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-lhiprtc"]
     subprocess.check_call(cmd)
     return out
 

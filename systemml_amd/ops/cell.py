@@ -1,0 +1,498 @@
+"""Fused cellwise operators at run time (reference: runtime/codegen/SpoofCellwise.java and the
+SpoofOperator / SpoofCUDA instructions that execute the classes the codegen compiler emits).
+
+A `CellProgram` is the lowered form of one fused DAG (compiler/codegen.py): the DAG's leaves
+are its inputs, preloaded into registers 0..n_in-1, and every fused binary / unary operator is
+one instruction (kind, op, dst, a, b) over at most 16 registers; an optional aggregate
+(sum / sumsq / mean / min / max over all cells, rows or columns) consumes the output register.
+
+On the MI355X the whole program runs as ONE pass over the output cells: every input is read
+once, intermediates stay in VGPRs, and only the result (or the aggregate) is written.  The
+kernel is GENERATED per program and operand signature (`generate`: the DAG as straight-line
+HIP code in a `Spec` struct over the templates of ops/hip/cell_rtc.inc), compiled once by
+hipRTC for the device's gfx target (ops/hip/rtc.hip) and cached in memory and on disk by the
+source hash -- the reference compiles its generated operator classes the same way.  When the
+run-time compiler is unavailable (or SYSML_CELL_RTC=0) the prebuilt register-program
+interpreter of ops/hip/cell.hip runs the same program.  Everywhere else -- CPU backend, sparse / compressed / constant-column /
+row-partitioned operands, shapes outside the broadcast modes the kernel supports -- the program
+runs instruction by instruction through ops/core.binary / unary / agg, i.e. exactly the
+operators the DAG had before fusion, so fusion never changes semantics or error behaviour.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import tempfile
+
+import torch
+
+from . import core as C
+from .backend import backend
+
+BIN_CODES = {"+": 1, "-": 2, "*": 3, "/": 4, "^": 5, "%%": 6, "%/%": 7, "==": 8, "!=": 9, "<": 10,
+             "<=": 11, ">": 12, ">=": 13, "&": 14, "|": 15, "xor": 16, "min": 17, "max": 18, "log": 19}
+UN_CODES = {"sq": 20,               # x ^ 2 (binary '^' with the literal 2, lowered to one multiply)
+            "neg": 32, "not": 33, "abs": 34, "exp": 35, "log": 36, "sqrt": 37, "round": 38, "floor": 39,
+            "ceil": 40, "sign": 41, "sin": 42, "cos": 43, "tan": 44, "asin": 45, "acos": 46, "atan": 47,
+            "sinh": 48, "cosh": 49, "tanh": 50, "sigmoid": 51}
+AGG_CODES = {"sum": 0, "sumsq": 1, "mean": 0, "min": 2, "max": 3}
+AGG_DIRS = {"all": 1, "row": 2, "col": 3}
+MAXIN, MAXOPS, NR = 8, 40, 16
+FULL, ROWV, COLV, HSCALAR, DSCALAR = range(5)
+
+stats = {"kernel": 0, "sequential": 0, "rtc_compiled": 0, "rtc_cache_hits": 0, "rtc_launches": 0,
+         "interpreter_launches": 0}
+RTC = os.environ.get("SYSML_CELL_RTC", "1") != "0"
+RTC_DIR = os.environ.get("SYSML_RTC_CACHE", os.path.join(tempfile.gettempdir(), "systemml_amd_rtc"))
+
+# C expressions of the operators ({a}, {b}: operand expressions of type T)
+_C_BIN = {"+": "({a} + {b})", "-": "({a} - {b})", "*": "({a} * {b})", "/": "({a} / {b})", "^": "pow({a}, {b})",
+          "%%": "sysml_rem<T>({a}, {b})", "%/%": "floor({a} / {b})", "==": "sysml_b<T>({a} == {b})",
+          "!=": "sysml_b<T>({a} != {b})", "<": "sysml_b<T>({a} < {b})", "<=": "sysml_b<T>({a} <= {b})",
+          ">": "sysml_b<T>({a} > {b})", ">=": "sysml_b<T>({a} >= {b})",
+          "&": "sysml_b<T>({a} != T(0) && {b} != T(0))", "|": "sysml_b<T>({a} != T(0) || {b} != T(0))",
+          "xor": "sysml_b<T>(({a} != T(0)) != ({b} != T(0)))", "min": "sysml_min<T>({a}, {b})",
+          "max": "sysml_max<T>({a}, {b})", "log": "(log({a}) / log({b}))"}
+_C_UN = {"sq": "({a} * {a})", "neg": "(-{a})", "not": "sysml_b<T>({a} == T(0))", "abs": "fabs({a})",
+         "exp": "exp({a})", "log": "log({a})", "sqrt": "sqrt({a})", "round": "floor({a} + T(0.5))",
+         "floor": "floor({a})", "ceil": "ceil({a})", "sign": "(T)(({a} > T(0)) - ({a} < T(0)))",
+         "sin": "sin({a})", "cos": "cos({a})", "tan": "tan({a})", "asin": "asin({a})", "acos": "acos({a})",
+         "atan": "atan({a})", "sinh": "sinh({a})", "cosh": "cosh({a})", "tanh": "tanh({a})",
+         "sigmoid": "(T(1) / (T(1) + exp(-{a})))"}
+
+
+class CellProgram:
+    """ops: tuple of (kind 'b' | 'u', op, dst, a, b) register instructions; n_in: inputs in
+    registers 0..n_in-1; out: result register; agg: None or (op, 'all' | 'row' | 'col')."""
+    __slots__ = ("ops", "n_in", "out", "agg", "_code")
+
+    def __init__(self, ops, n_in, out, agg=None):
+        self.ops = tuple(tuple(x) for x in ops)
+        self.n_in = n_in
+        self.out = out
+        self.agg = tuple(agg) if agg else None
+        self._code = {}
+
+    def key(self):
+        return (self.ops, self.n_in, self.out, self.agg)
+
+    def __eq__(self, other):
+        return isinstance(other, CellProgram) and self.key() == other.key()
+
+    def __hash__(self):
+        return hash(self.key())
+
+    def describe(self):
+        body = ",".join(o for _, o, _, _, _ in self.ops)
+        return f"cell[{body}]" + (f"|{self.agg[0]}-{self.agg[1]}" if self.agg else "")
+
+    def __repr__(self):
+        return self.describe()
+
+    def device_code(self, device):
+        """The instructions as an int32 (n_ops x 4) HBM array, uploaded once per device."""
+        t = self._code.get(device)
+        if t is None:
+            rows = []
+            for kind, o, d, a, b in self.ops:
+                op = BIN_CODES[o] if kind == "b" else UN_CODES[o]
+                for r in (d, a, b):
+                    if not 0 <= r < NR:
+                        raise ValueError(f"cell program register {r} out of range")
+                rows.append([op, d, a, b])
+            t = torch.tensor(rows or [[0, 0, 0, 0]], dtype=torch.int32).to(device)
+            self._code[device] = t
+        return t
+
+
+# ----------------------------------------------------------------------------- evaluation
+def evaluate(prog: CellProgram, args):
+    r = _kernel(prog, args) if backend.use_kernels else None
+    if r is not None:
+        stats["kernel"] += 1
+        return r
+    stats["sequential"] += 1
+    return sequential(prog, args)
+
+
+def sequential(prog: CellProgram, args):
+    """The fused DAG's original operators, one after the other."""
+    regs = list(args) + [None] * (NR - len(args))
+    for kind, o, d, a, b in prog.ops:
+        if kind == "b":
+            regs[d] = C.binary(o, regs[a], regs[b])
+        elif o == "sq":
+            regs[d] = C.binary("^", regs[a], 2)
+        else:
+            regs[d] = C.unary(o, regs[a])
+    r = regs[prog.out]
+    if prog.agg:
+        r = C.agg(prog.agg[0], prog.agg[1], r)
+    return r
+
+
+def _bin_ok(sa, sb):
+    """ops/core._check_bin_dims: the operand shapes a cellwise binary operator accepts."""
+    if sa == sb:
+        return True
+    (ra, ca), (rb, cb) = sa, sb
+    return ((ra == rb and (ca == 1 or cb == 1)) or (ca == cb and (ra == 1 or rb == 1)) or
+            (ra == 1 and ca == 1) or (rb == 1 and cb == 1) or (ca == 1 and rb == 1) or (ra == 1 and cb == 1))
+
+
+def out_shape(prog: CellProgram, shapes):
+    """Result shape of the program for input shapes (None: scalar); None if an operator would
+    reject its operands (the sequential path then raises the operator's own error)."""
+    regs = list(shapes) + [None] * (NR - len(shapes))
+    for kind, _, d, a, b in prog.ops:
+        if kind == "u":
+            regs[d] = regs[a]
+            continue
+        sa, sb = regs[a], regs[b]
+        if sa is None:
+            regs[d] = sb
+        elif sb is None:
+            regs[d] = sa
+        elif _bin_ok(sa, sb):
+            regs[d] = (max(sa[0], sb[0]), max(sa[1], sb[1]))
+        else:
+            return None
+    return regs[prog.out]
+
+
+class _In(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_void_p), ("s", ctypes.c_double), ("mode", ctypes.c_int), ("dtype", ctypes.c_int),
+                ("vec", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+class _Prog(ctypes.Structure):
+    _fields_ = [("inp", _In * MAXIN), ("rows", ctypes.c_int64), ("cols", ctypes.c_int64), ("total", ctypes.c_int64),
+                ("n_in", ctypes.c_int), ("n_ops", ctypes.c_int), ("out", ctypes.c_int), ("aggop", ctypes.c_int),
+                ("need_ij", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+_DT = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2}
+_Tensor = torch.Tensor
+_checked = []
+
+
+def _lib():
+    from . import kernels
+    L = kernels.load(required=True)
+    if not _checked:
+        L.sysml_cell.restype = ctypes.c_int
+        L.sysml_cell.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+        L.sysml_cell_blocks.restype = ctypes.c_int64
+        L.sysml_cell_blocks.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
+        L.sysml_cell_prog_size.restype = ctypes.c_int
+        if L.sysml_cell_prog_size() != ctypes.sizeof(_Prog):
+            raise RuntimeError("cell.hip Prog layout does not match ops/cell.py")
+        _checked.append(True)
+    return L
+
+
+# ----------------------------------------------------------------------------- code generation
+def _cases(vals):
+    expr = str(vals[-1])
+    for k in range(len(vals) - 2, -1, -1):
+        expr = f"(k == {k}) ? {vals[k]} : {expr}"
+    return expr
+
+
+def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant):
+    """HIP source of the fused kernel: the program as straight-line code over the cell values
+    of its inputs, instantiated into the flat / row / column kernel template."""
+    ct = "float" if T == torch.float32 else "double"
+    var = [f"x[{k}]" for k in range(prog.n_in)] + [None] * (NR - prog.n_in)
+    body = []
+    for q, (kind, o, d, a, b) in enumerate(prog.ops):
+        e = (_C_BIN[o] if kind == "b" else _C_UN[o]).format(a=var[a], b=var[b] if kind == "b" else "")
+        body.append(f"    const T v{q} = {e};")
+        var[d] = f"v{q}"
+    aggop = AGG_CODES[prog.agg[0]] if prog.agg else 0
+    need_ij = int(any(m in (ROWV, COLV) for m in modes))
+    if mode == 0:
+        call = "sysml_cell_flat<Spec, 0>(A);"
+    elif mode == 1:
+        call = "sysml_cell_flat<Spec, 1>(A);"
+    elif mode == 2:
+        call = f"sysml_cell_row<Spec, {variant}>(A);"
+    else:
+        call = f"sysml_cell_col<Spec, {variant}>(A);"
+    return (_prelude() + f"""
+// generated: {prog.describe()}
+struct Spec {{
+  typedef {ct} T;
+  static constexpr int NIN = {prog.n_in};
+  static constexpr int AGGOP = {aggop};
+  static constexpr int NEED_IJ = {need_ij};
+  static constexpr int mode(int k) {{ return {_cases(modes)}; }}
+  static constexpr int dt(int k) {{ return {_cases(dts)}; }}
+  static constexpr int vec(int k) {{ return {_cases(vecs)}; }}
+  static __device__ __forceinline__ T f(const T (&x)[NIN]) {{
+{chr(10).join(body)}
+    return {var[prog.out]};
+  }}
+}};
+
+extern "C" __global__ void __launch_bounds__(256) sysml_cell_k(const SysmlCellArgs A) {{ {call} }}
+""")
+
+
+_PRELUDE = []
+
+
+def _prelude():
+    if not _PRELUDE:
+        here = os.path.dirname(os.path.abspath(__file__))
+        with open(os.path.join(here, "hip", "cell_rtc.inc")) as f:
+            _PRELUDE.append("#pragma clang fp contract(off)\n" + f.read())
+    return _PRELUDE[0]
+
+
+class _RtcArgs(ctypes.Structure):
+    _fields_ = [("inp", ctypes.c_void_p * MAXIN), ("s", ctypes.c_double * MAXIN), ("rows", ctypes.c_int64),
+                ("cols", ctypes.c_int64), ("total", ctypes.c_int64), ("chunk", ctypes.c_int64),
+                ("out", ctypes.c_void_p), ("part", ctypes.c_void_p)]
+
+
+_rtc_funcs = {}
+_rtc_bound = []
+_arch = {}
+
+
+def _rtc_lib():
+    from . import kernels
+    L = kernels.load(required=True)
+    if not _rtc_bound:
+        L.sysml_rtc_compile.restype = ctypes.c_int
+        L.sysml_rtc_compile.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                        ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                        ctypes.c_char_p, ctypes.c_size_t]
+        L.sysml_rtc_code.restype = ctypes.c_int
+        L.sysml_rtc_code.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.sysml_rtc_load.restype = ctypes.c_int
+        L.sysml_rtc_load.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+        L.sysml_rtc_launch.restype = ctypes.c_int
+        L.sysml_rtc_launch.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p,
+                                       ctypes.c_size_t, ctypes.c_void_p]
+        _rtc_bound.append(True)
+    return L
+
+
+def gpu_arch(dev=None):
+    """gfx target of the device (e.g. 'gfx950'); the code objects are built for it."""
+    k = str(dev)
+    a = _arch.get(k)
+    if a is None:
+        try:
+            a = torch.cuda.get_device_properties(dev).gcnArchName.split(":")[0] or "gfx950"
+        except Exception:
+            a = "gfx950"
+        _arch[k] = a
+    return a
+
+
+def compile_source(src, arch):
+    """Code object bytes of `src` (hipRTC), through the on-disk cache keyed by source + arch."""
+    L = _rtc_lib()
+    h = hashlib.sha1((arch + "\0" + src).encode()).hexdigest()
+    path = os.path.join(RTC_DIR, f"cell-{h}.co")
+    try:
+        with open(path, "rb") as f:
+            stats["rtc_cache_hits"] += 1
+            return f.read()
+    except OSError:
+        pass
+    handle, size = ctypes.c_void_p(), ctypes.c_size_t()
+    log = ctypes.create_string_buffer(8192)
+    rc = L.sysml_rtc_compile(src.encode(), b"sysml_cell.hip", arch.encode(), ctypes.byref(handle),
+                             ctypes.byref(size), log, len(log))
+    if rc != 0:
+        raise RuntimeError(f"hipRTC compilation failed ({rc}): {log.value.decode(errors='replace')[:2000]}")
+    buf = ctypes.create_string_buffer(size.value)
+    rc = L.sysml_rtc_code(handle, buf)
+    if rc != 0:
+        raise RuntimeError(f"hipRTC code retrieval failed ({rc})")
+    code = buf.raw
+    stats["rtc_compiled"] += 1
+    try:
+        os.makedirs(RTC_DIR, exist_ok=True)
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(code)
+        os.replace(tmp, path)
+    except OSError:
+        pass
+    return code
+
+
+def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev):
+    key = (prog.key(), T, modes, dts, vecs, mode, variant, str(dev))
+    f = _rtc_funcs.get(key, False)
+    if f is not False:
+        return f
+    try:
+        code = compile_source(generate(prog, T, modes, dts, vecs, mode, variant), gpu_arch(dev))
+        L = _rtc_lib()
+        fn = ctypes.c_void_p()
+        cbuf = ctypes.create_string_buffer(code, len(code))
+        rc = L.sysml_rtc_load(cbuf, b"sysml_cell_k", ctypes.byref(fn))
+        if rc != 0:
+            raise RuntimeError(f"hipModuleLoadData failed ({rc})")
+        f = (fn, cbuf)
+    except RuntimeError as e:                 # interpreter kernel instead, once per signature
+        import warnings
+        warnings.warn(f"fused cell kernel not compiled, using the interpreter: {e}")
+        f = None
+    _rtc_funcs[key] = f
+    return f
+
+
+def _kernel(prog: CellProgram, args):
+    """One launch of the cell kernel, or None when the operands are outside its scope."""
+    from ..runtime.scalars import DevScalar
+    if len(args) != prog.n_in or len(prog.ops) > MAXOPS or prog.n_in > MAXIN:
+        return None
+    dev = None
+    shapes = []
+    f64 = False
+    bf16 = False
+    for x in args:
+        tx = type(x)
+        if tx is _Tensor:
+            if not x.is_cuda or x.layout is not torch.strided or x.dim() != 2 or x.dtype not in _DT:
+                return None
+            if dev is None:
+                dev = x.device
+            elif x.device != dev:
+                return None
+            f64 = f64 or x.dtype == torch.float64
+            bf16 = bf16 or x.dtype == torch.bfloat16
+            shapes.append(tuple(x.shape))
+        elif tx is DevScalar:
+            if not x.t.is_cuda or x.t.dtype not in _DT:
+                return None
+            shapes.append(None)
+        elif tx is float or tx is int or tx is bool:
+            shapes.append(None)
+        else:
+            return None
+    if dev is None:
+        return None
+    shp = out_shape(prog, shapes)
+    if shp is None:
+        return None
+    R, Cc = shp
+    if R <= 0 or Cc <= 0:
+        return None
+    T = torch.float64 if (f64 or (bf16 and backend.dtype == torch.float64)) else torch.float32
+    P = _Prog()
+    keep = []
+    need_ij = 0
+    for k, x in enumerate(args):
+        e = P.inp[k]
+        tx = type(x)
+        if tx is _Tensor:
+            if not x.is_contiguous():
+                x = x.contiguous()
+            keep.append(x)
+            r, c = x.shape
+            e.p = x.data_ptr()
+            e.dtype = _DT[x.dtype]
+            if (r, c) == (R, Cc):
+                e.mode = FULL
+                e.vec = int(e.p % 16 == 0)
+            elif r == 1 and c == 1:
+                e.mode = DSCALAR
+            elif r == 1 and c == Cc:
+                e.mode = ROWV
+                need_ij = 1
+            elif c == 1 and r == R:
+                e.mode = COLV
+                need_ij = 1
+            else:
+                return None
+        elif tx is DevScalar:
+            t = x.t.reshape(1)
+            keep.append(t)
+            e.p = t.data_ptr()
+            e.dtype = _DT[t.dtype]
+            e.mode = DSCALAR
+        else:
+            e.mode = HSCALAR
+            e.s = float(x)
+    P.rows, P.cols, P.total = R, Cc, R * Cc
+    P.n_in, P.n_ops, P.out = prog.n_in, len(prog.ops), prog.out
+    P.need_ij = need_ij
+    agg = prog.agg
+    mode = 0
+    if agg:
+        P.aggop = AGG_CODES[agg[0]]
+        mode = AGG_DIRS[agg[1]]
+    L = _lib()
+    nblk = L.sysml_cell_blocks(mode, R, Cc)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    dt = 0 if T == torch.float32 else 1
+    out = part = None
+    if mode == 0:
+        out = torch.empty((R, Cc), dtype=T, device=dev)
+    elif mode == 1:
+        part = torch.empty(nblk, dtype=torch.float64, device=dev)
+    elif mode == 2:
+        out = torch.empty((R, 1), dtype=T, device=dev)
+    else:
+        part = torch.empty((nblk, Cc), dtype=torch.float64, device=dev)
+    launched = False
+    if RTC:
+        modes = tuple(P.inp[k].mode for k in range(prog.n_in))
+        dts = tuple(P.inp[k].dtype for k in range(prog.n_in))
+        vecs = tuple(P.inp[k].vec for k in range(prog.n_in))
+        if mode == 2:
+            variant = 1 if Cc <= 8 else (4 if Cc <= 32 else (16 if Cc <= 128 else 64))
+        elif mode == 3:
+            variant = 8 if Cc <= 8 else 64
+        else:
+            variant = 0
+        f = _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev)
+        if f is not None:
+            A = _RtcArgs()
+            for k in range(prog.n_in):
+                A.inp[k] = P.inp[k].p
+                A.s[k] = P.inp[k].s
+            A.rows, A.cols, A.total = R, Cc, R * Cc
+            A.chunk = (R + nblk - 1) // nblk
+            A.out = out.data_ptr() if out is not None else 0
+            A.part = part.data_ptr() if part is not None else 0
+            gx, gy = (nblk, 1) if mode != 3 else ((Cc + variant - 1) // variant, nblk)
+            rc = _rtc_lib().sysml_rtc_launch(f[0], gx, gy, 256, ctypes.byref(A), ctypes.sizeof(A), st)
+            if rc != 0:
+                raise RuntimeError(f"fused cell kernel launch failed: {rc}")
+            stats["rtc_launches"] += 1
+            launched = True
+    if not launched:
+        code = prog.device_code(dev)
+        rc = L.sysml_cell(dt, mode, ctypes.byref(P), code.data_ptr(), out.data_ptr() if out is not None else 0,
+                          part.data_ptr() if part is not None else 0, nblk, st)
+        if rc != 0:
+            raise RuntimeError(f"sysml_cell failed: {rc}")
+        stats["interpreter_launches"] += 1
+    from . import kernels
+    kernels._count("cell")
+    del keep
+    if mode == 0:
+        return out
+    o = agg[0]
+    if mode == 1:
+        r = part.sum() if AGG_CODES[o] <= 1 else (part.min() if o == "min" else part.max())
+        if o == "mean":
+            r = r / (R * Cc)
+        return C._lazy_out(r)
+    if mode == 2:
+        return out / Cc if o == "mean" else out
+    r = part.sum(0, keepdim=True) if AGG_CODES[o] <= 1 else (part.amin(0, keepdim=True) if o == "min"
+                                                             else part.amax(0, keepdim=True))
+    r = r.to(T)
+    return r / R if o == "mean" else r

@@ -19,15 +19,15 @@ from . import builtins as B
 from .scalars import DevScalar
 
 
-_SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat"}
+_SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
-_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "rix", "t"}
+_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "rix", "t", "cell"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
-_LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "t", "tak"}
+_LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "t", "tak", "cell"}
 # operators that compute on matrix operands (placement applies); the rest move values around
-_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "wquat", "tak", "t", "rix", "lix", "bi"}
+_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "wquat", "tak", "t", "rix", "lix", "bi", "cell"}
 transfer_stats = {"h2d": 0, "d2h": 0, "h2d_bytes": 0, "d2h_bytes": 0}   # -stats (utils/stats.gpu_report)
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
@@ -190,6 +190,13 @@ def _make_impl(h):
         return (lambda ctx, a: Q.execute(p, a)), "wquat-" + p["kind"]
     if op == "tak":
         return (lambda ctx, a: C.tak(a[0], a[1])), "tak+*"
+    if op == "cell":
+        # fused cellwise DAG (compiler/codegen.py): one ops/hip/cell.hip pass on the MI355X;
+        # sparse / compressed / constant-column / distributed operands run the original
+        # operators one by one (ops/cell.sequential)
+        from ..ops import cell as CELL
+        prog = p["prog"]
+        return (lambda ctx, a: CELL.evaluate(prog, a)), "spoofCell"
     if op == "t":
         return (lambda ctx, a: C.transpose(a[0])), "r'"
     if op == "rix":

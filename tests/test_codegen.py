@@ -1,0 +1,238 @@
+"""Cell-template operator fusion (compiler/codegen.py, ops/cell.py, ops/hip/cell.hip).
+
+Reference tests: src/test/java/org/apache/sysml/test/integration/functions/codegen/
+CellwiseTmplTest.java (fused cellwise DAGs with none / full / row / column aggregation must
+match the unfused plan and must show up as spoof operators in the plan).  CPU: plan shape and
+exact equality with fusion disabled.  GPU: one HIP kernel per fused DAG against an fp64 torch
+evaluation of the same operators, every opcode, broadcast mode, input dtype and aggregate."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from systemml_amd.api import executor as EX
+from systemml_amd.conf import DMLConfig
+
+SCRIPT = """
+Z = exp(X * 2 - y) / (1 + abs(X)) + w
+s = sum((X - 0.5)^2 * y + sqrt(abs(X)))
+r = rowSums(sigmoid(X) * X - w)
+c = colMeans(log(abs(X) + 1) * y)
+mx = max(tanh(X) - X %% 0.3)
+mn = rowMins(floor(X * 3) + (X > 0.5))
+q = sum(Z) + s + sum(r) + sum(c) + mx + sum(mn)
+"""
+
+
+def _run(cfg, n=57, m=13):
+    rng = np.random.default_rng(n * m)
+    ins = {"X": rng.uniform(-1, 2, (n, m)), "y": rng.uniform(0.5, 1.5, (n, 1)), "w": rng.uniform(0, 1, (1, m))}
+    cs = EX.compile_script(SCRIPT, {}, inputs=ins, outputs=["q", "Z", "r", "c"], config=cfg)
+    res, _ = EX.execute(cs, ins)
+    return cs, res
+
+
+def _fused_hops(cs):
+    text = EX.explain(cs.cp, "hops")
+    return [ln for ln in text.splitlines() if "cell[" in ln]
+
+
+def test_cell_plans_and_parity_with_unfused():
+    cs, res = _run(DMLConfig(gpu=False))
+    fused = _fused_hops(cs)
+    # Z (block output), full-sum, row / col aggregates, max, rowMins
+    assert any("|sum-all" in ln for ln in fused), fused
+    assert any("|sum-row" in ln for ln in fused), fused
+    assert any("|mean-col" in ln for ln in fused), fused
+    assert any("|max-all" in ln for ln in fused), fused
+    assert any("|min-row" in ln for ln in fused), fused
+    cs0, ref = _run(DMLConfig(gpu=False, fusion=False))
+    assert not _fused_hops(cs0)
+    for k in ("q", "Z", "r", "c"):
+        a, b = res[k], ref[k]
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b), k
+        else:
+            assert a == b, k
+
+
+def test_shared_intermediates_are_materialised():
+    src = """
+    X = rand(rows=20, cols=4, seed=5)
+    T = exp(X) + 1
+    a = sum(T * 2)
+    b = sum(T / 3)
+    print(a + b)
+    """
+    cs = EX.compile_script(src, {}, config=DMLConfig(gpu=False))
+    fused = _fused_hops(cs)
+    # T has two consumers: it is computed once, each aggregate fuses only its own operator
+    assert len(fused) == 3, fused
+    assert any("cell[exp,+]" in ln for ln in fused)
+
+
+def test_sequential_fallback_errors_like_unfused():
+    src = """
+    X = rand(rows=5, cols=3, seed=1)
+    Y = rand(rows=4, cols=3, seed=2)
+    Z = exp(X) + Y * 2
+    print(sum(Z))
+    """
+    with pytest.raises(Exception) as e1:
+        EX.run(src, config=DMLConfig(gpu=False))
+    assert "5x3" in str(e1.value) and "4x3" in str(e1.value)
+
+
+# ----------------------------------------------------------------------------- GPU kernel
+def _ref_eval(prog, args):
+    """fp64 torch evaluation of a CellProgram (the test's independent reference)."""
+    import systemml_amd.ops.core as C
+    B = {"+": torch.add, "-": torch.sub, "*": torch.mul, "/": torch.div, "^": torch.pow,
+         "%%": torch.remainder, "%/%": lambda a, b: torch.floor(a / b),
+         "==": lambda a, b: (a == b).double(), "!=": lambda a, b: (a != b).double(),
+         "<": lambda a, b: (a < b).double(), "<=": lambda a, b: (a <= b).double(),
+         ">": lambda a, b: (a > b).double(), ">=": lambda a, b: (a >= b).double(),
+         "&": lambda a, b: ((a != 0) & (b != 0)).double(), "|": lambda a, b: ((a != 0) | (b != 0)).double(),
+         "xor": lambda a, b: ((a != 0) ^ (b != 0)).double(), "min": torch.minimum, "max": torch.maximum,
+         "log": lambda a, b: torch.log(a) / torch.log(b)}
+    U = dict(C.UN)
+    U["sq"] = lambda x: x * x
+    regs = []
+    for a in args:
+        if isinstance(a, torch.Tensor):
+            regs.append(a.double().cpu())
+        else:
+            regs.append(torch.tensor(float(a), dtype=torch.float64))
+    regs += [None] * (16 - len(regs))
+    for kind, o, d, a, b in prog.ops:
+        regs[d] = B[o](regs[a], regs[b]) if kind == "b" else U[o](regs[a])
+    r = regs[prog.out]
+    if prog.agg:
+        o, dr = prog.agg
+        dim = None if dr == "all" else (1 if dr == "row" else 0)
+        f = {"sum": torch.sum, "sumsq": lambda t, **k: torch.sum(t * t, **k), "mean": torch.mean,
+             "min": torch.amin, "max": torch.amax}[o]
+        r = f(r) if dim is None else f(r, dim=dim, keepdim=True)
+    return r
+
+
+BIN_OPS = ["+", "-", "*", "/", "^", "%%", "%/%", "==", "!=", "<", "<=", ">", ">=", "&", "|", "xor", "min",
+           "max", "log"]
+UN_OPS = ["sq", "neg", "not", "abs", "exp", "log", "sqrt", "round", "floor", "ceil", "sign", "sin", "cos",
+          "tan", "asin", "acos", "atan", "sinh", "cosh", "tanh", "sigmoid"]
+
+
+def _mk(shape, dt, seed, lo=0.2, hi=1.7):
+    g = torch.Generator().manual_seed(seed)
+    t = torch.rand(shape, generator=g, dtype=torch.float64) * (hi - lo) + lo
+    return t.to(dt)
+
+
+def _check(prog, args, dt_out, tol, rtc=True):
+    from systemml_amd.ops import cell, kernels
+    from systemml_amd.ops.backend import backend
+    cell.RTC = rtc
+    n_rtc = cell.stats["rtc_launches"]
+    backend.configure(DMLConfig(gpu=True, precision="single" if dt_out == torch.float32 else "double"))
+    dev = torch.device("cuda:0")
+    dargs = [a.to(dev) if isinstance(a, torch.Tensor) else a for a in args]
+    c0 = kernels.counters.get("cell", 0)
+    try:
+        got = cell._kernel(prog, dargs)
+    finally:
+        cell.RTC = True
+    assert got is not None
+    torch.cuda.synchronize()
+    assert kernels.counters.get("cell", 0) == c0 + 1
+    assert cell.stats["rtc_launches"] == n_rtc + (1 if rtc else 0)     # generated kernel vs interpreter
+    ref = _ref_eval(prog, [a.double() if isinstance(a, torch.Tensor) else a for a in args])
+    g = torch.as_tensor(got.value() if hasattr(got, "value") else got, dtype=torch.float64).cpu()
+    if isinstance(got, torch.Tensor):
+        assert got.dtype == dt_out
+    ref = ref.reshape(g.shape)
+    fin = torch.isfinite(ref)
+    assert torch.equal(torch.isnan(g), torch.isnan(ref))
+    scale = ref[fin].abs().max().item() + 1e-30 if fin.any() else 1.0
+    err = ((g[fin] - ref[fin]).abs().max().item() / scale) if fin.any() else 0.0
+    assert err < tol, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,tol", [(torch.float64, 1e-12), (torch.float32, 2e-6)])
+@pytest.mark.parametrize("op", BIN_OPS)
+def test_cell_kernel_binary_ops(op, dt, tol):
+    from systemml_amd.ops.cell import CellProgram
+    # (X op Y) * 1.5 over a ragged 37 x 29 matrix
+    prog = CellProgram([("b", op, 3, 0, 1), ("b", "*", 3, 3, 2)], 3, 3)
+    X, Y = _mk((37, 29), dt, 1), _mk((37, 29), dt, 2)
+    if op in ("==", "!=", "<=", ">="):
+        Y[::3] = X[::3]
+    _check(prog, [X, Y, 1.5], dt, tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rtc", [True, False])
+@pytest.mark.parametrize("dt,tol", [(torch.float64, 1e-12), (torch.float32, 4e-6)])
+@pytest.mark.parametrize("op", UN_OPS)
+def test_cell_kernel_unary_ops(op, dt, tol, rtc):
+    from systemml_amd.ops.cell import CellProgram
+    lo, hi = (-0.9, 0.9) if op in ("asin", "acos", "atanh") else (-2.5, 2.5)
+    if op in ("log", "sqrt"):
+        lo, hi = 0.05, 3.0
+    prog = CellProgram([("u", op, 1, 0, 0), ("b", "+", 1, 1, 0)], 1, 1)
+    X = _mk((41, 23), dt, 3, lo, hi)
+    _check(prog, [X], dt, tol, rtc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", [None, ("sum", "all"), ("sumsq", "all"), ("mean", "all"), ("min", "all"),
+                                 ("max", "all"), ("sum", "row"), ("mean", "row"), ("max", "row"),
+                                 ("sum", "col"), ("min", "col"), ("mean", "col")])
+@pytest.mark.parametrize("shape", [(1000, 5), (3001, 7), (257, 130), (9, 1000), (4099, 1)])
+@pytest.mark.parametrize("rtc", [True, False])
+def test_cell_kernel_broadcast_and_aggregates(shape, agg, rtc):
+    from systemml_amd.ops.cell import CellProgram
+    from systemml_amd.runtime.scalars import DevScalar
+    n, m = shape
+    # exp(X * w - y) / (1 + abs(X)) - s  with w a row vector, y a column vector, s a 1x1 matrix
+    prog = CellProgram([("b", "*", 5, 0, 1), ("b", "-", 5, 5, 2), ("u", "exp", 5, 5, 0),
+                        ("u", "abs", 6, 0, 0), ("b", "+", 6, 6, 4), ("b", "/", 5, 5, 6),
+                        ("b", "-", 5, 5, 3)], 5, 5, agg)
+    X = _mk((n, m), torch.float32, 5, -1, 1)
+    w = _mk((1, m), torch.float32, 6)
+    y = _mk((n, 1), torch.float32, 7)
+    s = _mk((1, 1), torch.float32, 8)
+    _check(prog, [X, w, y, s, 1.0], torch.float32, 3e-6 if agg is None or agg[0] in ("min", "max") else 1e-5, rtc)
+
+
+@pytest.mark.gpu
+def test_cell_kernel_bf16_inputs_views_and_device_scalars():
+    from systemml_amd.ops.cell import CellProgram
+    from systemml_amd.runtime.scalars import DevScalar
+    from systemml_amd.ops.backend import backend
+    backend.configure(DMLConfig(gpu=True, precision="single"))
+    dev = torch.device("cuda:0")
+    prog = CellProgram([("b", "*", 3, 0, 2), ("b", "+", 3, 3, 1), ("u", "sigmoid", 3, 3, 0)], 3, 3, ("sum", "row"))
+    X = _mk((5003, 64), torch.float64, 9, -2, 2).to(torch.bfloat16)
+    Y = _mk((5003, 65), torch.float32, 10)[:, 1:]       # strided view, not 16-B aligned
+    ds = DevScalar(torch.tensor(0.75, dtype=torch.float64, device=dev))
+    from systemml_amd.ops import cell
+    got = cell._kernel(prog, [X.to(dev), Y.to(dev), ds])
+    ref = torch.sigmoid(X.double() * 0.75 + Y.double()).sum(1, keepdim=True)
+    err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err
+
+
+@pytest.mark.gpu
+def test_fused_script_on_gpu_matches_cp():
+    from systemml_amd.ops import kernels
+    _, ref = _run(DMLConfig(gpu=False), n=3001, m=37)
+    c0 = kernels.counters.get("cell", 0)
+    _, got = _run(DMLConfig(gpu=True, precision="double", gpu_min_cells=0), n=3001, m=37)
+    assert kernels.counters.get("cell", 0) >= c0 + 5
+    for k in ("q", "Z", "r", "c"):
+        a, b = got[k], ref[k]
+        a = a.double().cpu() if isinstance(a, torch.Tensor) else torch.tensor(float(a))
+        b = b.double().cpu() if isinstance(b, torch.Tensor) else torch.tensor(float(b))
+        assert torch.allclose(a, b, rtol=1e-9, atol=1e-9), k
