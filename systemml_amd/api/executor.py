@@ -61,6 +61,8 @@ def compile_script(source, args=None, inputs=(), outputs=(), config=None, pydml=
     t2 = time.perf_counter()
     cs = CompiledScript(cp, config, set(inputs), list(outputs), t1 - t0, t2 - t1)
     cs.source = source
+    cs.compile_args = dict(args=args, inputs=inputs, outputs=outputs, pydml=pydml, filename=filename,
+                           base_dir=base_dir)
     return cs
 
 

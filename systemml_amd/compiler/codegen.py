@@ -146,6 +146,7 @@ def fuse_cells(bb):
         root.op = "cell"
         root.inputs = list(leaves)
         root.named = []
-        root.p = {"o": prog.describe(), "prog": prog}
+        lines = sorted({getattr(o.pos, "line", None) for o in ops + [root]} - {None})
+        root.p = {"o": prog.describe(), "prog": prog, "lines": lines}   # debugger: fused source lines
         n += len(ops)
     return n

@@ -65,6 +65,12 @@ class Debugger:
         self.stepping = False
         cs = self.cs
         config = cs.config
+        if getattr(config, "fusion", False) and getattr(cs, "compile_args", None) is not None:
+            # debug mode runs the unfused plan (as the reference's debug mode disables block
+            # merging): every statement keeps its own instructions and its variables
+            import dataclasses
+            config = dataclasses.replace(config, fusion=False)
+            cs = self.cs = EX.compile_script(cs.source, config=config, **cs.compile_args)
         EX.backend.configure(config)
         from ..runtime.program import ExecutionContext, exec_blocks
         self._keep_slots(cs.cp)
@@ -111,16 +117,21 @@ class Debugger:
 
     def on_instruction(self, ctx, ins, slots=None):
         self.cur_slots = slots
-        pos = getattr(ins.hop, "pos", None)
+        hop = getattr(ins, "hop", None)
+        pos = getattr(hop, "pos", None)
         line = getattr(pos, "line", None)
-        if line is None or line == self.last_line:
-            return
-        self.last_line = line
-        self.cur_line = line
-        if self.stepping or line in self.breakpoints:
-            self.stepping = False
-            self._w(f"Breakpoint at line {line}: {self._src(line)}")
-            self._interact(ctx)
+        # a fused operator (compiler/codegen.py) covers several source lines: each of them
+        # is visited in order, so breakpoints on the fused statements still fire
+        lines = list(getattr(hop, "p", {}).get("lines") or ([] if line is None else [line]))
+        for line in lines:
+            if line == self.last_line:
+                continue
+            self.last_line = line
+            self.cur_line = line
+            if self.stepping or line in self.breakpoints:
+                self.stepping = False
+                self._w(f"Breakpoint at line {line}: {self._src(line)}")
+                self._interact(ctx)
 
     def _interact(self, ctx):
         while True:
