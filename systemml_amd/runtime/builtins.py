@@ -810,39 +810,63 @@ def b_aggregate(ctx, target=None, groups=None, fn="sum", weights=None, ngroups=N
 # ============================================================================
 # distributions (reference: ParameterizedBuiltinCPInstruction cdf/invcdf)
 # ============================================================================
-def _dist_fn(dist, q=None, p=None, lower=True, **prm):
-    from scipy import stats as st
-    dist = str(dist).lower()
+def _num(v):
+    """Distribution parameter: a float, or (matrix parameter, an extension over the
+    reference's scalar-only cdf) an fp64 numpy array broadcast cell-wise against the target."""
+    if isinstance(v, Tensor) and v.numel() != 1:
+        return C.cvt(v).detach().double().cpu().numpy()
+    return _float(v)
+
+
+def _dist_fns(dist, prm):
+    """(cdf, sf, ppf) of a distribution as plain scipy.special ufuncs: no frozen
+    scipy.stats object per call, so scalar p-value loops (e.g. stratstats' fStat_tailprob)
+    cost microseconds per call."""
+    from scipy import special as sp
+    _float = _num      # noqa: N806 -- parameters may be matrices
     if dist == "normal":
-        d = st.norm(loc=_float(prm.get("mean", 0.0)), scale=_float(prm.get("sd", 1.0)))
-    elif dist == "exp":
-        d = st.expon(scale=1.0 / _float(prm.get("rate", 1.0)))
-    elif dist == "chisq":
-        d = st.chi2(_float(prm["df"]))
-    elif dist == "f":
-        d = st.f(_float(prm["df1"]), _float(prm["df2"]))
-    elif dist == "t":
-        d = st.t(_float(prm["df"]))
-    else:
-        raise DMLRuntimeError(f"unsupported distribution '{dist}'")
+        mu, sd = _float(prm.get("mean", 0.0)), _float(prm.get("sd", 1.0))
+        return (lambda x: sp.ndtr((x - mu) / sd), lambda x: sp.ndtr((mu - x) / sd),
+                lambda u: sp.ndtri(u) * sd + mu)
+    if dist == "exp":
+        r = _float(prm.get("rate", 1.0))
+        return (lambda x: -np.expm1(-r * np.maximum(x, 0.0)), lambda x: np.exp(-r * np.maximum(x, 0.0)),
+                lambda u: -np.log1p(-u) / r)
+    if dist == "chisq":
+        k = _float(prm["df"])
+        return (lambda x: sp.chdtr(k, np.maximum(x, 0.0)), lambda x: sp.chdtrc(k, np.maximum(x, 0.0)),
+                lambda u: sp.chdtri(k, 1.0 - u))
+    if dist == "f":
+        a, b = _float(prm["df1"]), _float(prm["df2"])
+        return (lambda x: sp.fdtr(a, b, np.maximum(x, 0.0)), lambda x: sp.fdtrc(a, b, np.maximum(x, 0.0)),
+                lambda u: sp.fdtri(a, b, u))
+    if dist == "t":
+        k = _float(prm["df"])
+        return (lambda x: sp.stdtr(k, x), lambda x: sp.stdtr(k, -x), lambda u: sp.stdtrit(k, u))
+    raise DMLRuntimeError(f"unsupported distribution '{dist}'")
+
+
+def _dist_fn(dist, q=None, p=None, lower=True, **prm):
+    dist = str(dist).lower()
     x = q if q is not None else p
+    if isinstance(x, torch.Tensor) and dist == "normal":
+        # element-wise over a matrix (extension over the reference's scalar-only cdf);
+        # the normal family stays on the device via torch.special
+        mu, sd = _float(prm.get("mean", 0.0)), _float(prm.get("sd", 1.0))
+        if q is not None:
+            z = (x - mu) / sd
+            return torch.special.ndtr(z if lower else -z)
+        return torch.special.ndtri(x) * sd + mu
+    cdf, sf, ppf = _dist_fns(dist, prm)
+    fn = (cdf if lower else sf) if q is not None else ppf
     if isinstance(x, torch.Tensor):
-        # element-wise over a matrix (extension over the reference's scalar-only cdf):
-        # the normal family stays on the device via torch.special, others go through scipy
-        if dist == "normal":
-            mu, sd = _float(prm.get("mean", 0.0)), _float(prm.get("sd", 1.0))
-            if q is not None:
-                z = (x - mu) / sd
-                return torch.special.ndtr(z if lower else -z)
-            return torch.special.ndtri(x) * sd + mu
-        xn = x.detach().double().cpu().numpy()
-        r = (d.cdf(xn) if lower else d.sf(xn)) if q is not None else d.ppf(xn)
-        return torch.from_numpy(r).to(device=x.device, dtype=x.dtype)
-    if q is not None:
-        v = _float(q)
-        return float(d.cdf(v) if lower else d.sf(v))
-    v = _float(p)
-    return float(d.ppf(v))
+        xn = C.cvt(x).detach().double().cpu().numpy()
+        r = np.array(np.broadcast_to(np.asarray(fn(xn), dtype=np.float64), xn.shape))
+        return torch.from_numpy(r).to(device=x.device, dtype=_dt())
+    r = fn(_float(x))
+    if isinstance(r, np.ndarray) and r.size != 1:      # scalar target, matrix parameters
+        return torch.from_numpy(np.ascontiguousarray(r, dtype=np.float64)).to(device=_dev(), dtype=_dt())
+    return float(r)
 
 
 @builtin("cdf")
