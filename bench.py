@@ -17,6 +17,7 @@ X is stored bf16 (fp32 accumulation in every kernel); all vectors/iterates are f
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -153,29 +154,42 @@ def main():
     from concurrent.futures import ThreadPoolExecutor
     pool = ThreadPoolExecutor(1)
 
+    def compile_lr():
+        return EX.compile_script(src_lr, args_lr, inputs={"X": X1, "y": y1}, outputs=["B_out"], config=cfg)
+
     def compile_mlr():
         return EX.compile_script(src_mlr, args_mlr, inputs={"X": X2, "Y_vec": lab}, outputs=["B_out"], config=cfg)
 
-    def step(stats=None):
-        # both scripts are parsed + compiled inside every step; MultiLogReg's compilation runs on
-        # a host thread while LinregCG executes (the GPU-bound execution releases the GIL at
-        # each device wait), as a pipelined driver would
-        cs1 = EX.compile_script(src_lr, args_lr, inputs={"X": X1, "y": y1}, outputs=["B_out"], config=cfg)
+    def step(stats=None, cs1=None, prefetch_next=False):
+        # both scripts are parsed + compiled once per step; the compilations run on a host
+        # thread while the GPU executes the previous script (MultiLogReg's while LinregCG
+        # runs, the next step's LinregCG while MultiLogReg runs; GPU-bound execution releases
+        # the GIL at each device wait), as a pipelined driver would
+        if cs1 is None:
+            cs1 = compile_lr()
         fut = None if a.no_overlap else pool.submit(compile_mlr)
         r1, _ = EX.execute(cs1, {"X": X1, "y": y1}, out=out, dist=ctx, stats=stats)
         cs2 = compile_mlr() if fut is None else fut.result()
+        nxt = pool.submit(compile_lr) if (prefetch_next and not a.no_overlap) else None
         r2, _ = EX.execute(cs2, {"X": X2, "Y_vec": lab}, out=out, dist=ctx, stats=stats)
-        return r1["B_out"], r2["B_out"]
+        return r1["B_out"], r2["B_out"], (nxt.result() if nxt is not None else None)
 
-    for _ in range(a.warmup):
-        step()
+    def run_steps(k, stats=None):
+        cs1 = None
+        for i in range(k):
+            _, _, cs1 = step(stats, cs1, prefetch_next=i + 1 < k)
+
+    run_steps(a.warmup)
+    # compiled programs and the data live for the whole run: move them out of the cyclic
+    # collector's generations so gen-2 collections during the steps stay short
+    gc.collect()
+    gc.freeze()
     if ctx:
         ctx.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     st = Statistics(enabled=True) if a.stats else None
-    for _ in range(a.steps):
-        b1, b2 = step(st)
+    run_steps(a.steps, st)
     torch.cuda.synchronize()
     if ctx:
         ctx.barrier()
