@@ -160,6 +160,8 @@ def execute(cs: CompiledScript, inputs=None, out=None, stats=None, dist=None):
                 stats.counters[f"compiled exec type {k_}"] = v_
             for k_, v_ in (getattr(cs.cp, "licm_stats", None) or {}).items():
                 stats.counters[f"rewrite {k_}"] = v_
+            for k_, v_ in (getattr(cs.cp, "rewrite_stats", None) or {}).items():
+                stats.counters[f"rewrite {k_}"] = stats.counters.get(f"rewrite {k_}", 0) + v_
             for k_, v_ in (getattr(cs.cp, "chain_stats", None) or {}).items():
                 stats.counters[f"mm-chain {k_}"] = v_
     from ..runtime.bufferpool import Evicted

@@ -10,6 +10,8 @@ HBM as early as possible (the reference's rmvar/cpvar bookkeeping).
 """
 from __future__ import annotations
 
+import threading
+
 from .hops import walk
 from .blocks import BasicBlock, IfBlock, WhileBlock, ForBlock, Predicate
 from . import rewrites as RW
@@ -69,8 +71,15 @@ def _linearize(roots, tail_writes, make_impl):
     return instrs, writes, len(order)
 
 
+_TLS = threading.local()    # .rw: rewrite counters of the program this thread compiles
+
+
 def compile_basic_block(bb: BasicBlock, make_impl, config=None):
-    RW.rewrite_block(bb, config)
+    st = RW.rewrite_block(bb, config)
+    acc = getattr(_TLS, "rw", None)
+    if acc is not None:
+        for k, v in st.items():
+            acc[k] = acc.get(k, 0) + v
     live = bb.live_out
     tail = []
     for name, h in bb.env_out.items():
@@ -112,10 +121,16 @@ def compile_blocks(blocks, make_impl, config=None):
 
 
 def compile_program(cp, make_impl, config=None):
-    compile_blocks(cp.blocks, make_impl, config)
-    for fb in cp.functions.values():
-        if fb.body is not None:
-            compile_blocks(fb.body, make_impl, config)
-        for p in fb.default_preds.values():
-            compile_predicate(p, make_impl, config)
+    prev = getattr(_TLS, "rw", None)
+    _TLS.rw = acc = {}
+    try:
+        compile_blocks(cp.blocks, make_impl, config)
+        for fb in cp.functions.values():
+            if fb.body is not None:
+                compile_blocks(fb.body, make_impl, config)
+            for p in fb.default_preds.values():
+                compile_predicate(p, make_impl, config)
+        cp.rewrite_stats = acc           # -stats "rewrite <rule>" counters
+    finally:
+        _TLS.rw = prev
     return cp

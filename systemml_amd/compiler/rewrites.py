@@ -67,6 +67,41 @@ def _bi_args(h):
     return out
 
 
+_NOT_CMP = {"==": "!=", "!=": "==", "<": ">=", ">=": "<", ">": "<=", "<=": ">"}
+
+
+def _num_lit(h):
+    return h.op == "lit" and isinstance(h.value, (int, float)) and not isinstance(h.value, bool)
+
+
+def _full_range(src, lo, hi, dimop):
+    """Index range [lo, hi] covering the whole dimension: empty (None) bounds, or 1 .. nrow/ncol(src)."""
+    if lo.op == "lit" and lo.value is None and hi.op == "lit" and hi.value is None:
+        return True
+    return _is_lit(lo, 1) and hi.op == "u" and hi.p["o"] == dimop and hi.inputs[0] is src
+
+
+def _vec_kind(h):
+    """'col' / 'row' when h is a column / row vector by construction, else None."""
+    if h.op == "agg" and h.p.get("dir") == "row":
+        return "col"
+    if h.op == "agg" and h.p.get("dir") == "col":
+        return "row"
+    if h.op == "t":
+        k = _vec_kind(h.inputs[0])
+        return {"col": "row", "row": "col"}.get(k)
+    if _is_ones_matrix(h) or (h.op == "bi" and h.p.get("name") in ("matrix", "rand")):
+        args = _bi_args(h) if h.p.get("name") == "matrix" else {}
+        if h.p.get("name") == "rand":
+            npos = h.p.get("npos", len(h.inputs) - len(h.named))
+            args = {n: h.inputs[npos + j] for j, n in enumerate(h.named)}
+        if set(args) & {"data", "rows", "cols"} and args.get("cols") is not None and _is_lit(args["cols"], 1):
+            return "col"
+        if args.get("rows") is not None and _is_lit(args["rows"], 1):
+            return "row"
+    return None
+
+
 class Rewriter:
     def __init__(self, config=None):
         self.config = config
@@ -105,6 +140,9 @@ class Rewriter:
 
     # ------------------------------------------------------------------ rules
     def apply_rules(self, h: Hop) -> Hop:
+        m = self._rw_algebraic(h)
+        if m is not h:
+            return m
         op = h.op
         if op == "b":
             return self._rw_binary(h)
@@ -135,6 +173,147 @@ class Rewriter:
             return self._match_onehot(h)
         if op == "bi" and h.p.get("name") in ("cbind", "append"):
             return self._match_cbind_const(h)
+        return h
+
+    # ------------------------------------------------------------------ algebraic simplification
+    # (reference: hops/rewrite/RewriteAlgebraicSimplificationStatic.java and the size-guarded
+    # rules of RewriteAlgebraicSimplificationDynamic.java; each rule names its method there)
+    def _hit(self, name, h):
+        self._count(name)
+        return h
+
+    def _rw_algebraic(self, h):
+        op = h.op
+        # rules that look through an intermediate apply only when this hop is its sole
+        # consumer (the reference's parent-count checks): otherwise the intermediate is
+        # computed anyway and the rewrite would duplicate work
+        if any(c.id in self.multi for c in h.inputs if c.op not in ("lit", "tread")):
+            return h
+        if op == "agg":
+            x = h.inputs[0]
+            o, d = h.p["o"], h.p["dir"]
+            # removeUnnecessaryAggregates: sum(rowSums(X)) / sum(colSums(X)) -> sum(X), same for min / max
+            if d == "all" and x.op == "agg" and x.p["dir"] in ("row", "col") and x.p["o"] == o \
+                    and o in ("sum", "min", "max"):
+                return self._hit("unnecessary-aggregate",
+                                 Hop("agg", [x.inputs[0]], {"o": o, "dir": "all"}, dt="S", dim1=0, dim2=0, pos=h.pos))
+            # full aggregates are transpose-invariant (simplifyUnaryAggReorgOperation)
+            if d == "all" and x.op == "t" and o in ("sumsq", "min", "max", "mean", "prod"):
+                return self._hit("agg-transpose", Hop("agg", [x.inputs[0]], dict(h.p), dt="S", dim1=0, dim2=0,
+                                                      pos=h.pos))
+            # pushdownUnaryAggTransposeOperation: colSums(t(X)) -> t(rowSums(X)) (and row <-> col)
+            if d in ("row", "col") and x.op == "t" and o in ("sum", "mean", "min", "max", "sumsq", "prod"):
+                inner = Hop("agg", [x.inputs[0]], {"o": o, "dir": "col" if d == "row" else "row"}, dt="M",
+                            pos=h.pos)
+                return self._hit("agg-transpose-pushdown", Hop("t", [inner], dt="M", pos=h.pos))
+            # pushdownSumBinaryMult: sum(s * X) -> s * sum(X), sum(X / s) -> sum(X) / s
+            if d == "all" and o == "sum" and x.op == "b" and x.p["o"] in ("*", "/"):
+                a, b = x.inputs
+                if x.p["o"] == "*" and a.dt == "S" and b.dt == "M":
+                    a, b = b, a
+                if a.dt == "M" and b.dt == "S":
+                    inner = Hop("agg", [a], {"o": "sum", "dir": "all"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                    return self._hit("sum-scalar-pushdown", Hop("b", [inner, b], {"o": x.p["o"]}, dt="S", pos=h.pos))
+            # sum(-X) -> -sum(X)
+            if d == "all" and o == "sum" and x.op == "u" and x.p["o"] == "neg" and x.dt == "M":
+                inner = Hop("agg", [x.inputs[0]], {"o": "sum", "dir": "all"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                return self._hit("sum-neg-pushdown", Hop("u", [inner], {"o": "neg"}, dt="S", pos=h.pos))
+            # simplifyTraceMatrixMult: trace(X %*% Y) -> sum(X * t(Y))
+            if d == "all" and o == "trace" and x.op == "mm" and not x.p.get("transA"):
+                A, B = x.inputs
+                prod = Hop("b", [A, Hop("t", [B], dt="M", pos=h.pos)], {"o": "*"}, dt="M", pos=h.pos)
+                return self._hit("trace-mm", Hop("agg", [prod], {"o": "sum", "dir": "all"}, dt="S", dim1=0, dim2=0,
+                                                 pos=h.pos))
+            # simplifySumDiagToTrace: sum(diag(X)) -> trace(X) (X square: diag returns its diagonal)
+            if d == "all" and o == "sum" and x.op == "bi" and x.p.get("name") == "diag" and len(x.inputs) == 1:
+                X = x.inputs[0]
+                if X.op == "tsmm":      # square by construction (hop dims are not trusted)
+                    return self._hit("sum-diag-trace", Hop("agg", [X], {"o": "trace", "dir": "all"}, dt="S", dim1=0,
+                                                           dim2=0, pos=h.pos))
+            # simplifyColSumsMVMult / simplifyRowSumsMVMult for operands that are vectors by
+            # construction (aggregate outputs, transposes of them, 1-column datagens: dims of
+            # hops inside re-used function bodies are not trusted):
+            # colSums(X * y) -> t(y) %*% X (y: column vector), rowSums(X * v) -> X %*% t(v) (v: row vector)
+            if d in ("row", "col") and o == "sum" and x.op == "b" and x.p["o"] == "*" and x.dt == "M":
+                for X, v in ((x.inputs[0], x.inputs[1]), (x.inputs[1], x.inputs[0])):
+                    if X.dt != "M" or v.dt != "M":
+                        continue
+                    if d == "col" and _vec_kind(v) == "col" and _vec_kind(X) is None:
+                        return self._hit("colsums-mv", Hop("mm", [v, X], {"transA": True}, dt="M", pos=h.pos))
+                    if d == "row" and _vec_kind(v) == "row" and _vec_kind(X) is None:
+                        return self._hit("rowsums-mv", Hop("mm", [X, Hop("t", [v], dt="M", pos=h.pos)], {}, dt="M",
+                                                           pos=h.pos))
+            return h
+        if op == "u":
+            x = h.inputs[0]
+            o = h.p["o"]
+            # idempotent unary operators: abs(abs(X)) -> abs(X) (round/floor/ceil/sign likewise)
+            if o in ("abs", "round", "floor", "ceil", "sign") and x.op == "u" and x.p["o"] == o:
+                return self._hit("idempotent-unary", x)
+            # simplifyNotOverComparisons: !(A == B) -> A != B, !(A < B) -> A >= B, ...
+            if o == "not" and x.op == "b" and x.p["o"] in _NOT_CMP:
+                return self._hit("not-over-comparison", Hop("b", list(x.inputs), {"o": _NOT_CMP[x.p["o"]]},
+                                                            dt=x.dt, pos=h.pos))
+            return h
+        if op == "b":
+            a, b = h.inputs
+            o = h.p["o"]
+            # A + (-B) -> A - B, A - (-B) -> A + B, (-A) + B -> B - A, (-A) * (-B) -> A * B
+            if o in ("+", "-") and b.op == "u" and b.p["o"] == "neg" and (a.dt == "M" or b.dt == "M"):
+                return self._hit("binary-negation", Hop("b", [a, b.inputs[0]], {"o": "-" if o == "+" else "+"},
+                                                        dt=h.dt, pos=h.pos))
+            if o == "+" and a.op == "u" and a.p["o"] == "neg" and (a.dt == "M" or b.dt == "M"):
+                return self._hit("binary-negation", Hop("b", [b, a.inputs[0]], {"o": "-"}, dt=h.dt, pos=h.pos))
+            if o in ("*", "/") and a.op == "u" and a.p["o"] == "neg" and b.op == "u" and b.p["o"] == "neg":
+                return self._hit("binary-negation", Hop("b", [a.inputs[0], b.inputs[0]], {"o": o}, dt=h.dt, pos=h.pos))
+            # fuseBinarySubDAGToUnaryOperation: 1 / (1 + exp(-X)) -> sigmoid(X)
+            if o == "/" and _is_lit(a, 1) and b.op == "b" and b.p["o"] == "+" and b.dt == "M":
+                l, r = b.inputs
+                e = r if _is_lit(l, 1) else (l if _is_lit(r, 1) else None)
+                if e is not None and e.op == "u" and e.p["o"] == "exp" and e.inputs[0].op == "u" \
+                        and e.inputs[0].p["o"] == "neg":
+                    return self._hit("sigmoid", Hop("u", [e.inputs[0].inputs[0]], {"o": "sigmoid"}, dt="M", pos=h.pos))
+            # simplifyMultiBinaryToBinaryOperation: X * X -> X ^ 2 (one operand read)
+            if o == "*" and a is b and a.dt == "M":
+                return self._hit("square", Hop("b", [a, lit(2)], {"o": "^"}, dt="M", pos=h.pos))
+            # literal chains: (X + c1) + c2 -> X + (c1 + c2), (X * c1) * c2 -> X * (c1 * c2)
+            if o in ("+", "*") and _num_lit(b) and a.op == "b" and a.p["o"] == o and a.dt == "M" \
+                    and _num_lit(a.inputs[1]):
+                c = S.binary(o, a.inputs[1].value, b.value)
+                return self._hit("literal-chain", Hop("b", [a.inputs[0], lit(c)], {"o": o}, dt="M", pos=h.pos))
+            return h
+        if op == "t":
+            x = h.inputs[0]
+            # t(t(A) %*% t(B))... and t(X) %*% t(Y) handled in _rw_mm; t(s * X) keeps scalars outside
+            return h
+        if op == "mm" and not h.p.get("transA"):
+            a, b = h.inputs
+            # simplifyTransposeMatrixMult-style: t(X) %*% t(Y) -> t(Y %*% X) (one transpose)
+            if a.op == "t" and b.op == "t" and a.inputs[0] is not b.inputs[0]:
+                inner = Hop("mm", [b.inputs[0], a.inputs[0]], {}, dt="M", pos=h.pos)
+                return self._hit("transpose-mm", Hop("t", [inner], dt="M", pos=h.pos))
+            return h
+        if op == "bi":
+            name = h.p.get("name")
+            # removeUnnecessaryReorgOperation: rev(rev(X)) -> X
+            if name == "rev" and len(h.inputs) == 1 and h.inputs[0].op == "bi" \
+                    and h.inputs[0].p.get("name") == "rev" and len(h.inputs[0].inputs) == 1:
+                return self._hit("rev-rev", h.inputs[0].inputs[0])
+            # removeUnnecessaryReshape: matrix(X, rows=nrow(X), cols=ncol(X)) -> X
+            if name == "matrix" and h.inputs and h.inputs[0].dt == "M":
+                args = _bi_args(h)
+                X, r, c = args.get("data"), args.get("rows"), args.get("cols")
+                if set(args) <= {"data", "rows", "cols"} and r is not None and c is not None \
+                        and r.op == "u" and r.p["o"] == "nrow" and r.inputs[0] is X \
+                        and c.op == "u" and c.p["o"] == "ncol" and c.inputs[0] is X:
+                    return self._hit("unnecessary-reshape", X)
+            return h
+        if op == "rix":
+            # removeUnnecessaryRightIndexing: X[1:nrow(X), 1:ncol(X)] -> X
+            src, rl, ru, cl, cu = h.inputs
+            if src.dt == "M" and not h.p.get("list") and _full_range(src, rl, ru, "nrow") and _full_range(src, cl, cu, "ncol"):
+                return self._hit("unnecessary-indexing", src)
+            return h
         return h
 
     def _match_cbind_const(self, h):

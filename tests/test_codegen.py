@@ -61,8 +61,8 @@ def test_shared_intermediates_are_materialised():
     src = """
     X = rand(rows=20, cols=4, seed=5)
     T = exp(X) + 1
-    a = sum(T * 2)
-    b = sum(T / 3)
+    a = sum(T * 2 + X)
+    b = sum(T / 3 - X)
     print(a + b)
     """
     cs = EX.compile_script(src, {}, config=DMLConfig(gpu=False))

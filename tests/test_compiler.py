@@ -204,3 +204,62 @@ def test_softmax_gradient_fusion_matches_unfused():
         res, _ = EX.execute(cs, {"X": X, "Y_vec": y}, out=lambda s: None)
         outs[fuse] = res["B_out"].numpy()
     np.testing.assert_allclose(outs[True], outs[False], rtol=1e-10, atol=1e-12)
+
+
+ALGEBRAIC_CASES = [
+    ("s = sum(rowSums(X))", "unnecessary-aggregate"),
+    ("s = max(colMaxs(X))", "unnecessary-aggregate"),
+    ("s = min(t(X))", "agg-transpose"),
+    ("R = colSums(t(X))", "agg-transpose-pushdown"),
+    ("R = rowMeans(t(X))", "agg-transpose-pushdown"),
+    ("s = sum(2.5 * X)", "sum-scalar-pushdown"),
+    ("s = sum(X / 4)", "sum-scalar-pushdown"),
+    ("s = sum(-X)", "sum-neg-pushdown"),
+    ("s = trace(X %*% Y)", "trace-mm"),
+    ("R = abs(abs(X - 0.5))", "idempotent-unary"),
+    ("R = !(X > 0.5)", "not-over-comparison"),
+    ("R = X + (-Y)", "binary-negation"),
+    ("R = X - (-Y)", "binary-negation"),
+    ("R = (-X) + Y", "binary-negation"),
+    ("R = 1 / (1 + exp(-X))", "sigmoid"),
+    ("R = X * X + 1", "square"),
+    ("R = (X + 2) + 3", "literal-chain"),
+    ("R = (X * 2) * 3", "literal-chain"),
+    ("R = t(X) %*% t(Y)", "transpose-mm"),
+    ("R = rev(rev(X))", "rev-rev"),
+    ("R = matrix(X, rows=nrow(X), cols=ncol(X)) + 1", "unnecessary-reshape"),
+    ("R = X[1:nrow(X), 1:ncol(X)] + 1", "unnecessary-indexing"),
+    ("R = X[, ] * 2", "unnecessary-indexing"),
+    ("s = sum(diag(t(X) %*% X))", "sum-diag-trace"),
+]
+
+
+@pytest.mark.parametrize("src,rule", ALGEBRAIC_CASES)
+def test_algebraic_simplification_rules(src, rule):
+    """Each static algebraic rewrite fires (its -stats counter) and leaves results unchanged
+    (reference: RewriteAlgebraicSimplificationStatic / Dynamic)."""
+    rng = np.random.default_rng(3)
+    X = rng.random((6, 6))
+    Y = rng.random((6, 6)) - 0.5
+    out = "s" if src.startswith("s ") else "R"
+    cs = compile_script(src, inputs={"X": X, "Y": Y}, outputs=[out], config=CFG)
+    assert cs.cp.rewrite_stats.get(rule, 0) >= 1, cs.cp.rewrite_stats
+    on = _run(src, {"X": X, "Y": Y}, [out])[out]
+    off = run(src, inputs={"X": X, "Y": Y}, outputs=[out], config=DMLConfig(gpu=False, rewrites=False),
+              out=lambda s: None)[out]
+    off = off.numpy() if hasattr(off, "numpy") else off
+    np.testing.assert_allclose(np.asarray(on, float), np.asarray(off, float), rtol=1e-12, atol=1e-12)
+
+
+def test_mv_aggregate_rewrites_with_known_shapes():
+    """colSums(X * y) -> t(y) %*% X and rowSums(X * v) -> X %*% t(v) for operands that are
+    vectors by construction (simplifyColSumsMVMult / simplifyRowSumsMVMult)."""
+    rng = np.random.default_rng(4)
+    X, Z = rng.random((7, 5)), rng.random((7, 5))
+    y, v = Z.sum(1, keepdims=True), Z.sum(0, keepdims=True)
+    src = "A = colSums(X * rowSums(Z))\nB = rowSums(colSums(Z) * X)"
+    r = _run(src, {"X": X, "Z": Z}, ["A", "B"])
+    np.testing.assert_allclose(r["A"], (X * y).sum(0, keepdims=True), rtol=1e-12)
+    np.testing.assert_allclose(r["B"], (X * v).sum(1, keepdims=True), rtol=1e-12)
+    cs = compile_script(src, inputs={"X": X, "Z": Z}, outputs=["A", "B"], config=CFG)
+    assert cs.cp.rewrite_stats.get("colsums-mv") == 1 and cs.cp.rewrite_stats.get("rowsums-mv") == 1
