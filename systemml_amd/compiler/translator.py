@@ -116,6 +116,8 @@ class Translator:
 
     # ------------------------------------------------------------------ compile
     def compile(self, prog: A.Program, inputs=(), outputs=(), input_types=None):
+        from .parfor_deps import check_program
+        check_program(prog)          # parfor loop dependency analysis (ParForStatementBlock.validate)
         main_ctx = self._register_file(prog, DEFAULT_NS, prog.source_path)
         self.inputs = set(inputs)
         self.input_types = dict(input_types or {})

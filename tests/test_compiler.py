@@ -263,3 +263,44 @@ def test_mv_aggregate_rewrites_with_known_shapes():
     np.testing.assert_allclose(r["B"], (X * v).sum(1, keepdims=True), rtol=1e-12)
     cs = compile_script(src, inputs={"X": X, "Z": Z}, outputs=["A", "B"], config=CFG)
     assert cs.cp.rewrite_stats.get("colsums-mv") == 1 and cs.cp.rewrite_stats.get("rowsums-mv") == 1
+
+
+PARFOR_DEP_ERRORS = [
+    # scalar accumulation: every iteration reads and writes s
+    ("s = 0\nparfor (i in 1:4) { s = s + i }\nprint(s)", "s"),
+    # output dependency: every iteration writes the same cell
+    ("R = matrix(0, 4, 1)\nparfor (i in 1:4) { R[1, 1] = i }\nprint(sum(R))", "R"),
+    # data dependency: reads the previous iteration's row
+    ("R = matrix(0, 4, 1)\nparfor (i in 2:4) { R[i, 1] = as.scalar(R[i - 1, 1]) + 1 }\nprint(sum(R))", "R"),
+    # whole-object read of a per-iteration result
+    ("R = matrix(0, 4, 1)\nparfor (i in 1:4) { R[i, 1] = sum(R) + i }\nprint(sum(R))", "R"),
+    # plain write of a variable read after the loop
+    ("parfor (i in 1:4) { x = i * 2 }\nprint(x)", "x"),
+]
+
+PARFOR_DEP_OK = [
+    # per-iteration rows / columns, also through a body variable computed from i
+    "R = matrix(0, 4, 3)\nparfor (i in 1:4) { j = i * 1\n  R[j, ] = matrix(i, 1, 3) }\nprint(sum(R))",
+    "R = matrix(0, 2, 4)\nparfor (i in 1:4) { R[, i] = matrix(i, 2, 1) }\nprint(sum(R))",
+    # read and write through the same subscript; iteration-private temporaries
+    "R = matrix(1, 4, 1)\nparfor (i in 1:4) { t = as.scalar(R[i, 1]) * 2\n  R[i, 1] = t }\nprint(sum(R))",
+    # nested loop variable in the subscript
+    "R = matrix(0, 3, 3)\nparfor (i in 1:3) { for (j in 1:3) { R[i, j] = i + j } }\nprint(sum(R))",
+    # a temporary re-assigned before its next read after the loop
+    "parfor (i in 1:3) { x = i }\nx = 5\nprint(x)",
+    # check=0 disables the analysis
+    "s = 0\nparfor (i in 1:4, check=0) { s = i }\nprint(s)",
+]
+
+
+@pytest.mark.parametrize("src,var", PARFOR_DEP_ERRORS)
+def test_parfor_dependency_analysis_rejects(src, var):
+    from systemml_amd.parser.errors import LanguageError
+    with pytest.raises(LanguageError) as e:
+        compile_script(src, config=CFG)
+    assert "PARFOR loop dependency analysis" in str(e.value) and f" {var} [" in str(e.value)
+
+
+@pytest.mark.parametrize("src", PARFOR_DEP_OK)
+def test_parfor_dependency_analysis_accepts(src):
+    compile_script(src, config=CFG)
