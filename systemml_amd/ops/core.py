@@ -318,10 +318,19 @@ def binary(op, a, b):
         if not tb and op in ("*", "/") and isinstance(b, (int, float)) and not isinstance(b, bool) \
                 and (op == "*" or b != 0):
             return SP.scale(a, float(b), op)
+        fn = BIN.get(op)
+        r = SP.binary(op, a, b if not tb or SP.is_sparse(b) else cvt(b), fn) if fn is not None else None
+        if r is not None:
+            return r
         a = SP.densify(a)
     if tb and SP.is_sparse(b):
         if not ta and op == "*" and isinstance(a, (int, float)) and not isinstance(a, bool):
             return SP.scale(b, float(a), "*")
+        if op in ("*", "+") and ta:              # commutative: dense * sparse, sparse + sparse
+            fn = BIN.get(op)
+            r = SP.binary(op, b, cvt(a), fn) if fn is not None and not SP.is_sparse(a) and op == "*" else None
+            if r is not None:
+                return r
         b = SP.densify(b)
     if not ta and not tb:
         if is_dist(a) or is_dist(b):
@@ -406,6 +415,11 @@ def unary(op, x):
         fn = UN.get(op)
         if fn is None:
             raise DMLRuntimeError(f"unknown unary operator {op}")
+        if SP.is_sparse(x):
+            r = SP.unary(op, x, fn)
+            if r is not None:
+                return r
+            x = SP.densify(x)
         return fn(cvt(x))
     if is_dist(x):
         return _dist().unary(op, x)

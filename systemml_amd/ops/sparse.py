@@ -184,3 +184,88 @@ def scale(x, s, op):
 
 def transpose(x):
     return x.t().to_sparse_csr()
+
+
+# ----------------------------------------------------------------------------
+# sparse-safe cellwise operators (reference: LibMatrixBincell / LibMatrixUnary sparse paths,
+# BinaryOperator.isSparseSafe / UnaryOperator.sparseSafe): when f(0[, .]) = 0 the result keeps
+# the operand's non-zero pattern and only its stored values are transformed
+# ----------------------------------------------------------------------------
+SAFE_UNARY = {"abs", "sqrt", "round", "floor", "ceil", "sign", "sin", "tan", "asin", "atan", "sinh", "tanh",
+              "neg"}
+
+
+def _with_values(x, vals, prune=False):
+    """CSR with x's pattern and new stored values; `prune` drops cells that became zero
+    (comparisons, sign, round) so nnz() counts true non-zeros."""
+    if prune and bool((vals == 0).any()):
+        keep = vals != 0
+        rows, cols = _rows_of(x)[keep], x.col_indices()[keep]
+        return from_ijv(rows, cols, vals[keep], x.shape[0], x.shape[1], vals.dtype, vals.device)
+    return torch.sparse_csr_tensor(x.crow_indices(), x.col_indices(), vals, x.shape)
+
+
+def _rows_of(x):
+    crow = x.crow_indices()
+    counts = crow[1:] - crow[:-1]
+    return torch.repeat_interleave(torch.arange(x.shape[0], device=crow.device), counts)
+
+
+def unary(op, x, fn):
+    """f(X) for a sparse-safe unary f on a CSR matrix (None if f is not sparse-safe)."""
+    if op not in SAFE_UNARY or x.layout != torch.sparse_csr:
+        return None
+    return _with_values(x, fn(x.values()), prune=op in ("round", "floor", "ceil", "sign"))
+
+
+def _scalar_safe(op, s, fn):
+    """Is `X op s` zero wherever X is zero (so the result keeps X's pattern)?"""
+    try:
+        z = fn(torch.zeros((), dtype=torch.float64), torch.tensor(float(s), dtype=torch.float64))
+    except Exception:   # noqa: BLE001
+        return False
+    return bool(z == 0)
+
+
+def binary(op, a, b, fn):
+    """Sparse-safe `a op b` with CSR `a`; None if the operation must densify.
+
+    * sparse op scalar for any op with 0 op s == 0 (X * s, X / s (s != 0), X ^ s (s > 0),
+      X > s (s >= 0), X != 0, max(X, s <= 0) ...);
+    * sparse * dense (same shape, column or row vector broadcast): the dense operand is
+      gathered at the stored cells;
+    * sparse * sparse (intersection) and sparse +/- sparse (union) of equal shape."""
+    if a.layout != torch.sparse_csr:
+        return None
+    if not isinstance(b, torch.Tensor):
+        if isinstance(b, bool) or not isinstance(b, (int, float)):
+            return None
+        if not _scalar_safe(op, b, fn):
+            return None
+        v = a.values()
+        return _with_values(a, fn(v, torch.tensor(float(b), dtype=v.dtype, device=v.device)).to(v.dtype), prune=True)
+    if is_sparse(b):
+        if b.layout != torch.sparse_csr or tuple(b.shape) != tuple(a.shape):
+            return None
+        if op in ("+", "-"):
+            ac, bc = a.to_sparse_coo(), b.to_sparse_coo()
+            return ((ac + bc) if op == "+" else (ac - bc)).coalesce().to_sparse_csr()
+        if op == "*":
+            if torch.equal(a.crow_indices(), b.crow_indices()) and torch.equal(a.col_indices(), b.col_indices()):
+                return _with_values(a, a.values() * b.values())
+            r = (a.to_sparse_coo() * b.to_sparse_coo()).coalesce()
+            return r.to_sparse_csr()
+        return None
+    if op != "*" or b.dim() != 2:
+        return None
+    r, c = a.shape
+    if tuple(b.shape) == (r, c):
+        g = b[_rows_of(a), a.col_indices()]
+    elif tuple(b.shape) == (r, 1):
+        g = b[_rows_of(a), 0]
+    elif tuple(b.shape) == (1, c):
+        g = b[0, a.col_indices()]
+    else:
+        return None
+    v = a.values()
+    return _with_values(a, v * g.to(v.dtype))

@@ -22,7 +22,8 @@ from .scalars import DevScalar
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
 _CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "rix", "t", "cell"}
-_SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix"}
+_SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "round", "floor", "ceil", "sign",
+                    "sin", "tan", "asin", "atan", "sinh", "tanh", "neg"}       # ops/sparse.py SAFE_UNARY
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
 _LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "t", "tak", "cell"}

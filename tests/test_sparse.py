@@ -90,3 +90,46 @@ def test_spmm_hip_kernel(K, dt):
     np.testing.assert_allclose(gott.double().cpu().numpy(), (D.to(dt).double().T @ Bt.to(dt).double()).numpy(),
                                rtol=tol * 10, atol=tol * 10)
     assert kernels.counters["spmm"] > c0
+
+
+@pytest.mark.parametrize("gpu", [False, pytest.param(True, marks=pytest.mark.gpu)])
+def test_sparse_safe_cellwise_operators_keep_csr(gpu):
+    """Sparse-safe cellwise operators (f(0) = 0) keep the CSR pattern and match the dense
+    evaluation (reference: LibMatrixBincell / LibMatrixUnary sparse-safe paths); on the GPU
+    backend the CSR matrices live in HBM."""
+    cfg = DMLConfig(gpu=True, precision="double") if gpu else CFG
+    src = """A = rand(rows=600, cols=400, sparsity=0.02, min=-1, max=1, seed=5)
+B = rand(rows=600, cols=400, sparsity=0.02, min=-1, max=1, seed=6)
+D = rand(rows=600, cols=400, seed=7)
+y = rand(rows=600, cols=1, seed=8)
+v = rand(rows=1, cols=400, seed=9)
+U1 = abs(A)
+U2 = sign(A)
+U3 = -A
+U4 = sqrt(abs(A))
+S1 = A > 0
+S2 = A != 0
+S3 = A ^ 2
+S4 = max(A, 0)
+M1 = A * D
+M2 = D * A
+M3 = A * y
+M4 = A * v
+P1 = A * B
+P2 = A + B
+P3 = A - B
+n2 = sum(S1)
+"""
+    outs = ["A", "B", "D", "y", "v", "U1", "U2", "U3", "U4", "S1", "S2", "S3", "S4", "M1", "M2", "M3", "M4",
+            "P1", "P2", "P3", "n2"]
+    r = run(src, outputs=outs, config=cfg)
+    dn = lambda x: x.to_dense().cpu().numpy() if SP.is_sparse(x) else x.cpu().numpy()
+    A, B, D, y, v = (dn(r[k]) for k in ("A", "B", "D", "y", "v"))
+    ref = {"U1": np.abs(A), "U2": np.sign(A), "U3": -A, "U4": np.sqrt(np.abs(A)), "S1": (A > 0) * 1.0,
+           "S2": (A != 0) * 1.0, "S3": A ** 2, "S4": np.maximum(A, 0), "M1": A * D, "M2": D * A, "M3": A * y,
+           "M4": A * v, "P1": A * B, "P2": A + B, "P3": A - B}
+    for k, exp in ref.items():
+        assert SP.is_sparse(r[k]), k
+        np.testing.assert_allclose(dn(r[k]), exp, rtol=1e-12, atol=1e-12, err_msg=k)
+    assert r["S1"]._nnz() == int((A > 0).sum())           # no explicit zeros kept
+    np.testing.assert_allclose(r["n2"], (A > 0).sum())
