@@ -101,6 +101,12 @@ def init(backend=None, device=None):
         _CTX = None
         return None
     rank = int(os.environ.get("RANK", "0"))
+    # SYSML_DIST_BACKEND=gloo with SYSML_DIST_DEVICE=cuda rehearses the GPU SPMD path with
+    # several ranks on ONE GPU (RCCL refuses two ranks per device): same partitioning,
+    # kernels and collectives, host-staged transport
+    backend = backend or os.environ.get("SYSML_DIST_BACKEND") or None
+    if device is None and os.environ.get("SYSML_DIST_DEVICE") == "cuda" and torch.cuda.is_available():
+        device = torch.device("cuda", torch.cuda.current_device())
     if not tdist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
