@@ -123,6 +123,7 @@ def _hoist_block(bb: BasicBlock, variant, stats):
     bb.reads |= set(pre_env)
     pre = BasicBlock()
     pre.pos = bb.pos
+    pre.licm_pre = True          # runtime defers its errors to the first read (zero-trip loops)
     pre.env_out = pre_env
     pre.writes = set(pre_env)
     reads = set()

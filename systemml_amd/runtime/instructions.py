@@ -138,6 +138,16 @@ def _placed(fn, h):
     return run
 
 
+class DeferredError:
+    """Value of a variable whose (loop-invariant, hoisted) computation failed: the error is
+    raised when the loop body first reads it, so a loop that never runs never fails
+    (compiler/loops.py LICM)."""
+    __slots__ = ("err",)
+
+    def __init__(self, err):
+        self.err = err
+
+
 def _make_impl(h):
     op = h.op
     p = h.p
@@ -154,6 +164,8 @@ def _make_impl(h):
             except KeyError:
                 raise DMLRuntimeError(f"{pos}: Variable '{name}' is not defined" if pos else
                                       f"Variable '{name}' is not defined")
+            if type(v) is DeferredError:
+                raise v.err
             pool = ctx.pool
             if pool is not None:
                 if type(v) is Evicted:

@@ -153,6 +153,7 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
     def worker():
         wctx = ExecutionContext(ctx.program, ctx.config, stats=ctx.stats, out=ctx._out, dist=None)
         wctx.vars = dict(ctx.vars)
+        wctx.parfor_worker = True        # program.exec_block: serialise recompiling blocks
         while True:
             with lock:
                 if not queue:

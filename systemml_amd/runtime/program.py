@@ -10,6 +10,7 @@ a driver/worker split.
 from __future__ import annotations
 
 import sys
+import threading
 import time
 import weakref
 
@@ -206,8 +207,33 @@ def exec_blocks(ctx, blocks):
         exec_block(ctx, b)
 
 
+_BLOCK_LOCKS = weakref.WeakKeyDictionary()
+_LOCKS_GUARD = threading.Lock()
+
+
+def _block_lock(b):
+    with _LOCKS_GUARD:
+        lk = _BLOCK_LOCKS.get(b)
+        if lk is None:
+            lk = _BLOCK_LOCKS[b] = threading.Lock()
+        return lk
+
+
 def exec_block(ctx, b):
+    if isinstance(b, BasicBlock) and getattr(ctx, "parfor_worker", False) and \
+            (b.recompile or getattr(b, "exec_recompile", False)):
+        # dynamic recompilation replaces the block's plan (instructions, slot count, output
+        # slots) for the operand shapes at hand; parfor workers sharing the block must not
+        # interleave a recompilation with another worker's execution of the same block
+        with _block_lock(b):
+            return _exec_basic(ctx, b)
     if isinstance(b, BasicBlock):
+        return _exec_basic(ctx, b)
+    return _exec_control(ctx, b)
+
+
+def _exec_basic(ctx, b):
+    if True:
         if ctx.debugger is not None:
             ctx.debugger.cur_block = b
         if b.recompile:
@@ -223,7 +249,17 @@ def exec_block(ctx, b):
                 if ctx.config is not None and ctx.config.explain == "recompile_runtime":
                     ctx.print(f"# EXPLAIN (recompile_runtime): block at line "
                               f"{b.pos.line if b.pos else '?'}\n" + runtime_plan(b, "  "))
-        slots = exec_instrs(ctx, b.instrs, b.nslots)
+        if getattr(b, "licm_pre", False):
+            # hoisted loop invariants: a failure surfaces only if the loop reads the value
+            try:
+                slots = exec_instrs(ctx, b.instrs, b.nslots)
+            except DMLRuntimeError as e:
+                from .instructions import DeferredError
+                for name, _ in b.writes_slots:
+                    ctx.vars[name] = DeferredError(e)
+                return
+        else:
+            slots = exec_instrs(ctx, b.instrs, b.nslots)
         vars_ = ctx.vars
         for name, s in b.writes_slots:
             vars_[name] = slots[s]
@@ -232,6 +268,9 @@ def exec_block(ctx, b):
         if ctx.pool is not None:
             ctx.pool.maybe_evict(ctx.frames())
         return
+
+
+def _exec_control(ctx, b):
     if isinstance(b, IfBlock):
         if _to_bool(eval_pred(ctx, b.pred)):
             exec_blocks(ctx, b.then_blocks)

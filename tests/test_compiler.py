@@ -304,3 +304,26 @@ def test_parfor_dependency_analysis_rejects(src, var):
 @pytest.mark.parametrize("src", PARFOR_DEP_OK)
 def test_parfor_dependency_analysis_accepts(src):
     compile_script(src, config=CFG)
+
+
+def test_licm_zero_trip_loop_does_not_raise():
+    """A hoisted loop invariant that would fail (out-of-range slice) only fails when the loop
+    actually runs and reads it (LICM must not introduce errors for zero-trip loops)."""
+    src = """P = matrix(1, rows=5, cols=3)
+K = 7
+s = 0
+i = 0
+while (i < 0) {
+  Q = P[, 1:K]
+  s = s + sum(Q)
+  i = i + 1
+}
+"""
+    r = _run(src, outputs=["s"])
+    assert r["s"] == 0
+    cs = compile_script(src, outputs=["s"], config=CFG)
+    assert cs.cp.licm_stats.get("hoisted", 0) >= 1
+    bad = src.replace("while (i < 0)", "while (i < 1)")
+    with pytest.raises(Exception) as e:
+        _run(bad, outputs=["s"])
+    assert "line 6" in str(e.value) or "index" in str(e.value).lower()
