@@ -25,7 +25,8 @@ last and only sees what is left.
 from __future__ import annotations
 
 from .hops import walk
-from ..ops.cell import BIN_CODES, UN_CODES, AGG_CODES, MAXIN, MAXOPS, NR, CellProgram
+from ..ops.cell import BIN_CODES, UN_CODES, AGG_CODES, MAXIN, MAXOPS, NR, CellProgram, MultiAggProgram
+from .hops import Hop
 
 AGG_DIRS = ("all", "row", "col")
 
@@ -137,12 +138,18 @@ def fuse_cells(bb):
         if g is not None and h.id not in absorbed and len(g[0]) >= 2:
             plans.append((h, g[0], g[1], None))
     n = 0
+    built = []
     for root, ops, leaves, agg in plans:
         ra = _regalloc(ops, leaves)
         if ra is None:
             continue
         code, out = ra
-        prog = CellProgram(code, len(leaves), out, agg)
+        built.append((root, ops, leaves, CellProgram(code, len(leaves), out, agg)))
+    grouped = _multi_agg(built)
+    for root, ops, leaves, prog in built:
+        if root.id in grouped:
+            n += len(ops)
+            continue
         root.op = "cell"
         root.inputs = list(leaves)
         root.named = []
@@ -150,3 +157,62 @@ def fuse_cells(bb):
         root.p = {"o": prog.describe(), "prog": prog, "lines": lines}   # debugger: fused source lines
         n += len(ops)
     return n
+
+
+MAGG_MAX = 4
+
+
+def _multi_agg(built):
+    """MAgg template (reference: template/TemplateMultiAgg.java and the multi-aggregate
+    merge of PlanSelectionFuseCostBased): full aggregates of fused cell programs that read a
+    common matrix input are combined -- up to MAGG_MAX per group and MAXIN distinct inputs --
+    into one `magg` hop evaluated in a single pass (ops/cell.evaluate_multi); each original
+    aggregate hop becomes output i of it.  Aggregates that depend on each other are never
+    grouped.  Returns the ids of the replaced roots."""
+    cands = [b for b in built if b[3].agg and b[3].agg[1] == "all"]
+    if len(cands) < 2:
+        return set()
+    reach = {}
+    for root, _, leaves, _ in cands:
+        reach[root.id] = {h.id for h in walk(list(leaves))}
+    groups = []
+    for c in cands:
+        root, _, leaves, _ = c
+        mats = {h.id for h in leaves if h.dt == "M"}
+        placed = False
+        for g in groups:
+            if len(g) >= MAGG_MAX:
+                continue
+            gm = {h.id for x in g for h in x[2] if h.dt == "M"}
+            if not (mats & gm):
+                continue
+            union = {h.id for x in g for h in x[2]} | {h.id for h in leaves}
+            if len(union) > MAXIN:
+                continue
+            if any(root.id in reach[x[0].id] or x[0].id in reach[root.id] for x in g):
+                continue
+            g.append(c)
+            placed = True
+            break
+        if not placed:
+            groups.append([c])
+    done = set()
+    for g in groups:
+        if len(g) < 2:
+            continue
+        union = []
+        for _, _, leaves, _ in g:
+            for h in leaves:
+                if all(h is not u for u in union):
+                    union.append(h)
+        idx = {h.id: i for i, h in enumerate(union)}
+        m = MultiAggProgram([x[3] for x in g], [[idx[h.id] for h in x[2]] for x in g], len(union))
+        mh = Hop("magg", list(union), {"o": m.describe(), "prog": m}, dt="U", pos=g[0][0].pos)
+        for i, (root, ops, leaves, prog) in enumerate(g):
+            lines = sorted({getattr(o.pos, "line", None) for o in ops + [root]} - {None})
+            root.op = "fout"
+            root.inputs = [mh]
+            root.named = []
+            root.p = {"i": i, "lines": lines}
+            done.add(root.id)
+    return done

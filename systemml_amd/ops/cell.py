@@ -496,3 +496,183 @@ def _kernel(prog: CellProgram, args):
                                                              else part.amax(0, keepdim=True))
     r = r.to(T)
     return r / R if o == "mean" else r
+
+
+# ----------------------------------------------------------------------------- multi-aggregate
+class MultiAggProgram:
+    """MAgg template (reference: hops/codegen/template/TemplateMultiAgg.java, runtime
+    SpoofMultiAggregate): several full aggregates of cellwise programs over the same output
+    cells, evaluated in ONE pass over their shared inputs.  progs[k] reads its registers
+    0..n_in-1 from the union inputs maps[k][0..n_in-1]."""
+    __slots__ = ("progs", "maps", "n_in")
+
+    def __init__(self, progs, maps, n_in):
+        self.progs = tuple(progs)
+        self.maps = tuple(tuple(m) for m in maps)
+        self.n_in = n_in
+
+    def key(self):
+        return (tuple(p.key() for p in self.progs), self.maps, self.n_in)
+
+    def describe(self):
+        return "magg[" + ";".join(p.describe() for p in self.progs) + "]"
+
+    def __repr__(self):
+        return self.describe()
+
+
+def evaluate_multi(m: MultiAggProgram, args):
+    """Tuple of the aggregates: one fused kernel on the MI355X, else each program alone."""
+    r = _kernel_multi(m, args) if backend.use_kernels and RTC else None
+    if r is not None:
+        stats["magg_kernel"] = stats.get("magg_kernel", 0) + 1
+        return r
+    stats["magg_split"] = stats.get("magg_split", 0) + 1
+    return tuple(evaluate(p, [args[i] for i in mp]) for p, mp in zip(m.progs, m.maps))
+
+
+def generate_multi(m: MultiAggProgram, T, modes, dts, vecs):
+    ct = "float" if T == torch.float32 else "double"
+    body, outs = [], []
+    q = 0
+    for k, (prog, mp) in enumerate(zip(m.progs, m.maps)):
+        var = [f"x[{mp[r]}]" for r in range(prog.n_in)] + [None] * (NR - prog.n_in)
+        for kind, o, d, a, b in prog.ops:
+            e = (_C_BIN[o] if kind == "b" else _C_UN[o]).format(a=var[a], b=var[b] if kind == "b" else "")
+            body.append(f"    const T v{q} = {e};")
+            var[d] = f"v{q}"
+            q += 1
+        outs.append(f"    o[{k}] = {var[prog.out]};")
+    aggs = [AGG_CODES[p.agg[0]] for p in m.progs]
+    need_ij = int(any(x in (ROWV, COLV) for x in modes))
+    return (_prelude() + f"""
+// generated: {m.describe()}
+struct Spec {{
+  typedef {ct} T;
+  static constexpr int NIN = {m.n_in};
+  static constexpr int NOUT = {len(m.progs)};
+  static constexpr int NEED_IJ = {need_ij};
+  static constexpr int mode(int k) {{ return {_cases(modes)}; }}
+  static constexpr int dt(int k) {{ return {_cases(dts)}; }}
+  static constexpr int vec(int k) {{ return {_cases(vecs)}; }}
+  static constexpr int aggop(int k) {{ return {_cases(aggs)}; }}
+  static __device__ __forceinline__ void f(const T (&x)[NIN], T (&o)[NOUT]) {{
+{chr(10).join(body)}
+{chr(10).join(outs)}
+  }}
+}};
+
+extern "C" __global__ void __launch_bounds__(256) sysml_cell_k(const SysmlCellArgs A) {{ sysml_cell_magg<Spec>(A); }}
+""")
+
+
+def _kernel_multi(m: MultiAggProgram, args):
+    from ..runtime.scalars import DevScalar
+    if len(args) != m.n_in or m.n_in > MAXIN:
+        return None
+    dev, shapes, f64, bf16 = None, [], False, False
+    for x in args:
+        tx = type(x)
+        if tx is _Tensor:
+            if not x.is_cuda or x.layout is not torch.strided or x.dim() != 2 or x.dtype not in _DT:
+                return None
+            if dev is None:
+                dev = x.device
+            elif x.device != dev:
+                return None
+            f64 = f64 or x.dtype == torch.float64
+            bf16 = bf16 or x.dtype == torch.bfloat16
+            shapes.append(tuple(x.shape))
+        elif tx is DevScalar:
+            if not x.t.is_cuda or x.t.dtype not in _DT:
+                return None
+            shapes.append(None)
+        elif tx is float or tx is int or tx is bool:
+            shapes.append(None)
+        else:
+            return None
+    if dev is None:
+        return None
+    outs = {out_shape(p, [shapes[i] for i in mp]) for p, mp in zip(m.progs, m.maps)}
+    if len(outs) != 1:
+        return None                      # different cell domains: evaluated one by one
+    shp = outs.pop()
+    if shp is None or shp[0] <= 0 or shp[1] <= 0:
+        return None
+    R, Cc = shp
+    T = torch.float64 if (f64 or (bf16 and backend.dtype == torch.float64)) else torch.float32
+    A = _RtcArgs()
+    keep, modes, dts, vecs = [], [], [], []
+    for k, x in enumerate(args):
+        tx = type(x)
+        mode, dt, vec = HSCALAR, 0, 0
+        if tx is _Tensor:
+            if not x.is_contiguous():
+                x = x.contiguous()
+            keep.append(x)
+            r, c = x.shape
+            A.inp[k] = x.data_ptr()
+            dt = _DT[x.dtype]
+            if (r, c) == (R, Cc):
+                mode, vec = FULL, int(x.data_ptr() % 16 == 0)
+            elif r == 1 and c == 1:
+                mode = DSCALAR
+            elif r == 1 and c == Cc:
+                mode = ROWV
+            elif c == 1 and r == R:
+                mode = COLV
+            else:
+                return None
+        elif tx is DevScalar:
+            t = x.t.reshape(1)
+            keep.append(t)
+            A.inp[k] = t.data_ptr()
+            dt, mode = _DT[t.dtype], DSCALAR
+        else:
+            A.s[k] = float(x)
+        modes.append(mode)
+        dts.append(dt)
+        vecs.append(vec)
+    key = ("magg", m.key(), T, tuple(modes), tuple(dts), tuple(vecs), str(dev))
+    f = _rtc_funcs.get(key, False)
+    if f is False:
+        try:
+            code = compile_source(generate_multi(m, T, tuple(modes), tuple(dts), tuple(vecs)), gpu_arch(dev))
+            fn = ctypes.c_void_p()
+            cbuf = ctypes.create_string_buffer(code, len(code))
+            rc = _rtc_lib().sysml_rtc_load(cbuf, b"sysml_cell_k", ctypes.byref(fn))
+            if rc != 0:
+                raise RuntimeError(f"hipModuleLoadData failed ({rc})")
+            f = (fn, cbuf)
+        except RuntimeError as e:
+            import warnings
+            warnings.warn(f"multi-aggregate kernel not compiled, aggregates run separately: {e}")
+            f = None
+        _rtc_funcs[key] = f
+    if f is None:
+        return None
+    nout = len(m.progs)
+    nblk = _lib().sysml_cell_blocks(1, R, Cc)
+    part = torch.empty(nblk * nout, dtype=torch.float64, device=dev)
+    A.rows, A.cols, A.total = R, Cc, R * Cc
+    A.chunk = (R + nblk - 1) // nblk
+    A.out = 0
+    A.part = part.data_ptr()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    rc = _rtc_lib().sysml_rtc_launch(f[0], nblk, 1, 256, ctypes.byref(A), ctypes.sizeof(A), st)
+    if rc != 0:
+        raise RuntimeError(f"multi-aggregate kernel launch failed: {rc}")
+    stats["rtc_launches"] += 1
+    from . import kernels
+    kernels._count("magg")
+    del keep
+    P = part.view(nblk, nout)
+    res = []
+    for k, prog in enumerate(m.progs):
+        o = prog.agg[0]
+        col = P[:, k]
+        r = col.sum() if AGG_CODES[o] <= 1 else (col.min() if o == "min" else col.max())
+        if o == "mean":
+            r = r / (R * Cc)
+        res.append(C._lazy_out(r))
+    return tuple(res)

@@ -19,16 +19,19 @@ from . import builtins as B
 from .scalars import DevScalar
 
 
-_SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell"}
+_SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell",
+                  "magg"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
-_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "rix", "t", "cell"}
+_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "rix", "t", "cell", "magg"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "round", "floor", "ceil", "sign",
                     "sin", "tan", "asin", "atan", "sinh", "tanh", "neg"}       # ops/sparse.py SAFE_UNARY
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
-_LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "t", "tak", "cell"}
+_LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "t", "tak", "cell",
+                "magg"}
 # operators that compute on matrix operands (placement applies); the rest move values around
-_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "wquat", "tak", "t", "rix", "lix", "bi", "cell"}
+_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "wquat", "tak", "t", "rix", "lix", "bi", "cell",
+                "magg"}
 transfer_stats = {"h2d": 0, "d2h": 0, "h2d_bytes": 0, "d2h_bytes": 0}   # -stats (utils/stats.gpu_report)
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
@@ -210,6 +213,11 @@ def _make_impl(h):
         from ..ops import cell as CELL
         prog = p["prog"]
         return (lambda ctx, a: CELL.evaluate(prog, a)), "spoofCell"
+    if op == "magg":
+        # multi-aggregate template (compiler/codegen._multi_agg): a tuple of scalars, one pass
+        from ..ops import cell as CELL
+        mprog = p["prog"]
+        return (lambda ctx, a: CELL.evaluate_multi(mprog, a)), "spoofMA"
     if op == "t":
         return (lambda ctx, a: C.transpose(a[0])), "r'"
     if op == "rix":

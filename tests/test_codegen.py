@@ -67,9 +67,11 @@ def test_shared_intermediates_are_materialised():
     """
     cs = EX.compile_script(src, {}, config=DMLConfig(gpu=False))
     fused = _fused_hops(cs)
-    # T has two consumers: it is computed once, each aggregate fuses only its own operator
-    assert len(fused) == 3, fused
+    # T has two consumers: it is computed once; the two aggregates over T and X are one
+    # multi-aggregate pass (MAgg template)
+    assert len(fused) == 2, fused
     assert any("cell[exp,+]" in ln for ln in fused)
+    assert any("magg[" in ln for ln in fused), fused
 
 
 def test_sequential_fallback_errors_like_unfused():
@@ -236,3 +238,59 @@ def test_fused_script_on_gpu_matches_cp():
         a = a.double().cpu() if isinstance(a, torch.Tensor) else torch.tensor(float(a))
         b = b.double().cpu() if isinstance(b, torch.Tensor) else torch.tensor(float(b))
         assert torch.allclose(a, b, rtol=1e-9, atol=1e-9), k
+
+
+def test_multi_aggregate_template_parity():
+    """Full aggregates over shared inputs become one magg operator (reference
+    TemplateMultiAgg / MultiAggTmplTest) and match the unfused evaluation."""
+    src = """
+    a = sum(X * Y)
+    b = sum(X ^ 2)
+    c = sum(Y ^ 2 + 1)
+    d = max(X - Y)
+    e = min(abs(X) * 2)
+    q = a + b + c + d + e
+    """
+    rng = np.random.default_rng(11)
+    ins = {"X": rng.standard_normal((33, 7)), "Y": rng.standard_normal((33, 7))}
+    outs = ["a", "b", "c", "d", "e"]
+    cs = EX.compile_script(src, {}, inputs=ins, outputs=outs, config=DMLConfig(gpu=False))
+    text = EX.explain(cs.cp, "hops")
+    assert "magg[" in text, text
+    res, _ = EX.execute(cs, ins)
+    cs0 = EX.compile_script(src, {}, inputs=ins, outputs=outs, config=DMLConfig(gpu=False, fusion=False))
+    ref, _ = EX.execute(cs0, ins)
+    for k in outs:
+        assert float(res[k]) == pytest.approx(float(ref[k]), rel=1e-12), k
+
+
+@pytest.mark.gpu
+def test_multi_aggregate_kernel_gpu():
+    """One generated HIP kernel for the multi-aggregate (fp32 / fp64 / bf16 inputs, row and
+    column broadcast operands) against an fp64 torch evaluation."""
+    from systemml_amd.ops import cell as CELL
+    src = """
+    a = sum(X * Y)
+    b = sum((X - v) ^ 2)
+    c = max(X * w)
+    d = min(Y + v)
+    e = mean(X / 3)
+    """
+    rng = np.random.default_rng(12)
+    for dt in (torch.float32, torch.float64, torch.bfloat16):
+        X = torch.from_numpy(rng.standard_normal((1003, 37))).to("cuda", dt)
+        Y = torch.from_numpy(rng.standard_normal((1003, 37))).to("cuda", dt)
+        v = torch.from_numpy(rng.standard_normal((1003, 1))).to("cuda", torch.float32)
+        w = torch.from_numpy(rng.standard_normal((1, 37))).to("cuda", torch.float32)
+        ins = {"X": X, "Y": Y, "v": v, "w": w}
+        before = CELL.stats.get("magg_kernel", 0)
+        cs = EX.compile_script(src, {}, inputs=ins, outputs=list("abcde"), config=DMLConfig(gpu=True, precision="double"))
+        res, _ = EX.execute(cs, ins)
+        assert CELL.stats.get("magg_kernel", 0) > before
+        Xd, Yd, vd, wd = (t.double() for t in (X, Y, v, w))
+        ref = {"a": (Xd * Yd).sum(), "b": ((Xd - vd) ** 2).sum(), "c": (Xd * wd).max(), "d": (Yd + vd).min(),
+               "e": (Xd / 3).mean()}
+        for k, r in ref.items():
+            got = res[k]
+            got = float(got.value()) if hasattr(got, "value") else float(got)
+            assert got == pytest.approx(float(r), rel=1e-6 if dt == torch.float32 else 1e-9, abs=1e-9), (k, dt)
