@@ -56,28 +56,33 @@ def write(ctx, x, fname, format="text", **kw):
     a = _np(x)
     r, c = a.shape
     nnz = int(np.count_nonzero(a))
+    from ..ops import native as NAT
     if fmt in ("text", "ijv"):
-        i, j = np.nonzero(a)
-        with open(fname, "w") as f:
-            if len(i) == 0:
-                pass
-            for ii, jj in zip(i, j):
-                f.write(f"{ii + 1} {jj + 1} {S.java_double_str(float(a[ii, jj]))}\n")
+        open(fname, "w").close()
+        if not NAT.write_cells(fname, a, 1, append=True):
+            i, j = np.nonzero(a)
+            with open(fname, "w") as f:
+                for ii, jj in zip(i, j):
+                    f.write(f"{ii + 1} {jj + 1} {S.java_double_str(float(a[ii, jj]))}\n")
     elif fmt == "csv":
         sep = kw.get("sep", ",")
         header = str(kw.get("header", False)).upper() == "TRUE"
         with open(fname, "w") as f:
             if header:
                 f.write(sep.join(f"C{k + 1}" for k in range(c)) + "\n")
-            for row in a:
-                f.write(sep.join(S.java_double_str(float(v)) for v in row) + "\n")
+        if len(sep) != 1 or not NAT.write_cells(fname, a, 0, sep=sep, append=True):
+            with open(fname, "a") as f:
+                for row in a:
+                    f.write(sep.join(S.java_double_str(float(v)) for v in row) + "\n")
     elif fmt == "mm":
         i, j = np.nonzero(a)
         with open(fname, "w") as f:
             f.write("%%MatrixMarket matrix coordinate real general\n")
             f.write(f"{r} {c} {len(i)}\n")
-            for ii, jj in zip(i, j):
-                f.write(f"{ii + 1} {jj + 1} {S.java_double_str(float(a[ii, jj]))}\n")
+        if not NAT.write_cells(fname, a, 1, append=True):
+            with open(fname, "a") as f:
+                for ii, jj in zip(i, j):
+                    f.write(f"{ii + 1} {jj + 1} {S.java_double_str(float(a[ii, jj]))}\n")
     elif fmt == "binary":
         # the reference's binary-block SequenceFile (io/binaryblock.py): loads in SystemML
         from .binaryblock import write_binary_block

@@ -7,8 +7,11 @@
 // std::from_chars into a private buffer (rows counted first so the output is written
 // in place), and the result is one contiguous row-major double array owned by the
 // caller (sysml_free).
+#include <algorithm>
 #include <charconv>
 #include <cmath>
+#include <cstdio>
+#include <string>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -258,5 +261,113 @@ int64_t sysml_parse_ijv(const char* path, double** out, int threads) {
   *out = buf;
   return (int64_t)rows;
 }
+
+// ---------------------------------------------------------------------------------------
+// Writers (reference: runtime/io/WriterTextCSVParallel.java, WriterTextCellParallel.java):
+// cells formatted like java.lang.Double.toString from the shortest round-trip digits
+// (std::to_chars), rows formatted in parallel into per-thread buffers, written in order.
+// ---------------------------------------------------------------------------------------
+static int java_double(double d, char* out) {
+  if (std::isnan(d)) { std::memcpy(out, "NaN", 3); return 3; }
+  if (std::isinf(d)) {
+    if (d > 0) { std::memcpy(out, "Infinity", 8); return 8; }
+    std::memcpy(out, "-Infinity", 9); return 9;
+  }
+  if (d == 0.0) {
+    if (std::signbit(d)) { std::memcpy(out, "-0.0", 4); return 4; }
+    std::memcpy(out, "0.0", 3); return 3;
+  }
+  char buf[64];
+  auto r = std::to_chars(buf, buf + sizeof(buf), d, std::chars_format::scientific);
+  char* e = std::find(buf, r.ptr, 'e');
+  int exp10 = 0;
+  std::from_chars(e + 1 + (e[1] == '+'), r.ptr, exp10);     // [e+1, r.ptr): not NUL-terminated
+  char digits[32];
+  int nd = 0;
+  int k = 0;
+  bool neg = false;
+  if (buf[0] == '-') { neg = true; k = 1; }
+  for (; buf + k < e; ++k)
+    if (buf[k] != '.') digits[nd++] = buf[k];
+  while (nd > 1 && digits[nd - 1] == '0') --nd;
+  int o = 0;
+  if (neg) out[o++] = '-';
+  const double a = std::fabs(d);
+  if (a >= 1e-3 && a < 1e7) {
+    if (exp10 >= 0) {                      // ddd.ddd
+      for (int i = 0; i <= exp10; ++i) out[o++] = i < nd ? digits[i] : '0';
+      out[o++] = '.';
+      if (nd > exp10 + 1) for (int i = exp10 + 1; i < nd; ++i) out[o++] = digits[i];
+      else out[o++] = '0';
+    } else {                               // 0.000ddd
+      out[o++] = '0'; out[o++] = '.';
+      for (int i = 0; i < -exp10 - 1; ++i) out[o++] = '0';
+      for (int i = 0; i < nd; ++i) out[o++] = digits[i];
+    }
+    return o;
+  }
+  out[o++] = digits[0];
+  out[o++] = '.';
+  if (nd > 1) for (int i = 1; i < nd; ++i) out[o++] = digits[i];
+  else out[o++] = '0';
+  out[o++] = 'E';
+  auto r2 = std::to_chars(out + o, out + o + 8, exp10);
+  return (int)(r2.ptr - out);
+}
+
+// mode 0: dense rows joined by `sep` (csv); mode 1: "i j v" lines of the non-zeros (text / mm)
+int64_t sysml_write_cells(const char* path, const double* a, int64_t rows, int64_t cols, int mode, char sep,
+                          int append, int threads) {
+  FILE* f = std::fopen(path, append ? "ab" : "wb");
+  if (!f) return -1;
+  if (threads < 1) threads = 1;
+  const int64_t chunk = 4096;
+  std::vector<std::string> bufs(threads);
+  for (int64_t base = 0; base < rows; base += chunk * threads) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t) {
+      th.emplace_back([&, t]() {
+        std::string& b = bufs[t];
+        b.clear();
+        char cell[64], num[32];
+        const int64_t r0 = base + t * chunk, r1 = std::min(rows, r0 + chunk);
+        for (int64_t i = r0; i < r1; ++i) {
+          const double* row = a + i * cols;
+          if (mode == 0) {
+            for (int64_t j = 0; j < cols; ++j) {
+              if (j) b.push_back(sep);
+              const int n = java_double(row[j], cell);
+              b.append(cell, (size_t)n);
+            }
+            b.push_back('\n');
+          } else {
+            for (int64_t j = 0; j < cols; ++j) {
+              if (row[j] == 0.0) continue;
+              auto p = std::to_chars(num, num + 32, i + 1);
+              b.append(num, p.ptr - num);
+              b.push_back(' ');
+              p = std::to_chars(num, num + 32, j + 1);
+              b.append(num, p.ptr - num);
+              b.push_back(' ');
+              const int n = java_double(row[j], cell);
+              b.append(cell, (size_t)n);
+              b.push_back('\n');
+            }
+          }
+        }
+      });
+    }
+    for (auto& x : th) x.join();
+    for (int t = 0; t < threads; ++t)
+      if (!bufs[t].empty() && std::fwrite(bufs[t].data(), 1, bufs[t].size(), f) != bufs[t].size()) {
+        std::fclose(f);
+        return -2;
+      }
+  }
+  return std::fclose(f) == 0 ? 0 : -3;
+}
+
+// one Java-formatted double (tests / scalar writes)
+int sysml_java_double(double d, char* out) { return java_double(d, out); }
 
 }  // extern "C"

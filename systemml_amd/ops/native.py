@@ -36,6 +36,11 @@ def lib():
             L.sysml_parse_ijv.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_double)),
                                           ctypes.c_int]
             L.sysml_free.argtypes = [ctypes.c_void_p]
+            L.sysml_write_cells.restype = ctypes.c_int64
+            L.sysml_write_cells.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.c_int, ctypes.c_char, ctypes.c_int, ctypes.c_int]
+            L.sysml_java_double.restype = ctypes.c_int
+            L.sysml_java_double.argtypes = [ctypes.c_double, ctypes.c_char_p]
             _LIB = L
         except OSError:
             _LIB = None
@@ -89,3 +94,24 @@ def parse_ijv(path, threads=8):
     arr = np.ctypeslib.as_array(buf, shape=(max(n * 3, 1),))[: n * 3].copy().reshape(n, 3)
     L.sysml_free(buf)
     return arr
+
+
+def write_cells(path, a, mode, sep=",", append=False, threads=8):
+    """Write a dense fp64 matrix as csv rows (mode 0) or 'i j v' non-zero lines (mode 1)
+    with java.lang.Double.toString formatting; False when the library is unavailable."""
+    L = lib()
+    if L is None:
+        return False
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    r, c = a.shape
+    rc = L.sysml_write_cells(str(path).encode(), a.ctypes.data, r, c, mode, sep.encode()[:1], int(append), threads)
+    if rc != 0:
+        raise OSError(f"native writer failed ({rc}) for {path}")
+    return True
+
+
+def java_double(d):
+    L = lib()
+    buf = ctypes.create_string_buffer(64)
+    n = L.sysml_java_double(float(d), buf)
+    return buf.raw[:n].decode()

@@ -590,6 +590,10 @@ def b_table(ctx, A=None, B=None, W=None, odim1=None, odim2=None, *rest, **kw):
         a = torch.full((n,), float(A_), dtype=_dt(), device=_dev())
     if b is None:
         b = torch.full((n,), float(B_), dtype=_dt(), device=_dev())
+    # hybrid placement can leave one operand on the host and another in HBM
+    if b.device != a.device:
+        dev = a.device if a.is_cuda else b.device
+        a, b = a.to(dev), b.to(dev)
     if w is None:
         wv = torch.ones(n, dtype=_dt(), device=a.device)
     elif isinstance(w, Tensor):

@@ -177,3 +177,24 @@ def test_binary_block_sequencefile_roundtrip(tmp_path):
     q.write_bytes(body)
     got = BB.read_binary_block(str(q), 2, 5, brlen=2, bclen=3)
     np.testing.assert_array_equal(got, [[1, 2, 3, 0, 0], [4, 5, 6, 0, 9]])
+
+
+def test_native_text_writers_match_java_formatting(tmp_path):
+    """Native csv / ijv writers (ops/csrc/fastio.cpp) format cells exactly like
+    java.lang.Double.toString (runtime/scalars.java_double_str), special values included."""
+    from systemml_amd.ops import native
+    from systemml_amd.runtime.scalars import java_double_str
+    if native.lib() is None:
+        pytest.skip("native library not built")
+    rng = np.random.default_rng(8)
+    a = rng.standard_normal((700, 9)) * 10.0 ** rng.integers(-15, 15, (700, 9))
+    a[rng.random(a.shape) < 0.3] = 0.0
+    a[0, :6] = [np.nan, np.inf, -np.inf, -0.0, 1e7, 1e-3]
+    a[1, :4] = [9999999.0, 0.00099999, 5e-324, 1.7976931348623157e308]
+    native.write_cells(tmp_path / "a.csv", a, 0)
+    rows = (tmp_path / "a.csv").read_text().splitlines()
+    assert rows == [",".join(java_double_str(float(v)) for v in r) for r in a]
+    native.write_cells(tmp_path / "a.txt", a, 1)
+    i, j = np.nonzero(a)
+    want = [f"{ii + 1} {jj + 1} {java_double_str(float(a[ii, jj]))}" for ii, jj in zip(i, j)]
+    assert (tmp_path / "a.txt").read_text().splitlines() == want
