@@ -120,12 +120,13 @@ def cases(d):
     }
 
 
-def run_suite(script_dir, d, out_dir=None, only=None, out_lines=None):
+def run_suite(script_dir, d, out_dir=None, only=None, out_lines=None, config=None):
     """Run every case whose script exists in `script_dir` on the data in `d` (make_data); the
-    scripts' output files go to `out_dir` (default d/out).  Returns {name: None | exception}."""
+    scripts' output files go to `out_dir` (default d/out).  Returns {name: None | exception}.
+    `config`: DMLConfig of the runs (default: CP / host fp64)."""
     from systemml_amd.api import executor as EX
     from systemml_amd.conf import DMLConfig
-    cfg = DMLConfig(gpu=False)
+    cfg = config or DMLConfig(gpu=False)
     o = out_dir or f"{d}/out"
     os.makedirs(o, exist_ok=True)
     res = {}
