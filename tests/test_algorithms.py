@@ -410,12 +410,14 @@ def test_stratstats_against_numpy():
 
 
 def _km_ref(t, e):
+    """KM table at the event times (rows with at least one event: the reference's layout)."""
     ut = np.unique(t)
     n_risk = np.array([(t >= u).sum() for u in ut], float)
     d = np.array([e[t == u].sum() for u in ut], float)
     s = np.cumprod(1 - d / n_risk)
     gw = np.cumsum(d / np.maximum(n_risk * (n_risk - d), 1e-300) * (n_risk > d))
-    return ut, n_risk, d, s, s * np.sqrt(gw)
+    k = d > 0
+    return ut[k], n_risk[k], d[k], s[k], (s * np.sqrt(gw))[k]
 
 
 def test_kaplan_meier_and_logrank():
