@@ -6,7 +6,7 @@ one GPU).
 
     python bench_als.py [--rows R] [--cols C] [--per-row K] [--rank 10] [--maxi 5] [--steps 2]
 
-The ratings matrix is generated directly in HBM as CSR (K distinct-on-average random columns
+The ratings matrix is generated directly in HBM as canonical CSR (K distinct random columns
 per row, values 1..5), then scripts/algorithms/ALS-CG.dml (L2 regularisation, rank r, maxi
 outer iterations, loss check on) runs end to end: the weighted quaternary operators run as
 sampled products at the non-zeros (SDDMM kernel), the products with the ratings matrix as CSR
@@ -30,7 +30,10 @@ def ratings(rows, cols, per_row, seed=5):
     dev = torch.device("cuda")
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
-    colidx = torch.randint(0, cols, (rows, per_row), generator=g, device=dev).sort(dim=1).values
+    # distinct sorted columns per row: sorted draws from [0, cols - per_row] plus their rank
+    # (canonical CSR: no duplicate cells)
+    u = torch.randint(0, cols - per_row + 1, (rows, per_row), generator=g, device=dev).sort(dim=1).values
+    colidx = u + torch.arange(per_row, device=dev)
     vals = torch.randint(1, 6, (rows * per_row,), generator=g, device=dev).to(torch.float32)
     crow = torch.arange(0, rows * per_row + 1, per_row, device=dev, dtype=torch.int64)
     return torch.sparse_csr_tensor(crow, colidx.reshape(-1), vals, (rows, cols), device=dev)

@@ -688,13 +688,23 @@ def _match_wdivmm(a, b, transA, h):
     if mult:
         cands.append((q.inputs[1], q.inputs[0]))
     for W, R in cands:
-        m = _uv_eps(R) if not mult else (_uv(R) + (None,) if _uv(R) else None)
+        Xm = None
+        if mult and R.op == "b" and R.p["o"] == "-" and R.inputs[1].dt == "M" and _uv(R.inputs[0]):
+            # W * (U %*% t(V) - X): the residual form of ALS gradients (reference
+            # WDivMMType MULT_MINUS_LEFT / MULT_MINUS_RIGHT)
+            Xm = R.inputs[1]
+            m = _uv(R.inputs[0]) + (None,)
+            uvh = R.inputs[0]
+        else:
+            m = _uv_eps(R) if not mult else (_uv(R) + (None,) if _uv(R) else None)
+            uvh = R
         if m is None:
             continue
         U, V, e = m
         if (transA and other is U) or (not transA and other is V):
-            return _wq("wdivmm", [W, U, V] + ([e] if e is not None else []),
-                       {"left": transA, "mult": mult, "eps": e is not None}, "M", h, R)
+            ins = [W, U, V] + ([e] if e is not None else []) + ([Xm] if Xm is not None else [])
+            return _wq("wdivmm", ins, {"left": transA, "mult": mult, "eps": e is not None, "minus": Xm is not None},
+                       "M", h, uvh)
     return None
 
 

@@ -216,13 +216,19 @@ def wsigmoid(W, U, V, minus=False, log=False):
 
 
 # ------------------------------------------------------------------------------ wdivmm
-def wdivmm(W, U, V, left, mult=False, eps=None):
-    """left=False: (W op UV') %*% V  (m x r);  left=True: t(U) %*% (W op UV')  (r x n)."""
+def wdivmm(W, U, V, left, mult=False, eps=None, X=None):
+    """left=False: (W op UV') %*% V  (m x r);  left=True: t(U) %*% (W op UV')  (r x n);
+    with X (mult only): W * (UV' - X), the residual of the ALS gradients."""
     C = _C()
-    if SP.is_sparse(W) and _plain(U) and _plain(V):
+    if SP.is_sparse(W) and _plain(U) and _plain(V) and (X is None or _plain(X) or SP.is_sparse(X)):
         _check(U, V, W.shape[0], W.shape[1])
         dt = _cdt(W, U, V)
-        _, _, wv, uv = _sd(W, U, V, dt)
+        r, c, wv, uv = _sd(W, U, V, dt)
+        if X is not None:
+            if tuple(X.shape) != tuple(W.shape):
+                from ..parser.errors import DMLRuntimeError
+                raise DMLRuntimeError(f"wdivmm: X {tuple(X.shape)} does not match W {tuple(W.shape)}")
+            uv = uv - _values_at(X, W, r, c, dt)
         if mult:
             q = wv * uv
         else:
@@ -234,6 +240,8 @@ def wdivmm(W, U, V, left, mult=False, eps=None):
     uv = _uvt(U, V)
     if eps is not None:
         uv = C.binary("+", uv, eps)
+    if X is not None:
+        uv = C.binary("-", uv, SP.densify(X))
     q = C.binary("*", SP.densify(W), uv) if mult else _sparse_safe(W, C.binary("/", 1.0, uv))
     return C.mm(U, q, True) if left else C.mm(q, V)
 
@@ -283,7 +291,8 @@ def execute(p, a):
     if k == "wsigmoid":
         return wsigmoid(a[0], a[1], a[2], p.get("minus", False), p.get("log", False))
     if k == "wdivmm":
-        return wdivmm(a[0], a[1], a[2], p["left"], p.get("mult", False), eps)
+        return wdivmm(a[0], a[1], a[2], p["left"], p.get("mult", False), eps,
+                      X=a[-1] if p.get("minus") else None)
     if k == "wcemm":
         return wcemm(a[0], a[1], a[2], eps)
     if k == "wumm":

@@ -14,7 +14,10 @@ HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OURS = os.path.join(HERE, "systemml_amd", "scripts", "algorithms")
 ALGOS = ["LinearRegCG", "LinearRegDS", "GLM", "GLM-predict", "MultiLogReg", "l2-svm", "l2-svm-predict", "m-svm",
          "m-svm-predict", "naive-bayes", "naive-bayes-predict", "PCA", "Univar-Stats", "bivar-stats", "stratstats",
-         "ALS-CG", "KM", "Cox", "CsplineCG", "CsplineDS", "StepLinearRegDS"]
+         "KM", "Cox", "CsplineCG", "CsplineDS", "StepLinearRegDS"]
+# ALS-CG is left out: its unseeded random initialisation is drawn on the device by the GPU
+# backend, so the two runs start from different factors (tests/test_quaternary.py covers its
+# fused operators on both backends)
 
 
 def _read(path):
@@ -54,6 +57,8 @@ def test_algorithm_library_gpu_matches_cp(tmp_path):
         except Exception:   # noqa: BLE001 -- string frames
             continue
         compared += 1
+        if rel.startswith("pca"):
+            a, b = np.abs(a), np.abs(b)        # eigenvectors (and projections) up to sign
         if a.shape != b.shape:
             mism.append(f"{rel}: shape {a.shape} vs {b.shape}")
         elif not np.allclose(a, b, rtol=1e-6, atol=1e-8 * (np.nanmax(np.abs(a)) + 1), equal_nan=True):

@@ -242,3 +242,25 @@ def test_sddmm_hip_kernel_matches_fp32(r):
     assert got is not None
     torch.cuda.synchronize()
     np.testing.assert_allclose(got.cpu(), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_wdivmm_residual_forms_match_unfused():
+    """W * (U %*% t(V) - X) in both product orientations (the ALS-CG gradients) runs as a
+    sampled product at W's non-zeros and matches the unfused dense evaluation."""
+    import torch
+    from systemml_amd.api.executor import run, compile_script
+    from systemml_amd.conf import DMLConfig
+    g = torch.Generator().manual_seed(3)
+    R, C, k = 300, 200, 10
+    cols = torch.stack([torch.randperm(C, generator=g)[:k].sort().values for _ in range(R)])
+    X = torch.sparse_csr_tensor(torch.arange(0, R * k + 1, k), cols.reshape(-1),
+                                torch.randint(1, 6, (R * k,), generator=g).double(), (R, C))
+    U, V = torch.rand(R, 4, generator=g).double(), torch.rand(C, 4, generator=g).double()
+    for stmt in ("G = (W * (U %*% t(V) - X)) %*% V", "G = t(t(U) %*% (W * (U %*% t(V) - X)))"):
+        src = "W = (X != 0)\n" + stmt
+        ins = {"X": X, "U": U, "V": V}
+        cs = compile_script(src, inputs=ins, outputs=["G"], config=DMLConfig(gpu=False))
+        assert cs.cp.rewrite_stats.get("wquat-wdivmm") == 1, cs.cp.rewrite_stats
+        a = run(src, inputs=ins, outputs=["G"], config=DMLConfig(gpu=False), out=lambda s: None)["G"]
+        b = run(src, inputs=ins, outputs=["G"], config=DMLConfig(gpu=False, fusion=False), out=lambda s: None)["G"]
+        np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-12, atol=1e-10)
