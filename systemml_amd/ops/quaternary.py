@@ -234,9 +234,11 @@ def wdivmm(W, U, V, left, mult=False, eps=None, X=None):
         else:
             q = wv / (uv + eps if eps is not None else uv)
         S = _sparse_like(W, q)
+        # the sampled matrix times a factor: CSR SpMM (ops/hip/spmm.hip on the MI355X; t(S)
+        # by atomic scatter, no transposed copy)
         if left:
-            return torch.sparse.mm(S.t().to_sparse_csr(), U.to(dt)).t().contiguous()
-        return torch.sparse.mm(S, V.to(dt))
+            return SP.mm(S, U.to(dt), transA=True).t().contiguous()
+        return SP.mm(S, V.to(dt))
     uv = _uvt(U, V)
     if eps is not None:
         uv = C.binary("+", uv, eps)
