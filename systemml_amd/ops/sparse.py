@@ -126,15 +126,49 @@ def _dense_rhs(b, dtype):
     return b.to(dtype) if b.dtype != dtype else b
 
 
+_TPLANS = {}        # CSR pattern -> (crow of t(A), col of t(A), permutation), see _transpose_plan
+
+
+def _transpose_plan(a):
+    """Structure of t(A) for CSR A and the permutation taking A's values to t(A)'s CSR order,
+    cached per pattern: a pattern that is multiplied transposed again and again (the ratings
+    of ALS, the sampled matrices of wdivmm built on it) pays the sort once, and every product
+    is a gather plus the row-parallel SpMM instead of an atomic scatter.  The entry holds the
+    pattern tensors, so their storage (the key) cannot be reused while it is cached."""
+    crow, col = a.crow_indices(), a.col_indices()
+    key = (crow.data_ptr(), col.data_ptr(), tuple(a.shape), col.numel())
+    p = _TPLANS.get(key)
+    if p is None:
+        r, c = a.shape
+        rows = torch.repeat_interleave(torch.arange(r, device=crow.device), crow[1:] - crow[:-1])
+        perm = torch.argsort(col * r + rows)
+        crowT = torch.zeros(c + 1, dtype=torch.int64, device=crow.device)
+        crowT[1:] = torch.cumsum(torch.bincount(col, minlength=c), 0)
+        p = (crowT, rows[perm].contiguous(), perm, crow, col)
+        if len(_TPLANS) >= 4:
+            _TPLANS.pop(next(iter(_TPLANS)))
+        _TPLANS[key] = p
+    return p
+
+
 def mm(a, b, transA=False):
     """a %*% b (or t(a) %*% b) with a and/or b sparse.  On the MI355X a CSR left operand with
-    a dense right operand runs the hand-written SpMM / SpMV kernel of ops/hip/spmm.hip (t(A)
-    as a scatter with atomics, no transposed copy of A)."""
+    a dense right operand runs the hand-written SpMM / SpMV kernel of ops/hip/spmm.hip; t(A)
+    uses the cached transposed structure of A's pattern (_transpose_plan) when the product
+    is wide enough to pay for the value gather, else the kernel's atomic scatter."""
     if is_sparse(a) and a.layout == torch.sparse_csr and a.is_cuda and not is_sparse(b):
         from .backend import backend
         if backend.use_kernels:
             from . import kernels
-            r = kernels.spmm(a, densify(b), transA)
+            bd = densify(b)
+            if transA and bd.dim() == 2 and bd.shape[1] >= 4:
+                crowT, colT, perm, _, _ = _transpose_plan(a)
+                at = torch.sparse_csr_tensor(crowT, colT, a.values()[perm], (a.shape[1], a.shape[0]),
+                                             device=a.device)
+                r = kernels.spmm(at, bd, False)
+                if r is not None:
+                    return r
+            r = kernels.spmm(a, bd, transA)
             if r is not None:
                 return r
     if is_sparse(a):
