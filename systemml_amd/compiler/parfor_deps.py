@@ -260,25 +260,46 @@ def _assigned(st):
     return out
 
 
+def _has_parfor(st, memo):
+    k = id(st)
+    r = memo.get(k)
+    if r is None:
+        if isinstance(st, A.For) and st.parfor:
+            r = True
+        elif isinstance(st, A.If):
+            r = any(_has_parfor(x, memo) for x in st.then_body) or any(_has_parfor(x, memo) for x in st.else_body)
+        elif isinstance(st, (A.For, A.While)):
+            r = any(_has_parfor(x, memo) for x in st.body)
+        else:
+            r = False
+        memo[k] = r
+    return r
+
+
 def check_program(prog: A.Program):
-    """Run the analysis on every parfor of the program and its functions (before translation)."""
+    """Run the analysis on every parfor of the program and its functions (before translation).
+    Only statement subtrees that contain a parfor are walked (the read-after sets are
+    computed there alone), so programs without parfor pay one linear scan."""
+    memo = {}
+
     def walk(stmts, defined, after, loop=False):
         defined = set(defined)
         for k, st in enumerate(stmts):
-            # upward-exposed reads that follow statement k: the rest of the list, what follows
-            # the list, and in a loop body the statements before k (next iteration)
-            e1, k1 = _exposed(stmts[k + 1:])
-            later = e1 | (after - k1)
-            if loop:
-                later |= _exposed(stmts[:k], k1)[0]
-            if isinstance(st, A.If):
-                walk(st.then_body, defined, later)
-                walk(st.else_body, defined, later)
-            elif isinstance(st, (A.For, A.While)):
-                if isinstance(st, A.For) and st.parfor:
-                    check_parfor(st, defined | later)
-                inner_after = later | (_expr_vars(st.pred, set()) if isinstance(st, A.While) else set())
-                walk(st.body, defined | ({st.var} if isinstance(st, A.For) else set()), inner_after, loop=True)
+            if _has_parfor(st, memo):
+                # upward-exposed reads that follow statement k: the rest of the list, what
+                # follows the list, and in a loop body the statements before k (next iteration)
+                e1, k1 = _exposed(stmts[k + 1:])
+                later = e1 | (after - k1)
+                if loop:
+                    later |= _exposed(stmts[:k], k1)[0]
+                if isinstance(st, A.If):
+                    walk(st.then_body, defined, later)
+                    walk(st.else_body, defined, later)
+                elif isinstance(st, (A.For, A.While)):
+                    if isinstance(st, A.For) and st.parfor:
+                        check_parfor(st, defined | later)
+                    inner_after = later | (_expr_vars(st.pred, set()) if isinstance(st, A.While) else set())
+                    walk(st.body, defined | ({st.var} if isinstance(st, A.For) else set()), inner_after, loop=True)
             defined |= _assigned(st)
 
     walk(prog.statements, set(), set())
@@ -286,5 +307,5 @@ def check_program(prog: A.Program):
     for ns in (prog.namespaces or {}).values():
         fns.extend(ns.values())
     for fd in fns:
-        if not getattr(fd, "external", False):
+        if not getattr(fd, "external", False) and any(_has_parfor(x, memo) for x in fd.body):
             walk(fd.body, {p.name for p in fd.inputs}, {p.name for p in fd.outputs})
