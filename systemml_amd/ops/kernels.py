@@ -345,28 +345,35 @@ def mmchain(ctype, X, V, W=None):
     kp = _kpad(K)
     code, adt = _xcode(X)
     Vp = _pad_cols(V, kp, adt, X.device).contiguous()
-    S = None
     sbc = 0
     if W is not None:
         if W.shape[0] != X.shape[0]:
             return None
         if mode == XTWXV and W.shape[1] == 1:
-            S = W.to(device=X.device, dtype=adt).contiguous()
             sbc = 1
-        elif W.shape[1] == K:
-            S = _pad_cols(W, kp, adt, X.device).contiguous()
-        else:
+        elif W.shape[1] != K:
             return None
+
+    def padded_S():
+        # the row-side operand as a contiguous, kp-wide copy (only the paths that need one
+        # build it: it is an N x kp pass over HBM per call)
+        if W is None:
+            return None
+        if sbc:
+            return W.to(device=X.device, dtype=adt).contiguous()
+        return _pad_cols(W, kp, adt, X.device).contiguous()
+
     if _c4_ok(X, mode, kp):
         Vf = _pad_cols(V, kp, torch.float32, X.device).contiguous()
         # W as is (strided views included) when the kernel reads no column past it: sbc broadcast
-        # or W already kp wide; otherwise the zero-padded copy S
-        src = W if (W is not None and (sbc or W.shape[1] == kp)) else S
+        # or W already kp wide; otherwise the zero-padded copy
+        src = W if (W is not None and (sbc or W.shape[1] == kp)) else padded_S()
         Sf, lds = _rows_f32(src, kp, sbc, X.device) if src is not None else (None, 0)
         R = _chain4(mode, X, kp, Vf, Sf, lds, sbc)
         if R is not None:
             _count("chain4.mmchain." + ctype)
             return _result(R if kp == K else R[:, :K].contiguous())
+    S = padded_S()
     if _mfma_ok(X, kp, mode):
         R = _mchain(mode, X, kp, V=V, S=S, sbc=sbc)
         if R is not None:
