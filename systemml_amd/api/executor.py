@@ -123,6 +123,9 @@ def convert_input(v, dist=None, config=None):
         t = v
         if t.dim() == 1:
             t = t.reshape(-1, 1)
+        if t.layout in (torch.sparse_csr, torch.sparse_coo):
+            from ..ops import sparse as SP
+            t = SP.canonical(t)
     else:
         raise TypeError(f"unsupported input type {type(v).__name__}")
     if dist is not None and config is not None and t.shape[0] >= config.dist_min_rows:

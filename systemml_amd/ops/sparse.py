@@ -40,6 +40,27 @@ def is_special(x) -> bool:
     return is_sparse(x) or type(x).__name__ in ("CompressedMatrix", "ConstCol")
 
 
+def canonical(x):
+    """CSR with strictly increasing column indices within every row (duplicate cells summed,
+    as a dense conversion would): the sparse-at-non-zeros operators (weighted quaternaries,
+    sparse-safe cellwise ops) assume one stored entry per cell."""
+    if x.layout == torch.sparse_coo:
+        return x.coalesce().to_sparse_csr()
+    if x.layout != torch.sparse_csr:
+        return x
+    crow, col = x.crow_indices(), x.col_indices()
+    if col.numel() < 2:
+        return x
+    inc = col[1:] > col[:-1]
+    starts = torch.zeros(col.numel(), dtype=torch.bool, device=col.device)
+    b = crow[1:-1]
+    starts[b[b < col.numel()]] = True                 # first entry of each row
+    if bool((inc | starts[1:]).all()):
+        return x
+    rows = torch.repeat_interleave(torch.arange(x.shape[0], device=crow.device), crow[1:] - crow[:-1])
+    return from_ijv(rows, col, x.values(), x.shape[0], x.shape[1], x.values().dtype, x.device)
+
+
 def nnz(x) -> int:
     if is_sparse(x):
         return int(x._nnz()) if x.layout != torch.sparse_coo else int(x.coalesce()._nnz())
