@@ -68,6 +68,7 @@ class ForBlock(Block):
         self.params = params or {}
         self.pos = pos
         self.result_vars = []     # parfor: variables written in body and live after
+        self.accumulators = []    # parfor: result variables only updated by `+=` (summed on merge)
 
 
 class FunctionBlock(Block):

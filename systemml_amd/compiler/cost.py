@@ -294,7 +294,7 @@ def _chain_operands(h, consumers):
     ops = []
 
     def rec(x, top):
-        if x.op == "mm" and not x.p.get("transA") and (top or consumers.get(x.id, 0) <= 1):
+        if x.op == "mm" and not x.p.get("transA") and not x.p.get("mvagg") and (top or consumers.get(x.id, 0) <= 1):
             rec(x.inputs[0], False)
             rec(x.inputs[1], False)
         else:
@@ -329,7 +329,7 @@ def _build(ops, split, i, j, pos):
 
 def _tree_cost(h, dims, consumers):
     """Flops of the current parenthesisation of a chain rooted at h."""
-    if h.op == "mm" and not h.p.get("transA") and consumers.get(h.id, 0) <= 1:
+    if h.op == "mm" and not h.p.get("transA") and not h.p.get("mvagg") and consumers.get(h.id, 0) <= 1:
         a, b = h.inputs
         (ra, ca), (_, cb) = dims[a.id], dims[b.id]
         return _tree_cost(a, dims, consumers) + _tree_cost(b, dims, consumers) + float(ra) * ca * cb
@@ -353,7 +353,7 @@ def optimize_mm_chains(roots, env, stats):
         r = memo.get(h.id)
         if r is not None:
             return r
-        if h.op == "mm" and not h.p.get("transA"):
+        if h.op == "mm" and not h.p.get("transA") and not h.p.get("mvagg"):
             ops = _chain_operands(h, consumers)
             if len(ops) >= 3:
                 ods = [dims.get(o.id, UNK) for o in ops]

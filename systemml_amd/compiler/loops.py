@@ -293,6 +293,20 @@ def _reads_in(blocks, v):
     return False
 
 
+def _in_parfor(blocks, v):
+    """True when `v` is assigned inside a parfor nested in `blocks`."""
+    for b in blocks:
+        if isinstance(b, IfBlock):
+            if _in_parfor(b.then_blocks, v) or _in_parfor(b.else_blocks, v):
+                return True
+        elif isinstance(b, (WhileBlock, ForBlock)):
+            if isinstance(b, ForBlock) and b.parfor and v in assigned_in(b.body):
+                return True
+            if _in_parfor(b.body, v):
+                return True
+    return False
+
+
 def _lix_in(blocks, v, out):
     for b in blocks:
         if isinstance(b, BasicBlock):
@@ -327,6 +341,10 @@ def mark_update_in_place(blocks, stats=None):
             cand = sorted(assigned_in(b.body) - ({b.var} if isinstance(b, ForBlock) else set()))
             for v in cand:
                 lixes = _lix_in(b.body, v, [])
+                # a variable left-indexed inside a nested parfor stays copy-on-write: the
+                # workers share the pre-loop buffer and merge by comparing against it
+                if _in_parfor(b.body, v):
+                    continue
                 if lixes and all(h.dt == "M" for h in lixes) and _uip_ok(b.body, v):
                     b.inplace_vars.append(v)
                     for h in lixes:

@@ -238,11 +238,14 @@ class Rewriter:
                 for X, v in ((x.inputs[0], x.inputs[1]), (x.inputs[1], x.inputs[0])):
                     if X.dt != "M" or v.dt != "M":
                         continue
+                    # (a 1x1 "vector" broadcasts as a scalar: the product keeps the original
+                    # aggregate as its run-time fallback, p["mvagg"])
                     if d == "col" and _vec_kind(v) == "col" and _vec_kind(X) is None:
-                        return self._hit("colsums-mv", Hop("mm", [v, X], {"transA": True}, dt="M", pos=h.pos))
-                    if d == "row" and _vec_kind(v) == "row" and _vec_kind(X) is None:
-                        return self._hit("rowsums-mv", Hop("mm", [X, Hop("t", [v], dt="M", pos=h.pos)], {}, dt="M",
+                        return self._hit("colsums-mv", Hop("mm", [v, X], {"transA": True, "mvagg": "col"}, dt="M",
                                                            pos=h.pos))
+                    if d == "row" and _vec_kind(v) == "row" and _vec_kind(X) is None:
+                        return self._hit("rowsums-mv", Hop("mm", [X, Hop("t", [v], dt="M", pos=h.pos)],
+                                                           {"mvagg": "row"}, dt="M", pos=h.pos))
             return h
         if op == "u":
             x = h.inputs[0]

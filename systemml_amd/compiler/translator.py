@@ -242,6 +242,10 @@ class Translator:
                         pb3 = _BBuilder(self, ctx, consts, types)
                         p_incr = Predicate(pb3.expr(st.incr), pb3.reads)
                     params = {}
+                    for nm, pr in (("from", p_from), ("to", p_to), ("increment", p_incr)):
+                        if pr is not None and pr.root.dt == "M":
+                            raise LanguageError(f"{st.pos}: {'parfor' if st.parfor else 'for'} loop {nm} "
+                                                f"expression must be a scalar, got a matrix")
                     for k, v in st.params.items():
                         pbk = _BBuilder(self, ctx, consts, types)
                         hv = pbk.expr(v)
@@ -258,6 +262,9 @@ class Translator:
                     finally:
                         self.cond_depth -= 1
                     fb = ForBlock(st.var, p_from, p_to, p_incr, body, parfor=st.parfor, params=params, pos=st.pos)
+                    if st.parfor:
+                        from .parfor_deps import loop_accumulators
+                        fb.accumulators = loop_accumulators(st)
                     blocks.append(fb)
                     cur = _BBuilder(self, ctx, consts, types)
                 else:
@@ -718,7 +725,7 @@ def _reads_unknown_size(e):
     return False
 
 
-_M_BUILTINS = ("matrix rand seq sample cbind rbind table ctable diag rev removeEmpty replace order solve inv "
+_M_BUILTINS = ("matrix rand Rand seq sample cbind rbind table ctable diag rev removeEmpty replace order solve inv "
                "inverse cholesky outer quantile interQuantile aggregate lower.tri upper.tri conv2d "
                "conv2d_backward_filter conv2d_backward_data max_pool avg_pool max_pool_backward "
                "avg_pool_backward bias_add bias_multiply transformapply transformcolmap transform").split()

@@ -304,12 +304,13 @@ def binary(op, a, b, fn):
             return None
         if op in ("+", "-"):
             ac, bc = a.to_sparse_coo(), b.to_sparse_coo()
-            return ((ac + bc) if op == "+" else (ac - bc)).coalesce().to_sparse_csr()
+            r = ((ac + bc) if op == "+" else (ac - bc)).coalesce().to_sparse_csr()
+            return _with_values(r, r.values(), prune=True)      # cells that cancelled are not stored
         if op == "*":
             if torch.equal(a.crow_indices(), b.crow_indices()) and torch.equal(a.col_indices(), b.col_indices()):
-                return _with_values(a, a.values() * b.values())
-            r = (a.to_sparse_coo() * b.to_sparse_coo()).coalesce()
-            return r.to_sparse_csr()
+                return _with_values(a, a.values() * b.values(), prune=True)
+            r = (a.to_sparse_coo() * b.to_sparse_coo()).coalesce().to_sparse_csr()
+            return _with_values(r, r.values(), prune=True)
         return None
     if op != "*" or b.dim() != 2:
         return None

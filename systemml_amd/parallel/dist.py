@@ -685,7 +685,13 @@ def lix(x, y, rl, ru, cl, cu):
             raise DMLRuntimeError(f"left indexing: {y.shape} does not match [{r0}:{r1},{c0}:{c1}]")
         ly = _repartition(ctx, y.local, ctx.all_partitions(n), win, nc)
     elif isinstance(y, torch.Tensor):
-        ly = y if (y.shape[0] == 1 and n != 1) else y[ws:we] if y.shape[0] == n else y
+        # validated on every rank before any rank returns early, so a mismatch raises
+        # everywhere instead of leaving the ranks with rows in the window blocked in the
+        # next collective
+        if tuple(y.shape) != (n, nc) and y.numel() != 1:
+            raise DMLRuntimeError(f"left indexing dimension mismatch: target [{r0}:{r1},{c0}:{c1}] "
+                                  f"vs source {y.shape[0]}x{y.shape[1]}")
+        ly = y if y.numel() == 1 else y[ws:we]
     else:
         ly = y
     if we <= ws:

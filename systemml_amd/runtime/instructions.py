@@ -192,6 +192,20 @@ def _make_impl(h):
     if op == "mm":
         tA = p.get("transA", False)
         f = C.mm
+        mv = p.get("mvagg")
+        if mv:
+            # product from simplifyColSums/RowSumsMVMult: when the "vector" turns out to be
+            # 1x1 (a scalar-like broadcast against a matrix of more rows / columns), evaluate
+            # the original colSums(X * v) / rowSums(X * v)
+            def mvf(ctx, a):
+                v, X = (a[0], a[1]) if mv == "col" else (a[1], a[0])
+                vs, xs = tuple(v.shape), tuple(X.shape)
+                n = xs[0] if mv == "col" else xs[1]
+                if vs == (1, 1) and n != 1:
+                    vv = v if mv == "col" else C.transpose(v)
+                    return C.agg("sum", mv, C.binary("*", X, vv))
+                return f(a[0], a[1], tA)
+            return mvf, ("ba+*T" if tA else "ba+*")
         return (lambda ctx, a: f(a[0], a[1], tA)), ("ba+*T" if tA else "ba+*")
     if op == "tsmm":
         left = p["left"]

@@ -9,7 +9,9 @@ Execution model:
     private copies of the symbol table;
   * result variables (written in the body and live after the loop) are merged into
     the original with the reference's "merge with compare" semantics: every cell a
-    worker changed relative to the pre-loop value is copied into the result.
+    worker changed relative to the pre-loop value is copied into the result;
+    accumulators (variables only updated by `+=`, ResultMergeLocalMemory's accumulate
+    mode) are merged as the pre-loop value plus every worker's increment.
 On the GPU / SPMD backends workers run on one stream in task order (same result,
 no host thread contention); `par=1` or `mode=LOCAL` with one worker is sequential.
 """
@@ -165,9 +167,27 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
     with ThreadPoolExecutor(max_workers=k) as ex:
         futs = [ex.submit(worker) for _ in range(k)]
         results = [f.result() for f in futs]
+    acc = set(getattr(b, "accumulators", ()))
     for v in result_vars:
-        ctx.vars[v] = _merge(base[v], [r[v] for r in results])
+        rs = [r[v] for r in results]
+        ctx.vars[v] = _accumulate(base[v], rs) if v in acc else _merge(base[v], rs)
     ctx.vars[b.var] = iters[-1]
+
+
+def _accumulate(base, results):
+    """Accumulator merge: base + sum over workers of (worker value - base)."""
+    out = base
+    for r in results:
+        if r is base:
+            continue
+        if isinstance(base, torch.Tensor) or isinstance(r, torch.Tensor):
+            rt = torch.as_tensor(r)
+            if isinstance(base, torch.Tensor) and rt.shape != base.shape:
+                raise DMLRuntimeError("parfor result merge: dimension change of an accumulator")
+            out = out + (rt.to(base.device if isinstance(base, torch.Tensor) else rt.device) - base)
+        else:
+            out = out + (r - base)
+    return out
 
 
 # ----------------------------------------------------------------------------
@@ -203,9 +223,29 @@ def exec_parfor_spmd(ctx, b, iters, fork, result_vars, base):
     _run_iters(wctx, b, iters[lo:hi], range(lo, hi), fork)
     from ..parallel import dist as D
     D.stats["parfor_remote"] = D.stats.get("parfor_remote", 0) + 1
+    acc = set(getattr(b, "accumulators", ()))
     for v in result_vars:
-        ctx.vars[v] = _merge_spmd(dist, base[v], wctx.vars.get(v), lo < hi, hi)
+        if v in acc:
+            ctx.vars[v] = _accumulate_spmd(dist, base[v], wctx.vars.get(v), lo < hi)
+        else:
+            ctx.vars[v] = _merge_spmd(dist, base[v], wctx.vars.get(v), lo < hi, hi)
     ctx.vars[b.var] = iters[-1]
+
+
+def _accumulate_spmd(dist, base, mine, ran):
+    """Accumulator merge across ranks: base + all-reduce-sum of every rank's increment."""
+    import torch.distributed as tdist
+    mine = mine if ran else base
+    if isinstance(base, torch.Tensor):
+        dev = dist.device if tdist.get_backend(dist.group) != "gloo" else torch.device("cpu")
+        b = base.to(dev)
+        m = torch.as_tensor(mine).to(device=dev, dtype=torch.float64)
+        if m.shape != b.shape:
+            raise DMLRuntimeError("parfor result merge: dimension change of an accumulator")
+        d = m - b.double()
+        dist.allreduce_(d, "sum")
+        return (b.double() + d).to(base.dtype).to(base.device)
+    return base + dist.allreduce_scalar(float(mine) - float(base), "sum")
 
 
 def _merge_spmd(dist, base, mine, ran, last_idx):
@@ -221,11 +261,16 @@ def _merge_spmd(dist, base, mine, ran, last_idx):
         else:
             m = b
             changed = torch.zeros(b.shape, dtype=torch.bool, device=dev)
-        buf = torch.stack([torch.where(changed, m, torch.zeros((), dtype=b.dtype, device=dev)).double(),
-                           changed.double()])
-        dist.allreduce_(buf, "sum")
-        any_changed = buf[1] > 0
-        out = torch.where(any_changed, buf[0].to(b.dtype), b)
+        # a cell changed on several ranks (possible with check=0) takes the value of the
+        # highest-ranked writer -- the rank that ran the latest iterations, as the sequential
+        # loop would leave it -- never a sum of the writers' values
+        owner = torch.where(changed, torch.full((), float(dist.rank), dtype=torch.float64, device=dev),
+                            torch.full((), -1.0, dtype=torch.float64, device=dev))
+        dist.allreduce_(owner, "max")
+        mine_wins = owner == float(dist.rank)
+        val = torch.where(mine_wins, m.double(), torch.zeros((), dtype=torch.float64, device=dev))
+        dist.allreduce_(val, "sum")
+        out = torch.where(owner >= 0, val.to(b.dtype), b)
         return out.to(base.device)
     # scalars / other values: the rank that ran the highest-numbered iteration changing it wins
     changed = ran and not _eq(mine, base)

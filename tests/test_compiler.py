@@ -276,6 +276,15 @@ PARFOR_DEP_ERRORS = [
     ("R = matrix(0, 4, 1)\nparfor (i in 1:4) { R[i, 1] = sum(R) + i }\nprint(sum(R))", "R"),
     # plain write of a variable read after the loop
     ("parfor (i in 1:4) { x = i * 2 }\nprint(x)", "x"),
+    # only the nested loop variable varies the subscript: every iteration writes R[1..n, 1]
+    ("R = matrix(0, 4, 1)\nparfor (i in 1:3) { for (j in 1:4) { R[j, 1] = i } }\nprint(sum(R))", "R"),
+    # non-linear subscripts: several iterations address the same row
+    ("R = matrix(0, 4, 2)\nparfor (i in 1:8) { R[ceil(i / 2), ] = matrix(i, 1, 2) }\nprint(sum(R))", "R"),
+    ("R = matrix(0, 16, 1)\nparfor (i in 1:4) { k = i * i\n  R[k - i, 1] = i }\nprint(sum(R))", "R"),
+    # overlapping row blocks: width 3 with step 2
+    ("R = matrix(0, 12, 1)\nparfor (i in 1:4) { R[2 * i - 1:2 * i + 1, 1] = matrix(i, 3, 1) }\nprint(sum(R))", "R"),
+    # the same subscript variable defined twice in the body
+    ("R = matrix(0, 8, 1)\nparfor (i in 1:4) { k = i\n  if (i > 2) { k = 1 }\n  R[k, 1] = i }\nprint(sum(R))", "R"),
 ]
 
 PARFOR_DEP_OK = [
@@ -290,6 +299,14 @@ PARFOR_DEP_OK = [
     "parfor (i in 1:3) { x = i }\nx = 5\nprint(x)",
     # check=0 disables the analysis
     "s = 0\nparfor (i in 1:4, check=0) { s = i }\nprint(s)",
+    # disjoint row blocks of a loop-invariant block size, and a scaled / shifted row index
+    "bs = 3\nR = matrix(0, 12, 2)\nparfor (i in 1:4) { R[(i - 1) * bs + 1:i * bs, ] = matrix(i, bs, 2) }\nprint(sum(R))",
+    "R = matrix(0, 9, 1)\nparfor (i in 1:4) { p = 2 * i + 1\n  R[p, 1] = i }\nprint(sum(R))",
+    # row blocks clipped at the end: beg:min(N, beg + bs - 1) (Caffe2DML allreduce scoring)
+    "N = 10\nbs = 3\nP = matrix(0, rows=N, cols=2)\nparfor (i in 1:4) { beg = (i - 1) * bs + 1\n"
+    "  end = min(N, beg + bs - 1)\n  P[beg:end, ] = matrix(i, rows=end - beg + 1, cols=2) }\nprint(sum(P))",
+    # column linear in i while the row follows a nested loop
+    "R = matrix(0, 4, 3)\nparfor (i in 1:3) { for (j in 1:4) { R[j, i] = i * j } }\nprint(sum(R))",
 ]
 
 
@@ -327,3 +344,18 @@ while (i < 0) {
     with pytest.raises(Exception) as e:
         _run(bad, outputs=["s"])
     assert "line 6" in str(e.value) or "index" in str(e.value).lower()
+
+
+def test_mv_aggregate_rewrite_keeps_scalar_broadcast():
+    """colSums(X * matrix(s,1,1)) / rowSums(X * matrix(s,1,1)): the 1x1 operand broadcasts as
+    a scalar; the MV-product rewrite must not turn it into a non-conforming product."""
+    import numpy as np
+    from systemml_amd.api.executor import run
+    X = np.arange(12.0).reshape(4, 3)
+    r = run("s = 2.5\nA = colSums(X * matrix(s, 1, 1))\nB = rowSums(X * matrix(s, 1, 1))\n"
+            "C = colSums(X * rowSums(X))\nD = rowSums(X * colSums(X))",
+            inputs={"X": X}, outputs=["A", "B", "C", "D"], config=CFG)
+    np.testing.assert_allclose(r["A"].numpy(), 2.5 * X.sum(0, keepdims=True))
+    np.testing.assert_allclose(r["B"].numpy(), 2.5 * X.sum(1, keepdims=True))
+    np.testing.assert_allclose(r["C"].numpy(), (X * X.sum(1, keepdims=True)).sum(0, keepdims=True))
+    np.testing.assert_allclose(r["D"].numpy(), (X * X.sum(0, keepdims=True)).sum(1, keepdims=True))

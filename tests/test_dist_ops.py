@@ -83,7 +83,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+SRC_BAD_LIX = """
+X = rand(rows=90, cols=30, seed=1)
+X[1:10, 1:2] = matrix(1, rows=3, cols=2)
+s = sum(X)
+"""
+
+
+def _worker(rank, world, port, q, mode="ops"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
@@ -91,6 +98,15 @@ def _worker(rank, world, port, q):
         from systemml_amd.conf import DMLConfig
         ctx = D.init(backend="gloo")
         D.reset_stats()
+        if mode == "badlix":
+            from systemml_amd.api import executor as EX
+            cs = EX.compile_script(SRC_BAD_LIX, {}, outputs=["s"], config=DMLConfig(gpu=False, dist_min_rows=20))
+            try:
+                EX.execute(cs, {}, out=lambda s: None, dist=ctx)
+                q.put((rank, "no error", None, None, None))
+            except Exception as e:  # noqa: BLE001
+                q.put((rank, None, type(e).__name__ + ": " + str(e), None, None))
+            return
         out, kinds = _run(DMLConfig(gpu=False, dist_min_rows=20, seed=3), ctx)
         q.put((rank, out, kinds, dict(D.stats), dict(D.fallback_sites)))
         D.shutdown()
@@ -99,12 +115,12 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc(), None, None, None))
 
 
-def _spmd(world):
+def _spmd(world, mode="ops"):
     import torch.multiprocessing as mp
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -130,6 +146,15 @@ def test_dist_operators_match_single_process(world):
         for k in ("T2", "S2", "Tb", "wl"):
             assert not kinds[k].startswith("dist"), (k, kinds[k])
         assert stats["alltoall"] > 0
+
+
+def test_dist_lix_shape_error_raises_on_every_rank():
+    """A left-indexing source of the wrong shape into a row window only rank 0 owns: every
+    rank reports the error (no rank moves on to the next collective and hangs)."""
+    res = _spmd(2, "badlix")
+    for rank, err_none, msg, _, _ in res:
+        assert err_none is None, (rank, err_none)
+        assert "dimension mismatch" in msg, (rank, msg)
 
 
 def test_partitioned_reads(tmp_path):

@@ -19,6 +19,16 @@ S = matrix(0, rows=1, cols=7)
 parfor (j in 2:6, par=2) {
   S[1, j] = j * j
 }
+A = matrix(7, rows=3, cols=2)
+acc = 0
+parfor (i in 1:10) {
+  A += matrix(i, rows=3, cols=2)
+  acc += i
+}
+C = matrix(0, rows=1, cols=2)
+parfor (i in 1:4, check=0) {
+  C[1, 1] = i
+}
 z = sum(R) + sum(S)
 """
 
@@ -27,6 +37,7 @@ source("nn/examples/mnist_lenet_distrib_sgd.dml") as dsgd
 [X, Y] = dsgd::generate_dummy_data(48, 1, 12, 12, 4)
 [W1, b1, W2, b2, W3, b3, W4, b4] = dsgd::train(X, Y, X[1:8, ], Y[1:8, ], 1, 12, 12, 6, 4, 1)
 """
+SIMPLE_OUT = ["R", "S", "z", "A", "acc", "C"]
 LENET_OUT = ["W1", "b1", "W2", "b2", "W3", "b3", "W4", "b4"]
 
 
@@ -56,7 +67,7 @@ def _worker(rank, world, port, q):
         from systemml_amd.parallel import dist as D
         ctx = D.init(backend="gloo")
         D.reset_stats()
-        a = _run(SRC_SIMPLE, ["R", "S", "z"], ctx)
+        a = _run(SRC_SIMPLE, SIMPLE_OUT, ctx)
         b = _run(SRC_LENET, LENET_OUT, ctx)
         q.put((rank, a, b, dict(D.stats)))
         D.shutdown()
@@ -67,7 +78,8 @@ def _worker(rank, world, port, q):
 
 def test_spmd_parfor_matches_single_process():
     import torch.multiprocessing as mp
-    ref_a = _run(SRC_SIMPLE, ["R", "S", "z"])
+    ref_a = _run(SRC_SIMPLE, SIMPLE_OUT)
+    assert ref_a["A"].min() == 62 and ref_a["acc"] == 55 and ref_a["C"][0, 0] == 4
     ref_b = _run(SRC_LENET, LENET_OUT)
     world = 2
     port = _free_port()

@@ -395,3 +395,21 @@ def test_exec_types_decided_by_size_and_recompiled_at_runtime():
     # known sizes at compile time: chosen statically, nothing deferred
     cs = compile_script("A = rand(rows=400, cols=30)\nB = A %*% t(A)\nprint(sum(B))", config=cfg)
     assert cs.cp.exec_types.get("deferred", 0) == 0 and cs.cp.exec_types.get("GPU", 0) > 0
+
+
+@pytest.mark.parametrize("par", [1, 4])
+def test_parfor_accumulators(par):
+    """Accumulator result variables (`+=` only in the body; reference
+    functions/parfor/parfor_accumulator*.dml): merged as pre-loop value plus every worker's
+    increment, for matrices and scalars, sequential and threaded."""
+    src = f"""
+    R = matrix(7, rows=4, cols=3)
+    s = 1
+    parfor (i in 1:10, par={par}) {{
+      R += matrix(i, rows=4, cols=3)
+      s += i * 2
+    }}
+    """
+    res, _ = R(src, outputs=["R", "s"])
+    np.testing.assert_array_equal(M(res, "R"), np.full((4, 3), 62.0))
+    assert float(res["s"]) == 111

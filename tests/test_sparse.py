@@ -133,3 +133,17 @@ n2 = sum(S1)
         np.testing.assert_allclose(dn(r[k]), exp, rtol=1e-12, atol=1e-12, err_msg=k)
     assert r["S1"]._nnz() == int((A > 0).sum())           # no explicit zeros kept
     np.testing.assert_allclose(r["n2"], (A > 0).sum())
+
+
+def test_sparse_union_prunes_cancelled_cells():
+    """A - B of CSR operands where values cancel stores no explicit zeros (nnz counts true
+    non-zeros, quaternary fast paths never visit cancelled cells)."""
+    import torch
+    from systemml_amd.ops import sparse as S
+    a = torch.tensor([[1., 0, 2], [0, 3, 0]], dtype=torch.float64).to_sparse_csr()
+    b = torch.tensor([[1., 0, 0], [0, 3, 1]], dtype=torch.float64).to_sparse_csr()
+    r = S.binary("-", a, b, torch.sub)
+    assert r.layout == torch.sparse_csr and S.nnz(r) == 2
+    assert torch.equal(r.to_dense(), a.to_dense() - b.to_dense())
+    r = S.binary("+", a, -1.0 * b.to_dense().to_sparse_csr(), torch.add)
+    assert S.nnz(r) == 2
