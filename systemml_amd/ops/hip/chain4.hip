@@ -383,6 +383,267 @@ chain4_kernel(const T* __restrict__ X, int64_t N, int D, const float* __restrict
   for (int i = threadIdx.x; i < D * K; i += BLOCK) dst[i] = red[i];
 }
 
+// ---------------------------------------------------------------------------------------------
+// Matrix-core variant for bf16 X and K = 4 (chain4m): both products of the chain run on
+// v_mfma_f32_4x4x4bf16_1k (16 independent 4x4x4 blocks per instruction), so the per-element VALU
+// work of the kernel above (bf16 unpack + 2 packed FMAs per element and phase) disappears.
+//   phase 1  U[row][k] = sum_d X[row][d] V[d][k]: block b of step s takes d = 64s + 4b .. +3
+//            (A: lane 4b+i = row i of the group, a plain ds_read_b64 of 4 bf16 of that row;
+//            B: lane 4b+j = V[d][j], V split into three exact bf16 planes h + l1 + l2 held in
+//            registers), the 16 block partials are summed by a transposing butterfly.
+//   phase 2  acc[d][k] += sum_rows X[row][d] G[row][k]: block b of step s owns d = 64s + 4b .. +3
+//            (A: lane 4b+i = X[rows 0..3][64s + 4b + i], one ds_read_b64_tr_b16 hardware-transposed
+//            read; B: lane 4b+j = G[rows 0..3][j], G split into three bf16 planes through a
+//            per-wave LDS scratch), accumulated in 4 fp32 registers per step.
+// Every operand product is exact in fp32 (bf16 x bf16), so the result matches the VALU kernel's
+// fp32 accumulation.  Ring, row-side operand and counted vmcnt are the kernel above's.
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s4 as_s4(u2 v) {
+  s4 r;
+  __builtin_memcpy(&r, &v, 8);
+  return r;
+}
+
+// exact three-plane bf16 split by truncation: v = h + l1 + l2 (each residual fits 8 bits)
+__device__ __forceinline__ void split3(float v, uint32_t& h, uint32_t& l1, uint32_t& l2) {
+  const uint32_t hb = __float_as_uint(v) & 0xffff0000u;
+  const float r1 = v - __uint_as_float(hb);
+  const uint32_t b1 = __float_as_uint(r1) & 0xffff0000u;
+  const float r2 = r1 - __uint_as_float(b1);
+  h = hb >> 16;
+  l1 = b1 >> 16;
+  l2 = __float_as_uint(r2) >> 16;
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int ROW_ROR4 = 0x124, ROW_ROR8 = 0x128;
+
+// 8 ds_read_b64 (plain or transposed) from one base address at immediate offsets o + 128 s, with
+// their lgkmcnt wait in the same asm statement (see lds_row)
+#define C4M_READ8(OP, dst, addr, o)                                                                      \
+  asm volatile(OP " %0, %8 offset:" #o "\n\t" OP " %1, %8 offset:" #o "+128\n\t" OP " %2, %8 offset:" #o \
+               "+256\n\t" OP " %3, %8 offset:" #o "+384\n\t" OP " %4, %8 offset:" #o "+512\n\t" OP       \
+               " %5, %8 offset:" #o "+640\n\t" OP " %6, %8 offset:" #o "+768\n\t" OP " %7, %8 offset:" #o  \
+               "+896\n\ts_waitcnt lgkmcnt(0)"                                                            \
+               : "=&v"(dst[0]), "=&v"(dst[1]), "=&v"(dst[2]), "=&v"(dst[3]), "=&v"(dst[4]), "=&v"(dst[5]), \
+                 "=&v"(dst[6]), "=&v"(dst[7])                                                            \
+               : "v"(addr)                                                                               \
+               : "memory")
+
+template <int J>
+constexpr size_t lds_bytes_m() {
+  constexpr size_t ring = (size_t)WAVES * R * (J * 1024 + 256 + 64);
+  constexpr size_t red = (size_t)J * 512 * 4 * 4;
+  return ring > red ? ring : red;
+}
+
+template <int J, int MODE>
+__global__ void __launch_bounds__(BLOCK, 2)
+chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __restrict__ V, int ldv,
+               const float* __restrict__ S, int lds, int sbc, float* __restrict__ out,
+               float* __restrict__ U, int ldu, int64_t rows_per_block) {
+  constexpr int K = 4;
+  constexpr int NS = J * 8;                       // 64-column steps per row
+  constexpr int XB = J * 1024;
+  constexpr int SLOT = XB + 256 + 64;             // pitch = 16 banks mod 64: conflict-free 4-row reads
+  constexpr int NPR = J + 1;
+  constexpr bool SMG = (MODE == XTSMG);
+  constexpr int NSTG = SMG ? 1 : 0;
+  constexpr int NGR = R / G;
+  constexpr int WAITN = (NGR - 1) * (G * NPR + NSTG);
+  static_assert(NS % 8 == 0, "steps come in batches of 8");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int blk = lane >> 2, li = lane & 3;
+
+  // ---- V planes: bv[s][p] = plane p of V[64s + 4blk + e][li], e = 0..3 (zero past D)
+  s4 bv[NS][3];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    uint32_t h[4], l1[4], l2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int d = 64 * s + 4 * blk + e;
+      split3(d < D ? V[(int64_t)d * ldv + li] : 0.f, h[e], l1[e], l2[e]);
+    }
+    bv[s][0] = as_s4(u2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)});
+    bv[s][1] = as_s4(u2{l1[0] | (l1[1] << 16), l1[2] | (l1[3] << 16)});
+    bv[s][2] = as_s4(u2{l2[0] | (l2[1] << 16), l2[2] | (l2[3] << 16)});
+  }
+  f4 acc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = (r0 + rows_per_block < N) ? r0 + rows_per_block : N;
+  const int64_t rlast = r1 - 1;
+  int coff[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c0 = (j * 64 + lane) * 8;
+    coff[j] = (c0 < D) ? c0 : D - 8;
+  }
+  int scol;
+  if constexpr (SMG) scol = lane < sbc ? lane : sbc - 1;
+  else if constexpr (MODE == XTWXV || MODE == XTXVY) scol = sbc ? 0 : (lane < K ? lane : K - 1);
+  else scol = lane < K ? lane : K - 1;
+
+  lds_char* ring = (lds_char*)smem + wave * (R * SLOT);
+  float* const upad = U + N * (int64_t)ldu;
+
+  auto fetch = [&](int slot, int64_t rr) {
+    rr = (rr < rlast) ? rr : rlast;
+    const uint16_t* row = X + rr * (int64_t)D;
+    lds_char* sb = ring + slot * SLOT;
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(row + coff[j]),
+                                       (void __attribute__((address_space(3)))*)(sb + j * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(S + rr * (int64_t)lds + scol),
+                                     (void __attribute__((address_space(3)))*)(sb + XB), 4, 0, 0);
+  };
+
+  constexpr int STEP = WAVES * R;
+  int64_t base = r0 + wave;
+#pragma unroll
+  for (int q = 0; q < NGR; ++q) {
+    if constexpr (SMG) if (q > 0) *upad = 0.f;
+#pragma unroll
+    for (int s = 0; s < G; ++s) fetch(q * G + s, base + (q * G + s) * WAVES);
+  }
+
+  const int myrho = (lane >> 4) & 3, myk = lane & 3;   // (row, class) this lane owns after phase 1
+  // per-lane LDS addresses (bytes) relative to a group's first slot
+  const uint32_t a1 = (uint32_t)(li * SLOT + 8 * blk);                         // phase 1 row reads
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tg = lane >> 4;
+  const uint32_t a2 = (uint32_t)(tq * SLOT + 32 * tg + 8 * tp);                // phase 2 transposed reads
+  const uint32_t gsw = (uint32_t)(XB + 64 + ((myk * 4 + myrho) * 2));          // G scratch write (plane 0)
+  const uint32_t gsr = (uint32_t)(XB + 64 + li * 8);                            // G scratch read (plane 0)
+
+  for (; base < r1; base += STEP) {
+#pragma unroll
+    for (int q = 0; q < NGR; ++q) {
+      wait_vmcnt<WAITN>();
+      const uint32_t gb = (uint32_t)(uintptr_t)(ring + q * G * SLOT);
+      // ---- phase 1: three plane accumulators, 16 steps of 64 columns
+      f4 cu[3] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int h8 = 0; h8 < NS / 8; ++h8) {
+        u2 ar[8];
+        const uint32_t ad = gb + a1 + h8 * 1024;
+        C4M_READ8("ds_read_b64", ar, ad, 0);
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            cu[p] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(as_s4(ar[s]), bv[h8 * 8 + s][p], cu[p], 0, 0, 0);
+      }
+      // cu[p][i] on lane 4b+j: partial U[row i][class j] over block b's columns
+      float v4[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v4[i] = cu[0][i] + cu[1][i] + cu[2][i];
+      halve<0, 4>(v4, lane);            // lane bit 5 picks rows {0,1} / {2,3}
+      halve<1, 2>(v4, lane);            // lane bit 4 picks the row within the pair
+      float u = v4[0];
+      u += dppf<ROW_ROR8>(u);           // sum over lane bits 2, 3 (the remaining blocks)
+      u += dppf<ROW_ROR4>(u);
+      const int64_t myrow = base + (int64_t)(q * G + myrho) * WAVES;
+      const bool rvalid = myrow < r1;
+      const float sval = lds_f32(ring + (q * G + myrho) * SLOT + XB + 4 * myk);
+      float g;
+      if constexpr (MODE == XTXV) {
+        g = u;
+      } else if constexpr (MODE == XTWXV) {
+        g = sval * u;
+      } else if constexpr (MODE == XTXVY) {
+        g = u - sval;
+      } else if constexpr (MODE == XTPSXV) {
+        const float qv = sval * u;
+        float sq = qv + dpp<QP_X1>(qv);
+        sq += dpp<QP_X2>(sq);
+        g = qv - sval * sq;
+      } else {   // XTSMG: softmax over [u_1 .. u_kact, 0]
+        const bool act = myk < sbc;
+        float m = act ? u : 0.f;
+        m = fmaxf(m, dpp<QP_X1>(m));
+        m = fmaxf(m, dpp<QP_X2>(m));
+        m = fmaxf(m, 0.f);
+        const float e = act ? __expf(u - m) : 0.f;
+        float sm = e + dpp<QP_X1>(e);
+        sm += dpp<QP_X2>(sm);
+        sm += __expf(-m);
+        g = act ? e / sm - sval : 0.f;
+        const bool st = act && rvalid && (((lane >> 2) & 3) == 0);
+        float* dst = st ? U + myrow * (int64_t)ldu + myk : upad;
+        *dst = u;
+      }
+      g = rvalid ? g : 0.f;
+      // ---- G planes through the group's LDS scratch: Gs[p][class][row] bf16
+      {
+        uint32_t h, l1, l2;
+        split3(g, h, l1, l2);
+        const uint32_t w = gb + gsw;
+        asm volatile("ds_write_b16 %0, %1\n\tds_write_b16 %0, %2 offset:32\n\tds_write_b16 %0, %3 offset:64"
+                     :: "v"(w), "v"(h), "v"(l1), "v"(l2) : "memory");
+      }
+      u2 bg0, bg1, bg2;
+      {
+        const uint32_t r = gb + gsr;
+        asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %3 offset:32\n\tds_read_b64 %2, %3 offset:64\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(bg0), "=&v"(bg1), "=&v"(bg2) : "v"(r) : "memory");
+      }
+      const s4 bg[3] = {as_s4(bg0), as_s4(bg1), as_s4(bg2)};
+      // ---- phase 2: acc[s] += X^T[64s + ..][rows] G[rows][class]
+#pragma unroll
+      for (int h8 = 0; h8 < NS / 8; ++h8) {
+        u2 ar[8];
+        const uint32_t ad = gb + a2 + h8 * 1024;
+        C4M_READ8("ds_read_b64_tr_b16", ar, ad, 0);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int s = 0; s < 8; ++s)
+            acc[h8 * 8 + s] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(as_s4(ar[s]), bg[p], acc[h8 * 8 + s], 0, 0, 0);
+      }
+      // ---- refill the group's slots (their LDS reads have retired)
+#pragma unroll
+      for (int s = 0; s < G; ++s) fetch(q * G + s, base + STEP + (q * G + s) * WAVES);
+    }
+  }
+  wait_vmcnt<0>();
+
+  // ---- combine the 4 waves' accumulators: acc[s][i] on lane 4b+j = out[64s + 4b + i][j]
+  float* red = reinterpret_cast<float*>(smem);
+  __syncthreads();
+  for (int w = 0; w < WAVES; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int idx = (64 * s + 4 * blk + i) * K + li;
+          if (w == 0) red[idx] = acc[s][i];
+          else red[idx] += acc[s][i];
+        }
+    }
+    __syncthreads();
+  }
+  float* dst = out + (int64_t)blockIdx.x * D * K;
+  for (int i = threadIdx.x; i < D * K; i += BLOCK) dst[i] = red[i];
+}
+
+template <int J, int MODE>
+static int launch_m(bool occ, const void* X, int64_t N, int D, const float* V, int ldv, const float* S, int lds,
+                    int sbc, float* out, float* U, int ldu, int grid, int64_t rpb, hipStream_t st);
+
 static void allow_lds(const void* fn, size_t bytes) {
   static std::unordered_set<const void*> done;
   if (bytes <= 65536 || done.count(fn)) return;
@@ -430,9 +691,57 @@ static int route(int mode, int K, int J, bool occ, const void* X, int64_t N, int
   }
 }
 
+template <int J, int MODE>
+static int launch_m(bool occ, const void* X, int64_t N, int D, const float* V, int ldv, const float* S, int lds,
+                    int sbc, float* out, float* U, int ldu, int grid, int64_t rpb, hipStream_t st) {
+  auto kfn = chain4m_kernel<J, MODE>;
+  const size_t sh = lds_bytes_m<J>();
+  allow_lds(reinterpret_cast<const void*>(kfn), sh);
+  if (occ) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, BLOCK, sh) != hipSuccess) return -1;
+    return nb;
+  }
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(BLOCK), sh, st, (const uint16_t*)X, N, D, V, ldv, S, lds, sbc, out, U,
+                     ldu, rpb);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+static int route_m(int mode, int J, bool occ, const void* X, int64_t N, int D, const float* V, int ldv,
+                   const float* S, int lds, int sbc, float* out, float* U, int ldu, int grid, int64_t rpb,
+                   hipStream_t st) {
+#define C4M_CASE(MV)                                                                                       \
+  case MV:                                                                                                 \
+    return J == 1 ? launch_m<1, MV>(occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st)        \
+                  : launch_m<2, MV>(occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st);
+  switch (mode) {
+    C4M_CASE(XTXV) C4M_CASE(XTWXV) C4M_CASE(XTXVY) C4M_CASE(XTPSXV) C4M_CASE(XTSMG)
+    default: return -1;
+  }
+#undef C4M_CASE
+}
+
 }  // namespace sysml_c4
 
 extern "C" {
+
+// Matrix-core chain (bf16 X, K = 4): blocks per CU, and the launch (arguments as sysml_chain4).
+int sysml_chain4m_occupancy(int mode, int D) {
+  using namespace sysml_c4;
+  if (D <= 0 || D > 1024) return -1;
+  return route_m(mode, D <= 512 ? 1 : 2, true, nullptr, 0, D, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, 0, 0, 0,
+                 nullptr);
+}
+
+int sysml_chain4m(int mode, const void* X, int64_t N, int D, const float* V, int ldv, const float* S, int lds,
+                  int sbc, float* out, float* U, int ldu, int grid, int64_t rows_per_block, void* stream) {
+  using namespace sysml_c4;
+  if (D <= 0 || D > 1024 || (D & 7) || N <= 0 || grid <= 0 || (((uintptr_t)X) & 15)) return -1;
+  if (mode == XTSMG && (U == nullptr || sbc < 1 || sbc > 4)) return -1;
+  return route_m(mode, D <= 512 ? 1 : 2, false, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rows_per_block,
+                 (hipStream_t)stream);
+}
+
 
 // Blocks per CU of the kernel for (mode, xdtype, K, D) (the host sizes the grid from it).
 int sysml_chain4_occupancy(int mode, int xdtype, int K, int D) {

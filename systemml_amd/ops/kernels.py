@@ -95,6 +95,12 @@ def load(required=False):
                                ctypes.c_int64, ctypes.c_void_p]
     L.sysml_chain4_occupancy.restype = ctypes.c_int
     L.sysml_chain4_occupancy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.sysml_chain4m.restype = ctypes.c_int
+    L.sysml_chain4m.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p]
+    L.sysml_chain4m_occupancy.restype = ctypes.c_int
+    L.sysml_chain4m_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
     _lib = L
     return L
 
@@ -297,11 +303,21 @@ def _c4_ok(X, mode, kp):
     return not (mode == XTXV and kp == 4 and X.dtype == torch.bfloat16 and X.shape[1] > 512)
 
 
+def _c4m(X, kp):
+    """The matrix-core variant (chain4m_kernel: both products on 4x4x4 bf16 MFMAs) serves
+    bf16 X with K = 4; SYSML_C4M=0 keeps the VALU kernel (A/B switch)."""
+    return C4M and kp == 4 and X.dtype == torch.bfloat16
+
+
+C4M = os.environ.get("SYSML_C4M", "1") != "0"
+
+
 def _c4_grid(L, mode, X, kp):
     code = 0 if X.dtype == torch.bfloat16 else 1
-    key = (mode, code, kp, X.shape[1] > 512, X.device.index)
+    m = _c4m(X, kp)
+    key = (mode, code, kp, X.shape[1] > 512, X.device.index, m)
     if key not in _c4occ:
-        occ = L.sysml_chain4_occupancy(mode, code, kp, X.shape[1])
+        occ = L.sysml_chain4m_occupancy(mode, X.shape[1]) if m else L.sysml_chain4_occupancy(mode, code, kp, X.shape[1])
         cus = torch.cuda.get_device_properties(X.device).multi_processor_count
         _c4occ[key] = max(1, occ) * cus
     return _c4occ[key]
@@ -331,9 +347,16 @@ def _chain4(mode, X, kp, V, S, lds, sbc, U=None, ldu=0):
     part = torch.empty((grid, D * kp), dtype=torch.float32, device=X.device)
     if S is None:
         S, lds = V, 0      # the kernel streams a row-side operand in every mode: any valid memory
-    rc = L.sysml_chain4(mode, code, ctypes.c_void_p(X.data_ptr()), N, D, ctypes.c_void_p(V.data_ptr()), kp,
-                        ctypes.c_void_p(S.data_ptr()), lds, sbc, ctypes.c_void_p(part.data_ptr()),
-                        ctypes.c_void_p(U.data_ptr() if U is not None else 0), ldu, kp, grid, rpb, _stream())
+    if _c4m(X, kp):
+        rc = L.sysml_chain4m(mode, ctypes.c_void_p(X.data_ptr()), N, D, ctypes.c_void_p(V.data_ptr()), kp,
+                             ctypes.c_void_p(S.data_ptr()), lds, sbc, ctypes.c_void_p(part.data_ptr()),
+                             ctypes.c_void_p(U.data_ptr() if U is not None else 0), ldu, grid, rpb, _stream())
+        if rc == 0:
+            _count("chain4m")
+    else:
+        rc = L.sysml_chain4(mode, code, ctypes.c_void_p(X.data_ptr()), N, D, ctypes.c_void_p(V.data_ptr()), kp,
+                            ctypes.c_void_p(S.data_ptr()), lds, sbc, ctypes.c_void_p(part.data_ptr()),
+                            ctypes.c_void_p(U.data_ptr() if U is not None else 0), ldu, kp, grid, rpb, _stream())
     if rc != 0:
         return None
     return part.sum(0).reshape(D, kp)

@@ -251,3 +251,38 @@ def test_chain4_softmax_gradient(K, n, k):
     G64 = x64.t() @ (p - y)
     torch.testing.assert_close(U.double(), u64, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(G.double(), G64, rtol=2e-4, atol=2e-3 * G64.abs().max().item())
+
+
+@pytest.mark.parametrize("ctype", ["XtPSXv", "XtwXv", "XtXvy"])
+@pytest.mark.parametrize("n,d", [(70001, 1000), (4099, 512), (513, 136)])
+def test_chain4m_matrix_core_matches_valu(K, ctype, n, d):
+    """chain4m (both products on 4x4x4 bf16 MFMAs, V / G as exact three-plane bf16 splits) is as
+    accurate as the fp32 VALU row-group kernel against an fp64 reference, on random data."""
+    x = _mk(n, d, torch.bfloat16, seed=9)
+    x64 = x.double()
+    g0 = torch.Generator(device="cuda").manual_seed(4)
+    v = torch.randn((d, 4), generator=g0, device="cuda") * 0.05
+    w = torch.rand((n, 1 if ctype == "XtwXv" else 4), generator=g0, device="cuda")
+    u = x64 @ v.double()
+    w64 = w.double()
+    if ctype == "XtPSXv":
+        q = w64 * u
+        ref = x64.t() @ (q - w64 * q.sum(1, keepdim=True))
+    elif ctype == "XtwXv":
+        ref = x64.t() @ (w64 * u)
+    else:
+        ref = x64.t() @ (u - w64)
+    old = K.C4M
+    try:
+        c0 = K.counters.get("chain4m", 0)
+        K.C4M = True
+        r_m = K.mmchain(ctype, x, v, w)
+        assert K.counters.get("chain4m", 0) == c0 + 1
+        K.C4M = False
+        r_v = K.mmchain(ctype, x, v, w)
+    finally:
+        K.C4M = old
+    scale = ref.abs().max().item()
+    err_m = (r_m.double() - ref).abs().max().item() / scale
+    err_v = (r_v.double() - ref).abs().max().item() / scale
+    assert err_m < max(2e-5, 2 * err_v), (err_m, err_v)

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--cols", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--variants", default="")
     a = ap.parse_args()
     from systemml_amd.ops import kernels as K
     from systemml_amd.ops.backend import backend
@@ -34,10 +35,13 @@ def main():
     if a.only:
         cases = {k: v for k, v in cases.items() if k in a.only.split(",")}
     res = {}
-    variants = [("chain4", True), ("rowstream", False)]
+    variants = [("chain4m", True, True), ("chain4", True, False), ("rowstream", False, False)]
+    if a.variants:
+        variants = [v for v in variants if v[0] in a.variants.split(",")]
     for name0, fn in list(cases.items()):
-      for vname, flag in variants:
+      for vname, flag, mflag in variants:
         K.CHAIN4 = flag
+        K.C4M = mflag
         name = f"{name0}/{vname}"
         fn()
         ts = []
