@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--lazy", action="store_true",
                     help="HBM-resident lazy scalars (all matrices in HBM) instead of host scalars + hybrid "
                          "placement (measured slower on this benchmark: 511 vs 486 ms)")
+    ap.add_argument("--host-profile", default="",
+                    help="cProfile the timed steps (host time) and write the top functions to this file")
     ap.add_argument("--no-overlap", action="store_true",
                     help="compile MultiLogReg after LinregCG ran instead of overlapping the two")
     a = ap.parse_args()
@@ -153,6 +155,10 @@ def main():
 
     from concurrent.futures import ThreadPoolExecutor
     pool = ThreadPoolExecutor(1)
+    # the compile thread and the executing thread share the GIL: a short switch interval lets
+    # the executor take it back promptly after each device wait (the 5 ms default leaves the
+    # GPU idle while the compiler runs)
+    sys.setswitchinterval(0.0005)
 
     def compile_lr():
         return EX.compile_script(src_lr, args_lr, inputs={"X": X1, "y": y1}, outputs=["B_out"], config=cfg)
@@ -160,24 +166,25 @@ def main():
     def compile_mlr():
         return EX.compile_script(src_mlr, args_mlr, inputs={"X": X2, "Y_vec": lab}, outputs=["B_out"], config=cfg)
 
-    def step(stats=None, cs1=None, prefetch_next=False):
-        # both scripts are parsed + compiled once per step; the compilations run on a host
-        # thread while the GPU executes the previous script (MultiLogReg's while LinregCG
-        # runs, the next step's LinregCG while MultiLogReg runs; GPU-bound execution releases
-        # the GIL at each device wait), as a pipelined driver would
-        if cs1 is None:
-            cs1 = compile_lr()
-        fut = None if a.no_overlap else pool.submit(compile_mlr)
+
+    def compile_both():
+        return compile_lr(), compile_mlr()
+
+    def step(stats=None, cs=None, prefetch_next=False):
+        # both scripts are parsed + compiled once per step.  The next step's two compilations
+        # run on a host thread while this step's MultiLogReg executes (its ~350 ms of GPU work
+        # leaves the host mostly waiting on the device, which releases the GIL), as a
+        # pipelined driver would; LinregCG's short run keeps the host to itself
+        cs1, cs2 = cs if cs is not None else compile_both()
         r1, _ = EX.execute(cs1, {"X": X1, "y": y1}, out=out, dist=ctx, stats=stats)
-        cs2 = compile_mlr() if fut is None else fut.result()
-        nxt = pool.submit(compile_lr) if (prefetch_next and not a.no_overlap) else None
+        nxt = pool.submit(compile_both) if (prefetch_next and not a.no_overlap) else None
         r2, _ = EX.execute(cs2, {"X": X2, "Y_vec": lab}, out=out, dist=ctx, stats=stats)
         return r1["B_out"], r2["B_out"], (nxt.result() if nxt is not None else None)
 
     def run_steps(k, stats=None):
-        cs1 = None
+        cs = None
         for i in range(k):
-            _, _, cs1 = step(stats, cs1, prefetch_next=i + 1 < k)
+            _, _, cs = step(stats, cs, prefetch_next=i + 1 < k)
 
     run_steps(a.warmup)
     # compiled programs and the data live for the whole run: move them out of the cyclic
@@ -189,14 +196,30 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     st = Statistics(enabled=True) if a.stats else None
+    prof = None
+    if a.host_profile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     run_steps(a.steps, st)
     torch.cuda.synchronize()
+    if prof is not None:
+        prof.disable()
     if ctx:
         ctx.barrier()
     el = time.perf_counter() - t1
     if ctx:
         el = ctx.allreduce_scalar(el, "max")
     sec = el / a.steps
+    if prof is not None and rank == 0:
+        import io
+        import pstats
+        buf = io.StringIO()
+        ps = pstats.Stats(prof, stream=buf)
+        ps.sort_stats("tottime").print_stats(45)
+        ps.sort_stats("cumulative").print_stats(60)
+        with open(a.host_profile, "w") as f:
+            f.write(buf.getvalue())
     if rank == 0:
         if st is not None:
             print(st.report(25), file=sys.stderr)

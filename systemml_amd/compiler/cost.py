@@ -254,11 +254,11 @@ def physical_op(h, d, in_dims, et, config):
     an all-reduce), rmm (both row-partitioned: ring of the right operand's blocks), tsmm /
     mapmmchain (local fused kernel + all-reduce); GPU: MFMA GEMM, or a row-streaming kernel when
     the product is skinny (<= 8 columns) over a tall operand; CP: host GEMM."""
-    if et is None or h.op not in ("mm", "tsmm", "mmchain", "smgrad"):
+    if et is None or h.op not in ("mm", "tsmm", "mmchain", "smgrad", "smobj"):
         return None
     if h.op == "tsmm":
         return {"DIST": "tsmm+allreduce", "GPU": "mfma-tsmm", "CP": "cp-tsmm"}[et]
-    if h.op in ("mmchain", "smgrad"):
+    if h.op in ("mmchain", "smgrad", "smobj"):
         return {"DIST": "mapmmchain+allreduce", "GPU": "rowstream-chain", "CP": "cp-chain"}[et]
     a, b = in_dims[0], in_dims[1]
     if et == "DIST":

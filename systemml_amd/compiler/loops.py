@@ -94,7 +94,9 @@ def _hoist_block(bb: BasicBlock, variant, stats):
     def hoist(c):
         name = f"_licm{next(_names)}"
         pre_env[name] = c
-        hoisted[c.id] = Hop("tread", p={"name": name}, dt="M", dim1=c.dim1, dim2=c.dim2, pos=c.pos)
+        # licm_def: the hoisted expression, so fused-template matchers in the body can see
+        # through the transient read (rewrites.fuse_softmax_grad)
+        hoisted[c.id] = Hop("tread", p={"name": name, "licm_def": c}, dt="M", dim1=c.dim1, dim2=c.dim2, pos=c.pos)
 
     seen = set()
     for v in bb.env_out.values():        # an assigned value that is itself invariant

@@ -755,6 +755,9 @@ def rewrite_block(bb, config=None):
         n = fuse_softmax_grad(bb)
         if n:
             rw.stats["softmax-grad"] = n
+            nobj = sum(1 for h in H.walk(list(bb.roots) + list(bb.env_out.values())) if h.op == "smobj")
+            if nobj:
+                rw.stats["softmax-objective"] = nobj
         from .codegen import fuse_cells
         n = fuse_cells(bb)
         if n:
@@ -805,7 +808,77 @@ def _match_softmax_grad(G):
     zc = _bi_args(Z).get("cols")
     if zc is None or not _is_lit(zc, 1):
         return None
-    return X, U, U.inputs[1], Y, cu
+    return X, U, U.inputs[1], Y, cu, (P, L2, s)
+
+
+def _same_var(a, b):
+    """Same hop, or transient reads of the same variable (a loop-invariant read in the body and
+    its hoisted twin: the variable is not reassigned in between)."""
+    return a is b or (a.op == "tread" and b.op == "tread" and a.p.get("name") == b.p.get("name"))
+
+
+def _full_cols_rix(Y, cu):
+    """Y = Ybase[, 1:cu] (all rows, possibly hoisted out of the loop by LICM)  ->  Ybase, else None."""
+    if Y.op == "tread" and Y.p.get("licm_def") is not None:
+        Y = Y.p["licm_def"]
+    if Y.op != "rix":
+        return None
+    b, rl, ru, cl, cu2 = Y.inputs
+
+    def empty(x):
+        return x.op == "lit" and x.value is None
+    if empty(rl) and empty(ru) and _is_lit(cl, 1) and (cu2 is cu or (cu2.op == "lit" and cu.op == "lit"
+                                                                     and cu2.value == cu.value)):
+        return b
+    return None
+
+
+def _objective_terms(order, Yb, L2, s):
+    """The two data terms of the multinomial-logreg objective over the matched softmax:
+    sum(Yb * L2) (as agg-sum of a product or a tak+* dot) and sum(log(rowSums(E)))."""
+    s1 = s2 = None
+    yop = None
+
+    def pair(ins):
+        if len(ins) != 2:
+            return None
+        a, b = ins
+        if b is L2 and _same_var(a, Yb):
+            return a
+        if a is L2 and _same_var(b, Yb):
+            return b
+        return None
+    for h in order:
+        if s1 is None:
+            if h.op == "tak":
+                y = pair(h.inputs)
+                if y is not None:
+                    s1, yop = h, y
+            elif h.op == "agg" and h.p.get("o") == "sum" and h.p.get("dir") == "all":
+                x = h.inputs[0]
+                if x.op == "b" and x.p.get("o") == "*":
+                    y = pair(x.inputs)
+                    if y is not None:
+                        s1, yop = h, y
+        if s2 is None and h.op == "agg" and h.p.get("o") == "sum" and h.p.get("dir") == "all":
+            x = h.inputs[0]
+            if x.op == "u" and x.p.get("o") == "log" and x.inputs[0] is s:
+                s2 = h
+    return s1, s2, yop
+
+
+def _reaches(roots, target):
+    seen = set()
+    stack = list(roots)
+    while stack:
+        h = stack.pop()
+        if h is target:
+            return True
+        if h.id in seen:
+            continue
+        seen.add(h.id)
+        stack.extend(h.inputs)
+    return False
 
 
 def fuse_softmax_grad(bb):
@@ -823,39 +896,65 @@ def fuse_softmax_grad(bb):
 
     for r in list(bb.roots) + list(bb.env_out.values()):
         walk(r)
-    repl = {}
+    def apply(repl):
+        memo = {}
+
+        def sub(h):
+            r = repl.get(h.id)
+            if r is not None:
+                return r
+            if h.id in memo:
+                return h
+            memo[h.id] = True
+            h.inputs = [sub(c) for c in h.inputs]
+            return h
+
+        # the fused hop's own inputs must not be rewritten to its outputs
+        for r in repl.values():
+            F = r.inputs[0]
+            if F.id not in memo:
+                memo[F.id] = True
+                F.inputs = [sub(c) for c in F.inputs]
+        bb.roots = [sub(h) for h in bb.roots]
+        bb.env_out = {k: sub(v) for k, v in bb.env_out.items()}
+
+    nfused = 0
+    done = set()
     for h in order:
         m = _match_softmax_grad(h)
         if m is None:
             continue
-        X, U, V, Y, cu = m
-        if U.id in repl:
+        X, U, V, Y, cu, (P, L2, srow) = m
+        if U.id in done:
             continue
+        done.add(U.id)
+        # objective form (op smobj): the probabilities, the gradient and the objective's data
+        # terms in one pass, when nothing else reads X %*% V or the intermediate matrices
+        Yb = _full_cols_rix(Y, cu)
+        if Yb is not None:
+            s1, s2, yop = _objective_terms(order, Yb, L2, srow)
+            if s1 is not None and s2 is not None:
+                F = Hop("smobj", [X, V, yop, cu], {}, dt="U", pos=h.pos)
+                repl = {P.id: Hop("fout", [F], {"i": 0}, dt="M", pos=P.pos),
+                        h.id: Hop("fout", [F], {"i": 1}, dt="M", pos=h.pos),
+                        s1.id: Hop("fout", [F], {"i": 2}, dt="S", pos=s1.pos),
+                        s2.id: Hop("fout", [F], {"i": 3}, dt="S", pos=s2.pos)}
+                saved = (list(bb.roots), dict(bb.env_out), [list(x.inputs) for x in order])
+                apply(repl)
+                live = bb.live_out
+                outs = [v for k, v in bb.env_out.items() if live is None or k in live]
+                if not _reaches(list(bb.roots) + outs, U):
+                    nfused += 1
+                    continue
+                # another consumer still needs X %*% V: undo, fuse (U, G) only
+                bb.roots, bb.env_out = saved[0], saved[1]
+                for x, ins in zip(order, saved[2]):
+                    x.inputs = ins
         F = Hop("smgrad", [X, V, Y, cu], {}, dt="U", pos=h.pos)
-        repl[U.id] = Hop("fout", [F], {"i": 0}, dt="M", pos=U.pos)
-        repl[h.id] = Hop("fout", [F], {"i": 1}, dt="M", pos=h.pos)
-    if not repl:
-        return 0
-    memo = {}
-
-    def sub(h):
-        r = repl.get(h.id)
-        if r is not None:
-            return r
-        if h.id in memo:
-            return h
-        memo[h.id] = True
-        h.inputs = [sub(c) for c in h.inputs]
-        return h
-
-    # the fused hop's own inputs must not be rewritten to its outputs
-    for r in repl.values():
-        F = r.inputs[0]
-        memo[F.id] = True
-        F.inputs = [sub(c) for c in F.inputs]
-    bb.roots = [sub(h) for h in bb.roots]
-    bb.env_out = {k: sub(v) for k, v in bb.env_out.items()}
-    return len(repl) // 2
+        apply({U.id: Hop("fout", [F], {"i": 0}, dt="M", pos=U.pos),
+               h.id: Hop("fout", [F], {"i": 1}, dt="M", pos=h.pos)})
+        nfused += 1
+    return nfused
 
 
 def rewrite_pred(pred, config=None):

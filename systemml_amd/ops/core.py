@@ -682,6 +682,43 @@ def smgrad(X, V, Y, cu=None):
     return smgrad_ref(X, V, Y, kc)
 
 
+def smobj(X, V, Y, cu=None):
+    """Fused multinomial-logreg candidate evaluation with the objective (compiler op `smobj`,
+    rewrites.fuse_softmax_grad): with L = cbind(X %*% V, 0), LT = L - rowMaxs(L), E = exp(LT),
+    returns (P, G, s1, s2): P = E / rowSums(E), G = t(X) %*% (P[, 1:cu] - Y[, 1:cu]),
+    s1 = sum(Y * LT), s2 = sum(log(rowSums(E))) -- one pass over X on the MI355X."""
+    K = V.shape[1] if hasattr(V, "shape") else None
+    kc = K if cu is None else int(S.as_double(cu))
+    if is_dist(X):
+        return _dist().smobj(X, V, Y, kc)
+    if type(X) is not _CC and backend.use_kernels and isinstance(X, Tensor) and X.is_cuda \
+            and not SP.is_sparse(X) and kc == K and isinstance(V, Tensor) and isinstance(Y, Tensor) \
+            and not SP.is_sparse(Y):
+        from . import kernels
+        r = kernels.smobj(X, V, Y)
+        if r is not None:
+            return r
+    return smobj_ref(X, V, Y, kc)
+
+
+def smobj_ref(X, V, Y, kc):
+    if type(X) is _CC:
+        u, _ = AUG.smgrad(X, V, rix(Y, None, None, 1, kc), kc)
+    else:
+        u = mm(X, V)
+    lt = cvt(u) if not isinstance(u, Tensor) or SP.is_sparse(u) else u
+    lt = torch.cat([lt, torch.zeros((lt.shape[0], 1), dtype=lt.dtype, device=lt.device)], dim=1)
+    lt = lt - lt.max(dim=1, keepdim=True).values
+    e = torch.exp(lt)
+    rs = e.sum(dim=1, keepdim=True)
+    p = e / rs
+    Yd = cvt(SP.densify(Y)).to(device=lt.device, dtype=lt.dtype)
+    s1 = float((Yd * lt).sum().item())
+    s2 = float(torch.log(rs).sum().item())
+    g = binary("-", p[:, :kc], Yd[:, :kc])
+    return p, mm(X, g, transA=True), s1, s2
+
+
 def smgrad_ref(X, V, Y, kc):
     u = mm(X, V)
     lt = cvt(u) if not isinstance(u, Tensor) or SP.is_sparse(u) else u

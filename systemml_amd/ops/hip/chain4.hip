@@ -29,7 +29,10 @@
 
 namespace sysml_c4 {
 
-enum Mode { XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5, XTSMG = 10 };   // = rowstream.hip
+enum Mode { XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5, XTSMG = 10, XTSMGO = 11 };   // = rowstream.hip
+// XTSMGO (chain4m only): the softmax gradient plus the multinomial-logreg objective terms and
+// the full probability matrix -- P = softmax(cbind(X V, 0)) (N x (K+1)), G = t(X) (P[,1:K] -
+// Y[,1:K]), sum(Y * (L - rowMaxs(L))) and sum(log(rowSums(exp(L - rowMaxs(L))))), L = cbind(X V, 0)
 constexpr int WAVES = 4;
 constexpr int BLOCK = 64 * WAVES;
 constexpr int G = 4;     // rows per group
@@ -443,18 +446,19 @@ constexpr size_t lds_bytes_m() {
   return ring > red ? ring : red;
 }
 
-template <int J, int MODE>
+template <int J, int MODE, int VAR>
 __global__ void __launch_bounds__(BLOCK, 2)
 chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __restrict__ V, int ldv,
                const float* __restrict__ S, int lds, int sbc, float* __restrict__ out,
-               float* __restrict__ U, int ldu, int64_t rows_per_block) {
+               float* __restrict__ U, int ldu, int64_t rows_per_block, double* __restrict__ obj) {
   constexpr int K = 4;
   constexpr int NS = J * 8;                       // 64-column steps per row
   constexpr int XB = J * 1024;
   constexpr int SLOT = XB + 256 + 64;             // pitch = 16 banks mod 64: conflict-free 4-row reads
   constexpr int NPR = J + 1;
-  constexpr bool SMG = (MODE == XTSMG);
-  constexpr int NSTG = SMG ? 1 : 0;
+  constexpr bool OBJ = (MODE == XTSMGO);
+  constexpr bool SMG = (MODE == XTSMG) || OBJ;
+  constexpr int NSTG = OBJ ? 2 : SMG ? 1 : 0;
   constexpr int NGR = R / G;
   constexpr int WAITN = (NGR - 1) * (G * NPR + NSTG);
   static_assert(NS % 8 == 0, "steps come in batches of 8");
@@ -491,12 +495,14 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
     coff[j] = (c0 < D) ? c0 : D - 8;
   }
   int scol;
-  if constexpr (SMG) scol = lane < sbc ? lane : sbc - 1;
+  if constexpr (OBJ) scol = lane <= sbc ? lane : sbc;       // Y[, 1 .. K+1]
+  else if constexpr (SMG) scol = lane < sbc ? lane : sbc - 1;
   else if constexpr (MODE == XTWXV || MODE == XTXVY) scol = sbc ? 0 : (lane < K ? lane : K - 1);
   else scol = lane < K ? lane : K - 1;
 
   lds_char* ring = (lds_char*)smem + wave * (R * SLOT);
   float* const upad = U + N * (int64_t)ldu;
+  float o1 = 0.f, o2 = 0.f;     // XTSMGO: this lane's share of sum(Y * LT) and sum(log(rowSums(E)))
 
   auto fetch = [&](int slot, int64_t rr) {
     rr = (rr < rlast) ? rr : rlast;
@@ -515,6 +521,7 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
 #pragma unroll
   for (int q = 0; q < NGR; ++q) {
     if constexpr (SMG) if (q > 0) *upad = 0.f;
+    if constexpr (OBJ) if (q > 0) *upad = 0.f;
 #pragma unroll
     for (int s = 0; s < G; ++s) fetch(q * G + s, base + (q * G + s) * WAVES);
   }
@@ -526,19 +533,37 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
   const uint32_t a2 = (uint32_t)(tq * SLOT + 32 * tg + 8 * tp);                // phase 2 transposed reads
   const uint32_t gsw = (uint32_t)(XB + 64 + ((myk * 4 + myrho) * 2));          // G scratch write (plane 0)
   const uint32_t gsr = (uint32_t)(XB + 64 + li * 8);                            // G scratch read (plane 0)
+  const uint32_t asv = (uint32_t)(myrho * SLOT + XB + 4 * myk);                 // row-side value
 
   for (; base < r1; base += STEP) {
 #pragma unroll
     for (int q = 0; q < NGR; ++q) {
       wait_vmcnt<WAITN>();
       const uint32_t gb = (uint32_t)(uintptr_t)(ring + q * G * SLOT);
-      // ---- phase 1: three plane accumulators, 16 steps of 64 columns
+      // ---- phase 1: three plane accumulators, 16 steps of 64 columns; the first batch of
+      // row reads also fetches this lane's row-side value (one lgkmcnt wait for both)
       f4 cu[3] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+      float sval;
 #pragma unroll
       for (int h8 = 0; h8 < NS / 8; ++h8) {
         u2 ar[8];
         const uint32_t ad = gb + a1 + h8 * 1024;
-        C4M_READ8("ds_read_b64", ar, ad, 0);
+        if (VAR == 1 && h8 == 0) {
+          uint32_t sv;
+          asm volatile(
+              "ds_read_b64 %0, %9\n\tds_read_b64 %1, %9 offset:128\n\tds_read_b64 %2, %9 offset:256\n\t"
+              "ds_read_b64 %3, %9 offset:384\n\tds_read_b64 %4, %9 offset:512\n\tds_read_b64 %5, %9 offset:640\n\t"
+              "ds_read_b64 %6, %9 offset:768\n\tds_read_b64 %7, %9 offset:896\n\tds_read_b32 %8, %10\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(ar[0]), "=&v"(ar[1]), "=&v"(ar[2]), "=&v"(ar[3]), "=&v"(ar[4]), "=&v"(ar[5]), "=&v"(ar[6]),
+                "=&v"(ar[7]), "=&v"(sv)
+              : "v"(ad), "v"(gb + asv)
+              : "memory");
+          sval = __uint_as_float(sv);
+        } else {
+          C4M_READ8("ds_read_b64", ar, ad, 0);
+          if (VAR != 1 && h8 == 0) sval = lds_f32(ring + (q * G + myrho) * SLOT + XB + 4 * myk);
+        }
 #pragma unroll
         for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -554,9 +579,12 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
       float u = v4[0];
       u += dppf<ROW_ROR8>(u);           // sum over lane bits 2, 3 (the remaining blocks)
       u += dppf<ROW_ROR4>(u);
-      const int64_t myrow = base + (int64_t)(q * G + myrho) * WAVES;
-      const bool rvalid = myrow < r1;
-      const float sval = lds_f32(ring + (q * G + myrho) * SLOT + XB + 4 * myk);
+      // row of this lane's (row, class) value as a 32-bit offset from the wave-uniform base
+      // (64-bit address math stays scalar: it is register-pressure critical here)
+      const int roff = (q * G + myrho) * WAVES;
+      const int64_t left = r1 - base;
+      const bool rvalid = roff < (left < (int64_t)0x7fffffff ? (int)left : 0x7fffffff);
+      float* const ub = U + base * (int64_t)ldu;
       float g;
       if constexpr (MODE == XTXV) {
         g = u;
@@ -571,6 +599,12 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
         g = qv - sval * sq;
       } else {   // XTSMG: softmax over [u_1 .. u_kact, 0]
         const bool act = myk < sbc;
+        if constexpr (!OBJ) {
+          const bool st = act && rvalid && (((lane >> 2) & 3) == 0);
+          float* dst = st ? ub + (roff * ldu + myk) : upad;
+          *dst = u;
+          asm volatile("" ::: "memory");
+        }
         float m = act ? u : 0.f;
         m = fmaxf(m, dpp<QP_X1>(m));
         m = fmaxf(m, dpp<QP_X2>(m));
@@ -580,11 +614,26 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
         sm += dpp<QP_X2>(sm);
         sm += __expf(-m);
         g = act ? e / sm - sval : 0.f;
-        const bool st = act && rvalid && (((lane >> 2) & 3) == 0);
-        float* dst = st ? U + myrow * (int64_t)ldu + myk : upad;
-        *dst = u;
+        if constexpr (OBJ) {
+          const bool rep0 = rvalid && (((lane >> 2) & 3) == 0);
+          // probabilities of the K + 1 classes (the last one is the zero column of L) and the
+          // row's objective terms sum_k Y[r,k] (L[r,k] - max) and log(sum_k exp(L[r,k] - max))
+          const float rs = 1.f / sm;
+          const float ylast = lds_f32(ring + (q * G + myrho) * SLOT + XB + 4 * sbc);
+          float* d1 = (act && rep0) ? ub + (roff * ldu + myk) : upad;
+          *d1 = e * rs;
+          float* d2 = (myk == 0 && rep0) ? ub + (roff * ldu + sbc) : upad;
+          *d2 = __expf(-m) * rs;
+          float t1 = act ? sval * (u - m) : 0.f;
+          if (myk == 0) t1 -= ylast * m;
+          if (rep0) {
+            o1 += t1;
+            if (myk == 0) o2 += __logf(sm);
+          }
+        }
       }
       g = rvalid ? g : 0.f;
+      __builtin_amdgcn_sched_barrier(0);   // keep phase-2 work from being hoisted (register pressure)
       // ---- G planes through the group's LDS scratch: Gs[p][class][row] bf16
       {
         uint32_t h, l1, l2;
@@ -593,20 +642,40 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
         asm volatile("ds_write_b16 %0, %1\n\tds_write_b16 %0, %2 offset:32\n\tds_write_b16 %0, %3 offset:64"
                      :: "v"(w), "v"(h), "v"(l1), "v"(l2) : "memory");
       }
+      // ---- phase 2: acc[s] += X^T[64s + ..][rows] G[rows][class]; the G planes are read back
+      // together with the first batch of transposed X reads (one wait)
       u2 bg0, bg1, bg2;
-      {
-        const uint32_t r = gb + gsr;
-        asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %3 offset:32\n\tds_read_b64 %2, %3 offset:64\n\t"
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=&v"(bg0), "=&v"(bg1), "=&v"(bg2) : "v"(r) : "memory");
-      }
-      const s4 bg[3] = {as_s4(bg0), as_s4(bg1), as_s4(bg2)};
-      // ---- phase 2: acc[s] += X^T[64s + ..][rows] G[rows][class]
+      s4 bg[3];
 #pragma unroll
       for (int h8 = 0; h8 < NS / 8; ++h8) {
         u2 ar[8];
         const uint32_t ad = gb + a2 + h8 * 1024;
-        C4M_READ8("ds_read_b64_tr_b16", ar, ad, 0);
+        if (VAR == 1 && h8 == 0) {
+          asm volatile(
+              "ds_read_b64 %8, %11\n\tds_read_b64 %9, %11 offset:32\n\tds_read_b64 %10, %11 offset:64\n\t"
+              "ds_read_b64_tr_b16 %0, %12\n\tds_read_b64_tr_b16 %1, %12 offset:128\n\t"
+              "ds_read_b64_tr_b16 %2, %12 offset:256\n\tds_read_b64_tr_b16 %3, %12 offset:384\n\t"
+              "ds_read_b64_tr_b16 %4, %12 offset:512\n\tds_read_b64_tr_b16 %5, %12 offset:640\n\t"
+              "ds_read_b64_tr_b16 %6, %12 offset:768\n\tds_read_b64_tr_b16 %7, %12 offset:896\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=&v"(ar[0]), "=&v"(ar[1]), "=&v"(ar[2]), "=&v"(ar[3]), "=&v"(ar[4]), "=&v"(ar[5]), "=&v"(ar[6]),
+                "=&v"(ar[7]), "=&v"(bg0), "=&v"(bg1), "=&v"(bg2)
+              : "v"(gb + gsr), "v"(ad)
+              : "memory");
+          bg[0] = as_s4(bg0);
+          bg[1] = as_s4(bg1);
+          bg[2] = as_s4(bg2);
+        } else {
+          if (VAR != 1 && h8 == 0) {
+            asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %3 offset:32\n\tds_read_b64 %2, %3 offset:64\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(bg0), "=&v"(bg1), "=&v"(bg2) : "v"(gb + gsr) : "memory");
+            bg[0] = as_s4(bg0);
+            bg[1] = as_s4(bg1);
+            bg[2] = as_s4(bg2);
+          }
+          C4M_READ8("ds_read_b64_tr_b16", ar, ad, 0);
+        }
 #pragma unroll
         for (int p = 0; p < 3; ++p)
 #pragma unroll
@@ -638,11 +707,20 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
   }
   float* dst = out + (int64_t)blockIdx.x * D * K;
   for (int i = threadIdx.x; i < D * K; i += BLOCK) dst[i] = red[i];
+  if constexpr (OBJ) {
+    double d1 = o1, d2 = o2;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      d1 += __shfl_xor(d1, o, 64);
+      d2 += __shfl_xor(d2, o, 64);
+    }
+    if (lane == 0) {
+      obj[((int64_t)blockIdx.x * WAVES + wave) * 2] = d1;
+      obj[((int64_t)blockIdx.x * WAVES + wave) * 2 + 1] = d2;
+    }
+  }
 }
 
-template <int J, int MODE>
-static int launch_m(bool occ, const void* X, int64_t N, int D, const float* V, int ldv, const float* S, int lds,
-                    int sbc, float* out, float* U, int ldu, int grid, int64_t rpb, hipStream_t st);
 
 static void allow_lds(const void* fn, size_t bytes) {
   static std::unordered_set<const void*> done;
@@ -692,9 +770,10 @@ static int route(int mode, int K, int J, bool occ, const void* X, int64_t N, int
 }
 
 template <int J, int MODE>
-static int launch_m(bool occ, const void* X, int64_t N, int D, const float* V, int ldv, const float* S, int lds,
-                    int sbc, float* out, float* U, int ldu, int grid, int64_t rpb, hipStream_t st) {
-  auto kfn = chain4m_kernel<J, MODE>;
+static int launch_m(int var, bool occ, const void* X, int64_t N, int D, const float* V, int ldv, const float* S,
+                    int lds, int sbc, float* out, float* U, int ldu, int grid, int64_t rpb, hipStream_t st,
+                    double* obj) {
+  auto kfn = var == 1 ? chain4m_kernel<J, MODE, 1> : chain4m_kernel<J, MODE, 0>;
   const size_t sh = lds_bytes_m<J>();
   allow_lds(reinterpret_cast<const void*>(kfn), sh);
   if (occ) {
@@ -703,19 +782,19 @@ static int launch_m(bool occ, const void* X, int64_t N, int D, const float* V, i
     return nb;
   }
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(BLOCK), sh, st, (const uint16_t*)X, N, D, V, ldv, S, lds, sbc, out, U,
-                     ldu, rpb);
+                     ldu, rpb, obj);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-static int route_m(int mode, int J, bool occ, const void* X, int64_t N, int D, const float* V, int ldv,
+static int route_m(int var, int mode, int J, bool occ, const void* X, int64_t N, int D, const float* V, int ldv,
                    const float* S, int lds, int sbc, float* out, float* U, int ldu, int grid, int64_t rpb,
-                   hipStream_t st) {
+                   hipStream_t st, double* obj) {
 #define C4M_CASE(MV)                                                                                       \
   case MV:                                                                                                 \
-    return J == 1 ? launch_m<1, MV>(occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st)        \
-                  : launch_m<2, MV>(occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st);
+    return J == 1 ? launch_m<1, MV>(var, occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st, obj) \
+                  : launch_m<2, MV>(var, occ, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rpb, st, obj);
   switch (mode) {
-    C4M_CASE(XTXV) C4M_CASE(XTWXV) C4M_CASE(XTXVY) C4M_CASE(XTPSXV) C4M_CASE(XTSMG)
+    C4M_CASE(XTXV) C4M_CASE(XTWXV) C4M_CASE(XTXVY) C4M_CASE(XTPSXV) C4M_CASE(XTSMG) C4M_CASE(XTSMGO)
     default: return -1;
   }
 #undef C4M_CASE
@@ -729,17 +808,22 @@ extern "C" {
 int sysml_chain4m_occupancy(int mode, int D) {
   using namespace sysml_c4;
   if (D <= 0 || D > 1024) return -1;
-  return route_m(mode, D <= 512 ? 1 : 2, true, nullptr, 0, D, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, 0, 0, 0,
-                 nullptr);
+  return route_m(0, mode, D <= 512 ? 1 : 2, true, nullptr, 0, D, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, 0, 0, 0,
+                 nullptr, nullptr);
 }
 
+// XTSMGO: U receives P ((N + 1) x ldu, ldu >= sbc + 1, row N a scratch pad), S = Y with sbc + 1
+// columns, obj = grid x 4 x 2 doubles of per-wave objective partials.
 int sysml_chain4m(int mode, const void* X, int64_t N, int D, const float* V, int ldv, const float* S, int lds,
-                  int sbc, float* out, float* U, int ldu, int grid, int64_t rows_per_block, void* stream) {
+                  int sbc, float* out, float* U, int ldu, int grid, int64_t rows_per_block, void* stream, int variant,
+                  double* obj) {
   using namespace sysml_c4;
   if (D <= 0 || D > 1024 || (D & 7) || N <= 0 || grid <= 0 || (((uintptr_t)X) & 15)) return -1;
   if (mode == XTSMG && (U == nullptr || sbc < 1 || sbc > 4)) return -1;
-  return route_m(mode, D <= 512 ? 1 : 2, false, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rows_per_block,
-                 (hipStream_t)stream);
+  if (mode == XTSMGO && (U == nullptr || obj == nullptr || sbc < 1 || sbc > 4 || ldu < sbc + 1 || lds < sbc + 1))
+    return -1;
+  return route_m(variant, mode, D <= 512 ? 1 : 2, false, X, N, D, V, ldv, S, lds, sbc, out, U, ldu, grid, rows_per_block,
+                 (hipStream_t)stream, obj);
 }
 
 

@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libsysml_hip.so")
 _lib = None
 
 # modes (must match ops/hip/rowstream.hip)
-XV, XTG, XTXV, XTWXV, XTXVY, XTPSXV, ROWSSQ, COLSSQ, COLSUM, ROWSUM, XTSMG = range(11)
+XV, XTG, XTXV, XTWXV, XTXVY, XTPSXV, ROWSSQ, COLSSQ, COLSUM, ROWSUM, XTSMG, XTSMGO = range(12)
 _CHAIN = {"XtXv": XTXV, "XtwXv": XTWXV, "XtXvy": XTXVY, "XtPSXv": XTPSXV}
 MIN_ROWS = 2048       # below this the launch + partial reduction is not worth it
 MIN_D = 32            # a wave per row: narrower rows waste most lanes (torch handles those)
@@ -98,7 +98,8 @@ def load(required=False):
     L.sysml_chain4m.restype = ctypes.c_int
     L.sysml_chain4m.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                                ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p]
+                                ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                                ctypes.c_int, ctypes.c_void_p]
     L.sysml_chain4m_occupancy.restype = ctypes.c_int
     L.sysml_chain4m_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
     _lib = L
@@ -310,6 +311,9 @@ def _c4m(X, kp):
 
 
 C4M = os.environ.get("SYSML_C4M", "1") != "0"
+# kernel schedule variant (A/B tuning): 1 = row-side value and G planes read with the first
+# batch of row / transposed reads (one lgkmcnt wait less per phase; profiles/chain4m_kbench_r3.txt)
+C4M_VARIANT = int(os.environ.get("SYSML_C4M_VARIANT", "1"))
 
 
 def _c4_grid(L, mode, X, kp):
@@ -336,8 +340,9 @@ def _rows_f32(S, kp, sbc, device):
     return S, S.shape[1]
 
 
-def _chain4(mode, X, kp, V, S, lds, sbc, U=None, ldu=0):
-    """Launch chain4; returns the D x kp fp32 result (sum of the per-block partials)."""
+def _chain4(mode, X, kp, V, S, lds, sbc, U=None, ldu=0, obj=None):
+    """Launch chain4; returns the D x kp fp32 result (sum of the per-block partials).  `obj`
+    (XTSMGO): a list that receives the (grid * 4, 2) fp64 objective partials."""
     L = load(required=True)
     N, D = X.shape
     code = 0 if X.dtype == torch.bfloat16 else 1
@@ -348,9 +353,14 @@ def _chain4(mode, X, kp, V, S, lds, sbc, U=None, ldu=0):
     if S is None:
         S, lds = V, 0      # the kernel streams a row-side operand in every mode: any valid memory
     if _c4m(X, kp):
+        ob = None
+        if obj is not None:
+            ob = torch.empty((grid * 4, 2), dtype=torch.float64, device=X.device)
+            obj.append(ob)
         rc = L.sysml_chain4m(mode, ctypes.c_void_p(X.data_ptr()), N, D, ctypes.c_void_p(V.data_ptr()), kp,
                              ctypes.c_void_p(S.data_ptr()), lds, sbc, ctypes.c_void_p(part.data_ptr()),
-                             ctypes.c_void_p(U.data_ptr() if U is not None else 0), ldu, grid, rpb, _stream())
+                             ctypes.c_void_p(U.data_ptr() if U is not None else 0), ldu, grid, rpb, _stream(),
+                             C4M_VARIANT, ctypes.c_void_p(ob.data_ptr() if ob is not None else 0))
         if rc == 0:
             _count("chain4m")
     else:
@@ -410,6 +420,33 @@ def mmchain(ctype, X, V, W=None):
     _count("rowstream.mmchain." + ctype)
     R = part[:g].sum(0).reshape(X.shape[1], kp)
     return _result(R if kp == K else R[:, :K].contiguous())
+
+
+def smobj(X, V, Y):
+    """Multinomial-logreg candidate evaluation in one pass over X (chain4m mode XTSMGO):
+    with L = cbind(X %*% V, 0) and E = exp(L - rowMaxs(L)), returns (P, G, s1, s2):
+    P = E / rowSums(E) (N x (K+1)), G = t(X) %*% (P[, 1:K] - Y[, 1:K]),
+    s1 = sum(Y * (L - rowMaxs(L))), s2 = sum(log(rowSums(E))).  V is D x K (K <= 4), Y is
+    N x (K+1).  None when the matrix-core kernel does not apply (bf16 X only)."""
+    if not _ok_x(X) or X.dtype != torch.bfloat16:
+        return None
+    K = V.shape[1]
+    if K > 4 or Y.shape != (X.shape[0], K + 1) or V.shape[0] != X.shape[1]:
+        return None
+    kp = 4                  # the matrix-core kernel's class layout; classes past K are masked
+    if not (_c4_ok(X, XTSMG, kp) and _c4m(X, kp)):
+        return None
+    N = X.shape[0]
+    Vf = _pad_cols(V, kp, torch.float32, X.device).contiguous()
+    Yc, ldy = _rows_f32(Y, K + 1, 1, X.device)
+    Ppad = torch.empty((N + 1, K + 1), dtype=torch.float32, device=X.device)   # row N: kernel's pad row
+    ob = []
+    G = _chain4(XTSMGO, X, kp, Vf, Yc, ldy, K, U=Ppad, ldu=K + 1, obj=ob)
+    if G is None:
+        return None
+    _count("chain4m.smobj")
+    s = ob[0].sum(0).tolist()            # one device sync for both objective terms
+    return _result(Ppad[:N]), _result(G if kp == K else G[:, :K].contiguous()), s[0], s[1]
 
 
 def smgrad(X, V, Y):

@@ -599,6 +599,20 @@ def smgrad(X, V, Y, cu=None):
     return DistMatrix(u, X.nrows, u.shape[1], X.start, X.ctx), g
 
 
+def smobj(X, V, Y, kc):
+    """Row-partitioned fused softmax objective / gradient: each rank streams its rows once,
+    P stays row-distributed, the gradient and the two objective sums are all-reduced."""
+    C = _C()
+    if not _is_d(X):
+        return C.smobj(X, _bcast(V, "smobj"), _fallback(Y, "smobj:Y"), kc)
+    V = _bcast(V, "smobj")
+    p, g, s1, s2 = C.smobj(X.local, V, _align(Y, X), kc)
+    g = g.contiguous()
+    X.ctx.allreduce_(g, "sum")
+    s = X.ctx.allreduce_scalar(s1, "sum"), X.ctx.allreduce_scalar(s2, "sum")
+    return DistMatrix(p, X.nrows, p.shape[1], X.start, X.ctx), g, s[0], s[1]
+
+
 def transpose(x):
     """t(X) of a row-partitioned X (N x M).  Large M: the result is row-partitioned too and
     built with one all-to-all (rank r sends the transposed column block q of its rows to

@@ -22,16 +22,16 @@ from .scalars import DevScalar
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell",
                   "magg"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
-_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "rix", "t", "cell", "magg"}
+_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "rix", "t", "cell", "magg"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "round", "floor", "ceil", "sign",
                     "sin", "tan", "asin", "atan", "sinh", "tanh", "neg"}       # ops/sparse.py SAFE_UNARY
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
-_LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "t", "tak", "cell",
-                "magg"}
+_LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "smobj", "t", "tak",
+                 "cell", "magg"}
 # operators that compute on matrix operands (placement applies); the rest move values around
-_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "wquat", "tak", "t", "rix", "lix", "bi", "cell",
-                "magg"}
+_COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "wquat", "tak", "t", "rix", "lix", "bi",
+                 "cell", "magg"}
 transfer_stats = {"h2d": 0, "d2h": 0, "h2d_bytes": 0, "d2h_bytes": 0}   # -stats (utils/stats.gpu_report)
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
@@ -215,6 +215,8 @@ def _make_impl(h):
         return (lambda ctx, a: C.mmchain(t, a[0], a[1], a[2] if len(a) > 2 else None)), "mmchain-" + t
     if op == "smgrad":
         return (lambda ctx, a: C.smgrad(a[0], a[1], a[2], a[3] if len(a) > 3 else None)), "smgrad"
+    if op == "smobj":
+        return (lambda ctx, a: C.smobj(a[0], a[1], a[2], a[3] if len(a) > 3 else None)), "smobj"
     if op == "wquat":
         from ..ops import quaternary as Q
         return (lambda ctx, a: Q.execute(p, a)), "wquat-" + p["kind"]

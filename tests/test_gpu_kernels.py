@@ -286,3 +286,29 @@ def test_chain4m_matrix_core_matches_valu(K, ctype, n, d):
     err_m = (r_m.double() - ref).abs().max().item() / scale
     err_v = (r_v.double() - ref).abs().max().item() / scale
     assert err_m < max(2e-5, 2 * err_v), (err_m, err_v)
+
+
+@pytest.mark.parametrize("n,d,k", [(70001, 1000, 4), (4099, 512, 3), (30011, 136, 2), (513, 1000, 1)])
+def test_chain4m_softmax_objective(K, n, d, k):
+    """XTSMGO (compiler op smobj): probabilities, gradient and the two objective terms of the
+    multinomial-logreg candidate point in one pass, vs an fp64 reference."""
+    x = _mk(n, d, torch.bfloat16, seed=7)
+    x64 = x.double()
+    g0 = torch.Generator(device="cuda").manual_seed(6)
+    v = torch.randn((d, k), generator=g0, device="cuda") * 0.05
+    lab = torch.randint(0, k + 1, (n,), device="cuda", generator=g0)
+    y = torch.nn.functional.one_hot(lab, k + 1).float()
+    r = K.smobj(x, v, y)
+    assert r is not None
+    P, G, s1, s2 = r
+    L = torch.cat([x64 @ v.double(), torch.zeros((n, 1), device="cuda", dtype=torch.float64)], 1)
+    LT = L - L.max(1, keepdim=True).values
+    E = torch.exp(LT)
+    P64 = E / E.sum(1, keepdim=True)
+    G64 = x64.t() @ (P64[:, :k] - y.double()[:, :k])
+    torch.testing.assert_close(P.double(), P64, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(G.double(), G64, rtol=2e-4, atol=2e-4 * G64.abs().max().item())
+    r1 = (y.double() * LT).sum().item()
+    r2 = torch.log(E.sum(1)).sum().item()
+    assert abs(s1 - r1) <= 1e-4 * max(1.0, abs(r1)), (s1, r1)
+    assert abs(s2 - r2) <= 1e-4 * max(1.0, abs(r2)), (s2, r2)

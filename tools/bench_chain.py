@@ -35,13 +35,15 @@ def main():
     if a.only:
         cases = {k: v for k, v in cases.items() if k in a.only.split(",")}
     res = {}
-    variants = [("chain4m", True, True), ("chain4", True, False), ("rowstream", False, False)]
+    variants = [("chain4m", True, True, 1), ("chain4m.v0", True, True, 0), ("chain4", True, False, 0),
+                ("rowstream", False, False, 0)]
     if a.variants:
         variants = [v for v in variants if v[0] in a.variants.split(",")]
     for name0, fn in list(cases.items()):
-      for vname, flag, mflag in variants:
+      for vname, flag, mflag, var in variants:
         K.CHAIN4 = flag
         K.C4M = mflag
+        K.C4M_VARIANT = var
         name = f"{name0}/{vname}"
         fn()
         ts = []
