@@ -288,7 +288,7 @@ def test_chain4m_matrix_core_matches_valu(K, ctype, n, d):
     assert err_m < max(2e-5, 2 * err_v), (err_m, err_v)
 
 
-@pytest.mark.parametrize("n,d,k", [(70001, 1000, 4), (4099, 512, 3), (30011, 136, 2), (513, 1000, 1)])
+@pytest.mark.parametrize("n,d,k", [(70001, 1000, 4), (4099, 512, 3), (30011, 136, 2), (5003, 1000, 1)])
 def test_chain4m_softmax_objective(K, n, d, k):
     """XTSMGO (compiler op smobj): probabilities, gradient and the two objective terms of the
     multinomial-logreg candidate point in one pass, vs an fp64 reference."""
