@@ -19,6 +19,7 @@ import torch
 from ..parser.errors import DMLRuntimeError, DMLScriptStop
 from ..compiler.blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
 from . import scalars as S
+from .bufferpool import Evicted
 
 
 class ExecutionContext:
@@ -159,9 +160,83 @@ def _run_ins(ctx, ins, slots):
         return ins.fn(ctx, [slots[i] for i in ins.ins])
 
 
-def exec_instrs(ctx, instrs, nslots):
-    slots = [None] * nslots
+def _plan(owner, instrs, nslots):
+    """Fast-path plan of an instruction list: literals pre-filled into a slot template,
+    transient reads as (slot, name) pairs fetched up front, and the remaining compute
+    instructions.  Literals and variable reads are a majority of a solver loop's instructions;
+    within a basic block variables only change at the block's end, so reading them first is
+    equivalent.  Cached on the owning block / predicate for its current instruction list
+    (dynamic recompilation swaps the list)."""
+    cached = getattr(owner, "_plan", None)
+    if cached is not None and cached[0] is instrs:
+        return cached[1]
+    tmpl = [None] * nslots
+    reads = []
+    rest = []
+    for ins in instrs:
+        if ins.opcode == "lit":
+            tmpl[ins.out] = ins.hop.p["v"]
+        elif ins.opcode == "tread":
+            reads.append((ins.out, ins.hop.p["name"]))
+        else:
+            rest.append(ins)
+    plan = (tmpl, tuple(reads), tuple(rest))
+    owner._plan = (instrs, plan)
+    return plan
+
+
+_SLOW = object()
+DeferredError = None        # runtime/instructions.DeferredError, bound on first use (import cycle)
+
+
+def _exec_fast(ctx, plan):
+    global DeferredError
+    if DeferredError is None:
+        from .instructions import DeferredError as _D
+        DeferredError = _D
+    tmpl, reads, rest = plan
+    slots = tmpl.copy()
+    vars_ = ctx.vars
+    pool = ctx.pool
+    for s, name in reads:
+        v = vars_.get(name, _SLOW)
+        tv = type(v)
+        if v is _SLOW or tv is DeferredError:
+            return None             # undefined / deferred: the ordered path raises where it should
+        if pool is not None:
+            if tv is Evicted:
+                v = pool.restore(vars_, name, v)
+            pool.touch(vars_, name)
+        slots[s] = v
+    for ins in rest:
+        try:
+            try:
+                slots[ins.out] = ins.fn(ctx, [slots[i] for i in ins.ins])
+            except torch.OutOfMemoryError:
+                if ctx.pool is None or not ctx.pool.on_oom(ctx.frames()):
+                    raise
+                slots[ins.out] = ins.fn(ctx, [slots[i] for i in ins.ins])
+        except DMLScriptStop:
+            raise
+        except DMLRuntimeError as e:
+            raise _attach_pos(e, ins.hop.pos) from e
+        except (RuntimeError, ValueError, TypeError, IndexError, ZeroDivisionError) as e:
+            raise DMLRuntimeError(f"{ins.hop.pos}: error in {ins.opcode}: {e}") from e
+        for f in ins.free:
+            slots[f] = None
+    return slots
+
+
+FAST_PATH = True
+
+
+def exec_instrs(ctx, instrs, nslots, owner=None):
     stats = ctx.stats
+    if FAST_PATH and owner is not None and ctx.debugger is None and (stats is None or not stats.enabled):
+        slots = _exec_fast(ctx, _plan(owner, instrs, nslots))
+        if slots is not None:
+            return slots
+    slots = [None] * nslots
     if stats is not None and stats.enabled:
         sync = stats.sync
         for ins in instrs:
@@ -198,7 +273,7 @@ def exec_instrs(ctx, instrs, nslots):
 def eval_pred(ctx, pred):
     if pred.is_const:
         return pred.const
-    slots = exec_instrs(ctx, pred.instrs, pred.nslots)
+    slots = exec_instrs(ctx, pred.instrs, pred.nslots, pred)
     return slots[pred.out]
 
 
@@ -252,14 +327,14 @@ def _exec_basic(ctx, b):
         if getattr(b, "licm_pre", False):
             # hoisted loop invariants: a failure surfaces only if the loop reads the value
             try:
-                slots = exec_instrs(ctx, b.instrs, b.nslots)
+                slots = exec_instrs(ctx, b.instrs, b.nslots, b)
             except DMLRuntimeError as e:
                 from .instructions import DeferredError
                 for name, _ in b.writes_slots:
                     ctx.vars[name] = DeferredError(e)
                 return
         else:
-            slots = exec_instrs(ctx, b.instrs, b.nslots)
+            slots = exec_instrs(ctx, b.instrs, b.nslots, b)
         vars_ = ctx.vars
         for name, s in b.writes_slots:
             vars_[name] = slots[s]
