@@ -115,7 +115,16 @@ def main():
                          "the plans every step, to separate compilation from execution cost")
     ap.add_argument("--no-overlap", action="store_true",
                     help="compile MultiLogReg after LinregCG ran instead of overlapping the two")
+    ap.add_argument("--compiler", default="process", choices=["process", "thread"],
+                    help="where the next step's scripts compile while this step executes: a compiler "
+                         "process (api/compile_service.py, off the executor's interpreter lock) or a thread")
     a = ap.parse_args()
+
+    # the compiler service is started before anything touches the GPU (its process is spawned)
+    svc = None
+    if a.compiler == "process" and not a.no_overlap and not a.reuse_plans:
+        from systemml_amd.api.compile_service import CompileService
+        svc = CompileService()
 
     from systemml_amd.parallel import dist as D
     from systemml_amd.conf import DMLConfig
@@ -173,14 +182,28 @@ def main():
     def compile_both():
         return compile_lr(), compile_mlr()
 
+    class _Both:
+        """The two compilations of one step, requested from the compiler process."""
+
+        def __init__(self):
+            self.p1 = svc.submit(src_lr, args_lr, {"X": X1, "y": y1}, ["B_out"], cfg, world=world)
+            self.p2 = svc.submit(src_mlr, args_mlr, {"X": X2, "Y_vec": lab}, ["B_out"], cfg, world=world)
+
+        def result(self):
+            return self.p1.result(), self.p2.result()
+
     def step(stats=None, cs=None, prefetch_next=False):
         # both scripts are parsed + compiled once per step.  The next step's two compilations
         # run on a host thread while this step's MultiLogReg executes (its ~350 ms of GPU work
         # leaves the host mostly waiting on the device, which releases the GIL), as a
         # pipelined driver would; LinregCG's short run keeps the host to itself
         cs1, cs2 = cs if cs is not None else compile_both()
+        nxt = None
+        if svc is not None and prefetch_next:
+            nxt = _Both()            # compiles in the service process while this step runs
         r1, _ = EX.execute(cs1, {"X": X1, "y": y1}, out=out, dist=ctx, stats=stats)
-        nxt = pool.submit(compile_both) if (prefetch_next and not a.no_overlap) else None
+        if svc is None and prefetch_next and not a.no_overlap:
+            nxt = pool.submit(compile_both)
         r2, _ = EX.execute(cs2, {"X": X2, "Y_vec": lab}, out=out, dist=ctx, stats=stats)
         return r1["B_out"], r2["B_out"], (nxt.result() if nxt is not None else None)
 
@@ -244,6 +267,8 @@ def main():
                        "parallelism": f"dp{world}", "x_storage": a.xdtype, "accumulate": "fp32"},
         }
         print(json.dumps(res), flush=True)
+    if svc is not None:
+        svc.close()
     if ctx:
         D.shutdown()
 
