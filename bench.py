@@ -190,7 +190,10 @@ def main():
             self.p2 = svc.submit(src_mlr, args_mlr, {"X": X2, "Y_vec": lab}, ["B_out"], cfg, world=world)
 
         def result(self):
-            return self.p1.result(), self.p2.result()
+            r = self.p1.result(), self.p2.result()
+            if a.verbose:
+                print("compile service (worker s, wait s, hydrate s):", self.p1.times, self.p2.times, file=sys.stderr)
+            return r
 
     def step(stats=None, cs=None, prefetch_next=False):
         # both scripts are parsed + compiled once per step.  The next step's two compilations
@@ -209,13 +212,17 @@ def main():
 
     fixed = compile_both() if a.reuse_plans else None
 
-    def run_steps(k, stats=None):
-        cs = fixed
+    def run_steps(k, stats=None, cs=None):
+        # every step compiles the scripts of the step after it while it executes (the last
+        # warmup step compiles the first timed step's, the last timed step one more, awaited
+        # before the clock stops): each timed step carries one compilation of both scripts
+        cs = fixed if fixed is not None else cs
         for i in range(k):
-            _, _, cs = step(stats, cs, prefetch_next=(i + 1 < k) and fixed is None)
+            _, _, cs = step(stats, cs, prefetch_next=fixed is None and not a.no_overlap)
             cs = fixed if fixed is not None else cs
+        return cs
 
-    run_steps(a.warmup)
+    cs_next = run_steps(a.warmup)
     # compiled programs and the data live for the whole run: move them out of the cyclic
     # collector's generations so gen-2 collections during the steps stay short
     gc.collect()
@@ -230,7 +237,7 @@ def main():
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
-    run_steps(a.steps, st)
+    run_steps(a.steps, st, cs_next)
     torch.cuda.synchronize()
     if prof is not None:
         prof.disable()

@@ -160,10 +160,13 @@ def _worker(conn):
             return
         src, args, specs, outputs, config, world, kw = msg
         try:
+            import time
+            t0 = time.perf_counter()
             config._world = world
             inputs = {k: _stand_in(s) for k, s in specs.items()}
             cs = EX.compile_script(src, args, inputs=inputs, outputs=outputs, config=config, **kw)
-            conn.send(("ok", dehydrate(cs)))
+            blob = dehydrate(cs)
+            conn.send(("ok", (blob, time.perf_counter() - t0)))
         except BaseException as e:  # noqa: BLE001 - reported to the driver
             conn.send(("err", f"{type(e).__name__}: {e}"))
 
@@ -174,14 +177,20 @@ class _Pending:
         self.inputs = inputs
         self._value = None
         self._done = False
+        self.times = None      # (worker compile s, driver wait s, driver hydrate s)
 
     def result(self):
         if not self._done:
+            import time
+            t0 = time.perf_counter()
             with self.svc.lock:
                 status, payload = self.svc.conn.recv()
+            t1 = time.perf_counter()
             if status != "ok":
                 raise RuntimeError(f"compile service: {payload}")
-            self._value = hydrate(payload, self.inputs)
+            blob, tc = payload
+            self._value = hydrate(blob, self.inputs)
+            self.times = (tc, t1 - t0, time.perf_counter() - t1)
             self._done = True
         return self._value
 
