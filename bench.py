@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--lazy", action="store_true",
                     help="HBM-resident lazy scalars (all matrices in HBM) instead of host scalars + hybrid "
                          "placement (measured slower on this benchmark: 511 vs 486 ms)")
+    ap.add_argument("--sample-profile", default="",
+                    help="wall-clock stack samples of the timed steps (tools/stack_sampler.py) written here")
     ap.add_argument("--host-profile", default="",
                     help="cProfile the timed steps (host time) and write the top functions to this file")
     ap.add_argument("--reuse-plans", action="store_true",
@@ -232,6 +234,10 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     st = Statistics(enabled=True) if a.stats else None
+    sampler = None
+    if a.sample_profile:
+        from tools.stack_sampler import Sampler
+        sampler = Sampler().__enter__()
     prof = None
     if a.host_profile:
         import cProfile
@@ -241,6 +247,10 @@ def main():
     torch.cuda.synchronize()
     if prof is not None:
         prof.disable()
+    if sampler is not None:
+        sampler.__exit__(None, None, None)
+        if rank == 0:
+            sampler.report(a.sample_profile)
     if ctx:
         ctx.barrier()
     el = time.perf_counter() - t1

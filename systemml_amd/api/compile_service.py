@@ -152,9 +152,13 @@ def _stand_in(spec):
 
 
 def _worker(conn):
+    import gc
     sys.setrecursionlimit(_REC_LIMIT)
     from . import executor as EX
+    # cyclic garbage is collected between requests, never in the middle of a compilation
+    gc.disable()
     while True:
+        gc.collect()
         msg = conn.recv()
         if msg is None:
             return
