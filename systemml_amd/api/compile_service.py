@@ -155,10 +155,8 @@ def _worker(conn):
     import gc
     sys.setrecursionlimit(_REC_LIMIT)
     from . import executor as EX
-    # cyclic garbage is collected between requests, never in the middle of a compilation
-    gc.disable()
+    first = True
     while True:
-        gc.collect()
         msg = conn.recv()
         if msg is None:
             return
@@ -171,6 +169,12 @@ def _worker(conn):
             cs = EX.compile_script(src, args, inputs=inputs, outputs=outputs, config=config, **kw)
             blob = dehydrate(cs)
             conn.send(("ok", (blob, time.perf_counter() - t0)))
+            if first:
+                # the compiler's modules and caches are loaded now: freeze them out of the cyclic
+                # collector so later collections only scan a compilation's own garbage
+                first = False
+                gc.collect()
+                gc.freeze()
         except BaseException as e:  # noqa: BLE001 - reported to the driver
             conn.send(("err", f"{type(e).__name__}: {e}"))
 
