@@ -221,6 +221,224 @@ mchain_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Wide products (up to 16 columns): U = X %*% V and R = t(X) %*% G for 5..16 classes (the
+// 10-class MultiLogReg of BASELINE config #3).  Same tile pipeline as mchain_kernel, but the
+// three bf16 rounding planes of V / G are separate MFMAs accumulating into one tile whose M / N
+// dimension holds the 16 columns themselves (mchain_kernel stacks the planes in the spare rows,
+// which caps it at 4 columns).
+// Waves per block: the fused chains at D > 768 hold V's planes, the R accumulators and the
+// staged X tile at once, which at 8 waves exceeds 128 VGPRs; 16 waves halve each wave's slice.
+template <int MODE, int KS>
+constexpr int wide_waves() { return (MODE != XV && MODE != XTG && KS == 4) ? 16 : WAVES; }
+
+template <int MODE, int KS>
+__global__ void __launch_bounds__((64 * wide_waves<MODE, KS>()), MIN_WAVES_PER_SIMD)
+wide_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
+            const uint16_t* __restrict__ VW,   // [3][16][Dp] bf16: plane p of V[:, k] in row 16p + k
+            const float* __restrict__ S, int lds, int K,
+            float* __restrict__ out, int ldo, int64_t tiles_per_block) {
+  constexpr int WV = wide_waves<MODE, KS>();
+  constexpr int BLK = 64 * WV;
+  constexpr int Dp = KS * 256;
+  constexpr int ROWB = Dp * 2 + 16;
+  constexpr int CH = Dp / 8;
+  constexpr int NST = TR * CH / BLK;
+  constexpr int KC = Dp / (32 * WV);  // 32-column chunks of this wave's slice (phase 1)
+  constexpr int NB = Dp / (16 * WV);  // 16-column blocks of this wave's slice (phase 2)
+  static_assert(NST * BLK == TR * CH && KC * 32 * WV == Dp, "wide tile shape");
+  // phase 1: U = X V on the tile (XV and the chains); phase 2: R += t(X_tile) G (XTG and chains)
+  constexpr bool P1 = (MODE != XTG);
+  constexpr bool P2 = (MODE != XV);
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Xs = smem;
+  float* Ured = reinterpret_cast<float*>(smem + TR * ROWB);         // [WV][TR][16]
+  uint16_t* G3 = reinterpret_cast<uint16_t*>(Ured + WV * TR * 16);  // [3][TR][16]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int i16 = lane & 15;
+  const int q = i16 >> 2, p = i16 & 3;
+  const int dsl = wave * (Dp / WV);
+
+  bf8 afr[P1 ? 3 : 1][P1 ? KC : 1];
+  if constexpr (P1) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int ks = 0; ks < KC; ++ks)
+        afr[pl][ks] = *reinterpret_cast<const bf8*>(VW + ((int64_t)pl * 16 + i16) * Dp + dsl + ks * 32 + 8 * g);
+  }
+  f4 acc[P2 ? NB : 1];
+#pragma unroll
+  for (int b = 0; b < (P2 ? NB : 1); ++b) acc[b] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_block;
+  const int64_t t1 = (t0 + tiles_per_block < ntiles) ? t0 + tiles_per_block : ntiles;
+
+  u4 st[NST];
+  uint32_t stok = 0;
+  auto gload = [&](int64_t t) {
+    stok = 0;
+#pragma unroll
+    for (int j = 0; j < NST; ++j) {
+      const int id = j * BLK + tid;
+      const int row = id / CH, ch = id - (id / CH) * CH;
+      const int64_t r = t * TR + row;
+      const bool ok = (r < N) && (ch * 8 < D);
+      stok |= (ok ? 1u : 0u) << j;
+      const int64_t off = ok ? r * (int64_t)D + ch * 8 : 0;
+      st[j] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(X + off));
+    }
+  };
+  auto swrite = [&]() {
+#pragma unroll
+    for (int j = 0; j < NST; ++j) {
+      const int id = j * BLK + tid;
+      const int row = id / CH, ch = id - (id / CH) * CH;
+      const u4 z = {0u, 0u, 0u, 0u};
+      *reinterpret_cast<u4*>(Xs + row * ROWB + ch * 16) = ((stok >> j) & 1u) ? st[j] : z;
+    }
+  };
+  // this thread's S value of the tile (threads 0..255: row tid / 16, column tid % 16):
+  // G for XTG, w for XTWXV (one column), y for XTXVY, P for XTPSXV
+  auto svals = [&](int64_t t) -> float {
+    if (tid >= TR * 16) return 0.f;
+    const int row = tid >> 4, col = tid & 15;
+    const int64_t r = t * TR + row;
+    if constexpr (MODE == XTWXV) return (r < N && col < K) ? S[r * (int64_t)lds] : 0.f;
+    return (r < N && col < K) ? S[r * (int64_t)lds + col] : 0.f;
+  };
+
+  if (t0 < t1) {
+    gload(t0);
+    swrite();
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  for (int64_t t = t0; t < t1; ++t) {
+    float gv = 0.f;
+    if constexpr (MODE != XV && MODE != XTXV) gv = svals(t);
+    if (t + 1 < t1) gload(t + 1);
+
+    if constexpr (P1) {
+      f4 u = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KC; ++ks) {
+        const bf8 b = *reinterpret_cast<const bf8*>(Xs + i16 * ROWB + (dsl + ks * 32 + 8 * g) * 2);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[pl][ks], b, u, 0, 0, 0);
+      }
+      // u[i] = partial U[row i16][column 4g + i] over this wave's columns of X
+      *reinterpret_cast<f4*>(Ured + (wave * TR + i16) * 16 + 4 * g) = u;
+      __syncthreads();
+      if (tid < TR * 16) {
+        const int row = tid >> 4, col = tid & 15;
+        float uu = 0.f;
+#pragma unroll
+        for (int w = 0; w < WV; ++w) uu += Ured[(w * TR + row) * 16 + col];
+        if constexpr (MODE == XV) {
+          const int64_t r = t * TR + row;
+          if (r < N && col < K) out[r * (int64_t)ldo + col] = uu;
+        } else if constexpr (MODE == XTXV) {
+          gv = uu;
+        } else if constexpr (MODE == XTWXV) {
+          gv *= uu;
+        } else if constexpr (MODE == XTXVY) {
+          gv = uu - gv;
+        } else {
+          // g = P * u - P * rowSums(P * u): the 16 columns of a row are 16 consecutive lanes
+          const float qv = gv * uu;
+          float rs = qv;
+#pragma unroll
+          for (int m = 1; m < 16; m <<= 1) rs += __shfl_xor(rs, m, 16);
+          gv = qv - gv * rs;
+        }
+        // padded rows / columns stay zero: U's padding is zero and S is read as zero there
+      }
+    }
+    if constexpr (P2) {
+      if (tid < TR * 16) {
+        const uint16_t h = f2bf(gv);
+        float rem = gv - bf2f(h);
+        const uint16_t l1 = f2bf(rem);
+        rem -= bf2f(l1);
+        const uint16_t l2 = f2bf(rem);
+        G3[tid] = h;
+        G3[TR * 16 + tid] = l1;
+        G3[2 * TR * 16 + tid] = l2;
+      }
+      __syncthreads();
+      s4 bfr[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bfr[pl] = tr_read(G3 + pl * TR * 16 + (4 * g + q) * 16 + 4 * p);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int dblk = dsl + b * 16;
+        const s4 a = tr_read(Xs + (4 * g + q) * ROWB + (dblk + 4 * p) * 2);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) acc[b] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bfr[pl], acc[b], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (t + 1 < t1) {
+      swrite();
+      __syncthreads();
+    }
+  }
+
+  if constexpr (P2) {
+    // acc[b][i] = R[d = dsl + 16b + 4g + i][column i16]
+    float* dst = out + (int64_t)blockIdx.x * D * K;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = dsl + b * 16 + 4 * g + i;
+        if (i16 < K && d < D) dst[(int64_t)d * K + i16] = acc[b][i];
+      }
+  }
+}
+
+template <int MODE, int KS>
+static size_t lds_bytes_wide() {
+  return (size_t)TR * (KS * 512 + 16) + wide_waves<MODE, KS>() * TR * 16 * 4 + 3 * TR * 16 * 2;
+}
+
+template <int MODE, int KS>
+static int launch_wide(bool occ, const void* X, int64_t N, int D, const void* VW, const float* S, int lds, int K,
+                       float* out, int ldo, int grid, hipStream_t st) {
+  const size_t sh = lds_bytes_wide<MODE, KS>();
+  constexpr int blk = 64 * wide_waves<MODE, KS>();
+  if (occ) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wide_kernel<MODE, KS>, blk, sh) != hipSuccess) return -1;
+    return nb;
+  }
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t tpb = (ntiles + grid - 1) / grid;
+  hipLaunchKernelGGL((wide_kernel<MODE, KS>), dim3(grid), dim3(blk), sh, st, (const uint16_t*)X, N, D,
+                     (const uint16_t*)VW, S, lds, K, out, ldo, tpb);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <int MODE>
+static int dispatch_wide(int ks, bool occ, const void* X, int64_t N, int D, const void* VW, const float* S, int lds,
+                         int K, float* out, int ldo, int grid, hipStream_t st) {
+  switch (ks) {
+    case 1: return launch_wide<MODE, 1>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case 2: return launch_wide<MODE, 2>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case 3: return launch_wide<MODE, 3>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case 4: return launch_wide<MODE, 4>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    default: return -1;
+  }
+}
+
 template <int MODE, int KS>
 static size_t lds_bytes() {
   return (size_t)TR * (KS * 64 * WAVES + 16) + WAVES * TR * 16 * 4 + WAVES * TR * 16 * 2;
@@ -293,6 +511,37 @@ int sysml_mchain(int mode, const void* X, int64_t N, int D, const void* V3T, con
                  float* out, int ldo, int grid, hipStream_t stream) {
   if (D <= 0 || D > 1024 || (D & 7) || K < 1 || K > 4 || grid <= 0) return -1;
   return sysml_mc::route(mode, (D + 255) / 256, false, X, N, D, V3T, S, lds, sbc, K, out, ldo, grid, stream);
+}
+
+// Wide products and chains (K <= 16 columns; V as [3][16][Dp] bf16 planes).
+static int wide_route(int mode, int ks, bool occ, const void* X, int64_t N, int D, const void* VW, const float* S,
+                      int lds, int K, float* out, int ldo, int grid, hipStream_t st) {
+  using namespace sysml_mc;
+  switch (mode) {
+    case XV: return dispatch_wide<XV>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case XTG: return dispatch_wide<XTG>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case XTXV: return dispatch_wide<XTXV>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case XTWXV: return dispatch_wide<XTWXV>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case XTXVY: return dispatch_wide<XTXVY>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case XTPSXV: return dispatch_wide<XTPSXV>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    default: return -1;
+  }
+}
+
+int sysml_mwide_occupancy(int mode, int D) {
+  if (D <= 0 || D > 1024) return -1;
+  return wide_route(mode, (D + 255) / 256, true, nullptr, 0, D, nullptr, nullptr, 0, 0, nullptr, 0, 0, nullptr);
+}
+
+// mode XV: out N x ldo; XTG and the chains (XTXV, XTWXV w: N x 1, XTXVY y: N x K, XTPSXV P: N x K;
+// lds = leading dimension of S): out grid x (D*K) per-block partials of the D x K result.
+int sysml_mwide(int mode, const void* X, int64_t N, int D, const void* VW, const float* S, int lds, int K, float* out,
+                int ldo, int grid, hipStream_t stream) {
+  if (D <= 0 || D > 1024 || (D & 7) || K < 1 || K > 16 || grid <= 0 || N <= 0) return -1;
+  if (mode != sysml_mc::XTG && VW == nullptr) return -1;
+  if (mode != sysml_mc::XV && mode != sysml_mc::XTXV && (S == nullptr || lds < (mode == sysml_mc::XTWXV ? 1 : K)))
+    return -1;
+  return wide_route(mode, (D + 255) / 256, false, X, N, D, VW, S, lds, K, out, ldo, grid, stream);
 }
 
 }  // extern "C"

@@ -102,6 +102,12 @@ def load(required=False):
                                 ctypes.c_int, ctypes.c_void_p]
     L.sysml_chain4m_occupancy.restype = ctypes.c_int
     L.sysml_chain4m_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.sysml_mwide.restype = ctypes.c_int
+    L.sysml_mwide.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                              ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_int, ctypes.c_void_p]
+    L.sysml_mwide_occupancy.restype = ctypes.c_int
+    L.sysml_mwide_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
     _lib = L
     return L
 
@@ -179,6 +185,60 @@ def _mchain(mode, X, kp, V=None, S=None, sbc=0):
     return out.sum(0).reshape(D, kp)
 
 
+WIDE_MAX = 16
+
+
+def _wide_ok(X, K):
+    """Wide MFMA products (5..16 columns, e.g. the 10-class MultiLogReg): bf16 X only."""
+    return (MFMA and X.dtype == torch.bfloat16 and 4 < K <= WIDE_MAX and X.shape[1] % 8 == 0 and
+            X.shape[1] <= 1024 and X.is_contiguous() and X.data_ptr() % 16 == 0)
+
+
+def _wide_planes(V, D, device):
+    """V (D x K, K <= 16) -> [3][16][Dp] bf16: plane p (hi, lo, lo2 rounding residues) of
+    V[:, k] in row k of plane p."""
+    K = V.shape[1]
+    Dp = 256 * ((D + 255) // 256)
+    v = V.to(device=device, dtype=torch.float32)
+    VW = torch.zeros((3, 16, Dp), dtype=torch.bfloat16, device=device)
+    for pl in range(3):
+        h = v.to(torch.bfloat16)
+        VW[pl, :K, :D] = h.t()
+        v = v - h.to(torch.float32)
+    return VW
+
+
+def _mwide(mode, X, V=None, G=None, sbc=0):
+    """Wide products and chains with up to 16 columns (ops/hip/mfma_chain.hip wide_kernel):
+    each of the three bf16 planes of V / G is its own MFMA into a 16-column tile.
+    mode XV: U = X %*% V; XTG: t(X) %*% G; chains (XTXV / XTWXV / XTXVY / XTPSXV, G = the
+    row-side operand w / y / P): t(X) %*% g(X %*% V) in one pass over X."""
+    L = load(required=True)
+    N, D = X.shape
+    key = ("wide", mode, D, X.device.index)
+    if key not in _occ:
+        occ = L.sysml_mwide_occupancy(mode, D)
+        cus = torch.cuda.get_device_properties(X.device).multi_processor_count
+        _occ[key] = max(1, occ) * cus if occ > 0 else -1
+    grid = min(_occ[key], (N + 15) // 16)
+    if grid <= 0:
+        return None
+    K = V.shape[1] if V is not None else G.shape[1]
+    VW = _wide_planes(V, D, X.device) if V is not None else None
+    S, lds = _rows_f32(G, K, sbc, X.device) if G is not None else (None, 0)
+    vp = ctypes.c_void_p(VW.data_ptr() if VW is not None else 0)
+    sp = ctypes.c_void_p(S.data_ptr() if S is not None else 0)
+    if mode == XV:
+        out = torch.empty((N, K), dtype=torch.float32, device=X.device)
+        rc = L.sysml_mwide(mode, ctypes.c_void_p(X.data_ptr()), N, D, vp, sp, lds, K,
+                           ctypes.c_void_p(out.data_ptr()), K, grid, _stream())
+        return out if rc == 0 else None
+    part = torch.empty((grid, D * K), dtype=torch.float32, device=X.device)
+    rc = L.sysml_mwide(mode, ctypes.c_void_p(X.data_ptr()), N, D, vp, sp, lds, K,
+                       ctypes.c_void_p(part.data_ptr()), 0, grid, _stream())
+    return part.sum(0).reshape(D, K) if rc == 0 else None
+
+
 def _xcode(x):
     if x.dtype == torch.bfloat16:
         return 0, torch.float32
@@ -240,8 +300,15 @@ def _result(t):
 
 
 def xv(X, V):
-    """U = X %*% V for tall X (N x D, D <= 1024) and skinny V (D x K, K <= 8)."""
+    """U = X %*% V for tall X (N x D, D <= 1024) and skinny V (D x K, K <= 8; bf16 X: K <= 16)."""
     K = V.shape[1]
+    if _wide_ok(X, K):
+        U = _mwide(XV, X, V=V)
+        if U is not None:
+            _count("mfma.xv_wide")
+            return _result(U)
+    if K > 8:
+        return None
     kp = _kpad(K)
     code, adt = _xcode(X)
     if X.dtype == torch.bfloat16 and K > 4:
@@ -265,8 +332,15 @@ def xv(X, V):
 
 
 def xtg(X, G):
-    """R = t(X) %*% G for tall X and skinny G (N x K, K <= 8)."""
+    """R = t(X) %*% G for tall X and skinny G (N x K, K <= 8; bf16 X: K <= 16)."""
     K = G.shape[1]
+    if _wide_ok(X, K):
+        R = _mwide(XTG, X, G=G)
+        if R is not None:
+            _count("mfma.xtg_wide")
+            return _result(R)
+    if K > 8:
+        return None
     kp = _kpad(K)
     code, adt = _xcode(X)
     Gp = _pad_cols(G, kp, adt, X.device).contiguous()
@@ -377,7 +451,6 @@ def mmchain(ctype, X, V, W=None):
     K = V.shape[1]
     kp = _kpad(K)
     code, adt = _xcode(X)
-    Vp = _pad_cols(V, kp, adt, X.device).contiguous()
     sbc = 0
     if W is not None:
         if W.shape[0] != X.shape[0]:
@@ -396,6 +469,13 @@ def mmchain(ctype, X, V, W=None):
             return W.to(device=X.device, dtype=adt).contiguous()
         return _pad_cols(W, kp, adt, X.device).contiguous()
 
+    if _wide_ok(X, K):
+        R = _mwide(mode, X, V=V, G=W, sbc=sbc)
+        if R is not None:
+            _count("mfma.mmchain_wide." + ctype)
+            return _result(R)
+    if kp is None:
+        return None
     if _c4_ok(X, mode, kp):
         Vf = _pad_cols(V, kp, torch.float32, X.device).contiguous()
         # W as is (strided views included) when the kernel reads no column past it: sbc broadcast
@@ -414,6 +494,7 @@ def mmchain(ctype, X, V, W=None):
             return _result(R if kp == K else R[:, :K].contiguous())
     grid = _grid(X.shape[0])
     part = torch.empty((grid, X.shape[1] * kp), dtype=adt, device=X.device)
+    Vp = _pad_cols(V, kp, adt, X.device).contiguous()
     rc, g = _launch(mode, X, V=Vp, S=S, sbc=sbc, K=kp, out=part, grid=grid)
     if rc != 0:
         return None
@@ -501,7 +582,7 @@ def try_mm(a, b, transA):
         b = b.to(a.device)
     if _ok_x(a):
         K = b.shape[1]
-        if K <= 8:
+        if K <= 8 or (K <= WIDE_MAX and a.dtype == torch.bfloat16):
             if transA and b.shape[0] == a.shape[0]:
                 r = xtg(a, b)
                 if r is not None:
@@ -515,7 +596,9 @@ def try_mm(a, b, transA):
 
 
 def try_mmchain(ctype, X, v, w):
-    if not _ok_x(X) or not isinstance(v, torch.Tensor) or v.shape[1] > 8 or v.shape[0] != X.shape[1]:
+    if not _ok_x(X) or not isinstance(v, torch.Tensor) or v.shape[0] != X.shape[1]:
+        return None
+    if v.shape[1] > (WIDE_MAX if _wide_ok(X, v.shape[1]) else 8):
         return None
     if w is not None and not isinstance(w, torch.Tensor):
         return None

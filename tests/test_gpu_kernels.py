@@ -144,6 +144,72 @@ def test_mfma_exact_integer_layout(K, n, d, k, mfma_all):
     assert K.counters.get("mfma.mmchain.XtXv", 0) > c0.get("mfma.mmchain.XtXv", 0)
 
 
+@pytest.mark.parametrize("n", [1, 17, 4099])
+@pytest.mark.parametrize("d", [8, 264, 1000, 1024])
+@pytest.mark.parametrize("k", [5, 9, 16])
+def test_wide_mfma_exact_integer_layout(K, n, d, k):
+    """5..16-column products (wide_kernel: planes as separate MFMAs, columns in the tile's M / N
+    dimension) are exact on small integers: any layout slip shows as a wrong element."""
+    x = _ints((n, d), -3, 3, 40 + d).to(torch.bfloat16)
+    x64 = x.double()
+    v = _ints((d, k), -2, 2, 50 + k)
+    g = _ints((n, k), -2, 2, 60 + n)
+    c0 = dict(K.counters)
+    torch.testing.assert_close(K.xv(x, v).double(), x64 @ v, rtol=0, atol=0)
+    torch.testing.assert_close(K.xtg(x, g).double(), x64.t() @ g, rtol=0, atol=0)
+    assert K.counters.get("mfma.xv_wide", 0) > c0.get("mfma.xv_wide", 0)
+    assert K.counters.get("mfma.xtg_wide", 0) > c0.get("mfma.xtg_wide", 0)
+
+
+@pytest.mark.parametrize("n", [1, 17, 4099])
+@pytest.mark.parametrize("d", [8, 264, 1000])
+@pytest.mark.parametrize("k", [5, 9, 16])
+@pytest.mark.parametrize("ctype", ["XtXv", "XtwXv", "XtXvy", "XtPSXv"])
+def test_wide_mfma_chains(K, n, d, k, ctype):
+    """Fused wide chains t(X) %*% g(X %*% V) (one pass over X, 16-wave blocks at D > 768) on
+    small integers: exact up to fp32 accumulation of the final products."""
+    x = _ints((n, d), -2, 2, 70 + d).to(torch.bfloat16)
+    x64 = x.double()
+    v = _ints((d, k), -1, 1, 80 + k)
+    u = x64 @ v
+    w = None
+    if ctype == "XtXv":
+        g = u
+    elif ctype == "XtwXv":
+        w = _ints((n, 1), -2, 2, 90)
+        g = w * u
+    elif ctype == "XtXvy":
+        w = _ints((n, k), -2, 2, 91)
+        g = u - w
+    else:
+        w = _ints((n, k + 1), -1, 1, 92)[:, :k]          # strided view, like P[, 1:K]
+        q = w * u
+        g = q - w * q.sum(1, keepdim=True)
+    ref = x64.t() @ g
+    c0 = K.counters.get("mfma.mmchain_wide." + ctype, 0)
+    r = K.mmchain(ctype, x, v, w)
+    assert K.counters.get("mfma.mmchain_wide." + ctype, 0) == c0 + 1
+    err = (r.double() - ref).abs().max().item() / max(ref.abs().max().item(), 1.0)
+    assert err < 1e-6, err
+
+
+@pytest.mark.parametrize("k", [6, 10, 16])
+def test_wide_mfma_fp32_operands(K, k):
+    """fp32 V / G are split into three bf16 planes: products match fp64 to fp32 accuracy, and
+    `%*%` routes 10-column shapes (10-class MultiLogReg) to the wide kernel."""
+    n, d = 30011, 1000
+    x = _mk(n, d, torch.bfloat16, seed=7)
+    x64 = x.double()
+    v = torch.randn((d, k), device="cuda", dtype=torch.float64)
+    g = torch.randn((n, k), device="cuda", dtype=torch.float64)
+    u = K.try_mm(x, v, False)
+    ref = x64 @ v
+    assert (u.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    r = K.try_mm(x, g, True)
+    ref2 = x64.t() @ g
+    assert (r.double() - ref2).abs().max().item() / ref2.abs().max().item() < 2e-6
+
+
 @pytest.mark.parametrize("ctype", ["XtXv", "XtwXv", "XtXvy", "XtPSXv"])
 @pytest.mark.parametrize("k", [1, 2, 4])
 def test_mfma_matches_rowstream(K, ctype, k, mfma_all):
