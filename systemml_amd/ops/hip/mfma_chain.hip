@@ -33,7 +33,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4 lds_s4;
 
-enum Mode { XV = 0, XTG = 1, XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5 };  // = rowstream.hip
+enum Mode { XV = 0, XTG = 1, XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5,  // = rowstream.hip
+            XTSMG = 10, XTSMGO = 11 };                                      // = chain4.hip (wide kernel only)
 
 constexpr int WAVES = 8;
 constexpr int BLOCK = 64 * WAVES;
@@ -237,7 +238,8 @@ __global__ void __launch_bounds__((64 * wide_waves<MODE, KS>()), MIN_WAVES_PER_S
 wide_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
             const uint16_t* __restrict__ VW,   // [3][16][Dp] bf16: plane p of V[:, k] in row 16p + k
             const float* __restrict__ S, int lds, int K,
-            float* __restrict__ out, int ldo, int64_t tiles_per_block) {
+            float* __restrict__ out, int ldo, int64_t tiles_per_block,
+            float* __restrict__ U, int ldu, double* __restrict__ obj) {
   constexpr int WV = wide_waves<MODE, KS>();
   constexpr int BLK = 64 * WV;
   constexpr int Dp = KS * 256;
@@ -305,14 +307,17 @@ wide_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
     }
   };
   // this thread's S value of the tile (threads 0..255: row tid / 16, column tid % 16):
-  // G for XTG, w for XTWXV (one column), y for XTXVY, P for XTPSXV
+  // G for XTG, w for XTWXV (one column), y for XTXVY, P for XTPSXV, Y for the softmax modes
+  // (XTSMGO reads Y's K + 1 columns)
+  constexpr int SX = (MODE == XTSMGO) ? 1 : 0;
   auto svals = [&](int64_t t) -> float {
     if (tid >= TR * 16) return 0.f;
     const int row = tid >> 4, col = tid & 15;
     const int64_t r = t * TR + row;
     if constexpr (MODE == XTWXV) return (r < N && col < K) ? S[r * (int64_t)lds] : 0.f;
-    return (r < N && col < K) ? S[r * (int64_t)lds + col] : 0.f;
+    return (r < N && col < K + SX) ? S[r * (int64_t)lds + col] : 0.f;
   };
+  float o1 = 0.f, o2 = 0.f;   // XTSMGO objective terms of this thread's rows
 
   if (t0 < t1) {
     gload(t0);
@@ -351,13 +356,34 @@ wide_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
           gv *= uu;
         } else if constexpr (MODE == XTXVY) {
           gv = uu - gv;
-        } else {
+        } else if constexpr (MODE == XTPSXV) {
           // g = P * u - P * rowSums(P * u): the 16 columns of a row are 16 consecutive lanes
           const float qv = gv * uu;
           float rs = qv;
 #pragma unroll
           for (int m = 1; m < 16; m <<= 1) rs += __shfl_xor(rs, m, 16);
           gv = qv - gv * rs;
+        } else {
+          // softmax over L = [u_0 .. u_{K-1}, 0] (K <= 15: the zero class is column K)
+          const int64_t r = t * TR + row;
+          const bool rv = r < N;
+          const float lv = col < K ? uu : 0.f;
+          float m = col <= K ? lv : -INFINITY;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+          const float e = col <= K ? __expf(lv - m) : 0.f;
+          float se = e;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) se += __shfl_xor(se, o, 16);
+          const float pr = e / se;
+          if constexpr (MODE == XTSMG) {
+            if (rv && col < K) U[r * (int64_t)ldu + col] = uu;
+          } else {
+            if (rv && col <= K) U[r * (int64_t)ldu + col] = pr;
+            if (rv && col <= K) o1 += gv * (lv - m);
+            if (rv && col == 0) o2 += __logf(se);
+          }
+          gv = (rv && col < K) ? pr - gv : 0.f;
         }
         // padded rows / columns stay zero: U's padding is zero and S is read as zero there
       }
@@ -392,6 +418,18 @@ wide_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
     }
   }
 
+  if constexpr (MODE == XTSMGO) {
+    double d1 = o1, d2 = o2;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      d1 += __shfl_xor(d1, o, 64);
+      d2 += __shfl_xor(d2, o, 64);
+    }
+    if (lane == 0) {
+      obj[((int64_t)blockIdx.x * WV + wave) * 2] = d1;
+      obj[((int64_t)blockIdx.x * WV + wave) * 2 + 1] = d2;
+    }
+  }
   if constexpr (P2) {
     // acc[b][i] = R[d = dsl + 16b + 4g + i][column i16]
     float* dst = out + (int64_t)blockIdx.x * D * K;
@@ -412,7 +450,7 @@ static size_t lds_bytes_wide() {
 
 template <int MODE, int KS>
 static int launch_wide(bool occ, const void* X, int64_t N, int D, const void* VW, const float* S, int lds, int K,
-                       float* out, int ldo, int grid, hipStream_t st) {
+                       float* out, int ldo, int grid, hipStream_t st, float* U, int ldu, double* obj) {
   const size_t sh = lds_bytes_wide<MODE, KS>();
   constexpr int blk = 64 * wide_waves<MODE, KS>();
   if (occ) {
@@ -423,18 +461,18 @@ static int launch_wide(bool occ, const void* X, int64_t N, int D, const void* VW
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t tpb = (ntiles + grid - 1) / grid;
   hipLaunchKernelGGL((wide_kernel<MODE, KS>), dim3(grid), dim3(blk), sh, st, (const uint16_t*)X, N, D,
-                     (const uint16_t*)VW, S, lds, K, out, ldo, tpb);
+                     (const uint16_t*)VW, S, lds, K, out, ldo, tpb, U, ldu, obj);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 template <int MODE>
 static int dispatch_wide(int ks, bool occ, const void* X, int64_t N, int D, const void* VW, const float* S, int lds,
-                         int K, float* out, int ldo, int grid, hipStream_t st) {
+                         int K, float* out, int ldo, int grid, hipStream_t st, float* U, int ldu, double* obj) {
   switch (ks) {
-    case 1: return launch_wide<MODE, 1>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
-    case 2: return launch_wide<MODE, 2>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
-    case 3: return launch_wide<MODE, 3>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
-    case 4: return launch_wide<MODE, 4>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case 1: return launch_wide<MODE, 1>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st, U, ldu, obj);
+    case 2: return launch_wide<MODE, 2>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st, U, ldu, obj);
+    case 3: return launch_wide<MODE, 3>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st, U, ldu, obj);
+    case 4: return launch_wide<MODE, 4>(occ, X, N, D, VW, S, lds, K, out, ldo, grid, st, U, ldu, obj);
     default: return -1;
   }
 }
@@ -515,33 +553,45 @@ int sysml_mchain(int mode, const void* X, int64_t N, int D, const void* V3T, con
 
 // Wide products and chains (K <= 16 columns; V as [3][16][Dp] bf16 planes).
 static int wide_route(int mode, int ks, bool occ, const void* X, int64_t N, int D, const void* VW, const float* S,
-                      int lds, int K, float* out, int ldo, int grid, hipStream_t st) {
+                      int lds, int K, float* out, int ldo, int grid, hipStream_t st, float* U, int ldu, double* obj) {
   using namespace sysml_mc;
+#define SYSML_WIDE(M) return dispatch_wide<M>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st, U, ldu, obj)
   switch (mode) {
-    case XV: return dispatch_wide<XV>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
-    case XTG: return dispatch_wide<XTG>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
-    case XTXV: return dispatch_wide<XTXV>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
-    case XTWXV: return dispatch_wide<XTWXV>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
-    case XTXVY: return dispatch_wide<XTXVY>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
-    case XTPSXV: return dispatch_wide<XTPSXV>(ks, occ, X, N, D, VW, S, lds, K, out, ldo, grid, st);
+    case XV: SYSML_WIDE(XV);
+    case XTG: SYSML_WIDE(XTG);
+    case XTXV: SYSML_WIDE(XTXV);
+    case XTWXV: SYSML_WIDE(XTWXV);
+    case XTXVY: SYSML_WIDE(XTXVY);
+    case XTPSXV: SYSML_WIDE(XTPSXV);
+    case XTSMG: SYSML_WIDE(XTSMG);
+    case XTSMGO: SYSML_WIDE(XTSMGO);
     default: return -1;
   }
+#undef SYSML_WIDE
 }
 
 int sysml_mwide_occupancy(int mode, int D) {
   if (D <= 0 || D > 1024) return -1;
-  return wide_route(mode, (D + 255) / 256, true, nullptr, 0, D, nullptr, nullptr, 0, 0, nullptr, 0, 0, nullptr);
+  return wide_route(mode, (D + 255) / 256, true, nullptr, 0, D, nullptr, nullptr, 0, 0, nullptr, 0, 0, nullptr,
+                    nullptr, 0, nullptr);
 }
 
-// mode XV: out N x ldo; XTG and the chains (XTXV, XTWXV w: N x 1, XTXVY y: N x K, XTPSXV P: N x K;
-// lds = leading dimension of S): out grid x (D*K) per-block partials of the D x K result.
+// Wide products and chains (K <= 16 columns; V as [3][16][Dp] bf16 planes).  Mode XV: out N x ldo;
+// XTG and the chains (XTXV, XTWXV w: N x 1, XTXVY y: N x K, XTPSXV P: N x K; lds = leading
+// dimension of S): out grid x (D*K) per-block partials of the D x K result.  Softmax modes
+// (K <= 15, S = Y): XTSMG writes U = X V to U (N x ldu); XTSMGO reads Y's K + 1 columns, writes
+// the K + 1 class probabilities to U and per-wave objective partials to obj (grid * waves x 2).
 int sysml_mwide(int mode, const void* X, int64_t N, int D, const void* VW, const float* S, int lds, int K, float* out,
-                int ldo, int grid, hipStream_t stream) {
+                int ldo, int grid, hipStream_t stream, float* U, int ldu, double* obj) {
+  using namespace sysml_mc;
   if (D <= 0 || D > 1024 || (D & 7) || K < 1 || K > 16 || grid <= 0 || N <= 0) return -1;
-  if (mode != sysml_mc::XTG && VW == nullptr) return -1;
-  if (mode != sysml_mc::XV && mode != sysml_mc::XTXV && (S == nullptr || lds < (mode == sysml_mc::XTWXV ? 1 : K)))
-    return -1;
-  return wide_route(mode, (D + 255) / 256, false, X, N, D, VW, S, lds, K, out, ldo, grid, stream);
+  if (mode != XTG && VW == nullptr) return -1;
+  const int scols = mode == XTWXV ? 1 : mode == XTSMGO ? K + 1 : K;
+  if (mode != XV && mode != XTXV && (S == nullptr || lds < scols)) return -1;
+  if (mode == XTSMG || mode == XTSMGO) {
+    if (K > 15 || U == nullptr || ldu < scols || (mode == XTSMGO && obj == nullptr)) return -1;
+  }
+  return wide_route(mode, (D + 255) / 256, false, X, N, D, VW, S, lds, K, out, ldo, grid, stream, U, ldu, obj);
 }
 
 }  // extern "C"

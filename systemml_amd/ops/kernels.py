@@ -105,7 +105,7 @@ def load(required=False):
     L.sysml_mwide.restype = ctypes.c_int
     L.sysml_mwide.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-                              ctypes.c_int, ctypes.c_void_p]
+                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     L.sysml_mwide_occupancy.restype = ctypes.c_int
     L.sysml_mwide_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
     _lib = L
@@ -208,11 +208,13 @@ def _wide_planes(V, D, device):
     return VW
 
 
-def _mwide(mode, X, V=None, G=None, sbc=0):
+def _mwide(mode, X, V=None, G=None, sbc=0, U=None, obj=None):
     """Wide products and chains with up to 16 columns (ops/hip/mfma_chain.hip wide_kernel):
     each of the three bf16 planes of V / G is its own MFMA into a 16-column tile.
     mode XV: U = X %*% V; XTG: t(X) %*% G; chains (XTXV / XTWXV / XTXVY / XTPSXV, G = the
-    row-side operand w / y / P): t(X) %*% g(X %*% V) in one pass over X."""
+    row-side operand w / y / P): t(X) %*% g(X %*% V) in one pass over X.  Softmax modes (G = Y):
+    XTSMG writes X %*% V into U, XTSMGO the K + 1 class probabilities, appending its
+    (blocks * waves, 2) fp64 objective partials to the list `obj`."""
     L = load(required=True)
     N, D = X.shape
     key = ("wide", mode, D, X.device.index)
@@ -225,18 +227,29 @@ def _mwide(mode, X, V=None, G=None, sbc=0):
         return None
     K = V.shape[1] if V is not None else G.shape[1]
     VW = _wide_planes(V, D, X.device) if V is not None else None
-    S, lds = _rows_f32(G, K, sbc, X.device) if G is not None else (None, 0)
+    S, lds = _rows_f32(G, G.shape[1], sbc, X.device) if G is not None else (None, 0)
+    up = ctypes.c_void_p(U.data_ptr() if U is not None else 0)
+    ldu = U.stride(0) if U is not None else 0
+    ob = None
+    if mode == XTSMGO:
+        ob = torch.empty((grid * 16, 2), dtype=torch.float64, device=X.device)
+        ob.zero_()
+    op = ctypes.c_void_p(ob.data_ptr() if ob is not None else 0)
     vp = ctypes.c_void_p(VW.data_ptr() if VW is not None else 0)
     sp = ctypes.c_void_p(S.data_ptr() if S is not None else 0)
     if mode == XV:
         out = torch.empty((N, K), dtype=torch.float32, device=X.device)
         rc = L.sysml_mwide(mode, ctypes.c_void_p(X.data_ptr()), N, D, vp, sp, lds, K,
-                           ctypes.c_void_p(out.data_ptr()), K, grid, _stream())
+                           ctypes.c_void_p(out.data_ptr()), K, grid, _stream(), up, ldu, op)
         return out if rc == 0 else None
     part = torch.empty((grid, D * K), dtype=torch.float32, device=X.device)
     rc = L.sysml_mwide(mode, ctypes.c_void_p(X.data_ptr()), N, D, vp, sp, lds, K,
-                       ctypes.c_void_p(part.data_ptr()), 0, grid, _stream())
-    return part.sum(0).reshape(D, K) if rc == 0 else None
+                       ctypes.c_void_p(part.data_ptr()), 0, grid, _stream(), up, ldu, op)
+    if rc != 0:
+        return None
+    if obj is not None and ob is not None:
+        obj.append(ob)
+    return part.sum(0).reshape(D, K)
 
 
 def _xcode(x):
@@ -512,8 +525,20 @@ def smobj(X, V, Y):
     if not _ok_x(X) or X.dtype != torch.bfloat16:
         return None
     K = V.shape[1]
-    if K > 4 or Y.shape != (X.shape[0], K + 1) or V.shape[0] != X.shape[1]:
+    if Y.shape != (X.shape[0], K + 1) or V.shape[0] != X.shape[1]:
         return None
+    if K > 4:
+        if not (_wide_ok(X, K) and K < WIDE_MAX):
+            return None
+        N = X.shape[0]
+        P = torch.empty((N, K + 1), dtype=torch.float32, device=X.device)
+        ob = []
+        G = _mwide(XTSMGO, X, V=V, G=Y, sbc=1, U=P, obj=ob)
+        if G is None:
+            return None
+        _count("mfma.smobj_wide")
+        s = ob[0].sum(0).tolist()
+        return _result(P), _result(G), s[0], s[1]
     kp = 4                  # the matrix-core kernel's class layout; classes past K are masked
     if not (_c4_ok(X, XTSMG, kp) and _c4m(X, kp)):
         return None
@@ -537,8 +562,17 @@ def smgrad(X, V, Y):
     if not _ok_x(X) or X.dtype not in (torch.bfloat16, torch.float32):
         return None
     K = V.shape[1]
-    if K > 4 or Y.shape != (X.shape[0], K) or V.shape[0] != X.shape[1]:
+    if Y.shape != (X.shape[0], K) or V.shape[0] != X.shape[1]:
         return None
+    if K > 4:
+        if not (_wide_ok(X, K) and K < WIDE_MAX):
+            return None
+        U = torch.empty((X.shape[0], K), dtype=torch.float32, device=X.device)
+        G = _mwide(XTSMG, X, V=V, G=Y, sbc=1, U=U)
+        if G is None:
+            return None
+        _count("mfma.smgrad_wide")
+        return _result(U), _result(G)
     kp = _kpad(K)
     N, D = X.shape
     if _c4_ok(X, XTSMG, kp):

@@ -378,3 +378,34 @@ def test_chain4m_softmax_objective(K, n, d, k):
     r2 = torch.log(E.sum(1)).sum().item()
     assert abs(s1 - r1) <= 1e-4 * max(1.0, abs(r1)), (s1, r1)
     assert abs(s2 - r2) <= 1e-4 * max(1.0, abs(r2)), (s2, r2)
+
+
+@pytest.mark.parametrize("n,d,k", [(70001, 1000, 9), (4099, 512, 15), (30011, 136, 5), (2053, 1024, 7)])
+def test_wide_softmax_objective_and_gradient(K, n, d, k):
+    """Wide softmax modes (5..15 classes + the zero class, e.g. the 10-class MultiLogReg):
+    XTSMGO probabilities / gradient / objective terms and XTSMG (U, gradient) vs fp64."""
+    x = _mk(n, d, torch.bfloat16, seed=8)
+    x64 = x.double()
+    g0 = torch.Generator(device="cuda").manual_seed(9)
+    v = torch.randn((d, k), generator=g0, device="cuda") * 0.05
+    lab = torch.randint(0, k + 1, (n,), device="cuda", generator=g0)
+    y = torch.nn.functional.one_hot(lab, k + 1).float()
+    c0 = dict(K.counters)
+    P, G, s1, s2 = K.smobj(x, v, y)
+    U64 = x64 @ v.double()
+    L = torch.cat([U64, torch.zeros((n, 1), device="cuda", dtype=torch.float64)], 1)
+    LT = L - L.max(1, keepdim=True).values
+    E = torch.exp(LT)
+    P64 = E / E.sum(1, keepdim=True)
+    G64 = x64.t() @ (P64[:, :k] - y.double()[:, :k])
+    torch.testing.assert_close(P.double(), P64, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(G.double(), G64, rtol=2e-4, atol=2e-4 * G64.abs().max().item())
+    r1 = (y.double() * LT).sum().item()
+    r2 = torch.log(E.sum(1)).sum().item()
+    assert abs(s1 - r1) <= 1e-4 * max(1.0, abs(r1)), (s1, r1)
+    assert abs(s2 - r2) <= 1e-4 * max(1.0, abs(r2)), (s2, r2)
+    U, G2 = K.smgrad(x, v, y[:, :k])
+    torch.testing.assert_close(U.double(), U64, rtol=1e-5, atol=1e-5 * U64.abs().max().item())
+    torch.testing.assert_close(G2.double(), G64, rtol=2e-4, atol=2e-4 * G64.abs().max().item())
+    assert K.counters.get("mfma.smobj_wide", 0) == c0.get("mfma.smobj_wide", 0) + 1
+    assert K.counters.get("mfma.smgrad_wide", 0) == c0.get("mfma.smgrad_wide", 0) + 1
