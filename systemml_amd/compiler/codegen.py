@@ -161,6 +161,252 @@ def fuse_cells(bb):
 
 MAGG_MAX = 4
 
+# ----------------------------------------------------------------------------- Row template
+ROW_AGG_OPS = ("sum", "sumsq", "mean", "min", "max")
+
+
+def _row_body_kind(h):
+    """Role of h inside a Row-template region: 'cell' | 'ragg' | 'dot' | None (not fusable)."""
+    if h.dt != "M":
+        return None
+    if _cellwise(h):
+        return "cell"
+    if h.op == "agg" and h.p.get("dir") == "row" and h.p.get("o") in ROW_AGG_OPS and len(h.inputs) == 1:
+        return "ragg"
+    if h.op == "mm" and not h.p.get("transA") and not h.p.get("mvagg") and len(h.inputs) == 2 \
+            and h.inputs[1].dim2 in (-1, 1) and h.inputs[0].dim2 != 1:
+        return "dot"
+    return None
+
+
+def _row_root_kind(h):
+    """Output type when h ends a Row-template region ('col' | 'all' | 'tmv'), else None."""
+    if h.dt == "M" and h.op == "agg" and len(h.inputs) == 1:
+        if h.p.get("dir") == "col" and h.p.get("o") in ("sum", "sumsq", "mean"):
+            return "col"
+    if h.op == "agg" and h.p.get("dir") == "all" and h.p.get("o") in ROW_AGG_OPS and len(h.inputs) == 1 \
+            and h.inputs[0].dt == "M":
+        return "all"
+    if h.dt == "M" and h.op == "mm" and h.p.get("transA") and not h.p.get("mvagg") and len(h.inputs) == 2 \
+            and h.inputs[1].dim2 in (-1, 1):
+        return "tmv"
+    return None
+
+
+def _body_inputs(h, kind):
+    """Inputs of a region hop that may join the region (a dot's side vector never does)."""
+    if kind == "dot":
+        return [h.inputs[0]]
+    return _operands(h) if kind == "cell" else list(h.inputs)
+
+
+def _size_class(h, memo):
+    """Structural size class of a hop's value for the materialisation cost model: 1.0 for a
+    full N x D matrix, 1e-3 for a per-row N x 1 vector (row aggregates, matrix-vector
+    products) or a small side vector, 0 for scalars.  Known dimensions decide where present;
+    an unknown matrix is priced as a full one (the conservative choice: recomputation that
+    would have to read it is never free)."""
+    r = memo.get(h.id)
+    if r is not None:
+        return r
+    if h.dt == "S" or h.op == "lit":
+        r = 0.0
+    elif h.dim1 >= 0 and h.dim2 >= 0:
+        r = 0.0 if h.dim1 * h.dim2 <= 1 else (1.0 if (h.dim1 > 1 and h.dim2 > 1) else 1e-3)
+    else:
+        k = _row_body_kind(h)
+        if k in ("ragg", "dot"):
+            r = 1e-3
+        elif k == "cell":
+            r = max((_size_class(c, memo) for c in _operands(h)), default=0.0)
+        else:
+            r = 1.0
+    memo[h.id] = r
+    return r
+
+
+def _recompute_cost(c, region, leafset, memo, depth=0):
+    """HBM cost (in full-matrix units) of evaluating hop c inside a region instead of reading
+    its materialised value: the inputs it needs that the region does not already read; fusable
+    inputs are themselves priced as min(read, recompute)."""
+    kind = _row_body_kind(c)
+    tot = 0.0
+    for i, x in enumerate(c.inputs):
+        if x.id in region or x.id in leafset or x.dt == "S" or x.op == "lit":
+            continue
+        if kind == "dot" and i == 1:
+            tot += 1e-3                          # the D x 1 side vector
+            continue
+        if kind == "cell" and c.op == "b" and _is_sq(c) and i == 1:
+            continue
+        sx = _size_class(x, memo)
+        if depth < 4 and _row_body_kind(x) is not None:
+            sx = min(sx, _recompute_cost(x, region, leafset, memo, depth + 1))
+        tot += sx
+    return tot
+
+
+def _consumers(order):
+    cons = {}
+    for h in order:
+        for c in h.inputs:
+            cons.setdefault(c.id, []).append(h)
+    return cons
+
+
+def fuse_rows(bb, costed=True):
+    """Row template (reference: hops/codegen/template/TemplateRow.java, cplan/CNodeRow.java):
+    regions of cellwise operators, row aggregates and matrix-vector products over the rows of
+    a tall matrix, ending in a row / cellwise value, a column aggregate, a full aggregate or
+    t(.) %*% a per-row scalar, become ONE generated kernel (ops/rowgen.py).
+
+    Region growth, from the last operator of the block backwards:
+      * closure -- an operator whose consumers are ALL in the region (and which is not a block
+        output) joins it: the value never leaves registers;
+      * cost-based recomputation (reference: the materialisation-point enumeration of
+        hops/codegen/opt/PlanSelectionFuseCostBasedV2.java) -- a shared operator joins a region
+        as a private recomputed copy when that costs no more HBM traffic than reading its
+        materialised value (`_recompute_cost` <= its size class): e.g. X %*% v used by three
+        row regions that all stream X anyway is recomputed in each, and the separate pass over
+        X that would have materialised it disappears once no consumer is left.
+    A region is only formed when the Cell template cannot do its work in one pass: it must
+    contain a row aggregate or matrix-vector product whose result is used again inside the
+    region, or end in a column / full aggregate or t(.) %*% over such a result.  Returns the
+    number of fused operators."""
+    from ..ops.rowgen import RowProgram, MAXIN as RMAXIN, MAXOPS as RMAXOPS
+    live = getattr(bb, "live_out", None)
+    allroots = list(bb.roots) + list(bb.env_out.values())
+    outs = {h.id for h in bb.roots} | {h.id for k, h in bb.env_out.items() if live is None or k in live}
+    tried = set()
+    n = 0
+    memo = {}
+    while True:
+        order = walk(allroots)
+        pos = {h.id: i for i, h in enumerate(order)}
+        consumers = _consumers(order)
+        formed = False
+        for root in reversed(order):
+            if root.id in tried:
+                continue
+            tried.add(root.id)
+            r = _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXIN, RMAXOPS)
+            if r:
+                n += r
+                formed = True
+                break                          # the DAG changed: recompute order and consumers
+        if not formed:
+            return n
+
+
+def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXIN, RMAXOPS):
+    rk = _row_root_kind(root)
+    bk = _row_body_kind(root)
+    if rk is None and bk is None:
+        return 0
+    region = {root.id}
+    kinds = {}
+    if rk is None:
+        kinds[root.id] = bk
+        starts = _body_inputs(root, bk)
+    else:
+        starts = list(root.inputs) if rk == "tmv" else [root.inputs[0]]
+    members = [root]
+    dup = set()
+    leafset = {c.id for c in starts}
+    frontier = list(starts)
+    changed = True
+    while changed:
+        changed = False
+        for c in list(frontier):
+            if c.id in region:
+                continue
+            ck = _row_body_kind(c)
+            if ck is None:
+                continue
+            # closure: every consumer is in the region and none of them is a recomputed copy
+            # (a copied operator stays alive outside the region and still reads c)
+            closed = c.id not in outs and all(p.id in region and p.id not in dup for p in consumers.get(c.id, ()))
+            if not closed:
+                if not costed:
+                    continue
+                # ties go to recomputation: equal reads, and the materialising write disappears
+                # once every consumer recomputes
+                if _recompute_cost(c, region, leafset, memo) > _size_class(c, memo) + 1e-2:
+                    continue
+                dup.add(c.id)
+            region.add(c.id)
+            kinds[c.id] = ck
+            members.append(c)
+            leafset.discard(c.id)
+            for x in _body_inputs(c, ck) + ([c.inputs[1]] if ck == "dot" else []):
+                if x.id not in region:
+                    leafset.add(x.id)
+            frontier.extend(_body_inputs(c, ck))
+            changed = True
+    body = sorted((h for h in members if h.id in kinds), key=lambda h: pos[h.id])
+    reds = [h for h in body if kinds[h.id] in ("ragg", "dot")]
+    if not reds:
+        return 0
+    internal = any(any(p.id in kinds for p in consumers.get(r.id, ())) for r in reds)
+    if not (internal or (rk is not None and len(body) >= 2)):
+        return 0                 # a lone product / row aggregate: the plain operator is as good
+    if rk == "tmv" and kinds.get(root.inputs[0].id) is None and kinds.get(root.inputs[1].id) is None:
+        return 0
+    # leaves: inputs of region hops outside the region, side vectors of dots included
+    leaves = []
+
+    def leaf(x):
+        for i, y in enumerate(leaves):
+            if y is x:
+                return i
+        leaves.append(x)
+        return len(leaves) - 1
+    for h in body:
+        k = kinds[h.id]
+        for c in h.inputs:
+            if c.id not in kinds and not (k == "cell" and h.op == "b" and _is_sq(h) and c is h.inputs[1]):
+                leaf(c)
+    if rk is not None:
+        for c in (root.inputs if rk == "tmv" else root.inputs[:1]):
+            if c.id not in kinds:
+                leaf(c)
+    if len(leaves) > RMAXIN or len(body) > RMAXOPS:
+        return 0
+    nin = len(leaves)
+    idx = {}
+    ops = []
+
+    def ref(x):
+        return idx[x.id] if x.id in idx else leaf(x)
+    for h in body:
+        k = kinds[h.id]
+        if k == "cell":
+            if h.op == "b" and _is_sq(h):
+                ops.append(("u", "sq", ref(h.inputs[0]), 0))
+            elif h.op == "b":
+                ops.append(("b", h.p["o"], ref(h.inputs[0]), ref(h.inputs[1])))
+            else:
+                ops.append(("u", h.p["o"], ref(h.inputs[0]), 0))
+        elif k == "ragg":
+            ops.append(("ragg", h.p["o"], ref(h.inputs[0]), 0))
+        else:
+            ops.append(("dot", None, ref(h.inputs[0]), ref(h.inputs[1])))
+        idx[h.id] = nin + len(ops) - 1
+    if rk is None:
+        prog = RowProgram(nin, ops, idx[root.id], "row" if bk == "ragg" else "vec")
+    elif rk == "tmv":
+        prog = RowProgram(nin, ops, ref(root.inputs[0]), "tmv", extra=ref(root.inputs[1]))
+    else:
+        prog = RowProgram(nin, ops, ref(root.inputs[0]), rk, oagg=root.p["o"])
+    if len(leaves) != nin:
+        return 0
+    lines = sorted({getattr(o.pos, "line", None) for o in members} - {None})
+    root.op = "row"
+    root.inputs = list(leaves)
+    root.named = []
+    root.p = {"o": prog.describe(), "prog": prog, "lines": lines}
+    return len(body)
+
 
 def _multi_agg(built):
     """MAgg template (reference: template/TemplateMultiAgg.java and the multi-aggregate

@@ -112,6 +112,14 @@ def infer(h, dims, env):
         if d == UNK:
             return UNK
         return (d[0], 1) if agg[1] == "row" else (1, d[1])
+    if op == "row":
+        from ..ops.rowgen import out_shape
+        if h.p["prog"].otype == "all":
+            return SCALAR
+        if not all(x == SCALAR or _known(x) for x in ins):
+            return UNK
+        s = out_shape(h.p["prog"], [None if x == SCALAR else x for x in ins])
+        return UNK if s is None else s
     if op == "agg":
         r, c = ins[0]
         d = h.p["dir"]

@@ -20,18 +20,18 @@ from .scalars import DevScalar
 
 
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell",
-                  "magg"}
+                  "magg", "row"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
-_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "rix", "t", "cell", "magg"}
+_CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "rix", "t", "cell", "magg", "row"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "round", "floor", "ceil", "sign",
                     "sin", "tan", "asin", "atan", "sinh", "tanh", "neg"}       # ops/sparse.py SAFE_UNARY
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
 _LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "smobj", "t", "tak",
-                 "cell", "magg"}
+                 "cell", "magg", "row"}
 # operators that compute on matrix operands (placement applies); the rest move values around
 _COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "wquat", "tak", "t", "rix", "lix", "bi",
-                 "cell", "magg"}
+                 "cell", "magg", "row"}
 transfer_stats = {"h2d": 0, "d2h": 0, "h2d_bytes": 0, "d2h_bytes": 0}   # -stats (utils/stats.gpu_report)
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
@@ -229,6 +229,11 @@ def _make_impl(h):
         from ..ops import cell as CELL
         prog = p["prog"]
         return (lambda ctx, a: CELL.evaluate(prog, a)), "spoofCell"
+    if op == "row":
+        # generated Row template (compiler/codegen.fuse_rows): one ops/rowgen.py kernel
+        from ..ops import rowgen as ROWG
+        rprog = p["prog"]
+        return (lambda ctx, a: ROWG.evaluate(rprog, a)), "spoofRA"
     if op == "magg":
         # multi-aggregate template (compiler/codegen._multi_agg): a tuple of scalars, one pass
         from ..ops import cell as CELL
