@@ -243,10 +243,17 @@ def lanes_for(D):
 
 
 def dcap_for(D):
-    for c in (64, 256, 1024, 2048, 4096, 8192, 16384):
-        if D <= c:
-            return c
-    return None
+    """LDS columns of a column-aggregate accumulator (D rounded up to 64)."""
+    return (D + 63) // 64 * 64 if D <= 16384 else None
+
+
+def lds_slices(G, dcap, T):
+    """Accumulator slices: one per row group (deterministic sums) when they fit in LDS, else
+    one slice shared by all groups through LDS atomics; 0 if even that does not fit."""
+    sz = 4 if T == torch.float32 else 8
+    if G * dcap * sz <= LDS_BYTES:
+        return G
+    return 1 if dcap * sz <= LDS_BYTES else 0
 
 
 # ----------------------------------------------------------------------------- code generation
@@ -267,7 +274,7 @@ def _comb(o, a, b):
     return f"sysml_{o}<T>({a}, {b})"
 
 
-def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1):
+def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None):
     """HIP source of the fused row kernel (see the module docstring for the phase structure)."""
     ct = "float" if T == torch.float32 else "double"
     n_in = prog.n_in
@@ -334,10 +341,17 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1):
             w(f"  const T c{i} = {op_expr(i, lambda j: cname[j])};")
             cname[i] = f"c{i}"
     colacc = ot in ("col", "tmv")
+    S = G if slices is None else slices
     if colacc:
-        w(f"  __shared__ T acc[G][{dcap}];")
-        w(f"  for (int q = tid; q < G * {dcap}; q += 256) (&acc[0][0])[q] = T(0);")
+        w(f"  __shared__ T acc[{S}][{dcap}];")
+        w(f"  for (int q = tid; q < {S} * {dcap}; q += 256) (&acc[0][0])[q] = T(0);")
         w("  __syncthreads();")
+
+    def col_add(ind, val):
+        if S == G:
+            w(f"{ind}acc[grp][d] += {val};")
+        else:
+            w(f"{ind}atomicAdd(&acc[0][d], {val});")
     if ot == "all":
         w(f"  T tot = {_RAGG_INIT[prog.oagg]};")
     w("  for (sysml_i64 row = (sysml_i64)blockIdx.x * G + grp; row < N; row += (sysml_i64)gridDim.x * G) {")
@@ -442,9 +456,9 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1):
                 if ot == "vec":
                     w(f"{ind}static_cast<T*>(A.out)[rowoff + d] = {v};")
                 elif ot == "col":
-                    w(f"{ind}acc[grp][d] += {v}{(' * ' + v) if prog.oagg == 'sumsq' else ''};")
+                    col_add(ind, f"{v}{(' * ' + v) if prog.oagg == 'sumsq' else ''}")
                 elif ot == "tmv":
-                    w(f"{ind}acc[grp][d] += {v} * {sname[prog.extra]};")
+                    col_add(ind, f"{v} * {sname[prog.extra]}")
                 else:
                     w(ind + _acc_step(prog.oagg, "tot", v))
                 close_loop("    ")
@@ -454,7 +468,7 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1):
         w("  __syncthreads();")
         w("  for (sysml_i64 d = tid; d < D; d += 256) {")
         w("    double s = 0.0;")
-        w("    for (int g = 0; g < G; ++g) s += (double)acc[g][d];")
+        w(f"    for (int g = 0; g < {S}; ++g) s += (double)acc[g][d];")
         w("    A.part[(sysml_i64)blockIdx.x * D + d] = s;")
         w("  }")
     elif ot == "all":
@@ -518,12 +532,12 @@ class _RowArgs(ctypes.Structure):
 _funcs = {}
 
 
-def _func(prog, T, modes, dts, kinds, L, dcap, vec, dev):
-    key = (prog.key(), T, modes, dts, L, dcap, vec, str(dev))
+def _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, dev):
+    key = (prog.key(), T, modes, dts, L, dcap, vec, slices, str(dev))
     f = _funcs.get(key, False)
     if f is not False:
         return f
-    src = generate(prog, T, modes, dts, kinds, L, dcap, vec)
+    src = generate(prog, T, modes, dts, kinds, L, dcap, vec, slices)
     code = compile_source(src, gpu_arch(dev))        # raises on a compile error: a generator bug
     fn = ctypes.c_void_p()
     cbuf = ctypes.create_string_buffer(code, len(code))
@@ -579,7 +593,7 @@ def _kernel(prog: RowProgram, args):
     dcap = 0
     if ot in ("col", "tmv"):
         dcap = dcap_for(D)
-        if dcap is None or G * dcap * (4 if T == torch.float32 else 8) > LDS_BYTES:
+        if dcap is None:
             return None
     A = _RowArgs()
     keep = []
@@ -611,9 +625,12 @@ def _kernel(prog: RowProgram, args):
     if vec > 1:
         L = lanes_for((D + vec - 1) // vec)
         G = 256 // L
-        if ot in ("col", "tmv") and G * dcap * (4 if T == torch.float32 else 8) > LDS_BYTES:
+    slices = G
+    if ot in ("col", "tmv"):
+        slices = lds_slices(G, dcap, T)
+        if slices == 0:
             return None
-    f = _func(prog, T, modes, dts, kinds, L, dcap, vec, dev)
+    f = _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, dev)
     ngrp = (N + G - 1) // G
     if ot in ("col", "tmv"):
         nblk = max(1, min(ngrp, 1024))
