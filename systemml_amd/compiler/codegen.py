@@ -408,6 +408,147 @@ def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXI
     return len(body)
 
 
+# ----------------------------------------------------------------------------- Outer template
+_SAFE_UN = {"abs", "sqrt", "sign", "neg", "round", "floor", "ceil", "sin", "tan", "asin", "atan", "sinh", "tanh"}
+
+
+def _lit0(h):
+    return h.op == "lit" and not isinstance(h.value, bool) and h.value == 0
+
+
+def _zero_where(h, W, ids):
+    """True when h's value is 0 wherever W's is (structural proof over the region `ids`)."""
+    if h is W:
+        return True
+    if h.id not in ids:
+        return False
+    if h.op == "b":
+        a, b = h.inputs
+        o = h.p.get("o")
+        if _is_sq(h):
+            return _zero_where(a, W, ids)
+        if o == "*":
+            return _zero_where(a, W, ids) or _zero_where(b, W, ids)
+        if o == "/":
+            return _zero_where(a, W, ids)
+        if o in ("+", "-"):
+            return _zero_where(a, W, ids) and _zero_where(b, W, ids)
+        if o == "!=":
+            return (_zero_where(a, W, ids) and _lit0(b)) or (_zero_where(b, W, ids) and _lit0(a))
+        if o == "^":
+            return b.op == "lit" and not isinstance(b.value, bool) and isinstance(b.value, (int, float)) \
+                and b.value > 0 and _zero_where(a, W, ids)
+        return False
+    if h.op == "u":
+        return h.p.get("o") in _SAFE_UN and _zero_where(h.inputs[0], W, ids)
+    return False
+
+
+def _outer_root(h):
+    """(output type, body hop, B) when h can end an Outer-template region."""
+    if _cellwise(h):
+        return "cell", h, None
+    if h.op == "agg" and h.p.get("dir") == "all" and h.p.get("o") == "sum" and len(h.inputs) == 1 \
+            and _cellwise(h.inputs[0]):
+        return "all", h.inputs[0], None
+    if h.op == "mm" and not h.p.get("mvagg") and len(h.inputs) == 2 and _cellwise(h.inputs[0]):
+        return ("right" if h.p.get("transA") else "left"), h.inputs[0], h.inputs[1]
+    return None
+
+
+def fuse_outer(bb):
+    """Outer-product template (reference: hops/codegen/template/TemplateOuterProduct.java):
+    a cellwise DAG over U %*% t(V) that is zero wherever a driver matrix W is zero (proved
+    structurally: W * g, g / ..., (W != 0), sums of such terms, f(0)=0 unaries) -- optionally
+    summed, or multiplied by a matrix from the left (f %*% B) or the right (t(f) %*% B) --
+    becomes one `outer` operator (ops/outer.py): with a sparse W the product is sampled at W's
+    non-zeros only.  The region grows by closure (single-consumer cellwise operators), and
+    U %*% t(V) must have no consumer outside it.  Returns the number of fused operators."""
+    from ..ops.outer import OuterProgram
+    from .rewrites import _uv
+    live = getattr(bb, "live_out", None)
+    allroots = list(bb.roots) + list(bb.env_out.values())
+    outs = {h.id for h in bb.roots} | {h.id for k, h in bb.env_out.items() if live is None or k in live}
+    order = walk(allroots)
+    pos = {h.id: i for i, h in enumerate(order)}
+    consumers = _consumers(order)
+    absorbed = set()
+    n = 0
+    for root in reversed(order):
+        if root.id in absorbed:
+            continue
+        r = _outer_root(root)
+        if r is None:
+            continue
+        otype, top, B = r
+        if top is not root and (top.id in outs or len(consumers.get(top.id, ())) != 1):
+            continue
+        region = {root.id, top.id}
+        members = [top] if top is root else [root, top]
+        frontier = list(_operands(top))
+        uvs = []
+        changed = True
+        while changed:
+            changed = False
+            for c in list(frontier):
+                if c.id in region:
+                    continue
+                if _uv(c) is not None and c.dt == "M":
+                    # the low-rank product is always recomputed inside the region (sampled at
+                    # the driver's non-zeros it costs less than reading a materialised m x n
+                    # value); other consumers keep their own copy
+                    region.add(c.id)
+                    uvs.append(c)
+                    changed = True
+                    continue
+                if c.id in absorbed or c.id in outs:
+                    continue
+                if not all(p.id in region for p in consumers.get(c.id, ())):
+                    continue
+                if not _cellwise(c):
+                    continue
+                region.add(c.id)
+                members.append(c)
+                frontier.extend(_operands(c))
+                changed = True
+        if len(uvs) != 1:
+            continue
+        uvh = uvs[0]
+        U, V = _uv(uvh)
+        ops = sorted((h for h in members if h.id in region and _cellwise(h)), key=lambda h: pos[h.id])
+        leaves = []
+        for h in ops:
+            for c in _operands(h):
+                if c.id not in region or c is uvh:
+                    if all(c is not y for y in leaves):
+                        leaves.append(c)
+        if len(leaves) > MAXIN or len(ops) > MAXOPS:
+            continue
+        ids = {h.id for h in ops}
+        W = next((x for x in leaves if x is not uvh and x.dt != "S" and x.op != "lit" and x is not U and x is not V
+                  and _zero_where(top, x, ids)), None)
+        if W is None:
+            continue
+        ra = _regalloc(ops, leaves)
+        if ra is None:
+            continue
+        code, out = ra
+        cprog = CellProgram(code, len(leaves), out)
+        ui = next(i for i, x in enumerate(leaves) if x is uvh)
+        wi = next(i for i, x in enumerate(leaves) if x is W)
+        prog = OuterProgram(cprog, ui, wi, otype)
+        ins = [U, V] + [x for x in leaves if x is not uvh] + ([B] if B is not None else [])
+        lines = sorted({getattr(o.pos, "line", None) for o in ops + [root, uvh]} - {None})
+        for h in ops + [root]:
+            absorbed.add(h.id)
+        root.op = "outer"
+        root.inputs = ins
+        root.named = []
+        root.p = {"o": prog.describe(), "prog": prog, "lines": lines}
+        n += len(ops) + 1
+    return n
+
+
 def _multi_agg(built):
     """MAgg template (reference: template/TemplateMultiAgg.java and the multi-aggregate
     merge of PlanSelectionFuseCostBased): full aggregates of fused cell programs that read a

@@ -112,6 +112,16 @@ def infer(h, dims, env):
         if d == UNK:
             return UNK
         return (d[0], 1) if agg[1] == "row" else (1, d[1])
+    if op == "outer":
+        prog = h.p["prog"]
+        ot = prog.otype
+        (m, _), (nn, _) = ins[0], ins[1]
+        if ot == "all":
+            return SCALAR
+        if ot == "cell":
+            return (m, nn)
+        kb = ins[-1][1]
+        return (m, kb) if ot == "left" else (nn, kb)
     if op == "row":
         from ..ops.rowgen import out_shape
         if h.p["prog"].otype == "all":

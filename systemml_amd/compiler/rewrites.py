@@ -758,7 +758,10 @@ def rewrite_block(bb, config=None):
             nobj = sum(1 for h in H.walk(list(bb.roots) + list(bb.env_out.values())) if h.op == "smobj")
             if nobj:
                 rw.stats["softmax-objective"] = nobj
-        from .codegen import fuse_cells, fuse_rows
+        from .codegen import fuse_cells, fuse_rows, fuse_outer
+        n = fuse_outer(bb)
+        if n:
+            rw.stats["outer-fused-ops"] = n
         n = fuse_rows(bb)
         if n:
             rw.stats["row-fused-ops"] = n

@@ -274,7 +274,7 @@ def _comb(o, a, b):
     return f"sysml_{o}<T>({a}, {b})"
 
 
-def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None):
+def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None, regs=False):
     """HIP source of the fused row kernel (see the module docstring for the phase structure)."""
     ct = "float" if T == torch.float32 else "double"
     n_in = prog.n_in
@@ -342,7 +342,14 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             cname[i] = f"c{i}"
     colacc = ot in ("col", "tmv")
     S = G if slices is None else slices
-    if colacc:
+    J = (dcap + L * vec - 1) // (L * vec) if (colacc and regs) else 0
+    if colacc and J:
+        w(f"  T racc[{J}][{vec}];")
+        w("  #pragma unroll")
+        w(f"  for (int jj = 0; jj < {J}; ++jj)")
+        w("    #pragma unroll")
+        w(f"    for (int u = 0; u < {vec}; ++u) racc[jj][u] = T(0);")
+    elif colacc:
         w(f"  __shared__ T acc[{S}][{dcap}];")
         w(f"  for (int q = tid; q < {S} * {dcap}; q += 256) (&acc[0][0])[q] = T(0);")
         w("  __syncthreads();")
@@ -376,7 +383,7 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             sname[i] = f"s{i}"
             emitted.add(i)
 
-    def vector_body(targets, indent, extra=()):
+    def vector_body(targets, indent, extra=(), reg=False):
         """Opens the element loop and emits the statements for the V nodes `targets` need
         (VEC > 1: the V leaves as one vector load per lane, then VEC unrolled elements);
         returns (name map, indent of the loop body)."""
@@ -391,11 +398,24 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             if kind != "in":
                 stack.extend([a] if kind == "u" else [a, b])
         names = dict(sname)
+        if reg:
+            # lane-owned column chunks jj (fixed per lane for every row of the group): the
+            # column accumulators stay in registers
+            w(f"{indent}#pragma unroll")
+            w(f"{indent}for (int jj = 0; jj < {J}; ++jj) {{")
         if vec == 1:
-            w(f"{indent}for (sysml_i64 d = lane; d < D; d += L) {{")
+            if reg:
+                w(f"{indent}  const sysml_i64 d = (sysml_i64)lane + (sysml_i64)jj * L;")
+                w(f"{indent}  if (d < D) {{")
+            else:
+                w(f"{indent}for (sysml_i64 d = lane; d < D; d += L) {{")
             ind = indent + "  "
         else:
-            w(f"{indent}for (sysml_i64 d0 = (sysml_i64)lane * {vec}; d0 < D; d0 += (sysml_i64)L * {vec}) {{")
+            if reg:
+                w(f"{indent}  const sysml_i64 d0 = ((sysml_i64)lane + (sysml_i64)jj * L) * {vec};")
+                w(f"{indent}  if (d0 < D) {{")
+            else:
+                w(f"{indent}for (sysml_i64 d0 = (sysml_i64)lane * {vec}; d0 < D; d0 += (sysml_i64)L * {vec}) {{")
             for k in sorted({j for j in need if j < n_in} | set(extra)):
                 base = "rowoff + d0" if modes[k] == FULL else "d0"
                 w(f"{indent}  T x{k}[{vec}]; sysml_ldv{vec}<T>(A.in[{k}], {dts[k]}, {base}, x{k});")
@@ -416,8 +436,10 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
                 names[k] = leaf_expr(k, True)
         return names, ind
 
-    def close_loop(indent):
+    def close_loop(indent, reg=False):
         w(f"{indent}}}" if vec == 1 else f"{indent}  }}\n{indent}}}")
+        if reg:
+            w(f"{indent}}}")
 
     nphase = max([final] + [p + 1 for p in red_phase.values()])
     for p in range(nphase + 1):
@@ -451,9 +473,15 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             elif ot == "all" and not vec_out:
                 w(f"    if (lane == 0) {{ {_acc_step(prog.oagg, 'tot', sname[prog.out])} }}")
             else:
-                names, ind = vector_body([prog.out], "    ")
+                regacc = colacc and J > 0
+                names, ind = vector_body([prog.out], "    ", reg=regacc)
                 v = names[prog.out]
-                if ot == "vec":
+                ridx = "racc[jj][u]" if vec > 1 else "racc[jj][0]"
+                if regacc:
+                    val = f"{v}{(' * ' + v) if prog.oagg == 'sumsq' else ''}" if ot == "col" else \
+                        f"{v} * {sname[prog.extra]}"
+                    w(f"{ind}{ridx} += {val};")
+                elif ot == "vec":
                     w(f"{ind}static_cast<T*>(A.out)[rowoff + d] = {v};")
                 elif ot == "col":
                     col_add(ind, f"{v}{(' * ' + v) if prog.oagg == 'sumsq' else ''}")
@@ -461,10 +489,28 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
                     col_add(ind, f"{v} * {sname[prog.extra]}")
                 else:
                     w(ind + _acc_step(prog.oagg, "tot", v))
-                close_loop("    ")
+                close_loop("    ", regacc)
             break
     w("  }")
-    if colacc:
+    if colacc and J:
+        # merge the row groups' register accumulators in a fixed order (deterministic)
+        w(f"  __shared__ T acc[1][{dcap}];")
+        w(f"  for (int q = tid; q < {dcap}; q += 256) acc[0][q] = T(0);")
+        w("  __syncthreads();")
+        w("  for (int g = 0; g < G; ++g) {")
+        w("    if (grp == g) {")
+        w("      #pragma unroll")
+        w(f"      for (int jj = 0; jj < {J}; ++jj)")
+        w("      #pragma unroll")
+        w(f"      for (int u = 0; u < {vec}; ++u) {{")
+        w(f"        const sysml_i64 d = ((sysml_i64)lane + (sysml_i64)jj * L) * {vec} + u;")
+        w("        if (d < D) acc[0][d] += racc[jj][u];")
+        w("      }")
+        w("    }")
+        w("    __syncthreads();")
+        w("  }")
+        w("  for (sysml_i64 d = tid; d < D; d += 256) A.part[(sysml_i64)blockIdx.x * D + d] = (double)acc[0][d];")
+    elif colacc:
         w("  __syncthreads();")
         w("  for (sysml_i64 d = tid; d < D; d += 256) {")
         w("    double s = 0.0;")
@@ -532,12 +578,12 @@ class _RowArgs(ctypes.Structure):
 _funcs = {}
 
 
-def _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, dev):
-    key = (prog.key(), T, modes, dts, L, dcap, vec, slices, str(dev))
+def _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, regs, dev):
+    key = (prog.key(), T, modes, dts, L, dcap, vec, slices, regs, str(dev))
     f = _funcs.get(key, False)
     if f is not False:
         return f
-    src = generate(prog, T, modes, dts, kinds, L, dcap, vec, slices)
+    src = generate(prog, T, modes, dts, kinds, L, dcap, vec, slices, regs)
     code = compile_source(src, gpu_arch(dev))        # raises on a compile error: a generator bug
     fn = ctypes.c_void_p()
     cbuf = ctypes.create_string_buffer(code, len(code))
@@ -626,11 +672,15 @@ def _kernel(prog: RowProgram, args):
         L = lanes_for((D + vec - 1) // vec)
         G = 256 // L
     slices = G
+    regs = False
     if ot in ("col", "tmv"):
+        sz = 4 if T == torch.float32 else 8
+        J = (dcap + L * vec - 1) // (L * vec)
+        regs = J * vec * sz <= 128 and dcap * sz <= LDS_BYTES     # <= 32 fp32 / 16 fp64 registers
         slices = lds_slices(G, dcap, T)
         if slices == 0:
             return None
-    f = _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, dev)
+    f = _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, regs, dev)
     ngrp = (N + G - 1) // G
     if ot in ("col", "tmv"):
         nblk = max(1, min(ngrp, 1024))

@@ -20,7 +20,7 @@ from .scalars import DevScalar
 
 
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell",
-                  "magg", "row"}
+                  "magg", "row", "outer"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
 _CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "rix", "t", "cell", "magg", "row"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "round", "floor", "ceil", "sign",
@@ -28,10 +28,10 @@ _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "rou
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
 _LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "smobj", "t", "tak",
-                 "cell", "magg", "row"}
+                 "cell", "magg", "row", "outer"}
 # operators that compute on matrix operands (placement applies); the rest move values around
 _COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "wquat", "tak", "t", "rix", "lix", "bi",
-                 "cell", "magg", "row"}
+                 "cell", "magg", "row", "outer"}
 transfer_stats = {"h2d": 0, "d2h": 0, "h2d_bytes": 0, "d2h_bytes": 0}   # -stats (utils/stats.gpu_report)
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
@@ -229,6 +229,12 @@ def _make_impl(h):
         from ..ops import cell as CELL
         prog = p["prog"]
         return (lambda ctx, a: CELL.evaluate(prog, a)), "spoofCell"
+    if op == "outer":
+        # Outer-product template (compiler/codegen.fuse_outer): sampled at a sparse driver's
+        # non-zeros (ops/outer.py)
+        from ..ops import outer as OUTR
+        oprog = p["prog"]
+        return (lambda ctx, a: OUTR.evaluate(oprog, a)), "spoofOP"
     if op == "row":
         # generated Row template (compiler/codegen.fuse_rows): one ops/rowgen.py kernel
         from ..ops import rowgen as ROWG
