@@ -235,6 +235,39 @@ def out_shape(prog: RowProgram, shapes):
     return r
 
 
+REG_BUDGET = 96            # cached fp32 values per lane (fp64 count twice)
+
+
+def plan_registers(prog, modes, kinds, D, L, vec, T, dcap):
+    """(J, cache): J lane-owned column chunks of VEC elements cover a row (0: the row is too
+    wide -- strided streaming loops instead); cache holds the input indices kept in registers
+    ('acc' for the column accumulators), chosen greedily within REG_BUDGET: the column
+    accumulators, then the N x D inputs (each row read from HBM once for every phase), then
+    the row-invariant 1 x D / side vectors."""
+    J = (D + L * vec - 1) // (L * vec)
+    if J * vec > 64:
+        return 0, frozenset()
+    per = J * vec * (1 if T == torch.float32 else 2)
+    used = 0
+    cache = []
+    if prog.otype in ("col", "tmv") and dcap and dcap * (4 if T == torch.float32 else 8) <= LDS_BYTES:
+        cache.append("acc")
+        used += per
+    vecuse = set()
+    for kind, o, a, b in prog.ops:
+        for x in ((a, b) if kind in ("b", "dot") else (a,)):
+            if x < prog.n_in and modes[x] in (FULL, ROWV, SIDE):
+                vecuse.add(x)
+    if prog.out < prog.n_in and modes[prog.out] in (FULL, ROWV, SIDE):
+        vecuse.add(prog.out)
+    for group in ((FULL,), (ROWV, SIDE)):
+        for k in sorted(vecuse):
+            if modes[k] in group and used + per <= REG_BUDGET:
+                cache.append(k)
+                used += per
+    return J, frozenset(cache)
+
+
 def lanes_for(D):
     L = 4
     while L < 64 and L * 4 < D:
@@ -274,7 +307,7 @@ def _comb(o, a, b):
     return f"sysml_{o}<T>({a}, {b})"
 
 
-def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None, regs=False):
+def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None, J=0, cache=frozenset()):
     """HIP source of the fused row kernel (see the module docstring for the phase structure)."""
     ct = "float" if T == torch.float32 else "double"
     n_in = prog.n_in
@@ -296,16 +329,6 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
     ot = prog.otype
     vec_out = kinds[prog.out] == "V"
     final = avail[prog.out] if ot != "tmv" else max(avail[prog.out], avail[prog.extra])
-
-    def leaf_expr(k, elem):
-        m, dt = modes[k], dts[k]
-        if m == FULL:
-            return f"sysml_ld<T>(A.in[{k}], {dt}, rowoff + d)"
-        if m in (ROWV, SIDE):
-            return f"sysml_ld<T>(A.in[{k}], {dt}, d)"
-        if m == COLV:
-            return f"s{k}"
-        return f"c{k}"
 
     def op_expr(i, ref):
         kind, o, a, b = nodes[i]
@@ -342,8 +365,9 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             cname[i] = f"c{i}"
     colacc = ot in ("col", "tmv")
     S = G if slices is None else slices
-    J = (dcap + L * vec - 1) // (L * vec) if (colacc and regs) else 0
-    if colacc and J:
+    structured = J > 0
+    creg = colacc and structured and "acc" in cache
+    if creg:
         w(f"  T racc[{J}][{vec}];")
         w("  #pragma unroll")
         w(f"  for (int jj = 0; jj < {J}; ++jj)")
@@ -359,6 +383,19 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             w(f"{ind}acc[grp][d] += {val};")
         else:
             w(f"{ind}atomicAdd(&acc[0][d], {val});")
+
+    def load_cached(k, base, indent):
+        w(f"{indent}T xr{k}[{J}][{vec}];")
+        w(f"{indent}#pragma unroll")
+        w(f"{indent}for (int jj = 0; jj < {J}; ++jj) {{")
+        w(f"{indent}  const sysml_i64 d0 = ((sysml_i64)lane + (sysml_i64)jj * L) * {vec};")
+        w(f"{indent}  if (d0 < D) sysml_ldv{vec}<T>(A.in[{k}], {dts[k]}, {base}, xr{k}[jj]);")
+        w(f"{indent}}}")
+
+    # row-invariant vectors (1 x D inputs, side vectors of products) cached once per kernel
+    for k in range(n_in):
+        if modes[k] in (ROWV, SIDE) and k in cache:
+            load_cached(k, "d0", "  ")
     if ot == "all":
         w(f"  T tot = {_RAGG_INIT[prog.oagg]};")
     w("  for (sysml_i64 row = (sysml_i64)blockIdx.x * G + grp; row < N; row += (sysml_i64)gridDim.x * G) {")
@@ -369,6 +406,10 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
         if kinds[k] == "S":
             w(f"    const T s{k} = sysml_ld<T>(A.in[{k}], {dts[k]}, row);")
             sname[k] = f"s{k}"
+    # the row itself: every N x D input read ONCE from HBM into registers, reused by all phases
+    for k in range(n_in):
+        if modes[k] == FULL and k in cache:
+            load_cached(k, "rowoff + d0", "    ")
 
     def sref(j):
         return sname[j]
@@ -383,10 +424,10 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             sname[i] = f"s{i}"
             emitted.add(i)
 
-    def vector_body(targets, indent, extra=(), reg=False):
-        """Opens the element loop and emits the statements for the V nodes `targets` need
-        (VEC > 1: the V leaves as one vector load per lane, then VEC unrolled elements);
-        returns (name map, indent of the loop body)."""
+    def vector_body(targets, indent, extra=()):
+        """Opens the element loop (lane-owned column chunks jj when structured, a strided
+        stream otherwise) and emits the statements for the V nodes `targets` need; returns
+        (name map, indent of the loop body)."""
         need = set()
         stack = list(targets)
         while stack:
@@ -398,48 +439,37 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             if kind != "in":
                 stack.extend([a] if kind == "u" else [a, b])
         names = dict(sname)
-        if reg:
-            # lane-owned column chunks jj (fixed per lane for every row of the group): the
-            # column accumulators stay in registers
+        if structured:
             w(f"{indent}#pragma unroll")
             w(f"{indent}for (int jj = 0; jj < {J}; ++jj) {{")
-        if vec == 1:
-            if reg:
-                w(f"{indent}  const sysml_i64 d = (sysml_i64)lane + (sysml_i64)jj * L;")
-                w(f"{indent}  if (d < D) {{")
-            else:
-                w(f"{indent}for (sysml_i64 d = lane; d < D; d += L) {{")
-            ind = indent + "  "
+            w(f"{indent}  const sysml_i64 d0 = ((sysml_i64)lane + (sysml_i64)jj * L) * {vec};")
+            w(f"{indent}  if (d0 < D) {{")
         else:
-            if reg:
-                w(f"{indent}  const sysml_i64 d0 = ((sysml_i64)lane + (sysml_i64)jj * L) * {vec};")
-                w(f"{indent}  if (d0 < D) {{")
-            else:
-                w(f"{indent}for (sysml_i64 d0 = (sysml_i64)lane * {vec}; d0 < D; d0 += (sysml_i64)L * {vec}) {{")
-            for k in sorted({j for j in need if j < n_in} | set(extra)):
-                base = "rowoff + d0" if modes[k] == FULL else "d0"
-                w(f"{indent}  T x{k}[{vec}]; sysml_ldv{vec}<T>(A.in[{k}], {dts[k]}, {base}, x{k});")
-                names[k] = f"x{k}[u]"
-            w(f"{indent}  #pragma unroll")
-            w(f"{indent}  for (int u = 0; u < {vec}; ++u) {{")
-            w(f"{indent}    const sysml_i64 d = d0 + u; (void)d;")
-            ind = indent + "    "
+            w(f"{indent}{{")
+            w(f"{indent}  for (sysml_i64 d0 = (sysml_i64)lane * {vec}; d0 < D; d0 += (sysml_i64)L * {vec}) {{")
+        for k in sorted({j for j in need if j < n_in} | set(extra)):
+            if k in cache and structured:
+                names[k] = f"xr{k}[jj][u]"
+                continue
+            base = "rowoff + d0" if modes[k] == FULL else "d0"
+            w(f"{indent}    T x{k}[{vec}]; sysml_ldv{vec}<T>(A.in[{k}], {dts[k]}, {base}, x{k});")
+            names[k] = f"x{k}[u]"
+        w(f"{indent}    #pragma unroll")
+        w(f"{indent}    for (int u = 0; u < {vec}; ++u) {{")
+        w(f"{indent}      const sysml_i64 d = d0 + u; (void)d;")
+        ind = indent + "      "
         for j in sorted(need):
             kind, o, a, b = nodes[j]
-            if kind == "in" and vec != 1:
+            if kind == "in":
                 continue
-            e = leaf_expr(j, True) if kind == "in" else op_expr(j, lambda x: names[x])
-            w(f"{ind}const T e{j} = {e};")
+            w(f"{ind}const T e{j} = {op_expr(j, lambda x: names[x])};")
             names[j] = f"e{j}"
-        for k in extra:
-            if vec == 1:
-                names[k] = leaf_expr(k, True)
         return names, ind
 
-    def close_loop(indent, reg=False):
-        w(f"{indent}}}" if vec == 1 else f"{indent}  }}\n{indent}}}")
-        if reg:
-            w(f"{indent}}}")
+    def close_loop(indent):
+        w(f"{indent}    }}")
+        w(f"{indent}  }}")
+        w(f"{indent}}}")
 
     nphase = max([final] + [p + 1 for p in red_phase.values()])
     for p in range(nphase + 1):
@@ -473,26 +503,22 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             elif ot == "all" and not vec_out:
                 w(f"    if (lane == 0) {{ {_acc_step(prog.oagg, 'tot', sname[prog.out])} }}")
             else:
-                regacc = colacc and J > 0
-                names, ind = vector_body([prog.out], "    ", reg=regacc)
+                names, ind = vector_body([prog.out], "    ")
                 v = names[prog.out]
-                ridx = "racc[jj][u]" if vec > 1 else "racc[jj][0]"
-                if regacc:
-                    val = f"{v}{(' * ' + v) if prog.oagg == 'sumsq' else ''}" if ot == "col" else \
-                        f"{v} * {sname[prog.extra]}"
-                    w(f"{ind}{ridx} += {val};")
+                cval = f"{v}{(' * ' + v) if prog.oagg == 'sumsq' else ''}" if ot == "col" else \
+                    (f"{v} * {sname[prog.extra]}" if ot == "tmv" else None)
+                if creg:
+                    w(f"{ind}racc[jj][u] += {cval};")
+                elif colacc:
+                    col_add(ind, cval)
                 elif ot == "vec":
                     w(f"{ind}static_cast<T*>(A.out)[rowoff + d] = {v};")
-                elif ot == "col":
-                    col_add(ind, f"{v}{(' * ' + v) if prog.oagg == 'sumsq' else ''}")
-                elif ot == "tmv":
-                    col_add(ind, f"{v} * {sname[prog.extra]}")
                 else:
                     w(ind + _acc_step(prog.oagg, "tot", v))
-                close_loop("    ", regacc)
+                close_loop("    ")
             break
     w("  }")
-    if colacc and J:
+    if creg:
         # merge the row groups' register accumulators in a fixed order (deterministic)
         w(f"  __shared__ T acc[1][{dcap}];")
         w(f"  for (int q = tid; q < {dcap}; q += 256) acc[0][q] = T(0);")
@@ -534,6 +560,10 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
 
 
 _ROW_PRELUDE = r"""
+template <typename T>
+__device__ __forceinline__ void sysml_ldv1(const void* p, int dt, sysml_i64 off, T (&o)[1]) {
+  o[0] = sysml_ld<T>(p, dt, off);
+}
 // vector loads of VEC adjacent elements (off a multiple of VEC, base 16-byte aligned)
 template <typename T>
 __device__ __forceinline__ void sysml_ldv4(const void* p, int dt, sysml_i64 off, T (&o)[4]) {
@@ -578,12 +608,12 @@ class _RowArgs(ctypes.Structure):
 _funcs = {}
 
 
-def _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, regs, dev):
-    key = (prog.key(), T, modes, dts, L, dcap, vec, slices, regs, str(dev))
+def _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, J, cache, dev):
+    key = (prog.key(), T, modes, dts, L, dcap, vec, slices, J, cache, str(dev))
     f = _funcs.get(key, False)
     if f is not False:
         return f
-    src = generate(prog, T, modes, dts, kinds, L, dcap, vec, slices, regs)
+    src = generate(prog, T, modes, dts, kinds, L, dcap, vec, slices, J, cache)
     code = compile_source(src, gpu_arch(dev))        # raises on a compile error: a generator bug
     fn = ctypes.c_void_p()
     cbuf = ctypes.create_string_buffer(code, len(code))
@@ -672,15 +702,12 @@ def _kernel(prog: RowProgram, args):
         L = lanes_for((D + vec - 1) // vec)
         G = 256 // L
     slices = G
-    regs = False
-    if ot in ("col", "tmv"):
-        sz = 4 if T == torch.float32 else 8
-        J = (dcap + L * vec - 1) // (L * vec)
-        regs = J * vec * sz <= 128 and dcap * sz <= LDS_BYTES     # <= 32 fp32 / 16 fp64 registers
+    J, cache = plan_registers(prog, modes, kinds, D, L, vec, T, dcap)
+    if ot in ("col", "tmv") and "acc" not in cache:
         slices = lds_slices(G, dcap, T)
         if slices == 0:
             return None
-    f = _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, regs, dev)
+    f = _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, J, cache, dev)
     ngrp = (N + G - 1) // G
     if ot in ("col", "tmv"):
         nblk = max(1, min(ngrp, 1024))
