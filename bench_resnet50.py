@@ -94,6 +94,7 @@ def main():
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--exact-fp32", action="store_true", help="convolutions on exact fp32 MFMA instead of bf16")
+    ap.add_argument("--no-fusion", action="store_true", help="disable operator fusion (codegen templates)")
     a = ap.parse_args()
     import torch
     from systemml_amd.api.executor import compile_script, execute
@@ -109,7 +110,7 @@ def main():
     n = a.batch * min(total, 2)
     X = rng.standard_normal((n, 3 * a.image * a.image)).astype(np.float32)
     Y = np.eye(1000, dtype=np.float32)[rng.integers(0, 1000, n)]
-    cfg = DMLConfig(precision="single", gpu_min_cells=0)
+    cfg = DMLConfig(precision="single", gpu_min_cells=0, fusion=not a.no_fusion)
     cs = compile_script(src, {"X": "X", "Y": "Y"}, inputs={"X": X, "Y": Y}, config=cfg,
                         filename=os.path.join(SCRIPTS_DIR, "resnet50_bench.dml"))
     out = []
@@ -128,6 +129,7 @@ def main():
                       "higher_is_better": True, "dtype": "fp32-exact" if a.exact_fp32 else "bf16 conv MFMA / fp32",
                       "data": "synthetic N(0,1) images, random labels, random-init weights",
                       "losses": [round(l, 4) for _, l, _ in steps], "wall_s": round(wall, 1),
+                      "step_ms": [round(ns / 1e6, 1) for _, _, ns in steps],
                       "kernel_counters": {k: v for k, v in K.counters.items() if k.startswith(("conv", "pool", "bias"))},
                       "config": {"model": "ResNet-50", "batch": a.batch, "image": a.image, "classes": 1000}}))
 

@@ -372,6 +372,11 @@ def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXI
                 leaf(c)
     if len(leaves) > RMAXIN or len(body) > RMAXOPS:
         return 0
+    # a few very long rows (e.g. N x (C*H*W) activations of a small batch): one row per lane
+    # group leaves the chip idle -- the unfused operators parallelise within rows instead
+    for x in leaves:
+        if x.dt == "M" and 0 < x.dim1 < 512 and x.dim2 > 1 and x.dim1 * x.dim2 >= (1 << 20):
+            return 0
     nin = len(leaves)
     idx = {}
     ops = []

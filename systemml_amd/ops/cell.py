@@ -351,15 +351,40 @@ def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev):
     return f
 
 
-def _kernel(prog: CellProgram, args):
-    """One launch of the cell kernel, or None when the operands are outside its scope."""
+_S = "s"
+_plans = {}
+
+
+def _signature(args):
+    """Hashable operand signature (shapes, dtypes, devices, layout, alignment) or None."""
+    from ..runtime.scalars import DevScalar
+    sig = []
+    for x in args:
+        tx = type(x)
+        if tx is _Tensor:
+            sig.append((x.shape, x.dtype, x.device, x.layout, x.is_contiguous(), x.data_ptr() & 15))
+        elif tx is DevScalar:
+            sig.append(("d", x.t.dtype, x.t.device))
+        elif tx is float or tx is int or tx is bool:
+            sig.append(_S)
+        else:
+            return None
+    return tuple(sig)
+
+
+class _Plan:
+    """Everything a launch of one program on one operand signature needs but the pointers."""
+    __slots__ = ("prog", "fn", "interp", "mode", "nblk", "gx", "gy", "R", "Cc", "T", "out_shape", "part_shape",
+                 "kinds", "P", "dev", "dev_index")
+
+
+def _make_plan(prog, args):
     from ..runtime.scalars import DevScalar
     if len(args) != prog.n_in or len(prog.ops) > MAXOPS or prog.n_in > MAXIN:
         return None
     dev = None
     shapes = []
-    f64 = False
-    bf16 = False
+    f64 = bf16 = False
     for x in args:
         tx = type(x)
         if tx is _Tensor:
@@ -376,10 +401,8 @@ def _kernel(prog: CellProgram, args):
             if not x.t.is_cuda or x.t.dtype not in _DT:
                 return None
             shapes.append(None)
-        elif tx is float or tx is int or tx is bool:
-            shapes.append(None)
         else:
-            return None
+            shapes.append(None)
     if dev is None:
         return None
     shp = out_shape(prog, shapes)
@@ -390,21 +413,17 @@ def _kernel(prog: CellProgram, args):
         return None
     T = torch.float64 if (f64 or (bf16 and backend.dtype == torch.float64)) else torch.float32
     P = _Prog()
-    keep = []
+    kinds = []
     need_ij = 0
     for k, x in enumerate(args):
         e = P.inp[k]
         tx = type(x)
         if tx is _Tensor:
-            if not x.is_contiguous():
-                x = x.contiguous()
-            keep.append(x)
             r, c = x.shape
-            e.p = x.data_ptr()
             e.dtype = _DT[x.dtype]
             if (r, c) == (R, Cc):
                 e.mode = FULL
-                e.vec = int(e.p % 16 == 0)
+                e.vec = int(x.is_contiguous() and x.data_ptr() % 16 == 0)
             elif r == 1 and c == 1:
                 e.mode = DSCALAR
             elif r == 1 and c == Cc:
@@ -415,15 +434,14 @@ def _kernel(prog: CellProgram, args):
                 need_ij = 1
             else:
                 return None
+            kinds.append("t")
         elif tx is DevScalar:
-            t = x.t.reshape(1)
-            keep.append(t)
-            e.p = t.data_ptr()
-            e.dtype = _DT[t.dtype]
+            e.dtype = _DT[x.t.dtype]
             e.mode = DSCALAR
+            kinds.append("d")
         else:
             e.mode = HSCALAR
-            e.s = float(x)
+            kinds.append("s")
     P.rows, P.cols, P.total = R, Cc, R * Cc
     P.n_in, P.n_ops, P.out = prog.n_in, len(prog.ops), prog.out
     P.need_ij = need_ij
@@ -434,18 +452,13 @@ def _kernel(prog: CellProgram, args):
         mode = AGG_DIRS[agg[1]]
     L = _lib()
     nblk = L.sysml_cell_blocks(mode, R, Cc)
-    st = torch.cuda.current_stream(dev).cuda_stream
-    dt = 0 if T == torch.float32 else 1
-    out = part = None
-    if mode == 0:
-        out = torch.empty((R, Cc), dtype=T, device=dev)
-    elif mode == 1:
-        part = torch.empty(nblk, dtype=torch.float64, device=dev)
-    elif mode == 2:
-        out = torch.empty((R, 1), dtype=T, device=dev)
-    else:
-        part = torch.empty((nblk, Cc), dtype=torch.float64, device=dev)
-    launched = False
+    pl = _Plan()
+    pl.prog, pl.mode, pl.nblk, pl.R, pl.Cc, pl.T, pl.kinds, pl.P, pl.dev = prog, mode, nblk, R, Cc, T, kinds, P, dev
+    pl.dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+    pl.out_shape = (R, Cc) if mode == 0 else ((R, 1) if mode == 2 else None)
+    pl.part_shape = (nblk,) if mode == 1 else ((nblk, Cc) if mode == 3 else None)
+    pl.fn = None
+    pl.gx, pl.gy = nblk, 1
     if RTC:
         modes = tuple(P.inp[k].mode for k in range(prog.n_in))
         dts = tuple(P.inp[k].dtype for k in range(prog.n_in))
@@ -458,24 +471,77 @@ def _kernel(prog: CellProgram, args):
             variant = 0
         f = _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev)
         if f is not None:
-            A = _RtcArgs()
-            for k in range(prog.n_in):
-                A.inp[k] = P.inp[k].p
-                A.s[k] = P.inp[k].s
-            A.rows, A.cols, A.total = R, Cc, R * Cc
-            A.chunk = (R + nblk - 1) // nblk
-            A.out = out.data_ptr() if out is not None else 0
-            A.part = part.data_ptr() if part is not None else 0
-            gx, gy = (nblk, 1) if mode != 3 else ((Cc + variant - 1) // variant, nblk)
-            rc = _rtc_lib().sysml_rtc_launch(f[0], gx, gy, 256, ctypes.byref(A), ctypes.sizeof(A), st)
-            if rc != 0:
-                raise RuntimeError(f"fused cell kernel launch failed: {rc}")
-            stats["rtc_launches"] += 1
-            launched = True
-    if not launched:
+            pl.fn = f[0]
+            if mode == 3:
+                pl.gx, pl.gy = (Cc + variant - 1) // variant, nblk
+    pl.interp = pl.fn is None
+    return pl
+
+
+_raw_stream = torch._C._cuda_getCurrentRawStream if hasattr(torch._C, "_cuda_getCurrentRawStream") else None
+
+
+def _kernel(prog: CellProgram, args):
+    """One launch of the cell kernel, or None when the operands are outside its scope.  The
+    launch plan (generated kernel, grid, modes) is cached per program and operand signature,
+    so a repeated call only fills the pointers and launches."""
+    sig = _signature(args)
+    if sig is None:
+        return None
+    key = (id(prog), sig, RTC)
+    pl = _plans.get(key, False)
+    if pl is False or (pl is not None and pl.prog is not prog):
+        pl = _make_plan(prog, args)
+        _plans[key] = pl
+    if pl is None:
+        return None
+    dev, T, mode = pl.dev, pl.T, pl.mode
+    out = torch.empty(pl.out_shape, dtype=T, device=dev) if pl.out_shape is not None else None
+    part = torch.empty(pl.part_shape, dtype=torch.float64, device=dev) if pl.part_shape is not None else None
+    st = _raw_stream(pl.dev_index) if _raw_stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    keep = []
+    if not pl.interp:
+        A = _RtcArgs()
+        for k, (x, kd) in enumerate(zip(args, pl.kinds)):
+            if kd == "t":
+                if not x.is_contiguous():
+                    x = x.contiguous()
+                    keep.append(x)
+                A.inp[k] = x.data_ptr()
+            elif kd == "d":
+                t = x.t.reshape(1)
+                keep.append(t)
+                A.inp[k] = t.data_ptr()
+            else:
+                A.s[k] = float(x)
+        A.rows, A.cols, A.total = pl.R, pl.Cc, pl.R * pl.Cc
+        A.chunk = (pl.R + pl.nblk - 1) // pl.nblk
+        A.out = out.data_ptr() if out is not None else 0
+        A.part = part.data_ptr() if part is not None else 0
+        rc = _rtc_lib().sysml_rtc_launch(pl.fn, pl.gx, pl.gy, 256, ctypes.byref(A), ctypes.sizeof(A), st)
+        if rc != 0:
+            raise RuntimeError(f"fused cell kernel launch failed: {rc}")
+        stats["rtc_launches"] += 1
+    else:
+        P = _Prog()
+        ctypes.memmove(ctypes.byref(P), ctypes.byref(pl.P), ctypes.sizeof(P))
+        for k, (x, kd) in enumerate(zip(args, pl.kinds)):
+            e = P.inp[k]
+            if kd == "t":
+                if not x.is_contiguous():
+                    x = x.contiguous()
+                keep.append(x)
+                e.p = x.data_ptr()
+            elif kd == "d":
+                t = x.t.reshape(1)
+                keep.append(t)
+                e.p = t.data_ptr()
+            else:
+                e.s = float(x)
         code = prog.device_code(dev)
-        rc = L.sysml_cell(dt, mode, ctypes.byref(P), code.data_ptr(), out.data_ptr() if out is not None else 0,
-                          part.data_ptr() if part is not None else 0, nblk, st)
+        dt = 0 if T == torch.float32 else 1
+        rc = _lib().sysml_cell(dt, mode, ctypes.byref(P), code.data_ptr(), out.data_ptr() if out is not None else 0,
+                               part.data_ptr() if part is not None else 0, pl.nblk, st)
         if rc != 0:
             raise RuntimeError(f"sysml_cell failed: {rc}")
         stats["interpreter_launches"] += 1
@@ -484,7 +550,9 @@ def _kernel(prog: CellProgram, args):
     del keep
     if mode == 0:
         return out
+    agg = prog.agg
     o = agg[0]
+    R, Cc = pl.R, pl.Cc
     if mode == 1:
         r = part.sum() if AGG_CODES[o] <= 1 else (part.min() if o == "min" else part.max())
         if o == "mean":

@@ -626,8 +626,14 @@ def _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, J, cache, dev):
     return f
 
 
-def _kernel(prog: RowProgram, args):
-    """One launch of the generated row kernel, or None when the operands are outside its scope."""
+class _Plan:
+    __slots__ = ("prog", "fn", "kinds", "N", "D", "T", "nblk", "ot", "vec_out", "dev", "dev_index")
+
+
+MIN_LANES = 32768          # fewer lanes in flight than this on a large input: torch's reductions win
+
+
+def _make_plan(prog: RowProgram, args):
     from ..runtime.scalars import DevScalar
     if len(args) != prog.n_in or prog.n_in > MAXIN or len(prog.ops) > MAXOPS:
         return None
@@ -650,10 +656,8 @@ def _kernel(prog: RowProgram, args):
             if not x.t.is_cuda or x.t.dtype not in _DT:
                 return None
             shapes.append(None)
-        elif tx is float or tx is int or tx is bool:
-            shapes.append(None)
         else:
-            return None
+            shapes.append(None)
     if dev is None:
         return None
     cl = classify(prog, shapes)
@@ -663,44 +667,38 @@ def _kernel(prog: RowProgram, args):
     # DevScalar inputs are device-resident 1 x 1 values
     modes = tuple(DSCALAR if type(x) is DevScalar else m for x, m in zip(args, modes))
     T = torch.float64 if (f64 or (bf16 and backend.dtype == torch.float64)) else torch.float32
-    L = lanes_for(D)
-    G = 256 // L
     ot = prog.otype
     dcap = 0
     if ot in ("col", "tmv"):
         dcap = dcap_for(D)
         if dcap is None:
             return None
-    A = _RowArgs()
-    keep = []
-    dts = []
+    dts, akinds, aligned = [], [], True
     for k, x in enumerate(args):
         tx = type(x)
         if tx is _Tensor:
-            if not x.is_contiguous():
-                x = x.contiguous()
-            keep.append(x)
-            A.inp[k] = x.data_ptr()
             dts.append(_DT[x.dtype])
+            akinds.append("t")
+            if modes[k] in (FULL, ROWV, SIDE) and not (x.is_contiguous() and x.data_ptr() % 16 == 0):
+                aligned = False
         elif tx is DevScalar:
-            t = x.t.reshape(1)
-            keep.append(t)
-            A.inp[k] = t.data_ptr()
-            dts.append(_DT[t.dtype])
+            dts.append(_DT[x.t.dtype])
+            akinds.append("d")
         else:
-            A.s[k] = float(x)
             dts.append(0)
+            akinds.append("s")
     dts = tuple(dts)
     vec = 1
     vleaves = [k for k, m in enumerate(modes) if m in (FULL, ROWV, SIDE)]
-    if all(A.inp[k] % 16 == 0 for k in vleaves):
+    if aligned:
         if D % 8 == 0 and all(dts[k] == 2 for k in vleaves):
             vec = 8
         elif D % 4 == 0:
             vec = 4
-    if vec > 1:
-        L = lanes_for((D + vec - 1) // vec)
-        G = 256 // L
+    L = lanes_for((D + vec - 1) // vec)
+    G = 256 // L
+    if N * L < MIN_LANES and N * D >= (1 << 20):
+        return None                     # a few very long rows: too little parallelism per row
     slices = G
     J, cache = plan_registers(prog, modes, kinds, D, L, vec, T, dcap)
     if ot in ("col", "tmv") and "acc" not in cache:
@@ -709,16 +707,49 @@ def _kernel(prog: RowProgram, args):
             return None
     f = _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, J, cache, dev)
     ngrp = (N + G - 1) // G
-    if ot in ("col", "tmv"):
-        nblk = max(1, min(ngrp, 1024))
-    elif ot == "all":
-        nblk = max(1, min(ngrp, 2048))
-    else:
-        nblk = max(1, min(ngrp, 16384))
+    pl = _Plan()
+    pl.prog, pl.fn, pl.kinds, pl.N, pl.D, pl.T, pl.ot, pl.dev = prog, f[0], akinds, N, D, T, ot, dev
+    pl.dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+    pl.nblk = max(1, min(ngrp, 1024 if ot in ("col", "tmv") else (2048 if ot == "all" else 16384)))
+    pl.vec_out = kinds[prog.out] == "V"
+    return pl
+
+
+_plans = {}
+
+
+def _kernel(prog: RowProgram, args):
+    """One launch of the generated row kernel, or None when the operands are outside its scope
+    (launch plans cached per program and operand signature)."""
+    from .cell import _signature, _raw_stream
+    sig = _signature(args)
+    if sig is None:
+        return None
+    key = (id(prog), sig)
+    pl = _plans.get(key, False)
+    if pl is False or (pl is not None and pl.prog is not prog):
+        pl = _make_plan(prog, args)
+        _plans[key] = pl
+    if pl is None:
+        return None
+    N, D, T, ot, dev, nblk = pl.N, pl.D, pl.T, pl.ot, pl.dev, pl.nblk
+    A = _RowArgs()
+    keep = []
+    for k, (x, kd) in enumerate(zip(args, pl.kinds)):
+        if kd == "t":
+            if not x.is_contiguous():
+                x = x.contiguous()
+                keep.append(x)
+            A.inp[k] = x.data_ptr()
+        elif kd == "d":
+            t = x.t.reshape(1)
+            keep.append(t)
+            A.inp[k] = t.data_ptr()
+        else:
+            A.s[k] = float(x)
     out = part = None
-    vec_out = kinds[prog.out] == "V"
     if ot in ("row", "vec"):
-        out = torch.empty((N, D) if vec_out else (N, 1), dtype=T, device=dev)
+        out = torch.empty((N, D) if pl.vec_out else (N, 1), dtype=T, device=dev)
     elif ot in ("col", "tmv"):
         part = torch.empty((nblk, D), dtype=torch.float64, device=dev)
     else:
@@ -726,8 +757,8 @@ def _kernel(prog: RowProgram, args):
     A.rows, A.cols = N, D
     A.out = out.data_ptr() if out is not None else 0
     A.part = part.data_ptr() if part is not None else 0
-    st = torch.cuda.current_stream(dev).cuda_stream
-    rc = _rtc_lib().sysml_rtc_launch(f[0], nblk, 1, 256, ctypes.byref(A), ctypes.sizeof(A), st)
+    st = _raw_stream(pl.dev_index) if _raw_stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    rc = _rtc_lib().sysml_rtc_launch(pl.fn, nblk, 1, 256, ctypes.byref(A), ctypes.sizeof(A), st)
     if rc != 0:
         raise RuntimeError(f"generated row kernel launch failed: {rc}")
     from . import kernels
@@ -743,5 +774,5 @@ def _kernel(prog: RowProgram, args):
     o = prog.oagg
     r = part.sum() if o in ("sum", "sumsq", "mean") else (part.min() if o == "min" else part.max())
     if o == "mean":
-        r = r / (N * (D if vec_out else 1))
+        r = r / (N * (D if pl.vec_out else 1))
     return C._lazy_out(r)
