@@ -594,8 +594,20 @@ def recompile_exec_types(bb, vars_, config):
     if getattr(bb, "_et_sig", None) == sig:
         return False
     bb._et_sig = sig
+    # a function body is entered with a different shape signature per call site (every layer
+    # of a network): the annotations of each signature are kept and re-applied
+    cache = getattr(bb, "_et_cache", None)
+    if cache is None:
+        cache = bb._et_cache = {}
+    saved = cache.get(sig)
+    if saved is not None:
+        for h, d1, d2, et, ph in saved:
+            h.dim1, h.dim2, h.exec_type, h.phys = d1, d2, et, ph
+        return True
     tops = list(bb.roots) + list(bb.env_out.values())
     annotate_dag(tops, dict(zip(names, sig)), config)
+    if len(cache) < 256:
+        cache[sig] = [(h, h.dim1, h.dim2, h.exec_type, h.phys) for h in H.walk(tops)]
     return True
 
 
