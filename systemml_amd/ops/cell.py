@@ -355,9 +355,15 @@ _S = "s"
 _plans = {}
 
 
+_DevScalar = []
+
+
 def _signature(args):
     """Hashable operand signature (shapes, dtypes, devices, layout, alignment) or None."""
-    from ..runtime.scalars import DevScalar
+    if not _DevScalar:
+        from ..runtime.scalars import DevScalar as _D
+        _DevScalar.append(_D)
+    DevScalar = _DevScalar[0]
     sig = []
     for x in args:
         tx = type(x)
@@ -375,7 +381,7 @@ def _signature(args):
 class _Plan:
     """Everything a launch of one program on one operand signature needs but the pointers."""
     __slots__ = ("prog", "fn", "interp", "mode", "nblk", "gx", "gy", "R", "Cc", "T", "out_shape", "part_shape",
-                 "kinds", "P", "dev", "dev_index")
+                 "kinds", "P", "dev", "dev_index", "launch", "count")
 
 
 def _make_plan(prog, args):
@@ -475,6 +481,9 @@ def _make_plan(prog, args):
             if mode == 3:
                 pl.gx, pl.gy = (Cc + variant - 1) // variant, nblk
     pl.interp = pl.fn is None
+    pl.launch = _rtc_lib().sysml_rtc_launch
+    from . import kernels
+    pl.count = kernels._count
     return pl
 
 
@@ -518,7 +527,7 @@ def _kernel(prog: CellProgram, args):
         A.chunk = (pl.R + pl.nblk - 1) // pl.nblk
         A.out = out.data_ptr() if out is not None else 0
         A.part = part.data_ptr() if part is not None else 0
-        rc = _rtc_lib().sysml_rtc_launch(pl.fn, pl.gx, pl.gy, 256, ctypes.byref(A), ctypes.sizeof(A), st)
+        rc = pl.launch(pl.fn, pl.gx, pl.gy, 256, ctypes.byref(A), ctypes.sizeof(A), st)
         if rc != 0:
             raise RuntimeError(f"fused cell kernel launch failed: {rc}")
         stats["rtc_launches"] += 1
@@ -545,8 +554,7 @@ def _kernel(prog: CellProgram, args):
         if rc != 0:
             raise RuntimeError(f"sysml_cell failed: {rc}")
         stats["interpreter_launches"] += 1
-    from . import kernels
-    kernels._count("cell")
+    pl.count("cell")
     del keep
     if mode == 0:
         return out

@@ -36,7 +36,8 @@ import torch
 
 from . import core as C
 from .backend import backend
-from .cell import (_C_BIN, _C_UN, _DT, _Tensor, _prelude, _rtc_lib, compile_source, gpu_arch)
+from .cell import (_C_BIN, _C_UN, _DT, _Tensor, _prelude, _raw_stream, _rtc_lib, _signature, compile_source,
+                   gpu_arch)
 
 ROW_AGGS = ("sum", "sumsq", "mean", "min", "max")
 COL_AGGS = ("sum", "sumsq", "mean")
@@ -627,7 +628,8 @@ def _func(prog, T, modes, dts, kinds, L, dcap, vec, slices, J, cache, dev):
 
 
 class _Plan:
-    __slots__ = ("prog", "fn", "kinds", "N", "D", "T", "nblk", "ot", "vec_out", "dev", "dev_index")
+    __slots__ = ("prog", "fn", "kinds", "N", "D", "T", "nblk", "ot", "vec_out", "dev", "dev_index", "launch",
+                 "count")
 
 
 MIN_LANES = 32768          # fewer lanes in flight than this on a large input: torch's reductions win
@@ -712,6 +714,9 @@ def _make_plan(prog: RowProgram, args):
     pl.dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
     pl.nblk = max(1, min(ngrp, 1024 if ot in ("col", "tmv") else (2048 if ot == "all" else 16384)))
     pl.vec_out = kinds[prog.out] == "V"
+    pl.launch = _rtc_lib().sysml_rtc_launch
+    from . import kernels
+    pl.count = kernels._count
     return pl
 
 
@@ -721,7 +726,6 @@ _plans = {}
 def _kernel(prog: RowProgram, args):
     """One launch of the generated row kernel, or None when the operands are outside its scope
     (launch plans cached per program and operand signature)."""
-    from .cell import _signature, _raw_stream
     sig = _signature(args)
     if sig is None:
         return None
@@ -758,11 +762,10 @@ def _kernel(prog: RowProgram, args):
     A.out = out.data_ptr() if out is not None else 0
     A.part = part.data_ptr() if part is not None else 0
     st = _raw_stream(pl.dev_index) if _raw_stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    rc = _rtc_lib().sysml_rtc_launch(pl.fn, nblk, 1, 256, ctypes.byref(A), ctypes.sizeof(A), st)
+    rc = pl.launch(pl.fn, nblk, 1, 256, ctypes.byref(A), ctypes.sizeof(A), st)
     if rc != 0:
         raise RuntimeError(f"generated row kernel launch failed: {rc}")
-    from . import kernels
-    kernels._count("row")
+    pl.count("row")
     del keep
     if out is not None:
         return out
