@@ -361,11 +361,14 @@ def ones(shape):
 
 
 def seq(start=None, stop=None, step=1):
+    """Column vector start, start + step, ..., stop -- stop INCLUDED, as DML's seq and the
+    reference's python/systemml/defmatrix.py seq (seq(3) is 0, 1, 2, 3)."""
+    if start is None and stop is None:
+        raise ValueError("Both start and stop cannot be None")
     if start is not None and stop is None:
         start, stop = 0, start
     start = 0 if start is None else start
-    # numpy-style exclusive stop -> DML inclusive sequence
-    return matrix._op(f"seq({start!r}, {stop - step!r}, {step!r})")
+    return matrix._op(f"seq({start!r}, {stop!r}, {step!r})")
 
 
 def rand(rows, cols, min=0.0, max=1.0, pdf="uniform", sparsity=1.0, seed=-1):

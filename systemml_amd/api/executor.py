@@ -113,6 +113,10 @@ def convert_input(v, dist=None, config=None):
             return SP.from_ijv(coo.row, coo.col, coo.data, coo.shape[0], coo.shape[1], backend.dtype,
                                backend.device)
         v = v.toarray()
+    if isinstance(v, (list, tuple)) and v and all(isinstance(x, str) for x in v):
+        # lines of CSV text: the no-Spark form of the reference's RDD<String> matrix input
+        # (MLContextConversionUtil.javaRDDStringCSVToMatrixObject)
+        v = np.asarray([[float(t) for t in ln.split(",")] for ln in v if ln.strip()], dtype=np.float64)
     if isinstance(v, (list, tuple)):
         v = np.asarray(v, dtype=np.float64)
     if isinstance(v, np.ndarray):

@@ -46,15 +46,20 @@ class Matrix:
         return self._tensor()
 
     def toDF(self):
+        """pandas DataFrame in the reference's layout: an __INDEX column (1-based row ids) then
+        C1..Cn (reference MLContextConversionUtil.matrixObjectToDataFrame)."""
         import pandas as pd
-        return pd.DataFrame(self.toNumPy(), columns=[f"C{i + 1}" for i in range(self.shape[1])])
+        a = self.toNumPy()
+        df = pd.DataFrame(a, columns=[f"C{i + 1}" for i in range(a.shape[1])])
+        df.insert(0, "__INDEX", np.arange(1, a.shape[0] + 1, dtype=np.float64))
+        return df
 
     @property
     def shape(self):
         return tuple(self._v.shape)
 
     def __repr__(self):
-        return f"Matrix{self.shape}"
+        return "Matrix"          # reference python/systemml/mlcontext.py Matrix.__repr__
 
 
 class Frame:
@@ -90,8 +95,9 @@ class MLResults:
         self.stats = stats
 
     def get(self, *names):
+        """One value, or a list of values for several names (reference MLResults.get)."""
         out = [_wrap(self._values[n]) for n in names]
-        return out[0] if len(out) == 1 else tuple(out)
+        return out[0] if len(out) == 1 else out
 
     def getNumPyArray(self, name):
         return self.get(name).toNumPy()

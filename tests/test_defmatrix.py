@@ -31,7 +31,7 @@ def test_solve_seq_full_and_setitem():
     b = rng.random((4, 1))
     x = sml.solve(sml.matrix(A), sml.matrix(b))
     np.testing.assert_allclose(x.toNumPy(), np.linalg.solve(A, b))
-    np.testing.assert_allclose(sml.seq(5).toNumPy().ravel(), np.arange(5))
+    np.testing.assert_allclose(sml.seq(5).toNumPy().ravel(), np.arange(6))      # stop included (reference)
     z = sml.full((2, 3), 7)
     z[0, 1] = 0
     np.testing.assert_allclose(z.toNumPy(), [[7, 0, 7], [7, 7, 7]])
