@@ -16,7 +16,7 @@ def main():
                 k = row.get("Kernel_Name") or row.get("Kernel-Name") or row.get("KernelName")
                 acc[k[:120]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     for k, cs in sorted(acc.items()):
-        if "sysml" not in k:
+        if "sysml" not in k and "row_k" not in k:
             continue
         print(k)
         for c, v in sorted(cs.items()):
