@@ -239,12 +239,13 @@ def out_shape(prog: RowProgram, shapes):
 REG_BUDGET = 96            # cached fp32 values per lane (fp64 count twice)
 
 
-def plan_registers(prog, modes, kinds, D, L, vec, T, dcap):
+def plan_registers(prog, modes, kinds, D, L, vec, T, dcap, dts=None):
     """(J, cache): J lane-owned column chunks of VEC elements cover a row (0: the row is too
     wide -- strided streaming loops instead); cache holds the input indices kept in registers
     ('acc' for the column accumulators), chosen greedily within REG_BUDGET: the column
     accumulators, then the N x D inputs (each row read from HBM once for every phase), then
     the row-invariant 1 x D / side vectors."""
+    dts = dts or tuple(0 for _ in modes)
     J = (D + L * vec - 1) // (L * vec)
     if J * vec > 64:
         return 0, frozenset()
@@ -261,11 +262,19 @@ def plan_registers(prog, modes, kinds, D, L, vec, T, dcap):
                 vecuse.add(x)
     if prog.out < prog.n_in and modes[prog.out] in (FULL, ROWV, SIDE):
         vecuse.add(prog.out)
-    for group in ((FULL,), (ROWV, SIDE)):
-        for k in sorted(vecuse):
-            if modes[k] in group and used + per <= REG_BUDGET:
-                cache.append(k)
-                used += per
+    full = [k for k in sorted(vecuse) if modes[k] == FULL]
+    pipe = bool(full) and used + 2 * per * len(full) <= REG_BUDGET and \
+        all(vec in (1, 4) or dts[k] == 2 for k in full)
+    for k in full:
+        if used + per * (2 if pipe else 1) <= REG_BUDGET:
+            cache.append(k)
+            used += per * (2 if pipe else 1)
+    if pipe and all(k in cache for k in full):
+        cache.append("pipe")
+    for k in sorted(vecuse):
+        if modes[k] in (ROWV, SIDE) and used + per <= REG_BUDGET:
+            cache.append(k)
+            used += per
     return J, frozenset(cache)
 
 
@@ -385,14 +394,32 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
         else:
             w(f"{ind}atomicAdd(&acc[0][d], {val});")
 
-    def load_cached(k, base, indent):
-        w(f"{indent}T xr{k}[{J}][{vec}];")
+    def load_cached(k, base, indent, name=None, declare=True, cond="d0 < D"):
+        name = name or f"xr{k}"
+        if declare:
+            w(f"{indent}T {name}[{J}][{vec}];")
         w(f"{indent}#pragma unroll")
         w(f"{indent}for (int jj = 0; jj < {J}; ++jj) {{")
         w(f"{indent}  const sysml_i64 d0 = ((sysml_i64)lane + (sysml_i64)jj * L) * {vec};")
-        w(f"{indent}  if (d0 < D) sysml_ldv{vec}<T>(A.in[{k}], {dts[k]}, {base}, xr{k}[jj]);")
+        w(f"{indent}  if ({cond}) sysml_ldv{vec}<T>(A.in[{k}], {dts[k]}, {base}, {name}[jj]);")
         w(f"{indent}}}")
 
+    # software pipelining of the cached row: the next row of the group is loaded (xn) while the
+    # current one (xr) is reduced, so every lane keeps its loads in flight across the phases
+    piped = [k for k in range(n_in) if modes[k] == FULL and k in cache and "pipe" in cache]
+
+    w("  const sysml_i64 first = (sysml_i64)blockIdx.x * G + grp;")
+    w("  (void)first;")
+    def load_raw(k, rowexpr, indent, declare):
+        if declare:
+            w(f"{indent}SysmlRaw<{dts[k]}, {vec}> rn{k}[{J}];")
+        w(f"{indent}#pragma unroll")
+        w(f"{indent}for (int jj = 0; jj < {J}; ++jj) {{")
+        w(f"{indent}  const sysml_i64 d0 = ((sysml_i64)lane + (sysml_i64)jj * L) * {vec};")
+        w(f"{indent}  if ({rowexpr} < N && d0 < D) rn{k}[jj].load(A.in[{k}], {rowexpr} * D + d0);")
+        w(f"{indent}}}")
+    for k in piped:
+        load_raw(k, "first", "  ", True)
     # row-invariant vectors (1 x D inputs, side vectors of products) cached once per kernel
     for k in range(n_in):
         if modes[k] in (ROWV, SIDE) and k in cache:
@@ -402,6 +429,13 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
     w("  for (sysml_i64 row = (sysml_i64)blockIdx.x * G + grp; row < N; row += (sysml_i64)gridDim.x * G) {")
     w("    const sysml_i64 rowoff = row * D;")
     w("    (void)rowoff;")
+    if piped:
+        w("    const sysml_i64 nxt = row + (sysml_i64)gridDim.x * G;")
+        for k in piped:
+            w(f"    T xr{k}[{J}][{vec}];")
+            w("    #pragma unroll")
+            w(f"    for (int jj = 0; jj < {J}; ++jj) rn{k}[jj].template get<T>(xr{k}[jj]);")
+            load_raw(k, "nxt", "    ", False)
     sname = dict(cname)
     for k in range(n_in):
         if kinds[k] == "S":
@@ -409,7 +443,7 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
             sname[k] = f"s{k}"
     # the row itself: every N x D input read ONCE from HBM into registers, reused by all phases
     for k in range(n_in):
-        if modes[k] == FULL and k in cache:
+        if modes[k] == FULL and k in cache and k not in piped:
             load_cached(k, "rowoff + d0", "    ")
 
     def sref(j):
@@ -598,6 +632,67 @@ __device__ __forceinline__ void sysml_ldv8(const void* p, int dt, sysml_i64 off,
 }
 """
 
+_ROW_PRELUDE += r"""
+// raw (unconverted) vector chunks: the next row's loads stay in flight in these registers and
+// are converted only when the row is reached (a conversion right after the load would wait)
+template <int DT, int V> struct SysmlRaw;
+template <> struct SysmlRaw<2, 8> {
+  uint4 q;
+  __device__ __forceinline__ void load(const void* p, sysml_i64 off) {
+    q = *reinterpret_cast<const uint4*>(static_cast<const unsigned short*>(p) + off);
+  }
+  template <typename T> __device__ __forceinline__ void get(T (&o)[8]) const {
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[2 * i] = (T)sysml_bf2f(w[i] & 0xffff); o[2 * i + 1] = (T)sysml_bf2f(w[i] >> 16); }
+  }
+};
+template <> struct SysmlRaw<2, 4> {
+  uint2 q;
+  __device__ __forceinline__ void load(const void* p, sysml_i64 off) {
+    q = *reinterpret_cast<const uint2*>(static_cast<const unsigned short*>(p) + off);
+  }
+  template <typename T> __device__ __forceinline__ void get(T (&o)[4]) const {
+    o[0] = (T)sysml_bf2f(q.x & 0xffff); o[1] = (T)sysml_bf2f(q.x >> 16);
+    o[2] = (T)sysml_bf2f(q.y & 0xffff); o[3] = (T)sysml_bf2f(q.y >> 16);
+  }
+};
+template <> struct SysmlRaw<2, 1> {
+  unsigned short q;
+  __device__ __forceinline__ void load(const void* p, sysml_i64 off) { q = static_cast<const unsigned short*>(p)[off]; }
+  template <typename T> __device__ __forceinline__ void get(T (&o)[1]) const { o[0] = (T)sysml_bf2f(q); }
+};
+template <> struct SysmlRaw<0, 4> {
+  float4 q;
+  __device__ __forceinline__ void load(const void* p, sysml_i64 off) {
+    q = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + off);
+  }
+  template <typename T> __device__ __forceinline__ void get(T (&o)[4]) const {
+    o[0] = (T)q.x; o[1] = (T)q.y; o[2] = (T)q.z; o[3] = (T)q.w;
+  }
+};
+template <> struct SysmlRaw<0, 1> {
+  float q;
+  __device__ __forceinline__ void load(const void* p, sysml_i64 off) { q = static_cast<const float*>(p)[off]; }
+  template <typename T> __device__ __forceinline__ void get(T (&o)[1]) const { o[0] = (T)q; }
+};
+template <> struct SysmlRaw<1, 4> {
+  double2 a, b;
+  __device__ __forceinline__ void load(const void* p, sysml_i64 off) {
+    a = *reinterpret_cast<const double2*>(static_cast<const double*>(p) + off);
+    b = *reinterpret_cast<const double2*>(static_cast<const double*>(p) + off + 2);
+  }
+  template <typename T> __device__ __forceinline__ void get(T (&o)[4]) const {
+    o[0] = (T)a.x; o[1] = (T)a.y; o[2] = (T)b.x; o[3] = (T)b.y;
+  }
+};
+template <> struct SysmlRaw<1, 1> {
+  double q;
+  __device__ __forceinline__ void load(const void* p, sysml_i64 off) { q = static_cast<const double*>(p)[off]; }
+  template <typename T> __device__ __forceinline__ void get(T (&o)[1]) const { o[0] = (T)q; }
+};
+"""
+
 _AGGC = {"sum": 0, "mean": 0, "sumsq": 0, "min": 2, "max": 3}   # partials of sumsq are already squared
 
 
@@ -693,8 +788,9 @@ def _make_plan(prog: RowProgram, args):
     vec = 1
     vleaves = [k for k, m in enumerate(modes) if m in (FULL, ROWV, SIDE)]
     if aligned:
-        if D % 8 == 0 and all(dts[k] == 2 for k in vleaves):
-            vec = 8
+        if D % 8 == 0 and any(dts[k] == 2 and modes[k] == FULL for k in vleaves) and \
+                all(dts[k] == 2 for k in vleaves if modes[k] == FULL):
+            vec = 8          # bf16 rows: 16-byte loads (other vectors as two 16-byte loads)
         elif D % 4 == 0:
             vec = 4
     L = lanes_for((D + vec - 1) // vec)
@@ -702,7 +798,7 @@ def _make_plan(prog: RowProgram, args):
     if N * L < MIN_LANES and N * D >= (1 << 20):
         return None                     # a few very long rows: too little parallelism per row
     slices = G
-    J, cache = plan_registers(prog, modes, kinds, D, L, vec, T, dcap)
+    J, cache = plan_registers(prog, modes, kinds, D, L, vec, T, dcap, dts)
     if ot in ("col", "tmv") and "acc" not in cache:
         slices = lds_slices(G, dcap, T)
         if slices == 0:
