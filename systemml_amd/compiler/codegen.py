@@ -36,9 +36,20 @@ def _is_sq(h):
     return h.p.get("o") == "^" and b.op == "lit" and not isinstance(b.value, bool) and b.value == 2
 
 
+_BIAS = {"bias_add": "bias+", "bias_multiply": "bias*"}
+
+
+def _is_bias(h):
+    """bias_add / bias_multiply (per-channel broadcast of a C x 1 vector over an N x (C*H*W)
+    operand): cellwise operators of the Cell template with a CHAN-mode second operand."""
+    return h.op == "bi" and h.p.get("name") in _BIAS and len(h.inputs) == 2 and not h.named
+
+
 def _cellwise(h):
     if h.dt != "M":
         return False
+    if _is_bias(h):
+        return True
     if h.op == "b":
         return h.p.get("o") in BIN_CODES and len(h.inputs) == 2
     if h.op == "u":
@@ -84,7 +95,9 @@ def _regalloc(ops, leaves):
             return None
         d = free.pop(0)
         reg[("op", h.id)] = d
-        if h.op == "b" and _is_sq(h):
+        if _is_bias(h):
+            code.append(("b", _BIAS[h.p["name"]], d, srcs[0], srcs[1]))
+        elif h.op == "b" and _is_sq(h):
             code.append(("u", "sq", d, srcs[0], 0))
         elif h.op == "b":
             code.append(("b", h.p["o"], d, srcs[0], srcs[1]))
@@ -111,8 +124,10 @@ def fuse_cells(bb):
         if not _cellwise(h):
             continue
         ops, leaves = [], []
-        for c in _operands(h):
+        for ci, c in enumerate(_operands(h)):
             g = groups.get(c.id)
+            if _is_bias(h) and ci == 1:
+                g = None                      # the per-channel operand is read by the kernel as is
             if g is not None and ncons.get(c.id, 0) == 1 and c.id not in absorbed:
                 nl = _merge_leaves(leaves, g[1])
                 if len(ops) + len(g[0]) + 1 <= MAXOPS and len(nl) <= MAXIN:
@@ -167,7 +182,7 @@ ROW_AGG_OPS = ("sum", "sumsq", "mean", "min", "max")
 
 def _row_body_kind(h):
     """Role of h inside a Row-template region: 'cell' | 'ragg' | 'dot' | None (not fusable)."""
-    if h.dt != "M":
+    if h.dt != "M" or _is_bias(h):
         return None
     if _cellwise(h):
         return "cell"
@@ -510,13 +525,13 @@ def fuse_outer(bb):
                     continue
                 if not all(p.id in region for p in consumers.get(c.id, ())):
                     continue
-                if not _cellwise(c):
+                if not _cellwise(c) or _is_bias(c):
                     continue
                 region.add(c.id)
                 members.append(c)
                 frontier.extend(_operands(c))
                 changed = True
-        if len(uvs) != 1:
+        if len(uvs) != 1 or _is_bias(top):
             continue
         uvh = uvs[0]
         U, V = _uv(uvh)
@@ -561,7 +576,8 @@ def _multi_agg(built):
     into one `magg` hop evaluated in a single pass (ops/cell.evaluate_multi); each original
     aggregate hop becomes output i of it.  Aggregates that depend on each other are never
     grouped.  Returns the ids of the replaced roots."""
-    cands = [b for b in built if b[3].agg and b[3].agg[1] == "all"]
+    cands = [b for b in built if b[3].agg and b[3].agg[1] == "all" and
+             not any(o in ("bias+", "bias*") for _, o, _, _, _ in b[3].ops)]
     if len(cands) < 2:
         return set()
     reach = {}

@@ -103,7 +103,8 @@ def infer(h, dims, env):
         if not mats or not all(_known(x) for x in mats):
             d = UNK
         else:
-            d = (max(x[0] for x in mats), max(x[1] for x in mats))
+            from ..ops.cell import out_shape
+            d = out_shape(h.p["prog"], [None if x == SCALAR else x for x in ins]) or UNK
         agg = h.p["prog"].agg
         if not agg:
             return d

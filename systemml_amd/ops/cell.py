@@ -39,7 +39,10 @@ UN_CODES = {"sq": 20,               # x ^ 2 (binary '^' with the literal 2, lowe
 AGG_CODES = {"sum": 0, "sumsq": 1, "mean": 0, "min": 2, "max": 3}
 AGG_DIRS = {"all": 1, "row": 2, "col": 3}
 MAXIN, MAXOPS, NR = 8, 40, 16
-FULL, ROWV, COLV, HSCALAR, DSCALAR = range(5)
+FULL, ROWV, COLV, HSCALAR, DSCALAR, CHAN = range(6)
+# per-channel broadcast operators (bias_add / bias_multiply: a C x 1 vector over the H*W columns
+# of each channel of an N x (C*H*W) operand); generated kernels only (mode CHAN)
+BIAS_OPS = {"bias+": "+", "bias*": "*"}
 
 stats = {"kernel": 0, "sequential": 0, "rtc_compiled": 0, "rtc_cache_hits": 0, "rtc_launches": 0,
          "interpreter_launches": 0}
@@ -53,7 +56,8 @@ _C_BIN = {"+": "({a} + {b})", "-": "({a} - {b})", "*": "({a} * {b})", "/": "({a}
           ">": "sysml_b<T>({a} > {b})", ">=": "sysml_b<T>({a} >= {b})",
           "&": "sysml_b<T>({a} != T(0) && {b} != T(0))", "|": "sysml_b<T>({a} != T(0) || {b} != T(0))",
           "xor": "sysml_b<T>(({a} != T(0)) != ({b} != T(0)))", "min": "sysml_min<T>({a}, {b})",
-          "max": "sysml_max<T>({a}, {b})", "log": "(log({a}) / log({b}))"}
+          "max": "sysml_max<T>({a}, {b})", "log": "(log({a}) / log({b}))", "bias+": "({a} + {b})",
+          "bias*": "({a} * {b})"}
 _C_UN = {"sq": "({a} * {a})", "neg": "(-{a})", "not": "sysml_b<T>({a} == T(0))", "abs": "fabs({a})",
          "exp": "exp({a})", "log": "log({a})", "sqrt": "sqrt({a})", "round": "floor({a} + T(0.5))",
          "floor": "floor({a})", "ceil": "ceil({a})", "sign": "(T)(({a} > T(0)) - ({a} < T(0)))",
@@ -96,6 +100,8 @@ class CellProgram:
         if t is None:
             rows = []
             for kind, o, d, a, b in self.ops:
+                if o in BIAS_OPS:
+                    raise ValueError("per-channel operators run in generated kernels only")
                 op = BIN_CODES[o] if kind == "b" else UN_CODES[o]
                 for r in (d, a, b):
                     if not 0 <= r < NR:
@@ -120,7 +126,10 @@ def sequential(prog: CellProgram, args):
     """The fused DAG's original operators, one after the other."""
     regs = list(args) + [None] * (NR - len(args))
     for kind, o, d, a, b in prog.ops:
-        if kind == "b":
+        if kind == "b" and o in BIAS_OPS:
+            from ..runtime import builtins as B
+            regs[d] = (B.b_bias_mult if o == "bias*" else B.b_bias_add)(None, regs[a], regs[b])
+        elif kind == "b":
             regs[d] = C.binary(o, regs[a], regs[b])
         elif o == "sq":
             regs[d] = C.binary("^", regs[a], 2)
@@ -145,11 +154,16 @@ def out_shape(prog: CellProgram, shapes):
     """Result shape of the program for input shapes (None: scalar); None if an operator would
     reject its operands (the sequential path then raises the operator's own error)."""
     regs = list(shapes) + [None] * (NR - len(shapes))
-    for kind, _, d, a, b in prog.ops:
+    for kind, o, d, a, b in prog.ops:
         if kind == "u":
             regs[d] = regs[a]
             continue
         sa, sb = regs[a], regs[b]
+        if o in BIAS_OPS:
+            if sa is None or sb is None or sb[1] != 1 or sb[0] <= 0 or sa[1] % sb[0]:
+                return None
+            regs[d] = sa
+            continue
         if sa is None:
             regs[d] = sb
         elif sb is None:
@@ -212,7 +226,7 @@ def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant):
         body.append(f"    const T v{q} = {e};")
         var[d] = f"v{q}"
     aggop = AGG_CODES[prog.agg[0]] if prog.agg else 0
-    need_ij = int(any(m in (ROWV, COLV) for m in modes))
+    need_ij = int(any(m in (ROWV, COLV, CHAN) for m in modes))
     if mode == 0:
         call = "sysml_cell_flat<Spec, 0>(A);"
     elif mode == 1:
@@ -381,7 +395,7 @@ def _signature(args):
 class _Plan:
     """Everything a launch of one program on one operand signature needs but the pointers."""
     __slots__ = ("prog", "fn", "interp", "mode", "nblk", "gx", "gy", "R", "Cc", "T", "out_shape", "part_shape",
-                 "kinds", "P", "dev", "dev_index", "launch", "count")
+                 "kinds", "P", "dev", "dev_index", "launch", "count", "hws")
 
 
 def _make_plan(prog, args):
@@ -418,12 +432,30 @@ def _make_plan(prog, args):
     if R <= 0 or Cc <= 0:
         return None
     T = torch.float64 if (f64 or (bf16 and backend.dtype == torch.float64)) else torch.float32
+    chan = {b for kind, o, d, a, b in prog.ops if o in BIAS_OPS}
+    if chan and (not RTC or any(k >= prog.n_in for k in chan)):
+        return None                   # per-channel operands: generated kernels only, inputs only
+    if chan:
+        other = {a for kind, o, d, a, b in prog.ops} | {b for kind, o, d, a, b in prog.ops
+                                                         if kind == "b" and o not in BIAS_OPS}
+        if chan & other or prog.out in chan:
+            return None               # also read as an ordinary operand
     P = _Prog()
     kinds = []
     need_ij = 0
+    hws = {}
     for k, x in enumerate(args):
         e = P.inp[k]
         tx = type(x)
+        if k in chan:
+            if tx is not _Tensor or x.shape[1] != 1 or Cc % x.shape[0]:
+                return None
+            e.dtype = _DT[x.dtype]
+            e.mode = CHAN
+            hws[k] = Cc // x.shape[0]
+            need_ij = 1
+            kinds.append("c")
+            continue
         if tx is _Tensor:
             r, c = x.shape
             e.dtype = _DT[x.dtype]
@@ -481,6 +513,9 @@ def _make_plan(prog, args):
             if mode == 3:
                 pl.gx, pl.gy = (Cc + variant - 1) // variant, nblk
     pl.interp = pl.fn is None
+    pl.hws = hws
+    if chan and pl.interp:
+        return None
     pl.launch = _rtc_lib().sysml_rtc_launch
     from . import kernels
     pl.count = kernels._count
@@ -512,11 +547,13 @@ def _kernel(prog: CellProgram, args):
     if not pl.interp:
         A = _RtcArgs()
         for k, (x, kd) in enumerate(zip(args, pl.kinds)):
-            if kd == "t":
+            if kd == "t" or kd == "c":
                 if not x.is_contiguous():
                     x = x.contiguous()
                     keep.append(x)
                 A.inp[k] = x.data_ptr()
+                if kd == "c":
+                    A.s[k] = pl.hws[k]
             elif kd == "d":
                 t = x.t.reshape(1)
                 keep.append(t)

@@ -299,3 +299,52 @@ def test_multi_aggregate_kernel_gpu():
             got = res[k]
             got = float(got.value()) if hasattr(got, "value") else float(got)
             assert got == pytest.approx(float(r), rel=1e-6 if dt == torch.float32 else 1e-9, abs=1e-9), (k, dt)
+
+
+BIAS_SCRIPT = """
+Xc = bias_add(X, -m)
+norm = bias_multiply(Xc, istd)
+out = max(bias_add(bias_multiply(norm, g), b), 0)
+s = sum(out)
+"""
+
+
+def _bias_inputs(N=6, C=10, HW=9, seed=0):
+    rng = np.random.default_rng(seed)
+    return {"X": rng.standard_normal((N, C * HW)), "m": rng.standard_normal((C, 1)), "istd": rng.random((C, 1)),
+            "g": rng.random((C, 1)), "b": rng.standard_normal((C, 1))}
+
+
+def test_bias_ops_fuse_with_cellwise_chains():
+    """bias_add / bias_multiply (per-channel broadcasts of batch-norm / scale layers) fuse into
+    the Cell template with the surrounding cellwise work; results equal the unfused plan."""
+    ins = _bias_inputs()
+    cs = EX.compile_script(BIAS_SCRIPT, {}, inputs=ins, outputs=["norm", "out", "s"], config=DMLConfig(gpu=False))
+    fused = _fused_hops(cs)
+    assert any("cell[bias+,bias*]" in ln for ln in fused), fused
+    assert any("cell[bias*,bias+,max]" in ln for ln in fused), fused
+    res, _ = EX.execute(cs, ins)
+    cs0 = EX.compile_script(BIAS_SCRIPT, {}, inputs=ins, outputs=["norm", "out", "s"],
+                            config=DMLConfig(gpu=False, fusion=False))
+    ref, _ = EX.execute(cs0, ins)
+    for k in ("norm", "out"):
+        assert torch.equal(res[k], ref[k]), k
+    assert float(res["s"]) == float(ref["s"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(6, 10, 9), (32, 64, 3136), (3, 7, 1)])
+def test_bias_ops_cell_kernel_gpu(shape):
+    from systemml_amd.ops import kernels
+    N, C, HW = shape
+    ins = _bias_inputs(N, C, HW, seed=N)
+    c0 = kernels.counters.get("cell", 0)
+    cfg = DMLConfig(gpu=True, precision="double", gpu_min_cells=0)
+    got, _ = EX.execute(EX.compile_script(BIAS_SCRIPT, {}, inputs=ins, outputs=["norm", "out", "s"], config=cfg), ins)
+    assert kernels.counters.get("cell", 0) >= c0 + 2
+    X, m, istd, g, b = (torch.from_numpy(ins[k]) for k in ("X", "m", "istd", "g", "b"))
+    ch = lambda v: v.reshape(1, C, 1)
+    norm = ((X.reshape(N, C, HW) - ch(m)) * ch(istd))
+    out = torch.clamp(norm * ch(g) + ch(b), min=0)
+    assert torch.allclose(got["norm"].double().cpu(), norm.reshape(N, -1), rtol=1e-12, atol=1e-12)
+    assert torch.allclose(got["out"].double().cpu(), out.reshape(N, -1), rtol=1e-12, atol=1e-12)
