@@ -122,8 +122,37 @@ def evaluate(prog: CellProgram, args):
     return sequential(prog, args)
 
 
+def _axpy_form(prog):
+    """(y, p, q, sign) when the program is y +/- p * q (or p * q + y) over its inputs, else None:
+    with one of p, q a host scalar the host runs it as ONE torch.add(y, x, alpha=+-s) -- the CG
+    update shape of iterative solvers (S + a * V, R - a * HV), where per-call dispatch dominates
+    on D x K matrices."""
+    f = prog._code.get("axpy", False)
+    if f is not False:
+        return f
+    f = None
+    if len(prog.ops) == 2 and not prog.agg:
+        (k1, o1, t, a1, b1), (k2, o2, d, a2, b2) = prog.ops
+        n = prog.n_in
+        if k1 == "b" and o1 == "*" and a1 < n and b1 < n and k2 == "b" and d == prog.out:
+            if o2 in ("+", "-") and b2 == t and a2 != t and a2 < n:
+                f = (a2, a1, b1, 1.0 if o2 == "+" else -1.0)
+            elif o2 == "+" and a2 == t and b2 != t and b2 < n:
+                f = (b2, a1, b1, 1.0)
+    prog._code["axpy"] = f
+    return f
+
+
 def sequential(prog: CellProgram, args):
     """The fused DAG's original operators, one after the other."""
+    ax = _axpy_form(prog)
+    if ax is not None:
+        y, p, q = args[ax[0]], args[ax[1]], args[ax[2]]
+        x, sc = (q, p) if (type(p) is float or type(p) is int) else (p, q)
+        if type(y) is _Tensor and type(x) is _Tensor and (type(sc) is float or type(sc) is int) and \
+                not y.is_cuda and y.layout is torch.strided and x.layout is torch.strided and \
+                y.dtype is torch.float64 and x.dtype is torch.float64 and y.shape == x.shape:
+            return torch.add(y, x, alpha=ax[3] * sc)
     regs = list(args) + [None] * (NR - len(args))
     for kind, o, d, a, b in prog.ops:
         if kind == "b" and o in BIAS_OPS:
