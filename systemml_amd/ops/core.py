@@ -470,6 +470,16 @@ def _var(x, dim=None):
 
 
 def agg(o, d, x):
+    # fast path: dense host tensors (the CP backend's solver state) -- no representation checks
+    if type(x) is Tensor and x.layout is _STRIDED and not x.is_cuda and x.dtype is not torch.bfloat16 \
+            and x.numel() > 0:
+        if d == "all":
+            if o == "sum":
+                return float(torch.sum(x))
+            if o == "sumsq":
+                return float(torch.sum(x * x))
+        elif o == "sum":
+            return torch.sum(x, dim=1 if d == "row" else 0, keepdim=True)
     if type(x) is _CC:
         return AUG.agg(o, d, x)
     if CMP.is_compressed(x):
@@ -560,6 +570,10 @@ def agg(o, d, x):
 
 def tak(a, b):
     """sum(a*b) without materialising the product (TernaryAggregate tak+*)."""
+    if type(a) is Tensor and type(b) is Tensor and a.layout is _STRIDED and b.layout is _STRIDED and \
+            not a.is_cuda and not b.is_cuda and a.dtype is b.dtype and a.dtype is not torch.bfloat16 and \
+            a.shape == b.shape:
+        return float(torch.dot(a.reshape(-1), b.reshape(-1)))
     if is_dist(a) or is_dist(b):
         return _dist().tak(a, b)
     a, b = SP.densify(a), SP.densify(b)
