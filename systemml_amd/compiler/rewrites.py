@@ -742,6 +742,9 @@ def cse(roots):
     return [visit(r) for r in roots], visit
 
 
+_ROWGEN = __import__('os').environ.get('SYSML_ROWGEN', '1') != '0'   # Row / Outer templates on
+
+
 def rewrite_block(bb, config=None):
     """Rewrite a BasicBlock's DAG in place (roots + env_out)."""
     rw = Rewriter(config)
@@ -759,12 +762,13 @@ def rewrite_block(bb, config=None):
             if nobj:
                 rw.stats["softmax-objective"] = nobj
         from .codegen import fuse_cells, fuse_rows, fuse_outer
-        n = fuse_outer(bb)
-        if n:
-            rw.stats["outer-fused-ops"] = n
-        n = fuse_rows(bb)
-        if n:
-            rw.stats["row-fused-ops"] = n
+        if _ROWGEN:
+            n = fuse_outer(bb)
+            if n:
+                rw.stats["outer-fused-ops"] = n
+            n = fuse_rows(bb)
+            if n:
+                rw.stats["row-fused-ops"] = n
         n = fuse_cells(bb)
         if n:
             rw.stats["cell-fused-ops"] = n
