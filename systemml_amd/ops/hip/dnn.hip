@@ -77,7 +77,7 @@ __device__ __forceinline__ int64_t out_index(const Conv& c, int m, int n) {
 // Element (row side):    A[ra + w]                     (W for FWD / BWD_DATA, dout for BWD_FILTER)
 // Element (column side): FWD / BWD_FILTER: X[cb + x] if (ch + y, cw + z) inside the image
 //                        BWD_DATA: dout[cb + x + th*Wo + tw], th = ch - y, tw = cw - z on the stride grid
-constexpr int TM = 64, TN = 64, NT = 256;
+constexpr int NT = 256;
 
 template <int PATH> struct PathCfg;                       // 0: bf16 MFMA, 1: f32, 2: f64
 template <> struct PathCfg<0> { static constexpr int BK = 32; typedef f4 acc_t; };
@@ -119,14 +119,19 @@ template <int PATH, typename TI> struct Store {
   }
 };
 
-template <int MODE, typename TI, int PATH, typename TO>
+// TM_ x TN_ output tile per 256-thread block, 2 x 2 waves of (TM_/2) x (TN_/2); 128 x 128 tiles
+// (4 x 4 MFMA 16x16 accumulators per wave) halve the gathered operand bytes per MFMA against
+// 64 x 64 and are used for the bf16 path whenever both GEMM dimensions reach 128.
+template <int MODE, typename TI, int PATH, typename TO, int TM_, int TN_>
 __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
   typedef PathCfg<PATH> Cfg;
   constexpr int BK = Cfg::BK, KV = BK / 4;
   typedef typename std::conditional<PATH == 0, __bf16, typename std::conditional<PATH == 1, float, double>::type>::type S;
   constexpr int LDK = PATH == 0 ? BK + 8 : BK + 1;       // bf16: 80-B rows; exact: odd stride
-  __shared__ __attribute__((aligned(16))) S As[TM][LDK];
-  __shared__ __attribute__((aligned(16))) S Bs[TN][LDK];
+  constexpr int FI = TM_ / 32, FJ = TN_ / 32;            // 16-wide MFMA fragments per wave
+  constexpr int RS = TM_ / 64, CS = TN_ / 64;            // row / column sets of the k-run mapping
+  __shared__ __attribute__((aligned(16))) S As[TM_][LDK];
+  __shared__ __attribute__((aligned(16))) S Bs[TN_][LDK];
   __shared__ int4 tab[2][BK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -134,36 +139,36 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
   const int ntile = c.tm * c.tn;
   const int tile = wg % ntile, split = wg / ntile;
   const int bm = tile % c.tm, bn = tile / c.tm;
-  const int m0 = bm * TM, n0 = bn * TN;
+  const int m0 = bm * TM_, n0 = bn * TN_;
   const int kbeg = split * c.kper;
   const int kend = min(c.K, kbeg + c.kper);
   const TI* __restrict__ Ap = (const TI*)(MODE == BWD_FILTER ? c.D : c.W);
   const TI* __restrict__ Bp = (const TI*)(MODE == BWD_DATA ? c.D : c.X);
   // Load mappings (which thread fetches which tile elements), chosen so that the lanes of one
   // load instruction touch consecutive addresses:
-  //   FWD / BWD_DATA  A: row tid/4, k (tid%4)*KV..+KV  (W rows are contiguous in k: 16-B loads)
-  //                   B: column tid%64, k (tid/64)*KV..  (lanes = consecutive output / input pixels)
+  //   FWD / BWD_DATA  A: rows tid/4 + 64 s, k (tid%4)*KV..+KV  (W rows contiguous in k: 16-B loads)
+  //                   B: columns tid%64 + 64 s, k (tid/64)*KV..  (lanes = consecutive pixels)
   //   BWD_FILTER      A, B: k = tid%BK (lanes = consecutive output pixels), RPT rows / columns each
   constexpr bool KL = MODE == BWD_FILTER;
-  constexpr int RPT = KL ? (TM * BK) / NT : 1;          // rows per thread in the k-lane mapping
-  const int ar = KL ? (tid / BK) * RPT : tid >> 2;
+  constexpr int RPTA = KL ? (TM_ * BK) / NT : RS;        // row slots per thread
+  constexpr int RPTB = KL ? (TN_ * BK) / NT : CS;        // column slots per thread
   const int ak = KL ? tid % BK : (tid & 3) * KV;
-  const int bc = KL ? (tid / BK) * RPT : tid & 63;
   const int bk = KL ? tid % BK : (tid >> 6) * KV;
-  constexpr int NA = KL ? RPT : KV;                      // elements per thread per operand
+  auto arow = [&](int q) { return KL ? (tid / BK) * RPTA + q : (tid >> 2) + 64 * q; };
+  auto bcol = [&](int q) { return KL ? (tid / BK) * RPTB + q : (tid & 63) + 64 * q; };
   // fixed per-thread row / column decode
-  int ra[KL ? RPT : 1];
-  bool mv[KL ? RPT : 1];
+  int ra[RPTA];
+  bool mv[RPTA];
 #pragma unroll
-  for (int q = 0; q < (KL ? RPT : 1); ++q) {
-    const int m = m0 + ar + q;
+  for (int q = 0; q < RPTA; ++q) {
+    const int m = m0 + arow(q);
     mv[q] = m < c.M;
     ra[q] = MODE == FWD ? m * c.K : (MODE == BWD_DATA ? m * c.KH * c.KW : m * c.Ho * c.Wo);
   }
-  int cb[KL ? RPT : 1], ch[KL ? RPT : 1], cw[KL ? RPT : 1];
+  int cb[RPTB], ch[RPTB], cw[RPTB];
 #pragma unroll
-  for (int q = 0; q < (KL ? RPT : 1); ++q) {
-    const int n = n0 + bc + q;
+  for (int q = 0; q < RPTB; ++q) {
+    const int n = n0 + bcol(q);
     cb[q] = 0; ch[q] = -(1 << 29); cw[q] = 0;
     if (n < c.Ncol) {
       if (MODE == FWD) {
@@ -185,7 +190,8 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
     }
   }
   const bool s1 = c.sh == 1 && c.sw == 1;
-  TI va[NA], vb[NA];
+  constexpr int NVA = KL ? RPTA : RS * KV, NVB = KL ? RPTB : CS * KV;
+  TI va[NVA], vb[NVB];
   auto build = [&](int buf, int k0) {
     if (tid < BK) {
       const int k = k0 + tid;
@@ -214,47 +220,62 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
     if constexpr (KL) {
       const int4 e = tab[buf][ak];
 #pragma unroll
-      for (int q = 0; q < RPT; ++q) {
-        va[q] = (mv[q] && e.w >= 0) ? Ap[ra[q] + e.w] : TI(0);
-        vb[q] = bval(e, q);
-      }
+      for (int q = 0; q < RPTA; ++q) va[q] = (mv[q] && e.w >= 0) ? Ap[ra[q] + e.w] : TI(0);
+#pragma unroll
+      for (int q = 0; q < RPTB; ++q) vb[q] = bval(e, q);
     } else {
-      // A: FWD rows are contiguous in k -> one 16-B load when the KV-run is in range and aligned
-      bool vec = false;
-      if constexpr (MODE == FWD && sizeof(TI) * KV == 16) vec = c.avec && mv[0] && (k0 + ak + KV) <= kend;
-      if (vec) {
-        typedef TI vt __attribute__((ext_vector_type(KV)));
-        const vt x = *(const vt*)(Ap + ra[0] + k0 + ak);
 #pragma unroll
-        for (int j = 0; j < KV; ++j) va[j] = x[j];
-      } else {
+      for (int q = 0; q < RS; ++q) {
+        // A: FWD rows are contiguous in k -> one 16-B load when the KV-run is in range and aligned
+        bool vec = false;
+        if constexpr (MODE == FWD && sizeof(TI) * KV == 16) vec = c.avec && mv[q] && (k0 + ak + KV) <= kend;
+        if (vec) {
+          typedef TI vt __attribute__((ext_vector_type(KV)));
+          const vt x = *(const vt*)(Ap + ra[q] + k0 + ak);
 #pragma unroll
-        for (int j = 0; j < KV; ++j) {
-          const int4 e = tab[buf][ak + j];
-          va[j] = (mv[0] && e.w >= 0) ? Ap[ra[0] + e.w] : TI(0);
+          for (int j = 0; j < KV; ++j) va[q * KV + j] = x[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < KV; ++j) {
+            const int4 e = tab[buf][ak + j];
+            va[q * KV + j] = (mv[q] && e.w >= 0) ? Ap[ra[q] + e.w] : TI(0);
+          }
         }
       }
 #pragma unroll
-      for (int j = 0; j < KV; ++j) vb[j] = bval(tab[buf][bk + j], 0);
+      for (int q = 0; q < CS; ++q)
+#pragma unroll
+        for (int j = 0; j < KV; ++j) vb[q * KV + j] = bval(tab[buf][bk + j], q);
     }
   };
   auto store = [&]() {
     if constexpr (KL) {
 #pragma unroll
-      for (int q = 0; q < RPT; ++q) {
-        As[ar + q][ak] = (S)va[q];
-        Bs[bc + q][bk] = (S)vb[q];
-      }
+      for (int q = 0; q < RPTA; ++q) As[arow(q)][ak] = (S)va[q];
+#pragma unroll
+      for (int q = 0; q < RPTB; ++q) Bs[bcol(q)][bk] = (S)vb[q];
     } else {
-      Store<PATH, TI>::template put<KV>(&As[ar][ak], va);
-      Store<PATH, TI>::template put<KV>(&Bs[bc][bk], vb);
+#pragma unroll
+      for (int q = 0; q < RS; ++q) {
+        TI r[KV];
+#pragma unroll
+        for (int j = 0; j < KV; ++j) r[j] = va[q * KV + j];
+        Store<PATH, TI>::template put<KV>(&As[arow(q)][ak], r);
+      }
+#pragma unroll
+      for (int q = 0; q < CS; ++q) {
+        TI r[KV];
+#pragma unroll
+        for (int j = 0; j < KV; ++j) r[j] = vb[q * KV + j];
+        Store<PATH, TI>::template put<KV>(&Bs[bcol(q)][bk], r);
+      }
     }
   };
-  typename Cfg::acc_t acc[2][2];
+  typename Cfg::acc_t acc[FI][FJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = 0;
   if (kbeg < kend) {
@@ -272,28 +293,28 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
     if (more) gather(buf ^ 1, k0 + BK);                  // next tile's loads overlap this tile's MFMAs
     if constexpr (PATH == 0) {
       const int kc = (lane >> 4) * 8;
-      bf8 fa[2], fb[2];
+      bf8 fa[FI], fb[FJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = *(const bf8*)&As[wr * 32 + i * 16 + (lane & 15)][kc];
+      for (int i = 0; i < FI; ++i) fa[i] = *(const bf8*)&As[wr * (TM_ / 2) + i * 16 + (lane & 15)][kc];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = *(const bf8*)&Bs[wc * 32 + j * 16 + (lane & 15)][kc];
+      for (int j = 0; j < FJ; ++j) fb[j] = *(const bf8*)&Bs[wc * (TN_ / 2) + j * 16 + (lane & 15)][kc];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     } else {
 #pragma unroll
       for (int ks = 0; ks < BK; ks += 4) {
         const int k = ks + (lane >> 4);
-        S fa[2], fb[2];
+        S fa[FI], fb[FJ];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) fa[i] = As[wr * 32 + i * 16 + (lane & 15)][k];
+        for (int i = 0; i < FI; ++i) fa[i] = As[wr * (TM_ / 2) + i * 16 + (lane & 15)][k];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = Bs[wc * 32 + j * 16 + (lane & 15)][k];
+        for (int j = 0; j < FJ; ++j) fb[j] = Bs[wc * (TN_ / 2) + j * 16 + (lane & 15)][k];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < FI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < FJ; ++j) {
             if constexpr (PATH == 1) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
             else acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
           }
@@ -307,13 +328,13 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
   TO* out = (TO*)c.out;
   const TO* bias = (const TO*)c.bias;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int mo = m0 + wr * 32 + i * 16 + (PATH == 2 ? (lane >> 4) + 4 * r : (lane >> 4) * 4 + r);
-        const int no = n0 + wc * 32 + j * 16 + (lane & 15);
+        const int mo = m0 + wr * (TM_ / 2) + i * 16 + (PATH == 2 ? (lane >> 4) + 4 * r : (lane >> 4) * 4 + r);
+        const int no = n0 + wc * (TN_ / 2) + j * 16 + (lane & 15);
         if (mo < c.M && no < c.Ncol) {
           TO v = (TO)acc[i][j][r];
           if (atomic) {
@@ -447,7 +468,16 @@ inline unsigned grid_for(int64_t n) {
 
 }  // namespace sysml_dnn
 
+namespace sysml_dnn {
+inline int conv_tile(int dtype, int64_t M, int64_t Nc) {
+  return ((dtype == 0 || dtype == 3) && M >= 128 && Nc >= 128) ? 128 : 64;
+}
+}  // namespace sysml_dnn
+
 extern "C" {
+
+// Output tile edge the launcher uses for a GEMM view (the host sizes split-K from it).
+int sysml_conv2d_tile(int dtype, int64_t M, int64_t Nc) { return sysml_dnn::conv_tile(dtype, M, Nc); }
 
 // dtype: 0 bf16 in (fp32 out), 1 fp32 exact, 2 fp64 exact, 3 fp32 in / bf16 MFMA / fp32 out.
 // mode: 0 forward, 1 backward data, 2 backward filter.  ksplit > 1 splits the GEMM depth over
@@ -479,9 +509,10 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   if ((int64_t)N * C * H * Wd >= (1LL << 31) || (int64_t)N * F * P >= (1LL << 31) || (int64_t)F * C * KK >= (1LL << 31))
     return -1;
   c.M = (int)M; c.Ncol = (int)Nc; c.K = (int)K;
-  c.tm = (int)((M + TM - 1) / TM);
-  c.tn = (int)((Nc + TN - 1) / TN);
   const bool bfmma = dtype == 0 || dtype == 3;
+  const int tile = conv_tile(dtype, M, Nc);          // 128 x 128 (bf16, both dims >= 128) or 64 x 64
+  c.tm = (int)((M + tile - 1) / tile);
+  c.tn = (int)((Nc + tile - 1) / tile);
   const int BK = bfmma ? 32 : 16;
   if (ksplit < 1) ksplit = 1;
   int64_t kper = (K + ksplit - 1) / ksplit;
@@ -504,13 +535,15 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
     else hipLaunchKernelGGL((KERN<BWD_FILTER, __VA_ARGS__>), g, t, 0, s, c);                 \
   } while (0)
   if (dtype == 0) {
-    LAUNCH(conv_kernel, __bf16, 0, float);
+    if (tile == 128) LAUNCH(conv_kernel, __bf16, 0, float, 128, 128);
+    else LAUNCH(conv_kernel, __bf16, 0, float, 64, 64);
   } else if (dtype == 3) {
-    LAUNCH(conv_kernel, float, 0, float);
+    if (tile == 128) LAUNCH(conv_kernel, float, 0, float, 128, 128);
+    else LAUNCH(conv_kernel, float, 0, float, 64, 64);
   } else if (dtype == 1) {
-    LAUNCH(conv_kernel, float, 1, float);
+    LAUNCH(conv_kernel, float, 1, float, 64, 64);
   } else if (dtype == 2) {
-    LAUNCH(conv_kernel, double, 2, double);
+    LAUNCH(conv_kernel, double, 2, double, 64, 64);
   } else {
     return -1;
   }

@@ -16,6 +16,10 @@ SHAPES = [  # N, C, H, W, F, K, stride, pad
     (4, 8, 7, 7, 6, 1, 1, 0),
     (2, 2, 9, 13, 3, 3, 2, 0),
     (1, 64, 14, 14, 96, 3, 1, 1),
+    # both GEMM dimensions >= 128 on the bf16 path: 128 x 128 tiles, ragged edges
+    (2, 130, 9, 11, 136, 3, 1, 1),
+    (3, 160, 8, 8, 200, 1, 1, 0),
+    (2, 129, 15, 15, 131, 3, 2, 1),
 ]
 
 
@@ -132,3 +136,38 @@ s = sum(p) + sum(dw) + sum(dx)
     assert abs(float(gpu["s"]) - float(cpu["s"])) < 1e-9 * abs(float(cpu["s"]))
     for k in ("conv2d", "conv2d_bwd_filter", "conv2d_bwd_data", "pool", "pool_bwd", "bias_add"):
         assert Kn.counters.get(k, 0) > c0.get(k, 0), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 130, 9, 11, 136, 3, 1, 1), (4, 256, 7, 7, 128, 1, 1, 0), (1, 64, 14, 14, 96, 3, 1, 1)])
+def test_conv2d_fp32_operands_on_bf16_mfma(shape):
+    """fp32 activations / filters computed on bf16 MFMA (the ResNet bench mode, dtype code 3):
+    against an fp64 reference of the bf16-rounded operands."""
+    from systemml_amd.ops import kernels as Kn
+    N, C, H, Wd, F_, K, s, p = shape
+    g = torch.Generator().manual_seed(7 + sum(shape))
+    X = torch.randn(N, C * H * Wd, generator=g, dtype=torch.float64)
+    W = torch.randn(F_, C * K * K, generator=g, dtype=torch.float64)
+    Xr, Wr = X.to(torch.bfloat16).double(), W.to(torch.bfloat16).double()
+    _, G, _, _ = _ref_conv(Xr, Wr, N, C, H, Wd, F_, K, s, p)
+    Gr = G.to(torch.bfloat16).double()
+    dev = torch.device("cuda:0")
+    old = Kn.CONV_BF16_FP32
+    Kn.CONV_BF16_FP32 = True
+    try:
+        Xd, Wdv, Gd = X.to(dev, torch.float32), W.to(dev, torch.float32), Gr.to(dev, torch.float32)
+        got = Kn.conv2d(0, Xd, Wdv, None, N, C, H, Wd, F_, K, K, s, s, p, p)
+        gx = Kn.conv2d(1, None, Wdv, Gd, N, C, H, Wd, F_, K, K, s, s, p, p)
+        gw = Kn.conv2d(2, Xd, None, Gd, N, C, H, Wd, F_, K, K, s, s, p, p)
+    finally:
+        Kn.CONV_BF16_FP32 = old
+    torch.cuda.synchronize()
+    x = Xr.reshape(N, C, H, Wd).requires_grad_(True)
+    w = Wr.reshape(F_, C, K, K).requires_grad_(True)
+    o = torch.nn.functional.conv2d(x, w, stride=s, padding=p)
+    o.backward(Gr.reshape(o.shape))
+    for name, a, b in (("fwd", got, o.reshape(N, -1).detach()), ("bwd_data", gx, x.grad.reshape(N, -1)),
+                       ("bwd_filter", gw, w.grad.reshape(F_, -1))):
+        a = a.double().cpu()
+        err = (a - b).abs().max().item() / (b.abs().max().item() + 1e-30)
+        assert err < 2e-2, (name, err)
