@@ -469,8 +469,11 @@ inline unsigned grid_for(int64_t n) {
 }  // namespace sysml_dnn
 
 namespace sysml_dnn {
+// 128 x 128 tiles only when they still give >= 2 workgroups per CU (256 CUs): a 256-filter
+// 14 x 14 layer at batch 64 has 196 such tiles and runs 1.5x faster on 64 x 64 ones
 inline int conv_tile(int dtype, int64_t M, int64_t Nc) {
-  return ((dtype == 0 || dtype == 3) && M >= 128 && Nc >= 128) ? 128 : 64;
+  if (!(dtype == 0 || dtype == 3) || M < 128 || Nc < 128) return 64;
+  return ((M + 127) / 128) * ((Nc + 127) / 128) >= 512 ? 128 : 64;
 }
 }  // namespace sysml_dnn
 
