@@ -745,6 +745,30 @@ def cse(roots):
 _ROWGEN = __import__('os').environ.get('SYSML_ROWGEN', '1') != '0'   # Row / Outer templates on
 
 
+def fuse_conv_bias(bb):
+    """bias_add(conv2d(X, W, ...), b) -> conv2d(X, W, ..., bias = b) when the convolution has no
+    other consumer (reference: hops/DnnOp CONV2D_BIAS_ADD): the bias is added in the
+    convolution kernel's epilogue instead of a second pass over the output.  Returns the
+    number of fused pairs."""
+    live = getattr(bb, "live_out", None)
+    tops = list(bb.roots) + list(bb.env_out.values())
+    outs = {h.id for h in bb.roots} | {h.id for k, h in bb.env_out.items() if live is None or k in live}
+    shared = count_consumers(tops)             # ids with more than one consumer
+    n = 0
+    for h in H.walk(tops):
+        if not (h.op == "bi" and h.p.get("name") == "bias_add" and len(h.inputs) == 2 and not h.named):
+            continue
+        c, b = h.inputs
+        if not (c.op == "bi" and c.p.get("name") == "conv2d" and "bias" not in c.named) or c.id in outs \
+                or c.id in shared:
+            continue
+        h.p = dict(c.p)
+        h.inputs = list(c.inputs) + [b]
+        h.named = list(c.named) + ["bias"]
+        n += 1
+    return n
+
+
 def rewrite_block(bb, config=None):
     """Rewrite a BasicBlock's DAG in place (roots + env_out)."""
     rw = Rewriter(config)
@@ -755,6 +779,9 @@ def rewrite_block(bb, config=None):
     bb.roots = roots
     bb.env_out = {k: visit(v) for k, v in bb.env_out.items()}
     if rw.enabled and rw.fuse:
+        n = fuse_conv_bias(bb)
+        if n:
+            rw.stats["conv2d-bias-add"] = n
         n = fuse_softmax_grad(bb)
         if n:
             rw.stats["softmax-grad"] = n

@@ -1015,9 +1015,12 @@ def _conv_params(kw):
 
 
 @builtin("conv2d")
-def b_conv2d(ctx, input=None, filter=None, **kw):
+def b_conv2d(ctx, input=None, filter=None, bias=None, **kw):
+    """conv2d; `bias` (F x 1) is set by the conv2d + bias_add fusion rewrite and added in the
+    convolution kernel's epilogue (reference: DnnOp CONV2D_BIAS_ADD)."""
     from ..ops import dnn
-    return dnn.conv2d(_mat(input), _mat(filter), **_conv_kw(kw))
+    b = None if bias is None else _mat(bias).reshape(-1)
+    return dnn.conv2d(_mat(input), _mat(filter), bias=b, **_conv_kw(kw))
 
 
 @builtin("conv2d_backward_filter")
