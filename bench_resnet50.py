@@ -114,6 +114,11 @@ def main():
     cs = compile_script(src, {"X": "X", "Y": "Y"}, inputs={"X": X, "Y": Y}, config=cfg,
                         filename=os.path.join(SCRIPTS_DIR, "resnet50_bench.dml"))
     out = []
+    # the compiled program lives for the whole run: keep it out of the cyclic collector's
+    # generations so gen-2 collections during the steps stay short (as bench.py does)
+    import gc
+    gc.collect()
+    gc.freeze()
     t = time.perf_counter()
     execute(cs, {"X": X, "Y": Y}, out=out.append)
     if torch.cuda.is_available():
