@@ -83,6 +83,11 @@ template <int PATH> struct PathCfg;                       // 0: bf16 MFMA, 1: f3
 template <> struct PathCfg<0> { static constexpr int BK = 32; typedef f4 acc_t; };
 template <> struct PathCfg<1> { static constexpr int BK = 16; typedef f4 acc_t; };
 template <> struct PathCfg<2> { static constexpr int BK = 16; typedef d4 acc_t; };
+// K-tile depth: 64 for the bf16 128 x 128 forward / backward-data tiles (half the barriers and
+// table decodes per MFMA), the path's default otherwise (split-K rounding uses the default)
+template <int PATH, int MODE, int TM_> struct KDepth {
+  static constexpr int BK = (PATH == 0 && MODE != BWD_FILTER && TM_ == 128) ? 64 : PathCfg<PATH>::BK;
+};
 
 template <int MODE>
 __device__ __forceinline__ int4 decode_k(const Conv& c, int k) {
@@ -105,10 +110,13 @@ template <int PATH, typename TI> struct Store;
 template <typename TI> struct Store<0, TI> {
   template <int KV>
   static __device__ __forceinline__ void put(__bf16* row, const TI (&v)[KV]) {
-    bf8 p;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) p[j] = (__bf16)v[j];
-    *(bf8*)row = p;
+    for (int h = 0; h < KV; h += 8) {
+      bf8 p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p[j] = (__bf16)v[h + j];
+      *(bf8*)(row + h) = p;
+    }
   }
 };
 template <int PATH, typename TI> struct Store {
@@ -125,9 +133,9 @@ template <int PATH, typename TI> struct Store {
 template <int MODE, typename TI, int PATH, typename TO, int TM_, int TN_>
 __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
   typedef PathCfg<PATH> Cfg;
-  constexpr int BK = Cfg::BK, KV = BK / 4;
+  constexpr int BK = KDepth<PATH, MODE, TM_>::BK, KV = BK / 4;
   typedef typename std::conditional<PATH == 0, __bf16, typename std::conditional<PATH == 1, float, double>::type>::type S;
-  constexpr int LDK = PATH == 0 ? BK + 8 : BK + 1;       // bf16: 80-B rows; exact: odd stride
+  constexpr int LDK = PATH == 0 ? BK + 8 : BK + 1;       // bf16: 80 / 144-B rows; exact: odd stride
   constexpr int FI = TM_ / 32, FJ = TN_ / 32;            // 16-wide MFMA fragments per wave
   constexpr int RS = TM_ / 64, CS = TN_ / 64;            // row / column sets of the k-run mapping
   __shared__ __attribute__((aligned(16))) S As[TM_][LDK];
@@ -228,7 +236,7 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
       for (int q = 0; q < RS; ++q) {
         // A: FWD rows are contiguous in k -> one 16-B load when the KV-run is in range and aligned
         bool vec = false;
-        if constexpr (MODE == FWD && sizeof(TI) * KV == 16) vec = c.avec && mv[q] && (k0 + ak + KV) <= kend;
+        if constexpr (MODE == FWD && (sizeof(TI) * KV) % 16 == 0) vec = c.avec && mv[q] && (k0 + ak + KV) <= kend;
         if (vec) {
           typedef TI vt __attribute__((ext_vector_type(KV)));
           const vt x = *(const vt*)(Ap + ra[q] + k0 + ak);
@@ -292,16 +300,20 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
     __syncthreads();
     if (more) gather(buf ^ 1, k0 + BK);                  // next tile's loads overlap this tile's MFMAs
     if constexpr (PATH == 0) {
-      const int kc = (lane >> 4) * 8;
-      bf8 fa[FI], fb[FJ];
 #pragma unroll
-      for (int i = 0; i < FI; ++i) fa[i] = *(const bf8*)&As[wr * (TM_ / 2) + i * 16 + (lane & 15)][kc];
+      for (int kk = 0; kk < BK; kk += 32) {
+        const int kc = kk + (lane >> 4) * 8;
+        bf8 fa[FI], fb[FJ];
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) fb[j] = *(const bf8*)&Bs[wc * (TN_ / 2) + j * 16 + (lane & 15)][kc];
+        for (int i = 0; i < FI; ++i) fa[i] = *(const bf8*)&As[wr * (TM_ / 2) + i * 16 + (lane & 15)][kc];
 #pragma unroll
-      for (int i = 0; i < FI; ++i)
+        for (int j = 0; j < FJ; ++j) fb[j] = *(const bf8*)&Bs[wc * (TN_ / 2) + j * 16 + (lane & 15)][kc];
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int j = 0; j < FJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int ks = 0; ks < BK; ks += 4) {
