@@ -348,3 +348,21 @@ def test_bias_ops_cell_kernel_gpu(shape):
     out = torch.clamp(norm * ch(g) + ch(b), min=0)
     assert torch.allclose(got["norm"].double().cpu(), norm.reshape(N, -1), rtol=1e-12, atol=1e-12)
     assert torch.allclose(got["out"].double().cpu(), out.reshape(N, -1), rtol=1e-12, atol=1e-12)
+
+
+def test_conv2d_bias_add_rewrite():
+    """bias_add(conv2d(..)) becomes one conv2d with a bias operand (reference DnnOp
+    CONV2D_BIAS_ADD) when the convolution has no other consumer; results are unchanged."""
+    src = """
+o = conv2d(X, W, input_shape=[4,2,6,6], filter_shape=[3,2,3,3], stride=[1,1], padding=[1,1])
+o = bias_add(o, b)
+s = sum(o)
+"""
+    rng = np.random.default_rng(2)
+    ins = {"X": rng.random((4, 72)), "W": rng.random((3, 18)) - 0.5, "b": rng.random((3, 1))}
+    cs = EX.compile_script(src, {}, inputs=ins, outputs=["o", "s"], config=DMLConfig(gpu=False))
+    assert cs.cp.rewrite_stats.get("conv2d-bias-add") == 1
+    res, _ = EX.execute(cs, ins)
+    cs0 = EX.compile_script(src, {}, inputs=ins, outputs=["o", "s"], config=DMLConfig(gpu=False, rewrites=False))
+    ref, _ = EX.execute(cs0, ins)
+    assert torch.allclose(res["o"], ref["o"], rtol=1e-12, atol=1e-12)
