@@ -378,12 +378,28 @@ UN = {
     "sin": torch.sin, "cos": torch.cos, "tan": torch.tan,
     "asin": torch.asin, "acos": torch.acos, "atan": torch.atan,
     "sinh": torch.sinh, "cosh": torch.cosh, "tanh": torch.tanh,
+    "cumsum": lambda x: _cum("cumsum", x),
+    "cumprod": lambda x: _cum("cumprod", x),
+    "cummin": lambda x: _cum("cummin", x),
+    "cummax": lambda x: _cum("cummax", x),
+    "sigmoid": torch.sigmoid,
+}
+
+_CUM_HOST = {
     "cumsum": lambda x: torch.cumsum(x, dim=0),
     "cumprod": lambda x: torch.cumprod(x, dim=0),
     "cummin": lambda x: torch.cummin(x, dim=0).values,
     "cummax": lambda x: torch.cummax(x, dim=0).values,
-    "sigmoid": torch.sigmoid,
 }
+
+
+def _cum(op, x):
+    """Column-wise cumulative aggregates: device matrices take the chunked HIP scan
+    (ops/hip/scan.hip), host matrices torch's."""
+    if x.is_cuda and backend.use_kernels:
+        from . import kernels
+        return kernels.cumagg(op, x)
+    return _CUM_HOST[op](x)
 
 
 def unary(op, x):

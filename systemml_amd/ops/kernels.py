@@ -108,6 +108,11 @@ def load(required=False):
                               ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     L.sysml_mwide_occupancy.restype = ctypes.c_int
     L.sysml_mwide_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.sysml_cumagg_chunks.restype = ctypes.c_int64
+    L.sysml_cumagg_chunks.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+    L.sysml_cumagg.restype = ctypes.c_int
+    L.sysml_cumagg.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
     _lib = L
     return L
 
@@ -821,6 +826,34 @@ def relu_backward(X, D):
     if rc != 0:
         raise RuntimeError(f"sysml_relu_backward failed: {rc}")
     _count("relu_backward")
+    return out
+
+
+# ----------------------------------------------------------------------------
+# Column-wise cumulative aggregates (ops/hip/scan.hip)
+# ----------------------------------------------------------------------------
+_CUM = {"cumsum": 0, "cumprod": 1, "cummin": 2, "cummax": 3}
+
+
+def cumagg(op, X):
+    """cumsum / cumprod / cummin / cummax down the rows of a device matrix (three-phase chunked
+    scan).  bf16 inputs scan in fp32."""
+    L = load(required=True)
+    if X.dtype not in (torch.float32, torch.float64):
+        X = X.float()
+    X = X.contiguous()
+    N, D = X.shape
+    out = torch.empty_like(X)
+    if N == 0 or D == 0:
+        return out
+    rows = ctypes.c_int64(0)
+    nchunk = L.sysml_cumagg_chunks(N, D, ctypes.byref(rows))
+    tot = torch.empty((nchunk, D), dtype=X.dtype, device=X.device)
+    rc = L.sysml_cumagg(0 if X.dtype == torch.float32 else 1, _CUM[op], X.data_ptr(), out.data_ptr(),
+                        tot.data_ptr(), N, D, nchunk, rows.value, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_cumagg failed: {rc}")
+    _count(op)
     return out
 
 
