@@ -4,14 +4,15 @@
 //
 // Three phases over row chunks, so that a tall matrix keeps the whole chip busy:
 //   A  every workgroup reduces its chunk of rows (per column) to one value      -> tot[chunk][col]
-//   B  per column, an exclusive scan of the chunk totals (sequential, <= a few thousand chunks)
+//   B  per column, an exclusive scan of the chunk totals
 //   C  every workgroup rescans its chunk from that offset and writes the result
 // Two thread mappings:
 //   wide   (D >= 64): a 64-column strip per workgroup, lane = column (each row read by the wave is
 //          one contiguous 256-B segment for fp32), the 4 waves take consecutive quarters of the
 //          chunk's rows and combine their partial results through LDS;
-//   narrow (D <  64): one column per workgroup row range, 4 consecutive elements per thread, a
+//   narrow (D <  64): one column per workgroup row range, 8 consecutive elements per thread, a
 //          wave-level inclusive scan by __shfl_up and a block level through LDS.
+// Phase B runs one workgroup per column over the chunk totals with the same block scan.
 // min / max propagate NaN like torch.cummin / cummax; sums accumulate in the element type.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -38,6 +39,7 @@ __device__ __forceinline__ T comb(T a, T b) {
 }
 
 constexpr int NT = 256;
+constexpr int UNR = 8;
 
 // ---- wide mapping ---------------------------------------------------------------------------
 // grid (nchunk, ceil(D / 64)); chunk = `rows` rows; PHASE 0: totals, 1: rescan with offsets
@@ -53,8 +55,18 @@ __global__ void __launch_bounds__(NT) wide_kernel(const T* __restrict__ X, T* __
   const int64_t w0 = min(r1, r0 + q * wave), w1 = min(r1, w0 + q);
   const bool live = col < D;
   T acc = ident<T, OP>();
-  if (live)
-    for (int64_t r = w0; r < w1; ++r) acc = comb<T, OP>(acc, X[r * D + col]);
+  if (live) {
+    // UNR independent row loads in flight per lane before they are combined in order
+    int64_t r = w0;
+    for (; r + UNR <= w1; r += UNR) {
+      T v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) v[u] = X[(r + u) * D + col];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) acc = comb<T, OP>(acc, v[u]);
+    }
+    for (; r < w1; ++r) acc = comb<T, OP>(acc, X[r * D + col]);
+  }
   part[wave][lane] = acc;
   __syncthreads();
   if (PHASE == 0) {
@@ -69,14 +81,26 @@ __global__ void __launch_bounds__(NT) wide_kernel(const T* __restrict__ X, T* __
   if (!live) return;
   T run = tot[(int64_t)blockIdx.x * D + col];          // exclusive offset of this chunk (phase B)
   for (int w = 0; w < wave; ++w) run = comb<T, OP>(run, part[w][lane]);
-  for (int64_t r = w0; r < w1; ++r) {
+  int64_t r = w0;
+  for (; r + UNR <= w1; r += UNR) {
+    T v[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) v[u] = X[(r + u) * D + col];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      run = comb<T, OP>(run, v[u]);
+      Y[(r + u) * D + col] = run;
+    }
+  }
+  for (; r < w1; ++r) {
     run = comb<T, OP>(run, X[r * D + col]);
     Y[r * D + col] = run;
   }
 }
 
-// ---- narrow mapping -------------------------------------------------------------------------
-// grid (nchunk, D); chunk = NT * 4 rows of one column
+// ---- block scan of E consecutive values per thread (narrow mapping and phase B) ------------
+constexpr int E = 8;            // values per thread: NT * E = 2048 rows per narrow chunk
+
 template <typename T, int OP>
 __device__ __forceinline__ T wave_incl_scan(T v, int lane) {
 #pragma unroll
@@ -87,49 +111,68 @@ __device__ __forceinline__ T wave_incl_scan(T v, int lane) {
   return v;
 }
 
+// v[] -> inclusive prefixes within the thread; returns the exclusive prefix of this thread inside
+// the workgroup and sets *total to the workgroup's total.  wsum: 4 LDS slots.
+template <typename T, int OP>
+__device__ __forceinline__ T block_scan(T (&v)[E], T* wsum, T* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 1; i < E; ++i) v[i] = comb<T, OP>(v[i - 1], v[i]);
+  const T incl = wave_incl_scan<T, OP>(v[E - 1], lane);
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  T pre = ident<T, OP>();
+  for (int w = 0; w < wave; ++w) pre = comb<T, OP>(pre, wsum[w]);
+  const T excl = __shfl_up(incl, 1, 64);
+  if (lane > 0) pre = comb<T, OP>(pre, excl);
+  T t = wsum[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) t = comb<T, OP>(t, wsum[w]);
+  *total = t;
+  return pre;
+}
+
+// ---- narrow mapping -------------------------------------------------------------------------
+// grid (nchunk, D); chunk = NT * E rows of one column
 template <typename T, int OP, int PHASE>
 __global__ void __launch_bounds__(NT) narrow_kernel(const T* __restrict__ X, T* __restrict__ Y, T* __restrict__ tot,
                                                     int64_t N, int D) {
   __shared__ T wsum[4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = blockIdx.y;
-  const int64_t base = (int64_t)blockIdx.x * (NT * 4) + threadIdx.x * 4;
-  T v[4];
+  const int64_t base = (int64_t)blockIdx.x * (NT * E) + threadIdx.x * E;
+  T v[E];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = (base + i < N) ? X[(base + i) * D + col] : ident<T, OP>();
-#pragma unroll
-  for (int i = 1; i < 4; ++i) v[i] = comb<T, OP>(v[i - 1], v[i]);
-  const T incl = wave_incl_scan<T, OP>(v[3], lane);  // inclusive over this wave's threads
-  if (lane == 63) wsum[wave] = incl;
-  __syncthreads();
+  for (int i = 0; i < E; ++i) v[i] = (base + i < N) ? X[(base + i) * D + col] : ident<T, OP>();
+  T total;
+  T pre = block_scan<T, OP>(v, wsum, &total);
   if (PHASE == 0) {
-    if (threadIdx.x == 0) {
-      T t = wsum[0];
-#pragma unroll
-      for (int w = 1; w < 4; ++w) t = comb<T, OP>(t, wsum[w]);
-      tot[(int64_t)blockIdx.x * D + col] = t;
-    }
+    if (threadIdx.x == 0) tot[(int64_t)blockIdx.x * D + col] = total;
     return;
   }
-  T pre = tot[(int64_t)blockIdx.x * D + col];          // chunk offset (phase B)
-  for (int w = 0; w < wave; ++w) pre = comb<T, OP>(pre, wsum[w]);
-  const T excl = __shfl_up(incl, 1, 64);
-  if (lane > 0) pre = comb<T, OP>(pre, excl);
+  pre = comb<T, OP>(tot[(int64_t)blockIdx.x * D + col], pre);   // chunk offset (phase B)
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < E; ++i)
     if (base + i < N) Y[(base + i) * D + col] = comb<T, OP>(pre, v[i]);
 }
 
-// ---- phase B: exclusive scan of the chunk totals per column --------------------------------
+// ---- phase B: exclusive scan of the chunk totals, one workgroup per column -----------------
 template <typename T, int OP>
 __global__ void __launch_bounds__(NT) offsets_kernel(T* __restrict__ tot, int64_t nchunk, int D) {
-  const int col = blockIdx.x * NT + threadIdx.x;
-  if (col >= D) return;
-  T run = ident<T, OP>();
-  for (int64_t c = 0; c < nchunk; ++c) {
-    const T t = tot[c * D + col];
-    tot[c * D + col] = run;
-    run = comb<T, OP>(run, t);
+  __shared__ T wsum[2][4];
+  const int col = blockIdx.x;
+  T carry = ident<T, OP>();
+  int it = 0;
+  for (int64_t b0 = 0; b0 < nchunk; b0 += NT * E, ++it) {
+    const int64_t base = b0 + threadIdx.x * E;
+    T v[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = (base + i < nchunk) ? tot[(base + i) * D + col] : ident<T, OP>();
+    T total;
+    const T pre = comb<T, OP>(carry, block_scan<T, OP>(v, wsum[it & 1], &total));
+#pragma unroll
+    for (int i = 0; i < E; ++i)     // exclusive: the prefix before element i
+      if (base + i < nchunk) tot[(base + i) * D + col] = i == 0 ? pre : comb<T, OP>(pre, v[i - 1]);
+    carry = comb<T, OP>(carry, total);
   }
 }
 
@@ -138,12 +181,12 @@ int launch(const T* X, T* Y, T* tot, int64_t N, int D, int64_t nchunk, int64_t r
   if (D >= 64) {
     const dim3 g((unsigned)nchunk, (unsigned)((D + 63) / 64));
     hipLaunchKernelGGL((wide_kernel<T, OP, 0>), g, dim3(NT), 0, s, X, Y, tot, N, D, rows);
-    hipLaunchKernelGGL((offsets_kernel<T, OP>), dim3((D + NT - 1) / NT), dim3(NT), 0, s, tot, nchunk, D);
+    hipLaunchKernelGGL((offsets_kernel<T, OP>), dim3(D), dim3(NT), 0, s, tot, nchunk, D);
     hipLaunchKernelGGL((wide_kernel<T, OP, 1>), g, dim3(NT), 0, s, X, Y, tot, N, D, rows);
   } else {
     const dim3 g((unsigned)nchunk, (unsigned)D);
     hipLaunchKernelGGL((narrow_kernel<T, OP, 0>), g, dim3(NT), 0, s, X, Y, tot, N, D);
-    hipLaunchKernelGGL((offsets_kernel<T, OP>), dim3((D + NT - 1) / NT), dim3(NT), 0, s, tot, nchunk, D);
+    hipLaunchKernelGGL((offsets_kernel<T, OP>), dim3(D), dim3(NT), 0, s, tot, nchunk, D);
     hipLaunchKernelGGL((narrow_kernel<T, OP, 1>), g, dim3(NT), 0, s, X, Y, tot, N, D);
   }
   return (int)hipGetLastError();
@@ -165,7 +208,7 @@ int64_t sysml_cumagg_chunks(int64_t N, int D, int64_t* rows) {
     *rows = r;
     return (N + r - 1) / r;
   }
-  *rows = sysml_scan::NT * 4;
+  *rows = sysml_scan::NT * sysml_scan::E;
   return (N + *rows - 1) / *rows;
 }
 
