@@ -24,6 +24,7 @@ import ctypes
 import hashlib
 import os
 import tempfile
+import time
 
 import torch
 
@@ -349,6 +350,7 @@ def compile_source(src, arch):
             return f.read()
     except OSError:
         pass
+    t0 = time.perf_counter()
     handle, size = ctypes.c_void_p(), ctypes.c_size_t()
     log = ctypes.create_string_buffer(8192)
     rc = L.sysml_rtc_compile(src.encode(), b"sysml_cell.hip", arch.encode(), ctypes.byref(handle),
@@ -361,6 +363,7 @@ def compile_source(src, arch):
         raise RuntimeError(f"hipRTC code retrieval failed ({rc})")
     code = buf.raw
     stats["rtc_compiled"] += 1
+    stats["rtc_compile_s"] = stats.get("rtc_compile_s", 0.0) + time.perf_counter() - t0
     try:
         os.makedirs(RTC_DIR, exist_ok=True)
         tmp = f"{path}.{os.getpid()}.tmp"

@@ -4,7 +4,8 @@ Records per-opcode counts and wall time (heavy hitters; on a GPU backend every i
 is synchronised before it is timed, so the times are execution and not launch times unless
 sync=False is requested), compile / execute time, dynamic-recompilation and buffer-pool
 counters, host<->HBM transfers made by the CP/GPU placement (count, bytes, time), the
-caching allocator's HBM statistics and the invocation counts of the in-tree HIP kernels."""
+caching allocator's HBM statistics, the generated (codegen) operators' launch and hipRTC
+compile / cache counts and the invocation counts of the in-tree HIP kernels."""
 from __future__ import annotations
 
 import time
@@ -69,6 +70,12 @@ def gpu_report():
                    f"{ms.get('allocated_bytes.all.peak', 0) / 1e9:.2f} / {ms.get('reserved_bytes.all.current', 0) / 1e9:.2f}")
         out.append(f"HBM allocations / frees / alloc retries:\t{ms.get('allocation.all.allocated', 0)} / "
                    f"{ms.get('allocation.all.freed', 0)} / {ms.get('num_alloc_retries', 0)}")
+    from ..ops import cell, outer, rowgen
+    cg = [f"{name}.{k}={round(v, 3) if isinstance(v, float) else v}"
+          for name, st in (("cell", cell.stats), ("row", rowgen.stats), ("outer", outer.stats))
+          for k, v in sorted(st.items()) if v]
+    if cg:                                      # Statistics.java "Codegen compile / class cache" lines
+        out.append("Codegen operators (launches, hipRTC compiles / cache hits):\t" + ", ".join(cg))
     from ..ops import kernels as K
     if K.counters:
         out.append("HIP kernel invocations:\t" + ", ".join(f"{k}={v}" for k, v in sorted(K.counters.items())))
