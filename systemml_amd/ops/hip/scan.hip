@@ -134,15 +134,31 @@ __device__ __forceinline__ T block_scan(T (&v)[E], T* wsum, T* total) {
 
 // ---- narrow mapping -------------------------------------------------------------------------
 // grid (nchunk, D); chunk = NT * E rows of one column
-template <typename T, int OP, int PHASE>
+// VEC (a single 16-B aligned column): the thread's E consecutive values move as 16-B vectors
+template <typename T>
+using vec16 = T __attribute__((ext_vector_type(16 / sizeof(T))));
+
+template <typename T, int OP, int PHASE, bool VEC>
 __global__ void __launch_bounds__(NT) narrow_kernel(const T* __restrict__ X, T* __restrict__ Y, T* __restrict__ tot,
                                                     int64_t N, int D) {
+  constexpr int W = 16 / sizeof(T);
   __shared__ T wsum[4];
   const int col = blockIdx.y;
   const int64_t base = (int64_t)blockIdx.x * (NT * E) + threadIdx.x * E;
+  const bool full = VEC && base + E <= N;
   T v[E];
+  if (full) {
+    const vec16<T>* p = reinterpret_cast<const vec16<T>*>(X + base);
 #pragma unroll
-  for (int i = 0; i < E; ++i) v[i] = (base + i < N) ? X[(base + i) * D + col] : ident<T, OP>();
+    for (int j = 0; j < E / W; ++j) {
+      const vec16<T> q = p[j];
+#pragma unroll
+      for (int k = 0; k < W; ++k) v[j * W + k] = q[k];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = (base + i < N) ? X[(base + i) * D + col] : ident<T, OP>();
+  }
   T total;
   T pre = block_scan<T, OP>(v, wsum, &total);
   if (PHASE == 0) {
@@ -150,6 +166,17 @@ __global__ void __launch_bounds__(NT) narrow_kernel(const T* __restrict__ X, T* 
     return;
   }
   pre = comb<T, OP>(tot[(int64_t)blockIdx.x * D + col], pre);   // chunk offset (phase B)
+  if (full) {
+    vec16<T>* p = reinterpret_cast<vec16<T>*>(Y + base);
+#pragma unroll
+    for (int j = 0; j < E / W; ++j) {
+      vec16<T> q;
+#pragma unroll
+      for (int k = 0; k < W; ++k) q[k] = comb<T, OP>(pre, v[j * W + k]);
+      p[j] = q;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < E; ++i)
     if (base + i < N) Y[(base + i) * D + col] = comb<T, OP>(pre, v[i]);
@@ -185,9 +212,16 @@ int launch(const T* X, T* Y, T* tot, int64_t N, int D, int64_t nchunk, int64_t r
     hipLaunchKernelGGL((wide_kernel<T, OP, 1>), g, dim3(NT), 0, s, X, Y, tot, N, D, rows);
   } else {
     const dim3 g((unsigned)nchunk, (unsigned)D);
-    hipLaunchKernelGGL((narrow_kernel<T, OP, 0>), g, dim3(NT), 0, s, X, Y, tot, N, D);
+    const bool vec = D == 1 && ((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0;
+    if (vec)
+      hipLaunchKernelGGL((narrow_kernel<T, OP, 0, true>), g, dim3(NT), 0, s, X, Y, tot, N, D);
+    else
+      hipLaunchKernelGGL((narrow_kernel<T, OP, 0, false>), g, dim3(NT), 0, s, X, Y, tot, N, D);
     hipLaunchKernelGGL((offsets_kernel<T, OP>), dim3(D), dim3(NT), 0, s, tot, nchunk, D);
-    hipLaunchKernelGGL((narrow_kernel<T, OP, 1>), g, dim3(NT), 0, s, X, Y, tot, N, D);
+    if (vec)
+      hipLaunchKernelGGL((narrow_kernel<T, OP, 1, true>), g, dim3(NT), 0, s, X, Y, tot, N, D);
+    else
+      hipLaunchKernelGGL((narrow_kernel<T, OP, 1, false>), g, dim3(NT), 0, s, X, Y, tot, N, D);
   }
   return (int)hipGetLastError();
 }
