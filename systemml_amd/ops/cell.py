@@ -245,9 +245,10 @@ def _cases(vals):
     return expr
 
 
-def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant):
+def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant, idx32=False):
     """HIP source of the fused kernel: the program as straight-line code over the cell values
-    of its inputs, instantiated into the flat / row / column kernel template."""
+    of its inputs, instantiated into the flat / row / column kernel template.  idx32: the
+    operand has < 2^31 cells (32-bit row / column arithmetic)."""
     ct = "float" if T == torch.float32 else "double"
     var = [f"x[{k}]" for k in range(prog.n_in)] + [None] * (NR - prog.n_in)
     body = []
@@ -272,6 +273,7 @@ struct Spec {{
   static constexpr int NIN = {prog.n_in};
   static constexpr int AGGOP = {aggop};
   static constexpr int NEED_IJ = {need_ij};
+  static constexpr int IDX32 = {int(bool(idx32))};
   static constexpr int mode(int k) {{ return {_cases(modes)}; }}
   static constexpr int dt(int k) {{ return {_cases(dts)}; }}
   static constexpr int vec(int k) {{ return {_cases(vecs)}; }}
@@ -375,13 +377,13 @@ def compile_source(src, arch):
     return code
 
 
-def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev):
-    key = (prog.key(), T, modes, dts, vecs, mode, variant, str(dev))
+def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, idx32=False):
+    key = (prog.key(), T, modes, dts, vecs, mode, variant, str(dev), idx32)
     f = _rtc_funcs.get(key, False)
     if f is not False:
         return f
     try:
-        code = compile_source(generate(prog, T, modes, dts, vecs, mode, variant), gpu_arch(dev))
+        code = compile_source(generate(prog, T, modes, dts, vecs, mode, variant, idx32), gpu_arch(dev))
         L = _rtc_lib()
         fn = ctypes.c_void_p()
         cbuf = ctypes.create_string_buffer(code, len(code))
@@ -539,7 +541,7 @@ def _make_plan(prog, args):
             variant = 8 if Cc <= 8 else 64
         else:
             variant = 0
-        f = _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev)
+        f = _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, R * Cc < 2 ** 31)
         if f is not None:
             pl.fn = f[0]
             if mode == 3:
@@ -697,6 +699,7 @@ struct Spec {{
   static constexpr int NIN = {m.n_in};
   static constexpr int NOUT = {len(m.progs)};
   static constexpr int NEED_IJ = {need_ij};
+  static constexpr int IDX32 = 0;
   static constexpr int mode(int k) {{ return {_cases(modes)}; }}
   static constexpr int dt(int k) {{ return {_cases(dts)}; }}
   static constexpr int vec(int k) {{ return {_cases(vecs)}; }}

@@ -460,6 +460,25 @@ __global__ void __launch_bounds__(256) bias_op(const T* __restrict__ X, const T*
   }
 }
 
+// P % 4 == 0: the whole N x (C*P) operand as 4-wide vectors (never straddling a channel), one
+// vector per thread -- 16-B (fp32) / 32-B (fp64) accesses instead of one scalar per thread
+template <typename T>
+__global__ void __launch_bounds__(256) bias_op_v4(const T* __restrict__ X, const T* __restrict__ b, T* __restrict__ O,
+                                                   int64_t nvec, int C, int P4, int mult, int relu) {
+  typedef T V __attribute__((ext_vector_type(4)));
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nvec) return;
+  const int ch = (int)((i / P4) % C);
+  const T bv = b ? b[ch] : (mult ? T(1) : T(0));
+  V v = reinterpret_cast<const V*>(X)[i];
+  v = mult ? v * bv : v + bv;
+  if (relu) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = v[k] > T(0) ? v[k] : T(0);
+  }
+  reinterpret_cast<V*>(O)[i] = v;
+}
+
 inline dim3 bias_grid(int64_t rows_ch, int P) {
   int64_t gy = (P + 255) / 256;
   if (gy > 1024) gy = 1024;
@@ -605,6 +624,19 @@ int sysml_bias_op(int dtype, const void* X, const void* b, void* out, int64_t to
   using namespace sysml_dnn;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (P <= 0 || total % P) return -1;
+  const bool v4 = P % 4 == 0 && (uintptr_t)X % (dtype == 1 ? 16 : 32) == 0 &&
+                  (uintptr_t)out % (dtype == 1 ? 16 : 32) == 0 && total / 4 < (int64_t)0x7fffffff * 256;
+  if (v4 && (dtype == 1 || dtype == 2)) {
+    const int64_t nvec = total / 4;
+    const dim3 g((unsigned)((nvec + 255) / 256));
+    if (dtype == 1)
+      hipLaunchKernelGGL(bias_op_v4<float>, g, dim3(256), 0, s, (const float*)X, (const float*)b, (float*)out, nvec, C,
+                         P / 4, mult, relu);
+    else
+      hipLaunchKernelGGL(bias_op_v4<double>, g, dim3(256), 0, s, (const double*)X, (const double*)b, (double*)out, nvec,
+                         C, P / 4, mult, relu);
+    return (int)hipGetLastError();
+  }
   const dim3 bg = bias_grid(total / P, P);
   if (dtype == 1)
     hipLaunchKernelGGL(bias_op<float>, bg, dim3(256), 0, s, (const float*)X, (const float*)b, (float*)out, C, P, mult,

@@ -333,7 +333,7 @@ def test_bias_ops_fuse_with_cellwise_chains():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(6, 10, 9), (32, 64, 3136), (3, 7, 1)])
+@pytest.mark.parametrize("shape", [(6, 10, 9), (32, 64, 3136), (3, 7, 1), (5, 3, 2), (7, 1, 1), (3, 5, 6)])
 def test_bias_ops_cell_kernel_gpu(shape):
     from systemml_amd.ops import kernels
     N, C, HW = shape

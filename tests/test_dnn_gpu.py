@@ -97,19 +97,24 @@ def test_pooling_kernels(cfg, dt):
         np.testing.assert_allclose(gx.double().cpu().numpy(), x.grad.reshape(N, -1).numpy(), rtol=tol, atol=tol)
 
 
-def test_bias_and_relu_backward_kernels():
+@pytest.mark.parametrize("P", [10, 12, 49, 3136])      # P % 4 == 0: the 4-wide vector kernel
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_bias_and_relu_backward_kernels(P, dt):
     from systemml_amd.ops import kernels as Kn
-    g = torch.Generator().manual_seed(3)
-    X = torch.randn(6, 4 * 10, generator=g, dtype=torch.float64)
+    g = torch.Generator().manual_seed(3 + P)
+    X = torch.randn(6, 4 * P, generator=g, dtype=torch.float64)
     b = torch.randn(4, 1, generator=g, dtype=torch.float64)
-    D = torch.randn(6, 40, generator=g, dtype=torch.float64)
+    D = torch.randn(6, 4 * P, generator=g, dtype=torch.float64)
     dev = torch.device("cuda:0")
-    xr = X.reshape(6, 4, 10)
-    np.testing.assert_allclose(Kn.bias_op(X.to(dev), b.to(dev)).cpu().numpy(),
-                               (xr + b.reshape(1, 4, 1)).reshape(6, -1).numpy())
-    np.testing.assert_allclose(Kn.bias_op(X.to(dev), b.to(dev), mult=True).cpu().numpy(),
-                               (xr * b.reshape(1, 4, 1)).reshape(6, -1).numpy())
-    np.testing.assert_allclose(Kn.relu_backward(X.to(dev), D.to(dev)).cpu().numpy(), (D * (X > 0)).numpy())
+    xr = X.reshape(6, 4, P)
+    Xd, bd = X.to(dev, dt), b.to(dev, dt)
+    tol = 1e-15 if dt == torch.float64 else 1e-6
+    np.testing.assert_allclose(Kn.bias_op(Xd, bd).double().cpu().numpy(),
+                               (xr + b.reshape(1, 4, 1)).reshape(6, -1).numpy(), rtol=tol, atol=tol)
+    np.testing.assert_allclose(Kn.bias_op(Xd, bd, mult=True).double().cpu().numpy(),
+                               (xr * b.reshape(1, 4, 1)).reshape(6, -1).numpy(), rtol=tol, atol=tol)
+    np.testing.assert_allclose(Kn.relu_backward(Xd, D.to(dev, dt)).double().cpu().numpy(), (D * (X > 0)).numpy(),
+                               rtol=tol, atol=tol)
 
 
 def test_lenet_builtins_use_hip_kernels_end_to_end():

@@ -1,0 +1,8 @@
+#!/bin/bash
+# per-channel kernels: GPU tests (dnn bias_op + generated CHAN cell kernels), kbench, ResNet
+R=$GRAFT_REPO_ROOT
+cd $R
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_dnn_gpu.py tests/test_codegen.py tests/test_scan_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_bias.log 2>&1 || exit $?
+timeout -k 10 200 python tools/bench_bias.py > gpurun_out/bias_kbench.log 2>&1 || exit $?
+timeout -k 10 300 python bench_resnet50.py --steps 4 --warmup 2 > gpurun_out/resnet256.log 2>&1
