@@ -369,16 +369,19 @@ struct Pool {
   int avg;
 };
 
-template <typename T>
+// I: index type of the flat cell loops (int below 2^31 cells: 32-bit divisions instead of the
+// emulated 64-bit ones)
+template <typename T, typename I>
 __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
   const T* __restrict__ X = (const T*)p.X;
   T* __restrict__ O = (T*)p.out;
-  const int64_t total = (int64_t)p.N * p.C * p.Ho * p.Wo;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int ow = (int)(i % p.Wo);
-    const int oh = (int)((i / p.Wo) % p.Ho);
-    const int64_t nc = i / ((int64_t)p.Wo * p.Ho);
-    const T* x = X + nc * p.H * p.W;
+  const I total = (I)p.N * p.C * p.Ho * p.Wo;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    const I q = i / p.Wo;
+    const int ow = (int)(i - q * p.Wo);
+    const I nc = q / p.Ho;
+    const int oh = (int)(q - nc * p.Ho);
+    const T* x = X + (int64_t)nc * p.H * p.W;
     const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
     T m = p.avg ? T(0) : -INFINITY;
     for (int a = 0; a < p.KH; ++a) {
@@ -396,20 +399,55 @@ __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
   }
 }
 
+// max pooling backward, pass 1: position (a * KW + b) of each window's first maximum (row-major
+// scan, as the forward pass), 255 for a window without a cell above -inf
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__ idx) {
+  const T* __restrict__ X = (const T*)p.X;
+  const I total = (I)p.N * p.C * p.Ho * p.Wo;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    const I q = i / p.Wo;
+    const int ow = (int)(i - q * p.Wo);
+    const I nc = q / p.Ho;
+    const int oh = (int)(q - nc * p.Ho);
+    const T* x = X + (int64_t)nc * p.H * p.W;
+    const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
+    T m = -INFINITY;
+    int am = 255;
+    for (int a = 0; a < p.KH; ++a) {
+      const int h = h0 + a;
+      if (h < 0 || h >= p.H) continue;
+      for (int b = 0; b < p.KW; ++b) {
+        const int w = w0 + b;
+        if (w < 0 || w >= p.W) continue;
+        const T v = x[h * p.W + w];
+        if (v > m) {
+          m = v;
+          am = a * p.KW + b;
+        }
+      }
+    }
+    idx[i] = (uint8_t)am;
+  }
+}
+
 // dX[n,c,h,w] = sum over windows containing (h,w) of dout / (KH*KW) (avg) or of dout where
-// (h,w) is the window's first maximum (max) -- recomputed per window, no atomics
-template <typename T>
-__global__ void __launch_bounds__(256) pool_bwd(Pool p) {
+// (h,w) is the window's first maximum (max: from pass 1's positions, or recomputed per window
+// when no position buffer is given) -- a gather, no atomics
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) pool_bwd(Pool p, const uint8_t* __restrict__ idx) {
   const T* __restrict__ X = (const T*)p.X;
   const T* __restrict__ D = (const T*)p.D;
   T* __restrict__ O = (T*)p.out;
-  const int64_t total = (int64_t)p.N * p.C * p.H * p.W;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int w = (int)(i % p.W);
-    const int h = (int)((i / p.W) % p.H);
-    const int64_t nc = i / ((int64_t)p.W * p.H);
-    const T* x = X + nc * p.H * p.W;
-    const T* d = D + nc * p.Ho * p.Wo;
+  const I total = (I)p.N * p.C * p.H * p.W;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    const I q = i / p.W;
+    const int w = (int)(i - q * p.W);
+    const I nc = q / p.H;
+    const int h = (int)(q - nc * p.H);
+    const T* x = X + (int64_t)nc * p.H * p.W;
+    const T* d = D + (int64_t)nc * p.Ho * p.Wo;
+    const uint8_t* ix = idx ? idx + (int64_t)nc * p.Ho * p.Wo : nullptr;
     // output windows covering (h, w): oh*sh - ph <= h <= oh*sh - ph + KH - 1
     const int ohl = max(0, (h + p.ph - p.KH + p.sh) / p.sh), ohh = min(p.Ho - 1, (h + p.ph) / p.sh);
     const int owl = max(0, (w + p.pw - p.KW + p.sw) / p.sw), owh = min(p.Wo - 1, (w + p.pw) / p.sw);
@@ -422,7 +460,10 @@ __global__ void __launch_bounds__(256) pool_bwd(Pool p) {
         if (w < w0 || w >= w0 + p.KW) continue;
         const T dv = d[oh * p.Wo + ow];
         if (p.avg) { g += dv / T(p.KH * p.KW); continue; }
-        // first maximum of the window (row-major scan, as the forward pass)
+        if (ix) {
+          if (ix[oh * p.Wo + ow] == (h - h0) * p.KW + (w - w0)) g += dv;
+          continue;
+        }
         T m = -INFINITY;
         int ah = -1, aw = -1;
         for (int a = 0; a < p.KH; ++a) {
@@ -460,18 +501,27 @@ __global__ void __launch_bounds__(256) bias_op(const T* __restrict__ X, const T*
   }
 }
 
-// P % 4 == 0: the whole N x (C*P) operand as 4-wide vectors (never straddling a channel), one
-// vector per thread -- 16-B (fp32) / 32-B (fp64) accesses instead of one scalar per thread
-template <typename T>
+// the whole N x (C*P) operand as 4-wide vectors, one per thread -- 16-B (fp32) / 32-B (fp64)
+// accesses instead of one scalar per thread.  UNI (P % 4 == 0): a vector never straddles a channel
+// plane, one channel per vector; otherwise the channel of each of the 4 cells.
+template <typename T, bool UNI>
 __global__ void __launch_bounds__(256) bias_op_v4(const T* __restrict__ X, const T* __restrict__ b, T* __restrict__ O,
-                                                   int64_t nvec, int C, int P4, int mult, int relu) {
+                                                   int64_t nvec, int C, int P, int mult, int relu) {
   typedef T V __attribute__((ext_vector_type(4)));
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= nvec) return;
-  const int ch = (int)((i / P4) % C);
-  const T bv = b ? b[ch] : (mult ? T(1) : T(0));
   V v = reinterpret_cast<const V*>(X)[i];
-  v = mult ? v * bv : v + bv;
+  const T dflt = mult ? T(1) : T(0);
+  if (UNI) {
+    const T bv = b ? b[(int)((i / (P / 4)) % C)] : dflt;
+    v = mult ? v * bv : v + bv;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const T bv = b ? b[(int)(((i * 4 + k) / P) % C)] : dflt;
+      v[k] = mult ? v[k] * bv : v[k] + bv;
+    }
+  }
   if (relu) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = v[k] > T(0) ? v[k] : T(0);
@@ -506,6 +556,21 @@ inline int conv_tile(int dtype, int64_t M, int64_t Nc) {
   if (!(dtype == 0 || dtype == 3) || M < 128 || Nc < 128) return 64;
   return ((M + 127) / 128) * ((Nc + 127) / 128) >= 512 ? 128 : 64;
 }
+}  // namespace sysml_dnn
+
+namespace sysml_dnn {
+
+template <typename T, typename I>
+void pool_launch(const Pool& p, int backward, uint8_t* ws, hipStream_t s) {
+  const int64_t nin = (int64_t)p.N * p.C * p.H * p.W, nout = (int64_t)p.N * p.C * p.Ho * p.Wo;
+  if (!backward) {
+    hipLaunchKernelGGL((pool_fwd<T, I>), dim3(grid_for(nout)), dim3(256), 0, s, p);
+    return;
+  }
+  if (ws && !p.avg) hipLaunchKernelGGL((pool_argmax<T, I>), dim3(grid_for(nout)), dim3(256), 0, s, p, ws);
+  hipLaunchKernelGGL((pool_bwd<T, I>), dim3(grid_for(nin)), dim3(256), 0, s, p, p.avg ? nullptr : ws);
+}
+
 }  // namespace sysml_dnn
 
 extern "C" {
@@ -595,9 +660,10 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   return (int)hipGetLastError();
 }
 
-// dtype 1 fp32, 2 fp64; backward: D = dout, out = dX
-int sysml_pool2d(int dtype, int backward, int avg, const void* X, const void* D, void* out, int N, int C, int H,
-                 int W, int KH, int KW, int sh, int sw, int ph, int pw, void* stream) {
+// dtype 1 fp32, 2 fp64; backward: D = dout, out = dX; ws: N*C*Ho*Wo bytes for the window argmax
+// positions of max-pooling backward (nullptr: recomputed per covered window)
+int sysml_pool2d_ws(int dtype, int backward, int avg, const void* X, const void* D, void* out, void* ws, int N, int C,
+                    int H, int W, int KH, int KW, int sh, int sw, int ph, int pw, void* stream) {
   using namespace sysml_dnn;
   Pool p;
   p.X = X; p.D = D; p.out = out; p.N = N; p.C = C; p.H = H; p.W = W; p.KH = KH; p.KW = KW; p.sh = sh; p.sw = sw;
@@ -605,18 +671,25 @@ int sysml_pool2d(int dtype, int backward, int avg, const void* X, const void* D,
   p.Ho = (H + 2 * ph - KH) / sh + 1;
   p.Wo = (W + 2 * pw - KW) / sw + 1;
   if (p.Ho <= 0 || p.Wo <= 0) return -1;
+  if (KH * KW > 255) ws = nullptr;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t n = backward ? (int64_t)N * C * H * W : (int64_t)N * C * p.Ho * p.Wo;
+  const bool small = (int64_t)N * C * H * W < (1LL << 31) && (int64_t)N * C * p.Ho * p.Wo < (1LL << 31);
+  uint8_t* w8 = static_cast<uint8_t*>(ws);
   if (dtype == 1) {
-    if (backward) hipLaunchKernelGGL(pool_bwd<float>, dim3(grid_for(n)), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(pool_fwd<float>, dim3(grid_for(n)), dim3(256), 0, s, p);
+    if (small) pool_launch<float, int>(p, backward, w8, s);
+    else pool_launch<float, int64_t>(p, backward, w8, s);
   } else if (dtype == 2) {
-    if (backward) hipLaunchKernelGGL(pool_bwd<double>, dim3(grid_for(n)), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(pool_fwd<double>, dim3(grid_for(n)), dim3(256), 0, s, p);
+    if (small) pool_launch<double, int>(p, backward, w8, s);
+    else pool_launch<double, int64_t>(p, backward, w8, s);
   } else {
     return -1;
   }
   return (int)hipGetLastError();
+}
+
+int sysml_pool2d(int dtype, int backward, int avg, const void* X, const void* D, void* out, int N, int C, int H,
+                 int W, int KH, int KW, int sh, int sw, int ph, int pw, void* stream) {
+  return sysml_pool2d_ws(dtype, backward, avg, X, D, out, nullptr, N, C, H, W, KH, KW, sh, sw, ph, pw, stream);
 }
 
 int sysml_bias_op(int dtype, const void* X, const void* b, void* out, int64_t total, int C, int P, int mult, int relu,
@@ -624,17 +697,23 @@ int sysml_bias_op(int dtype, const void* X, const void* b, void* out, int64_t to
   using namespace sysml_dnn;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (P <= 0 || total % P) return -1;
-  const bool v4 = P % 4 == 0 && (uintptr_t)X % (dtype == 1 ? 16 : 32) == 0 &&
+  const bool v4 = total % 4 == 0 && (uintptr_t)X % (dtype == 1 ? 16 : 32) == 0 &&
                   (uintptr_t)out % (dtype == 1 ? 16 : 32) == 0 && total / 4 < (int64_t)0x7fffffff * 256;
   if (v4 && (dtype == 1 || dtype == 2)) {
     const int64_t nvec = total / 4;
     const dim3 g((unsigned)((nvec + 255) / 256));
-    if (dtype == 1)
-      hipLaunchKernelGGL(bias_op_v4<float>, g, dim3(256), 0, s, (const float*)X, (const float*)b, (float*)out, nvec, C,
-                         P / 4, mult, relu);
-    else
-      hipLaunchKernelGGL(bias_op_v4<double>, g, dim3(256), 0, s, (const double*)X, (const double*)b, (double*)out, nvec,
-                         C, P / 4, mult, relu);
+    const bool uni = P % 4 == 0;
+#define SYSML_BIAS_V4(TT, U)                                                                                  \
+  hipLaunchKernelGGL((bias_op_v4<TT, U>), g, dim3(256), 0, s, (const TT*)X, (const TT*)b, (TT*)out, nvec, C, P, \
+                     mult, relu)
+    if (dtype == 1) {
+      if (uni) SYSML_BIAS_V4(float, true);
+      else SYSML_BIAS_V4(float, false);
+    } else {
+      if (uni) SYSML_BIAS_V4(double, true);
+      else SYSML_BIAS_V4(double, false);
+    }
+#undef SYSML_BIAS_V4
     return (int)hipGetLastError();
   }
   const dim3 bg = bias_grid(total / P, P);

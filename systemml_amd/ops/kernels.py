@@ -67,6 +67,8 @@ def load(required=False):
         [ctypes.c_void_p]
     L.sysml_pool2d.restype = ctypes.c_int
     L.sysml_pool2d.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 10 + [ctypes.c_void_p]
+    L.sysml_pool2d_ws.restype = ctypes.c_int
+    L.sysml_pool2d_ws.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 4 + [ctypes.c_int] * 10 + [ctypes.c_void_p]
     L.sysml_bias_op.restype = ctypes.c_int
     L.sysml_bias_op.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -786,8 +788,11 @@ def pool2d(backward, avg, X, D, N, C, H, W, KH, KW, sh, sw, ph, pw):
     Ho = (H + 2 * ph - KH) // sh + 1
     Wo = (W + 2 * pw - KW) // sw + 1
     out = torch.empty((N, C * (H * W if backward else Ho * Wo)), dtype=dt, device=X.device)
-    rc = L.sysml_pool2d(code, int(bool(backward)), int(bool(avg)), X.data_ptr(), _ptr(D), out.data_ptr(),
-                        N, C, H, W, KH, KW, sh, sw, ph, pw, _stream())
+    # max-pooling backward: window argmax positions (one byte per window) found in a first pass
+    ws = torch.empty((N * C * Ho * Wo,), dtype=torch.uint8, device=X.device) \
+        if backward and not avg and KH * KW <= 255 else None
+    rc = L.sysml_pool2d_ws(code, int(bool(backward)), int(bool(avg)), X.data_ptr(), _ptr(D), out.data_ptr(),
+                           _ptr(ws), N, C, H, W, KH, KW, sh, sw, ph, pw, _stream())
     if rc == -1:
         return None
     if rc != 0:

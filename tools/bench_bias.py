@@ -53,6 +53,17 @@ def main():
         print(f"{f'{N}x{C}x{HW}':>18s} {t1:10.3f} {nb / t1 / 1e9:6.2f} {t2:9.3f} {nb / t2 / 1e9:6.2f} {t3:9.3f}",
               flush=True)
         del X
+    # the ResNet stem's 3x3 / stride-2 max pooling and its backward pass (argmax positions + gather)
+    for N in (64, 256):
+        C, H, Wd = 64, 112, 112
+        X = torch.randn((N, C * H * Wd), device="cuda")
+        Ho = (H + 2 - 3) // 2 + 1
+        G = torch.randn((N, C * Ho * Ho), device="cuda")
+        tf = timed(lambda: Kn.pool2d(False, False, X, None, N, C, H, Wd, 3, 3, 2, 2, 1, 1), a.reps)
+        tb = timed(lambda: Kn.pool2d(True, False, X, G, N, C, H, Wd, 3, 3, 2, 2, 1, 1), a.reps)
+        print(f"max_pool {N}x{C}x{H}x{Wd} k3 s2: fwd {tf:.3f} ms ({(X.numel() + G.numel()) * 4 / tf / 1e9:.2f} TB/s), "
+              f"bwd {tb:.3f} ms ({(2 * X.numel() + G.numel()) * 4 / tb / 1e9:.2f} TB/s)", flush=True)
+        del X, G
 
 
 if __name__ == "__main__":
