@@ -17,6 +17,6 @@ SYSML_DIST_BACKEND=gloo SYSML_DIST_DEVICE=cuda timeout -k 10 400 python -m torch
     --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --rows 2000000 --steps 3 \
     --warmup 1 --verbose > gpurun_out/bench_2rank.log 2>&1
 rc=$?; echo "bench 2rank rc=$rc $(date)" >> $P; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python bench_resnet50.py --batch 32 --steps 5 --warmup 2 > gpurun_out/resnet.log 2>&1
+timeout -k 10 300 python bench_resnet50.py --steps 5 --warmup 2 > gpurun_out/resnet.log 2>&1
 rc=$?; echo "resnet rc=$rc $(date)" >> $P
 exit $rc
