@@ -53,6 +53,18 @@ def main():
         print(f"{f'{N}x{C}x{HW}':>18s} {t1:10.3f} {nb / t1 / 1e9:6.2f} {t2:9.3f} {nb / t2 / 1e9:6.2f} {t3:9.3f}",
               flush=True)
         del X
+    # column aggregate of a per-channel cell program (batch-norm variance: colSums((X bias+ m)^2))
+    cprog = CellProgram([("b", "bias+", 2, 0, 1), ("b", "*", 2, 2, 2)], 2, 2, ("sum", "col"))
+    for N, C, HW in ((256, 64, 56 * 56), (256, 256, 14 * 14), (64, 64, 112 * 112)):
+        X = torch.randn((N, C * HW), device="cuda")
+        m = torch.randn((C, 1), device="cuda")
+        assert cell._kernel(cprog, [X, m]) is not None
+        tc = timed(lambda: cell._kernel(cprog, [X, m]), a.reps)
+        x3 = X.view(N, C, HW)
+        tt = timed(lambda: ((x3 + m.view(1, C, 1)) ** 2).sum(0), a.reps)
+        print(f"colagg {N}x{C}x{HW}: cell {tc:.3f} ms ({X.numel() * 4 / tc / 1e9:.2f} TB/s), torch {tt:.3f} ms",
+              flush=True)
+        del X
     # the ResNet stem's 3x3 / stride-2 max pooling and its backward pass (argmax positions + gather)
     for N in (64, 256):
         C, H, Wd = 64, 112, 112
