@@ -431,6 +431,46 @@ __global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__
   }
 }
 
+// max pooling backward, pass 2: one thread per stride band cell (nc, bh, bw) -- the sh x sw input
+// cells with (h + ph) / sh == bh and (w + pw) / sw == bw share their covering windows
+// oh in [bh - (KH-1-dh)/sh, bh] (dh = h + ph - bh*sh), so the index arithmetic is done once per
+// band instead of once per cell; each cell sums the dout of the windows whose argmax it is
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) pool_bwd_band(Pool p, const uint8_t* __restrict__ idx) {
+  const T* __restrict__ D = (const T*)p.D;
+  T* __restrict__ O = (T*)p.out;
+  const int Bh = (p.H + p.ph + p.sh - 1) / p.sh, Bw = (p.W + p.pw + p.sw - 1) / p.sw;
+  const I total = (I)p.N * p.C * Bh * Bw;
+  for (I t = (I)blockIdx.x * 256 + threadIdx.x; t < total; t += (I)gridDim.x * 256) {
+    const I q = t / Bw;
+    const int bw = (int)(t - q * Bw);
+    const I nc = q / Bh;
+    const int bh = (int)(q - nc * Bh);
+    const T* d = D + (int64_t)nc * p.Ho * p.Wo;
+    const uint8_t* ix = idx + (int64_t)nc * p.Ho * p.Wo;
+    T* o = O + (int64_t)nc * p.H * p.W;
+    for (int dh = 0; dh < p.sh; ++dh) {
+      const int h = bh * p.sh + dh - p.ph;
+      if (h < 0 || h >= p.H) continue;
+      const int ohl = dh <= p.KH - 1 ? max(0, bh - (p.KH - 1 - dh) / p.sh) : bh + 1;
+      const int ohh = min(bh, p.Ho - 1);
+      for (int dw = 0; dw < p.sw; ++dw) {
+        const int w = bw * p.sw + dw - p.pw;
+        if (w < 0 || w >= p.W) continue;
+        const int owl = dw <= p.KW - 1 ? max(0, bw - (p.KW - 1 - dw) / p.sw) : bw + 1;
+        const int owh = min(bw, p.Wo - 1);
+        T g = 0;
+        for (int oh = ohl; oh <= ohh; ++oh) {
+          const int rh = (bh - oh) * p.sh + dh;           // row of (h, w) inside window (oh, ow)
+          for (int ow = owl; ow <= owh; ++ow)
+            if (ix[oh * p.Wo + ow] == rh * p.KW + (bw - ow) * p.sw + dw) g += d[oh * p.Wo + ow];
+        }
+        o[h * p.W + w] = g;
+      }
+    }
+  }
+}
+
 // dX[n,c,h,w] = sum over windows containing (h,w) of dout / (KH*KW) (avg) or of dout where
 // (h,w) is the window's first maximum (max: from pass 1's positions, or recomputed per window
 // when no position buffer is given) -- a gather, no atomics
@@ -567,8 +607,13 @@ void pool_launch(const Pool& p, int backward, uint8_t* ws, hipStream_t s) {
     hipLaunchKernelGGL((pool_fwd<T, I>), dim3(grid_for(nout)), dim3(256), 0, s, p);
     return;
   }
-  if (ws && !p.avg) hipLaunchKernelGGL((pool_argmax<T, I>), dim3(grid_for(nout)), dim3(256), 0, s, p, ws);
-  hipLaunchKernelGGL((pool_bwd<T, I>), dim3(grid_for(nin)), dim3(256), 0, s, p, p.avg ? nullptr : ws);
+  if (ws && !p.avg) {
+    const int64_t bands = (int64_t)p.N * p.C * ((p.H + p.ph + p.sh - 1) / p.sh) * ((p.W + p.pw + p.sw - 1) / p.sw);
+    hipLaunchKernelGGL((pool_argmax<T, I>), dim3(grid_for(nout)), dim3(256), 0, s, p, ws);
+    hipLaunchKernelGGL((pool_bwd_band<T, I>), dim3(grid_for(bands)), dim3(256), 0, s, p, ws);
+    return;
+  }
+  hipLaunchKernelGGL((pool_bwd<T, I>), dim3(grid_for(nin)), dim3(256), 0, s, p, nullptr);
 }
 
 }  // namespace sysml_dnn
