@@ -95,6 +95,9 @@ def _min(a, b):
     if not isinstance(a, Tensor):
         a, b = b, a
     if not isinstance(b, Tensor):
+        b = float(b)
+        if b == b:          # clamp: no scalar tensor upload, vectorised; NaN cells of a stay NaN
+            return torch.clamp(a, max=b)
         b = torch.tensor(b, dtype=a.dtype, device=a.device)
     return torch.minimum(a, b)
 
@@ -103,6 +106,9 @@ def _max(a, b):
     if not isinstance(a, Tensor):
         a, b = b, a
     if not isinstance(b, Tensor):
+        b = float(b)
+        if b == b:          # e.g. relu's max(X, 0)
+            return torch.clamp(a, min=b)
         b = torch.tensor(b, dtype=a.dtype, device=a.device)
     return torch.maximum(a, b)
 
