@@ -71,18 +71,25 @@ def build_script(layers, input_shape, steps, batch):
     gen = dl._Gen(layers, input_shape)
     params = dl.trainable(gen.layers)
     sc = dl._solver_consts({"type": "momentum", "base_lr": 0.01, "momentum": 0.9, "weight_decay": 1e-4})
-    lines = gen.sources("momentum") + ["X = read($X)", "Y = read($Y)", "N = nrow(X)", f"bs = {batch}",
-                                       "lr0 = 0.01", "lr = lr0", "it = 0"]
+    # benchSync (registered by main): waits for the device and returns a host clock in ns.  The
+    # calls sit in their own basic blocks (inside `if`), so every operator of the step has been
+    # issued before the device is synchronised: a step's time is its completed device work.
+    lines = gen.sources("momentum") + [
+        'benchSync = externalFunction(Matrix[Double] A) return (Double t) implemented in (classname="sysml.bench.Sync")',
+        "X = read($X)", "Y = read($Y)", "N = nrow(X)", f"bs = {batch}", "lr0 = 0.01", "lr = lr0", "it = 0",
+        "t0 = 0", "t1 = 0"]
     lines += gen.init()
     lines += dl._opt_init("momentum", params)
-    lines += [f"for (i in 1:{steps}) {{", "  t0 = time()", "  beg = ((i - 1) * bs) %% N + 1",
+    lines += [f"for (i in 1:{steps}) {{", "  if (i > 0) {", "    t0 = benchSync(X)", "  }",
+              "  beg = ((i - 1) * bs) %% N + 1",
               "  end = min(N, beg + bs - 1)", "  Xb = X[beg:end, ]", "  Yb = Y[beg:end, ]"]
     lines += ["  " + c for c in gen.forward(train=True)]
     lines.append(f"  loss = {gen.loss_expr()}")
     lines += ["  " + c for c in gen.backward()]
     lines += [f"  {a} = {b}" for a, b in gen.bn_updates()]
     lines += dl._opt_update(sc, gen, params, "  ")
-    lines += ['  print("STEP " + i + " loss " + loss + " ns " + (time() - t0))', "}"]
+    lines += ["  if (i > 0) {", f"    t1 = benchSync({params[-1]})", "  }",
+              '  print("STEP " + i + " loss " + loss + " ns " + as.integer(t1 - t0))', "}"]
     return "\n".join(lines)
 
 
@@ -102,6 +109,13 @@ def main():
     from systemml_amd.conf import DMLConfig
     from systemml_amd.ops import kernels as K
     K.CONV_BF16_FP32 = not a.exact_fp32
+    from systemml_amd.runtime.udf import register_udf
+
+    def bench_sync(ctx, A):
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        return (float(time.perf_counter_ns()),)
+    register_udf("sysml.bench.Sync", bench_sync)
     layers = resnet50_layers(image=a.image)
     shape = (3, a.image, a.image)
     total = a.steps + a.warmup
