@@ -491,6 +491,16 @@ def _var(x, dim=None):
     return torch.var(x, dim=dim, keepdim=True)
 
 
+_COLSUM = []
+
+
+def _colsum_kernel(x):
+    from . import cell
+    if not _COLSUM:
+        _COLSUM.append(cell.CellProgram([], 1, 0, ("sum", "col")))
+    return cell._kernel(_COLSUM[0], [x])
+
+
 def agg(o, d, x):
     # fast path: dense host tensors (the CP backend's solver state) -- no representation checks
     if type(x) is Tensor and x.layout is _STRIDED and not x.is_cuda and x.dtype is not torch.bfloat16 \
@@ -536,6 +546,12 @@ def agg(o, d, x):
     if o == "sumsq" and backend.use_kernels and x.is_cuda and x.numel() >= 1 << 16 and d in ("all", "row", "col"):
         from . import kernels
         return kernels.sumsq(x, d)
+    if o == "sum" and d == "col" and backend.use_kernels and x.is_cuda and x.shape[1] >= 2048 and x.shape[0] > 1:
+        # wide column sums (e.g. the batch-norm channel sums): the generated column-aggregate
+        # kernel (fp64 accumulation, 8 rows in flight per lane) instead of torch's strided reduction
+        r = _colsum_kernel(x)
+        if r is not None:
+            return r
     x = cvt(x)
     if d == "all":
         if x.numel() == 0:
