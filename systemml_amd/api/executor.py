@@ -6,6 +6,7 @@ Used by the MLContext, JMLC, CLI and bench front ends."""
 from __future__ import annotations
 
 import os
+import sys
 import time
 
 import numpy as np
@@ -41,9 +42,16 @@ class CompiledScript:
         self.t_compile = t_compile
 
 
+_REC_LIMIT = 50000
+
+
 def compile_script(source, args=None, inputs=(), outputs=(), config=None, pydml=False, filename="",
                    base_dir=None):
     config = config or get_default_config()
+    # inlined layer libraries make one basic block of a whole training step (thousands of HOPs
+    # deep); the recursive DAG passes need more than Python's default 1000 frames
+    if sys.getrecursionlimit() < _REC_LIMIT:
+        sys.setrecursionlimit(_REC_LIMIT)
     t0 = time.perf_counter()
     prog = parse(source, pydml=pydml, filename=filename)
     t1 = time.perf_counter()

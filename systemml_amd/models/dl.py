@@ -587,9 +587,12 @@ class _Gen:
             elif k == "flatten":
                 code.append(f"{o} = {x}")
             elif k == "batchnorm":
-                mode = '"train"' if train else '"test"'
-                code.append(f"[{o}, em_upd_{n}, ev_upd_{n}, cm_{n}, cv_{n}, cn_{n}] = bn2d::forward({x}, g_{n}, be_{n}, "
-                            f"{c}, {h}, {w}, {mode}, em_{n}, ev_{n}, {p['mu']}, {p['eps']})")
+                if train:           # the branch-free variant: inlined, fuses with what follows
+                    code.append(f"[{o}, em_upd_{n}, ev_upd_{n}, cm_{n}, cv_{n}, cn_{n}] = bn2d::forward_train({x}, "
+                                f"g_{n}, be_{n}, {c}, {h}, {w}, em_{n}, ev_{n}, {p['mu']}, {p['eps']})")
+                else:
+                    code.append(f"[{o}, em_upd_{n}, ev_upd_{n}, cm_{n}, cv_{n}, cn_{n}] = bn2d::forward({x}, g_{n}, "
+                                f"be_{n}, {c}, {h}, {w}, \"test\", em_{n}, ev_{n}, {p['mu']}, {p['eps']})")
             elif k == "scale":
                 code.append(f"{o} = ss2d::forward({x}, g_{n}, be_{n}, {c}, {h}, {w})")
             elif k == "eltwise":
@@ -680,7 +683,9 @@ class _Gen:
             elif k == "dense":
                 code.append(f"[g_in_{n}, dW_{n}, db_{n}] = affine::backward({dout}, {x}, W_{n}, b_{n})")
                 acc(b0, f"g_in_{n}")
-            elif k in ("relu", "sigmoid", "tanh", "softmax"):
+            elif k == "relu":       # from the output (y > 0 iff x > 0): the input need not stay live
+                acc(b0, f"relu::backward({dout}, {o})")
+            elif k in ("sigmoid", "tanh", "softmax"):
                 acc(b0, f"{k}::backward({dout}, {x})")
             elif k == "elu":
                 acc(b0, f"elu::backward({dout}, {x}, {p['alpha']})")
@@ -691,9 +696,8 @@ class _Gen:
             elif k == "flatten":
                 acc(b0, dout)
             elif k == "batchnorm":
-                code.append(f"[g_in_{n}, dg_{n}, dbe_{n}] = bn2d::backward({dout}, {o}, em_upd_{n}, ev_upd_{n}, cm_{n}, "
-                            f"cv_{n}, cn_{n}, {x}, g_{n}, be_{n}, {c}, {h}, {w}, \"train\", em_{n}, ev_{n}, "
-                            f"{p['mu']}, {p['eps']})")
+                code.append(f"[g_in_{n}, dg_{n}, dbe_{n}] = bn2d::backward_train({dout}, cv_{n}, cn_{n}, g_{n}, "
+                            f"{c}, {h}, {w}, {p['eps']})")
                 acc(b0, f"g_in_{n}")
             elif k == "scale":
                 code.append(f"[g_in_{n}, dg_{n}, dbe_{n}] = ss2d::backward({dout}, {o}, {x}, g_{n}, be_{n}, {c}, {h}, {w})")
