@@ -587,12 +587,9 @@ class _Gen:
             elif k == "flatten":
                 code.append(f"{o} = {x}")
             elif k == "batchnorm":
-                if train:           # the branch-free variant: inlined, fuses with what follows
-                    code.append(f"[{o}, em_upd_{n}, ev_upd_{n}, cm_{n}, cv_{n}, cn_{n}] = bn2d::forward_train({x}, "
-                                f"g_{n}, be_{n}, {c}, {h}, {w}, em_{n}, ev_{n}, {p['mu']}, {p['eps']})")
-                else:
-                    code.append(f"[{o}, em_upd_{n}, ev_upd_{n}, cm_{n}, cv_{n}, cn_{n}] = bn2d::forward({x}, g_{n}, "
-                                f"be_{n}, {c}, {h}, {w}, \"test\", em_{n}, ev_{n}, {p['mu']}, {p['eps']})")
+                mode = '"train"' if train else '"test"'
+                code.append(f"[{o}, em_upd_{n}, ev_upd_{n}, cm_{n}, cv_{n}, cn_{n}] = bn2d::forward({x}, g_{n}, be_{n}, "
+                            f"{c}, {h}, {w}, {mode}, em_{n}, ev_{n}, {p['mu']}, {p['eps']})")
             elif k == "scale":
                 code.append(f"{o} = ss2d::forward({x}, g_{n}, be_{n}, {c}, {h}, {w})")
             elif k == "eltwise":
@@ -696,8 +693,9 @@ class _Gen:
             elif k == "flatten":
                 acc(b0, dout)
             elif k == "batchnorm":
-                code.append(f"[g_in_{n}, dg_{n}, dbe_{n}] = bn2d::backward_train({dout}, cv_{n}, cn_{n}, g_{n}, "
-                            f"{c}, {h}, {w}, {p['eps']})")
+                code.append(f"[g_in_{n}, dg_{n}, dbe_{n}] = bn2d::backward({dout}, {o}, em_upd_{n}, ev_upd_{n}, cm_{n}, "
+                            f"cv_{n}, cn_{n}, {x}, g_{n}, be_{n}, {c}, {h}, {w}, \"train\", em_{n}, ev_{n}, "
+                            f"{p['mu']}, {p['eps']})")
                 acc(b0, f"g_in_{n}")
             elif k == "scale":
                 code.append(f"[g_in_{n}, dg_{n}, dbe_{n}] = ss2d::backward({dout}, {o}, {x}, g_{n}, be_{n}, {c}, {h}, {w})")
