@@ -106,22 +106,6 @@ def _regalloc(ops, leaves):
     return code, reg[("op", ops[-1].id)]
 
 
-def _cheap_recompute(g, max_ops=2):
-    """A cellwise group worth recomputing in several consumers: few operators over at most one
-    full-size matrix (every other leaf a vector or scalar of known size)."""
-    ops, leaves = g
-    if len(ops) > max_ops:
-        return False
-    chan = {_operands(o)[1].id for o in ops if _is_bias(o)}     # per-channel vectors of bias ops
-    big = 0
-    for x in leaves:
-        if x.dt != "M" or x.id in chan:
-            continue
-        if x.dim1 in (None, -1) or x.dim2 in (None, -1) or (x.dim1 > 1 and x.dim2 > 1):
-            big += 1
-    return big <= 1
-
-
 def fuse_cells(bb):
     """Fuse the cellwise sub-DAGs of a basic block; returns the number of fused operators."""
     live = getattr(bb, "live_out", None)
@@ -141,24 +125,16 @@ def fuse_cells(bb):
             continue
         ops, leaves = [], []
         for ci, c in enumerate(_operands(h)):
-            if any(c is o for o in ops):
-                continue                      # already computed in this program (X * X, diamonds)
             g = groups.get(c.id)
             if _is_bias(h) and ci == 1:
                 g = None                      # the per-channel operand is read by the kernel as is
-            if g is not None and c.id not in absorbed:
-                single = ncons.get(c.id, 0) == 1
-                # a shared producer is recomputed in each consumer when that reads no more HBM
-                # than its materialised value would (one full-size input, the rest vectors)
-                if single or _cheap_recompute(g):
-                    mops = ops + [o for o in g[0] if all(o is not q for q in ops)]
-                    nl = _merge_leaves(leaves, g[1])
-                    if len(mops) + 1 <= MAXOPS and len(nl) <= MAXIN:
-                        ops = mops
-                        leaves = nl
-                        if single:
-                            absorbed.add(c.id)
-                        continue
+            if g is not None and ncons.get(c.id, 0) == 1 and c.id not in absorbed:
+                nl = _merge_leaves(leaves, g[1])
+                if len(ops) + len(g[0]) + 1 <= MAXOPS and len(nl) <= MAXIN:
+                    ops += g[0]
+                    leaves = nl
+                    absorbed.add(c.id)
+                    continue
             leaves = _merge_leaves(leaves, [c])
         if len(leaves) > MAXIN:
             continue

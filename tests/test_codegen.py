@@ -322,9 +322,7 @@ def test_bias_ops_fuse_with_cellwise_chains():
     cs = EX.compile_script(BIAS_SCRIPT, {}, inputs=ins, outputs=["norm", "out", "s"], config=DMLConfig(gpu=False))
     fused = _fused_hops(cs)
     assert any("cell[bias+,bias*]" in ln for ln in fused), fused
-    # out's program either reads the materialised norm or recomputes it from X (the shared
-    # two-operator producer is cheap to recompute: same bytes read, one fewer dependency)
-    assert any("bias*,bias+,max]" in ln for ln in fused), fused
+    assert any("cell[bias*,bias+,max]" in ln for ln in fused), fused
     res, _ = EX.execute(cs, ins)
     cs0 = EX.compile_script(BIAS_SCRIPT, {}, inputs=ins, outputs=["norm", "out", "s"],
                             config=DMLConfig(gpu=False, fusion=False))
