@@ -360,6 +360,47 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
       }
 }
 
+// ---- backward data for few input channels -------------------------------------------------
+// dX = conv2d_backward_data with C <= 8 (an RGB stem): the implicit GEMM's M dimension is C, so
+// a 64-row MFMA tile would be > 90 % padding and, with a strided filter, most K taps are off the
+// stride grid.  Direct form instead: each thread owns one dX cell and sums dout * W over the
+// taps that land on the stride grid and over the filters (fp32 / fp64 accumulation).
+template <typename TI, typename TA>
+__global__ void __launch_bounds__(256) conv_bwd_data_direct(Conv c, TA* __restrict__ out) {
+  const TI* __restrict__ Wt = (const TI*)c.W;
+  const TI* __restrict__ D = (const TI*)c.D;
+  const int64_t total = (int64_t)c.N * c.C * c.H * c.Wd;
+  const int KK = c.KH * c.KW, P = c.Ho * c.Wo;
+  const int64_t fstride_w = (int64_t)c.C * KK;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    int64_t q = i / c.Wd;
+    const int w = (int)(i - q * c.Wd);
+    const int h = (int)(q % c.H);
+    q /= c.H;
+    const int ch = (int)(q % c.C);
+    const int64_t n = q / c.C;
+    const TI* dn = D + n * (int64_t)c.F * P;
+    const TI* wc = Wt + (int64_t)ch * KK;
+    TA acc = 0;
+    for (int kh = 0; kh < c.KH; ++kh) {
+      const int th = h + c.ph - kh;
+      if (th < 0 || th % c.sh) continue;
+      const int oh = th / c.sh;
+      if (oh >= c.Ho) continue;
+      for (int kw = 0; kw < c.KW; ++kw) {
+        const int tw = w + c.pw - kw;
+        if (tw < 0 || tw % c.sw) continue;
+        const int ow = tw / c.sw;
+        if (ow >= c.Wo) continue;
+        const TI* dp = dn + oh * c.Wo + ow;
+        const TI* wp = wc + kh * c.KW + kw;
+        for (int f = 0; f < c.F; ++f) acc += (TA)dp[(int64_t)f * P] * (TA)wp[f * fstride_w];
+      }
+    }
+    out[i] = acc;
+  }
+}
+
 // ---- pooling ----------------------------------------------------------------------------
 struct Pool {
   const void* X;
@@ -665,6 +706,18 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   c.ksplit = ksplit;
   c.kper = (int)kper;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (mode == BWD_DATA && C <= 8) {
+    const int64_t n = (int64_t)N * C * H * Wd;
+    const dim3 dg((unsigned)(n / 256 + 1 < 256 * 64 ? n / 256 + 1 : 256 * 64));
+    if (dtype == 0) hipLaunchKernelGGL((conv_bwd_data_direct<__bf16, float>), dg, dim3(256), 0, s, c, (float*)out);
+    else if (dtype == 1 || dtype == 3)
+      hipLaunchKernelGGL((conv_bwd_data_direct<float, float>), dg, dim3(256), 0, s, c, (float*)out);
+    else if (dtype == 2)
+      hipLaunchKernelGGL((conv_bwd_data_direct<double, double>), dg, dim3(256), 0, s, c, (double*)out);
+    else
+      return -1;
+    return (int)hipGetLastError();
+  }
   if (ksplit > 1) {
     const int64_t n = M * Nc;
     if (hipMemsetAsync(out, 0, n * (dtype == 2 ? 8 : 4), s) != hipSuccess) return (int)hipGetLastError();
