@@ -394,7 +394,19 @@ __global__ void __launch_bounds__(256) conv_bwd_data_direct(Conv c, TA* __restri
         if (ow >= c.Wo) continue;
         const TI* dp = dn + oh * c.Wo + ow;
         const TI* wp = wc + kh * c.KW + kw;
-        for (int f = 0; f < c.F; ++f) acc += (TA)dp[(int64_t)f * P] * (TA)wp[f * fstride_w];
+        // 8 filters' loads in flight before their products are accumulated (in filter order)
+        int f = 0;
+        for (; f + 8 <= c.F; f += 8) {
+          TA dv[8], wv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            dv[u] = (TA)dp[(int64_t)(f + u) * P];
+            wv[u] = (TA)wp[(f + u) * fstride_w];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc += dv[u] * wv[u];
+        }
+        for (; f < c.F; ++f) acc += (TA)dp[(int64_t)f * P] * (TA)wp[f * fstride_w];
       }
     }
     out[i] = acc;
