@@ -363,25 +363,25 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
 // ---- backward data for few input channels -------------------------------------------------
 // dX = conv2d_backward_data with C <= 8 (an RGB stem): the implicit GEMM's M dimension is C, so
 // a 64-row MFMA tile would be > 90 % padding and, with a strided filter, most K taps are off the
-// stride grid.  Direct form instead: each thread owns the C dX cells of one pixel and sums dout * W over the
+// stride grid.  Direct form instead: each thread owns one dX cell and sums dout * W over the
 // taps that land on the stride grid and over the filters (fp32 / fp64 accumulation).
 template <typename TI, typename TA>
 __global__ void __launch_bounds__(256) conv_bwd_data_direct(Conv c, TA* __restrict__ out) {
-  // one thread per (n, h, w): all C <= 8 channels at once, so each dout value is loaded once
-  // for every channel; 8 filters' loads in flight before they are accumulated (filter order)
   const TI* __restrict__ Wt = (const TI*)c.W;
   const TI* __restrict__ D = (const TI*)c.D;
-  const int64_t total = (int64_t)c.N * c.H * c.Wd;
-  const int KK = c.KH * c.KW, P = c.Ho * c.Wo, C = c.C;
-  const int64_t fstride_w = (int64_t)C * KK, HW = (int64_t)c.H * c.Wd;
+  const int64_t total = (int64_t)c.N * c.C * c.H * c.Wd;
+  const int KK = c.KH * c.KW, P = c.Ho * c.Wo;
+  const int64_t fstride_w = (int64_t)c.C * KK;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t n = i / HW;
-    const int r = (int)(i - n * HW);
-    const int h = r / c.Wd, w = r - (r / c.Wd) * c.Wd;
+    int64_t q = i / c.Wd;
+    const int w = (int)(i - q * c.Wd);
+    const int h = (int)(q % c.H);
+    q /= c.H;
+    const int ch = (int)(q % c.C);
+    const int64_t n = q / c.C;
     const TI* dn = D + n * (int64_t)c.F * P;
-    TA acc[8];
-#pragma unroll
-    for (int ch = 0; ch < 8; ++ch) acc[ch] = 0;
+    const TI* wc = Wt + (int64_t)ch * KK;
+    TA acc = 0;
     for (int kh = 0; kh < c.KH; ++kh) {
       const int th = h + c.ph - kh;
       if (th < 0 || th % c.sh) continue;
@@ -393,33 +393,23 @@ __global__ void __launch_bounds__(256) conv_bwd_data_direct(Conv c, TA* __restri
         const int ow = tw / c.sw;
         if (ow >= c.Wo) continue;
         const TI* dp = dn + oh * c.Wo + ow;
-        const TI* wp = Wt + kh * c.KW + kw;
+        const TI* wp = wc + kh * c.KW + kw;
+        // 8 filters' loads in flight before their products are accumulated (in filter order)
         int f = 0;
         for (; f + 8 <= c.F; f += 8) {
-          TA dv[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) dv[u] = (TA)dp[(int64_t)(f + u) * P];
+          TA dv[8], wv[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const TI* wf = wp + (f + u) * fstride_w;
-#pragma unroll
-            for (int ch = 0; ch < 8; ++ch)
-              if (ch < C) acc[ch] += dv[u] * (TA)wf[ch * KK];
+            dv[u] = (TA)dp[(int64_t)(f + u) * P];
+            wv[u] = (TA)wp[(f + u) * fstride_w];
           }
-        }
-        for (; f < c.F; ++f) {
-          const TA dv = (TA)dp[(int64_t)f * P];
-          const TI* wf = wp + f * fstride_w;
 #pragma unroll
-          for (int ch = 0; ch < 8; ++ch)
-            if (ch < C) acc[ch] += dv * (TA)wf[ch * KK];
+          for (int u = 0; u < 8; ++u) acc += dv[u] * wv[u];
         }
+        for (; f < c.F; ++f) acc += (TA)dp[(int64_t)f * P] * (TA)wp[f * fstride_w];
       }
     }
-    TA* o = out + n * C * HW + r;
-#pragma unroll
-    for (int ch = 0; ch < 8; ++ch)
-      if (ch < C) o[ch * HW] = acc[ch];
+    out[i] = acc;
   }
 }
 
@@ -729,7 +719,7 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   c.kper = (int)kper;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (mode == BWD_DATA && C <= 8) {
-    const int64_t n = (int64_t)N * H * Wd;
+    const int64_t n = (int64_t)N * C * H * Wd;
     const dim3 dg((unsigned)(n / 256 + 1 < 256 * 64 ? n / 256 + 1 : 256 * 64));
     if (dtype == 0) hipLaunchKernelGGL((conv_bwd_data_direct<__bf16, float>), dg, dim3(256), 0, s, c, (float*)out);
     else if (dtype == 1 || dtype == 3)
