@@ -257,6 +257,17 @@ def main():
     if ctx:
         el = ctx.allreduce_scalar(el, "max")
     sec = el / a.steps
+    # physical GPUs used: distinct devices over the ranks (a gloo rehearsal puts several ranks
+    # on one GPU and must not report them as several GPUs)
+    n_phys = 1
+    if ctx:
+        import torch.distributed as tdist
+        devs = [None] * world
+        tdist.all_gather_object(devs, (os.uname().nodename, torch.cuda.current_device()))
+        n_phys = len(set(devs))
+        if rank == 0 and a.verbose:
+            print(f"collectives per step: { {k: v / max(1, a.steps + a.warmup) for k, v in D.stats.items()} }",
+                  file=sys.stderr)
     if prof is not None and rank == 0:
         import io
         import pstats
@@ -272,7 +283,7 @@ def main():
         if a.verbose:
             print(f"datagen {t_gen:.2f}s, kernels {kernels.counters}, dist {D.stats}", file=sys.stderr)
         res = {
-            "metric": METRIC, "value": round(sec, 4), "unit": "s", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC, "value": round(sec, 4), "unit": "s", "n_gpus": n_phys, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(sec * 1000, 2), "higher_is_better": False,
             "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if a.xdtype == "bf16" else a.xdtype,
             "data": "synthetic (perftest generators genRandData4LogisticRegression / genRandData4Multinomial, "
@@ -281,7 +292,7 @@ def main():
                                 % (a.maxi, a.classes, a.moi, a.mii, "" if a.icpt == 0 else f"; icpt={a.icpt}",
                                    " [DIAGNOSTIC: plans reused, compilation excluded]" if a.reuse_plans else ""),
                        "global_batch": a.rows, "seq_len": a.cols, "rows": a.rows, "cols": a.cols,
-                       "parallelism": f"dp{world}", "x_storage": a.xdtype, "accumulate": "fp32"},
+                       "parallelism": f"dp{world}" if n_phys == world else f"dp{world} ({world} ranks on {n_phys} GPU)", "x_storage": a.xdtype, "accumulate": "fp32"},
         }
         print(json.dumps(res), flush=True)
     if svc is not None:

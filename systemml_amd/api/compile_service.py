@@ -160,7 +160,7 @@ def _worker(conn):
         msg = conn.recv()
         if msg is None:
             return
-        src, args, specs, outputs, config, world, kw = msg
+        seq, src, args, specs, outputs, config, world, kw = msg
         try:
             import time
             t0 = time.perf_counter()
@@ -168,7 +168,7 @@ def _worker(conn):
             inputs = {k: _stand_in(s) for k, s in specs.items()}
             cs = EX.compile_script(src, args, inputs=inputs, outputs=outputs, config=config, **kw)
             blob = dehydrate(cs)
-            conn.send(("ok", (blob, time.perf_counter() - t0)))
+            conn.send((seq, "ok", (blob, time.perf_counter() - t0)))
             if first:
                 # the compiler's modules and caches are loaded now: freeze them out of the cyclic
                 # collector so later collections only scan a compilation's own garbage
@@ -176,12 +176,13 @@ def _worker(conn):
                 gc.collect()
                 gc.freeze()
         except BaseException as e:  # noqa: BLE001 - reported to the driver
-            conn.send(("err", f"{type(e).__name__}: {e}"))
+            conn.send((seq, "err", f"{type(e).__name__}: {e}"))
 
 
 class _Pending:
-    def __init__(self, svc, inputs):
+    def __init__(self, svc, inputs, seq):
         self.svc = svc
+        self.seq = seq
         self.inputs = inputs
         self._value = None
         self._done = False
@@ -191,8 +192,7 @@ class _Pending:
         if not self._done:
             import time
             t0 = time.perf_counter()
-            with self.svc.lock:
-                status, payload = self.svc.conn.recv()
+            status, payload = self.svc.reply(self.seq)
             t1 = time.perf_counter()
             if status != "ok":
                 raise RuntimeError(f"compile service: {payload}")
@@ -204,7 +204,8 @@ class _Pending:
 
 
 class CompileService:
-    """One compiler process; requests are answered in order."""
+    """One compiler process; requests are answered in order and each reply carries its
+    request's sequence number, so results may be claimed in any order."""
 
     def __init__(self):
         ctx = mp.get_context("spawn")
@@ -213,11 +214,23 @@ class CompileService:
         self.proc.start()
         child.close()
         self.lock = threading.Lock()
+        self.seq = 0
+        self.replies = {}       # seq -> (status, payload) received while waiting for another
 
     def submit(self, source, args, inputs, outputs, config, world=1, **kw):
         specs = {k: input_spec(v) for k, v in (inputs or {}).items()}
-        self.conn.send((source, args, specs, list(outputs), config, world, kw))
-        return _Pending(self, inputs)
+        with self.lock:
+            self.seq += 1
+            seq = self.seq
+            self.conn.send((seq, source, args, specs, list(outputs), config, world, kw))
+        return _Pending(self, inputs, seq)
+
+    def reply(self, seq):
+        with self.lock:
+            while seq not in self.replies:
+                s, status, payload = self.conn.recv()
+                self.replies[s] = (status, payload)
+            return self.replies.pop(seq)
 
     def close(self):
         try:

@@ -381,23 +381,26 @@ class _Linear:
                                                 and self.disjoint(w1[1], w2[1]))
 
 
-def accumulators(body):
-    """Variables only updated through plain `+=` in the body and not otherwise used there:
-    parfor accumulators (reference parfor_accumulator tests), merged as the sum of every
-    worker's increments."""
+def accumulators(body, scalars=frozenset()):
+    """Matrix variables only updated through plain `+=` in the body and not otherwise used
+    there: parfor accumulators (reference parfor_accumulator tests), merged as the sum of
+    every worker's increments.  A scalar `s += ...` stays an output dependency, as in the
+    reference (ParForStatementBlock.rCheckCandidates accumulates matrices only)."""
     out = set()
     for v in body.acc_writes:
+        if v in scalars:
+            continue
         if v not in body.plain_writes and v not in body.reads_whole and v not in body.ix_writes \
                 and v not in body.reads_ix:
             out.add(v)
     return out
 
 
-def loop_accumulators(st: A.For):
+def loop_accumulators(st: A.For, scalars=frozenset()):
     """Accumulator variables (`v += ...` only) of a parfor statement."""
     body = _Body()
     body.stmts(st.body)
-    return sorted(accumulators(body))
+    return sorted(accumulators(body, scalars))
 
 
 def check_parfor(st: A.For, defined_before, scalars=frozenset()):
@@ -406,7 +409,7 @@ def check_parfor(st: A.For, defined_before, scalars=frozenset()):
     disables the analysis.  Records the loop's accumulator variables on `st.accumulators`."""
     body = _Body()
     body.stmts(st.body)
-    st.accumulators = sorted(accumulators(body))
+    st.accumulators = sorted(accumulators(body, scalars))
     chk = st.params.get("check")
     if isinstance(chk, A.Literal) and str(chk.value) in ("0", "False", "false", "FALSE"):
         return

@@ -149,6 +149,8 @@ class Translator:
             cp.licm_stats = hoist_program(cp)      # before liveness: adds blocks / variables
             from .loops import mark_program
             cp.licm_stats.update(mark_program(cp))
+            from .speculate import run as speculate
+            cp.licm_stats.update(speculate(cp, self.config))
         # liveness
         for fb in self.functions.values():
             if fb.body is not None:
@@ -264,7 +266,7 @@ class Translator:
                     fb = ForBlock(st.var, p_from, p_to, p_incr, body, parfor=st.parfor, params=params, pos=st.pos)
                     if st.parfor:
                         from .parfor_deps import loop_accumulators
-                        fb.accumulators = loop_accumulators(st)
+                        fb.accumulators = loop_accumulators(st, {v for v, d in types.items() if d == "S"})
                     blocks.append(fb)
                     cur = _BBuilder(self, ctx, consts, types)
                 else:
@@ -669,9 +671,14 @@ class _BBuilder:
             o = pos_args[2].value if len(pos_args) > 2 else nd["op"].value
             return self.binary(opmap[o], pos_args[0], pos_args[1], pos)
         if name == "exists":
+            # symbol-table probe (reference AggregateUnaryCPInstruction.java:130-136 EXISTS):
+            # a variable assigned earlier in this block is defined here; otherwise the frame
+            # is probed when the statement runs.  exists("X") names the variable by a string.
             a = args[0].value
-            vn = a.name if isinstance(a, A.Ident) else None
+            vn = a.name if isinstance(a, A.Ident) else (a.value if isinstance(a, A.Literal) and isinstance(a.value, str) else None)
             if vn is not None:
+                if vn in self.env:
+                    return H.lit(True, pos)
                 return self.mk("bi", [], p={"name": "exists", "var": vn}, dt="S", pos=pos, cse=False)
         if name == "ifelse" and all(h.op == "lit" for h in pos_args) and len(pos_args) == 3:
             return pos_args[1] if S.as_bool(pos_args[0].value) else pos_args[2]

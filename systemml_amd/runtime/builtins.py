@@ -134,8 +134,12 @@ def b_time(ctx):
 
 
 @builtin("exists")
-def b_exists(ctx, *a, **kw):
-    return False
+def b_exists(ctx, name, *a, **kw):
+    """exists("X") with a computed name: probes the current frame's variables (statically
+    named variables are resolved by the translator, compiler/translator.py)."""
+    if isinstance(name, str):
+        return name in ctx.vars
+    return True
 
 
 @builtin("toString")

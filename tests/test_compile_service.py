@@ -50,7 +50,7 @@ def test_service_process_compiles_in_order():
         p1 = svc.submit(src_l, dict(X="X", Y="y", B="B", icpt=0, reg=1e-6, tol=1e-12, maxi=50), {"X": X, "y": y},
                         ["beta"], cfg)
         p2 = svc.submit(src_m, ARGS, {"X": X, "Y_vec": lab}, ["B_out"], cfg)
-        cs1, cs2 = p1.result(), p2.result()
+        cs2, cs1 = p2.result(), p1.result()     # claimed out of order: each gets its own plan
     finally:
         svc.close()
     r1, _ = EX.execute(cs1, {"X": X, "y": y}, out=lambda s: None)

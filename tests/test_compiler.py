@@ -384,3 +384,32 @@ def test_multilogreg_forms_softmax_objective_template():
         res, _ = EX.execute(cs, {"X": X, "Y_vec": lab}, out=lambda s: None)
         outs.append(res["B_out"].numpy())
     np.testing.assert_allclose(outs[0], outs[1], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("icpt", [0, 2])
+def test_speculative_accept_gradient_fused_into_softmax_pass(icpt):
+    """MultiLogReg computes the gradient only when a step is accepted (reference
+    scripts/algorithms/MultiLogReg.dml:310-314); compiler/speculate.py evaluates it inside
+    the candidate point's fused softmax pass instead (same results, one pass over X)."""
+    import numpy as np
+    import torch
+    from systemml_amd.api import executor as EX
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.conf import DMLConfig
+    src = open(SCRIPTS_DIR + "/algorithms/MultiLogReg.dml").read()
+    g = torch.Generator().manual_seed(0)
+    X = torch.rand(1500, 20, dtype=torch.float64, generator=g)
+    y = (torch.argmax(X[:, :3] + 0.3 * torch.rand(1500, 3, generator=g, dtype=torch.float64), 1) + 1)
+    y = y.double().reshape(-1, 1)
+    args = dict(X="X", Y="Y", B="B", icpt=icpt, reg=0.01, tol=1e-6, moi=8, mii=5)
+    out = {}
+    for fuse in (True, False):
+        cfg = DMLConfig(gpu=False)
+        cfg.fusion = fuse
+        cs = EX.compile_script(src, args, inputs={"X": X, "Y_vec": y}, outputs=["B_out"], config=cfg)
+        if fuse:
+            assert cs.cp.licm_stats.get("speculative-fused-products") == 1
+            assert cs.cp.rewrite_stats.get("softmax-objective") == 1
+        r, _ = EX.execute(cs, {"X": X, "Y_vec": y}, out=lambda s: None)
+        out[fuse] = r["B_out"].numpy()
+    np.testing.assert_allclose(out[True], out[False], rtol=1e-9, atol=1e-11)

@@ -53,3 +53,11 @@ def test_parity_count():
     if not CASES:
         pytest.skip("reference test sources not mounted")
     assert len(CASES) >= 70
+
+
+def test_scalar_accumulation_is_an_output_dependency():
+    # the reference accumulates matrices only; a scalar `s += ...` in a parfor body
+    # is an output dependency (ParForStatementBlock.rCheckCandidates)
+    with pytest.raises(LanguageError):
+        compile_script("s = 0\nparfor (i in 1:4) { s += i }\nprint(s)")
+    compile_script("A = matrix(0, 2, 2)\nparfor (i in 1:4) { A += i }\nprint(sum(A))")

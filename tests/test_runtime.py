@@ -401,15 +401,48 @@ def test_exec_types_decided_by_size_and_recompiled_at_runtime():
 def test_parfor_accumulators(par):
     """Accumulator result variables (`+=` only in the body; reference
     functions/parfor/parfor_accumulator*.dml): merged as pre-loop value plus every worker's
-    increment, for matrices and scalars, sequential and threaded."""
+    increment, for matrices (scalars `+=` are output dependencies, as in the reference),
+    sequential and threaded."""
     src = f"""
     R = matrix(7, rows=4, cols=3)
-    s = 1
     parfor (i in 1:10, par={par}) {{
       R += matrix(i, rows=4, cols=3)
-      s += i * 2
     }}
     """
-    res, _ = R(src, outputs=["R", "s"])
+    res, _ = R(src, outputs=["R"])
     np.testing.assert_array_equal(M(res, "R"), np.full((4, 3), 62.0))
-    assert float(res["s"]) == 111
+
+
+def test_exists_identifier_and_string():
+    # reference AggregateUnaryCPInstruction.java:130-136: a symbol-table probe for both forms
+    _, out = R("""
+      X = matrix(1, 2, 2)
+      print(exists(X)); print(exists("X")); print(exists("Z"))
+      f = function(Matrix[Double] A) return (Boolean b) { b = exists(A) }
+      print(f(X))
+      n = "X"
+      print(exists(n))
+      while (FALSE) { W = 1 }
+      print(exists(W))
+    """)
+    assert out == ["TRUE", "TRUE", "FALSE", "TRUE", "TRUE", "FALSE"]
+
+
+def test_conv_bias_fusion_keeps_bias_add_semantics():
+    # ADVICE r3: the conv2d + bias_add fusion must not change bias_add's shape rules
+    src = """
+      X = rand(rows=2, cols=3*4*4, seed=1)
+      W = rand(rows=4, cols=3*2*2, seed=2)
+      b = rand(rows=$nb, cols=1, seed=3)
+      C = conv2d(X, W, input_shape=[2,3,4,4], filter_shape=[4,3,2,2], stride=[1,1], padding=[0,0])
+      out = bias_add(C, b)
+      ref = C + matrix(b %*% matrix(1, rows=1, cols=ncol(C) / nrow(b)), rows=1, cols=ncol(C))
+      d = max(abs(out - ref))
+    """
+    res, _ = R(src, outputs=["d"], args={"nb": 3})
+    assert float(res["d"]) < 1e-12
+    res, _ = R(src, outputs=["d"], args={"nb": 4})
+    assert float(res["d"]) < 1e-12
+    from systemml_amd.parser.errors import DMLRuntimeError
+    with pytest.raises(Exception):
+        R(src, outputs=["d"], args={"nb": 5})
