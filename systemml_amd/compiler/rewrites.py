@@ -743,6 +743,7 @@ def cse(roots):
 
 
 _ROWGEN = __import__('os').environ.get('SYSML_ROWGEN', '1') != '0'   # Row / Outer templates on
+_VECGEN = __import__('os').environ.get('SYSML_VECGEN', '1') != '0'   # Vector template on
 
 
 def fuse_conv_bias(bb):
@@ -796,6 +797,12 @@ def rewrite_block(bb, config=None):
             n = fuse_rows(bb)
             if n:
                 rw.stats["row-fused-ops"] = n
+        if _VECGEN and (config is None or getattr(config, "gpu", True)):
+            # Vector template: only a GPU backend has launches and round trips to save
+            from .vecgen import fuse_vectors
+            n = fuse_vectors(bb)
+            if n:
+                rw.stats["vector-fused-ops"] = n
         n = fuse_cells(bb)
         if n:
             rw.stats["cell-fused-ops"] = n

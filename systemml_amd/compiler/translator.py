@@ -156,6 +156,15 @@ class Translator:
             if fb.body is not None:
                 liveness(fb.body, set(o.name for o in fb.outputs))
         live_in = liveness(blocks, set(outputs) if outputs else None)
+        if self.config is None or getattr(self.config, "rewrites", True):
+            from .ifconv import run as ifconv
+            st = ifconv(cp, self.config)       # needs liveness; changes the block structure
+            if st:
+                cp.licm_stats.update(st)
+                for fb in self.functions.values():
+                    if fb.body is not None:
+                        liveness(fb.body, set(o.name for o in fb.outputs))
+                live_in = liveness(cp.blocks, set(outputs) if outputs else None)
         cp.inputs = live_in
         undefined = live_in - set(inputs)
         if undefined and self.config is not None and getattr(self.config, "strict_undefined", True):
@@ -692,6 +701,10 @@ class _BBuilder:
             # dynamic function call: resolve at runtime in this file context
             return self._eval_call(pos_args, named, pos)
         dt = _BI_DT.get(name, "U")
+        if name == "ifelse" and len(pos_args) == 3 and not named:
+            # a matrix operand makes the result a matrix; all-scalar operands a scalar
+            ds = [h.dt for h in pos_args]
+            dt = "M" if "M" in ds else ("S" if all(d == "S" for d in ds) else "U")
         if name in _DIST_FNS:
             tgt = nd.get("target", pos_args[0] if pos_args else None)
             dt = "M" if tgt is not None and tgt.dt == "M" else ("U" if tgt is None or tgt.dt == "U" else "S")

@@ -539,6 +539,15 @@ def b_ifelse(ctx, test, yes, no):
     return torch.where(tt != 0, yy, nn)
 
 
+@builtin("_sel")
+def b_sel(ctx, test, yes, no):
+    """Select of an if-converted branch (compiler/ifconv.py): a scalar test picks one operand
+    as is; a matrix test selects cellwise."""
+    if isinstance(test, Tensor) or C.is_dist(test):
+        return b_ifelse(ctx, test, yes, no)
+    return yes if _bool(test) else no
+
+
 @builtin("outer")
 def b_outer(ctx, a, b, op):
     x = _mat(a)

@@ -20,7 +20,7 @@ from .scalars import DevScalar
 
 
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell",
-                  "magg", "row", "outer"}
+                  "magg", "row", "outer", "vprog"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
 _CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "rix", "t", "cell", "magg", "row"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "round", "floor", "ceil", "sign",
@@ -28,7 +28,7 @@ _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "rou
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
 _LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "smobj", "t", "tak",
-                 "cell", "magg", "row", "outer"}
+                 "cell", "magg", "row", "outer", "vprog"}
 # operators that compute on matrix operands (placement applies); the rest move values around
 _COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "wquat", "tak", "t", "rix", "lix", "bi",
                  "cell", "magg", "row", "outer"}
@@ -240,6 +240,12 @@ def _make_impl(h):
         from ..ops import rowgen as ROWG
         rprog = p["prog"]
         return (lambda ctx, a: ROWG.evaluate(rprog, a)), "spoofRA"
+    if op == "vprog":
+        # Vector template (compiler/vecgen.py): a block's small-matrix + scalar algebra as one
+        # single-workgroup kernel, its original operators one by one elsewhere (ops/vprog.py)
+        from ..ops import vprog as VP
+        vprog_ = p["prog"]
+        return (lambda ctx, a: VP.evaluate(vprog_, ctx, a)), "spoofVec"
     if op == "magg":
         # multi-aggregate template (compiler/codegen._multi_agg): a tuple of scalars, one pass
         from ..ops import cell as CELL
@@ -284,6 +290,30 @@ def _make_impl(h):
         if name == "exists":
             var = p.get("var")
             return (lambda ctx, a: var in ctx.vars), "exists"
+        if name == "_vguard":
+            # guard of an if-converted block (compiler/ifconv.py)
+            from ..compiler.ifconv import MODE
+            from ..ops.vprog import VMAX
+            from ..ops.backend import backend as _be
+            gvars = p.get("vars", ())
+            gdef = p.get("defined", ())
+            force = MODE == "force"
+
+            def vguard(ctx, a):
+                vs = ctx.vars
+                for v in gdef:
+                    if v not in vs:
+                        return False
+                if force:
+                    return all(v in vs for v in gvars)
+                if not _be.on_gpu:
+                    return False
+                for v in gvars:
+                    x = vs.get(v)
+                    if type(x) is not torch.Tensor or x.numel() > VMAX or x.layout is not torch.strided:
+                        return False
+                return True
+            return vguard, "vguard"
         if name == "eval":
             from . import program as PR
             npos = p.get("npos", len(h.inputs))

@@ -380,7 +380,7 @@ def test_multilogreg_forms_softmax_objective_template():
         cfg.fusion = fuse
         cs = EX.compile_script(src, args, inputs={"X": X, "Y_vec": lab}, outputs=["B_out"], config=cfg)
         if fuse:
-            assert cs.cp.rewrite_stats.get("softmax-objective") == 1, cs.cp.rewrite_stats
+            assert cs.cp.rewrite_stats.get("softmax-objective", 0) >= 1, cs.cp.rewrite_stats
         res, _ = EX.execute(cs, {"X": X, "Y_vec": lab}, out=lambda s: None)
         outs.append(res["B_out"].numpy())
     np.testing.assert_allclose(outs[0], outs[1], rtol=1e-9, atol=1e-12)
@@ -409,7 +409,7 @@ def test_speculative_accept_gradient_fused_into_softmax_pass(icpt):
         cs = EX.compile_script(src, args, inputs={"X": X, "Y_vec": y}, outputs=["B_out"], config=cfg)
         if fuse:
             assert cs.cp.licm_stats.get("speculative-fused-products") == 1
-            assert cs.cp.rewrite_stats.get("softmax-objective") == 1
+            assert cs.cp.rewrite_stats.get("softmax-objective", 0) >= 1
         r, _ = EX.execute(cs, {"X": X, "Y_vec": y}, out=lambda s: None)
         out[fuse] = r["B_out"].numpy()
     np.testing.assert_allclose(out[True], out[False], rtol=1e-9, atol=1e-11)
