@@ -102,6 +102,43 @@ def _vec_kind(h):
     return None
 
 
+def _empty(h):
+    """(rows, cols) hops of an all-zero datagen matrix(0, rows, cols) (nnz == 0 by
+    construction), else None."""
+    if h.op != "bi" or h.p.get("name") != "matrix" or not h.inputs or not _is_lit(h.inputs[0], 0):
+        return None
+    args = _bi_args(h)
+    if set(args) - {"data", "rows", "cols"} or args.get("rows") is None or args.get("cols") is None:
+        return None
+    return args["rows"], args["cols"]
+
+
+def _zeros(r, c, pos):
+    return Hop("bi", [lit(0), r, c], {"name": "matrix", "npos": 1}, named=["rows", "cols"], dt="M", pos=pos)
+
+
+def _nrow(x, pos):
+    return Hop("u", [x], {"o": "nrow"}, dt="S", pos=pos)
+
+
+def _ncol(x, pos):
+    return Hop("u", [x], {"o": "ncol"}, dt="S", pos=pos)
+
+
+def _same_dims(X, r, c):
+    """The (rows, cols) hops r, c describe X's dimensions: nrow(X) / ncol(X), or literals equal
+    to X's known dimensions."""
+    def one(d, hop, which):
+        if hop.op == "u" and hop.p.get("o") == which and hop.inputs[0] is X:
+            return True
+        return d >= 0 and _num_lit(hop) and hop.value == d
+    return X.dt == "M" and one(X.dim1, r, "nrow") and one(X.dim2, c, "ncol")
+
+
+_EMPTY_SAFE_UNARY = {"abs", "sqrt", "round", "floor", "ceil", "sign", "neg", "sin", "tan", "asin", "atan", "sinh",
+                     "tanh"}
+
+
 class Rewriter:
     def __init__(self, config=None):
         self.config = config
@@ -140,6 +177,20 @@ class Rewriter:
 
     # ------------------------------------------------------------------ rules
     def apply_rules(self, h: Hop) -> Hop:
+        m = self._rw_empty(h)
+        if m is not h:
+            return m
+        if h.op == "b" and len(h.inputs) == 2:
+            # rules that check the consumers of the products they look through themselves
+            o = h.p["o"]
+            if o in ("+", "-"):
+                m = self._rw_distributive(h)
+                if m is not h:
+                    return m
+            if o == "*" and h.dt == "M":
+                m = self._rw_emult_chain(h)
+                if m is not h:
+                    return m
         m = self._rw_algebraic(h)
         if m is not h:
             return m
@@ -317,7 +368,147 @@ class Rewriter:
             if src.dt == "M" and not h.p.get("list") and _full_range(src, rl, ru, "nrow") and _full_range(src, cl, cu, "ncol"):
                 return self._hit("unnecessary-indexing", src)
             return h
+        if op == "lix" and not h.p.get("list") and not h.p.get("inplace"):
+            return self._rw_lix_chain(h)
         return h
+
+    def _rw_lix_chain(self, h):
+        """fuseLeftIndexingChainToAppend (reference RewriteAlgebraicSimplificationDynamic.java:285):
+        X[,1] = A; X[,2] = B -> X = cbind(A, B) for a two-column X (rows likewise -> rbind)."""
+        inner = h.inputs[0]
+        if inner.op != "lix" or inner.p.get("list") or inner.p.get("inplace") or inner.id in self.multi:
+            return h
+        X = inner.inputs[0]
+
+        def empty(x):
+            return x.op == "lit" and x.value is None
+
+        for full, sel, dim, name in (((2, 3), (4, 5), 1, "cbind"), ((4, 5), (2, 3), 0, "rbind")):
+            if not all(empty(z.inputs[i]) for z in (h, inner) for i in full):
+                continue
+            if not (_is_lit(inner.inputs[sel[0]], 1) and _is_lit(inner.inputs[sel[1]], 1)
+                    and _is_lit(h.inputs[sel[0]], 2) and _is_lit(h.inputs[sel[1]], 2)):
+                continue
+            ncl = X.dim2 if dim == 1 else X.dim1
+            e = _empty(X) if X.op == "bi" else None
+            if e is not None and _num_lit(e[dim]):
+                ncl = e[dim].value
+            A, B = inner.inputs[1], h.inputs[1]
+            if ncl == 2 and A.dt == "M" and B.dt == "M":
+                return self._hit("lix-chain-append", Hop("bi", [A, B], {"name": name, "npos": 2}, dt="M", pos=h.pos))
+        return h
+
+    # ------------------------------------------------------------------ empty operands
+    # (reference RewriteAlgebraicSimplificationDynamic: simplifyEmptyAggregate :747,
+    # simplifyEmptyUnaryOperation :776, simplifyEmptyReorgOperation :800, simplifyEmptyMatrixMult
+    # :879, simplifyEmptyBinaryOperation; "empty" = an all-zero datagen, known without sizes)
+    def _rw_empty(self, h):
+        op = h.op
+        if op == "agg" and len(h.inputs) == 1:
+            e = _empty(h.inputs[0])
+            if e is None or h.p["o"] not in ("sum", "sumsq", "mean", "min", "max", "prod"):
+                return h
+            d = h.p["dir"]
+            if d == "all":
+                return self._hit("empty-aggregate", lit(0.0))
+            r, c = e
+            return self._hit("empty-aggregate", _zeros(r, lit(1), h.pos) if d == "row" else _zeros(lit(1), c, h.pos))
+        if op == "u" and h.dt == "M" and h.p.get("o") in _EMPTY_SAFE_UNARY and _empty(h.inputs[0]) is not None:
+            return self._hit("empty-unary", h.inputs[0])
+        if op == "t":
+            e = _empty(h.inputs[0])
+            if e is not None:
+                return self._hit("empty-reorg", _zeros(e[1], e[0], h.pos))
+            return h
+        if op == "mm" and len(h.inputs) == 2:
+            A, B = h.inputs
+            tA = h.p.get("transA", False)
+            eA, eB = _empty(A), _empty(B)
+            if eB is not None:
+                rows = eA[1 if tA else 0] if eA is not None else (_ncol(A, h.pos) if tA else _nrow(A, h.pos))
+                return self._hit("empty-matrix-mult", _zeros(rows, eB[1], h.pos))
+            if eA is not None:
+                return self._hit("empty-matrix-mult", _zeros(eA[1] if tA else eA[0], _ncol(B, h.pos), h.pos))
+            return h
+        if op == "b" and h.dt == "M" and len(h.inputs) == 2:
+            a, b = h.inputs
+            o = h.p["o"]
+            ea, eb = _empty(a), _empty(b)
+            if o == "*":
+                for X, e, E in ((a, eb, b), (b, ea, a)):
+                    if e is None:
+                        continue
+                    if X.dt == "S" or _same_dims(X, *e):
+                        return self._hit("empty-binary", E)
+            if o in ("+", "-") and eb is not None and _same_dims(a, *eb):
+                return self._hit("empty-binary", a)
+            if o == "+" and ea is not None and _same_dims(b, *ea):
+                return self._hit("empty-binary", b)
+            if o == "-" and ea is not None and _same_dims(b, *ea):
+                return self._hit("empty-binary", Hop("u", [b], {"o": "neg"}, dt="M", pos=h.pos))
+        return h
+
+    # ------------------------------------------------------------------ chains of products
+    def _rw_distributive(self, h):
+        """simplifyDistributiveBinaryOperation (reference RewriteAlgebraicSimplificationStatic
+        .java:760): (X - Y*X) -> (1-Y)*X, (Y*X - X) -> (Y-1)*X, and the same for +; one
+        cellwise pass and one operator less, X and Y matrices."""
+        a, b = h.inputs
+        o = h.p["o"]
+        if a.dt != "M" or b.dt != "M":
+            return h
+        if a.op == "b" and a.p["o"] == "*" and a.id not in self.multi:
+            c1, c2 = a.inputs
+            if c1.dt == "M" and c2.dt == "M" and c1 is not c2 and (b is c1 or b is c2):
+                Y = c2 if b is c1 else c1
+                inner = Hop("b", [Y, lit(1)], {"o": o}, dt="M", pos=h.pos)
+                return self._hit("distributive-binary", Hop("b", [inner, b], {"o": "*"}, dt="M", pos=h.pos))
+        if b.op == "b" and b.p["o"] == "*" and b.id not in self.multi:
+            c1, c2 = b.inputs
+            if c1.dt == "M" and c2.dt == "M" and c1 is not c2 and (a is c1 or a is c2):
+                Y = c2 if a is c1 else c1
+                inner = Hop("b", [lit(1), Y], {"o": o}, dt="M", pos=h.pos)
+                return self._hit("distributive-binary", Hop("b", [inner, a], {"o": "*"}, dt="M", pos=h.pos))
+        return h
+
+    def _rw_emult_chain(self, h):
+        """RewriteElementwiseMultChainOptimization (reference
+        hops/rewrite/RewriteElementwiseMultChainOptimization.java:56): a chain of >= 3 cellwise
+        multiplicands with a repeated one, e.g. (B * A) * B -> A * B^2; scalars are multiplied
+        first, repeated operands become powers.  Chains through intermediates with other
+        consumers are left alone (their values are needed anyway)."""
+        leaves, count = [], {}
+
+        def collect(x, top):
+            if x.op == "b" and x.p["o"] == "*" and x.dt == "M" and (top or x.id not in self.multi):
+                for c in x.inputs:
+                    collect(c, False)
+                return
+            if x.id not in count:
+                leaves.append(x)
+                count[x.id] = 0
+            count[x.id] += 1
+        collect(h, True)
+        if sum(count.values()) < 3 or max(count.values()) < 2:
+            return h
+        scal = [x for x in leaves if x.dt == "S"]
+        mats = [x for x in leaves if x.dt != "S"]
+        terms = []
+        for x in scal + mats:
+            k = count[x.id]
+            if k == 1:
+                terms.append(x)
+            elif x.dt == "S":
+                for _ in range(k):
+                    terms.append(x)
+            else:
+                terms.append(Hop("b", [x, lit(k)], {"o": "^"}, dt="M", pos=h.pos))
+        r = terms[0]
+        for t in terms[1:]:
+            r = Hop("b", [r, t], {"o": "*"}, dt="M" if (r.dt == "M" or t.dt == "M") else "S", pos=h.pos)
+        if r.dt != "M":
+            return h
+        return self._hit("emult-chain", r)
 
     def _match_cbind_const(self, h):
         """cbind(X, matrix(1, rows=n, cols=1)) -> _cbind_const(X, 1, n): the intercept column
@@ -770,6 +961,53 @@ def fuse_conv_bias(bb):
     return n
 
 
+def _same_index(a, b):
+    return a is b or (a.op == "lit" and b.op == "lit" and a.value is not None and a.value == b.value)
+
+
+def vectorize_indexing(bb):
+    """RewriteIndexingVectorization.vectorizeRightIndexing (reference
+    hops/rewrite/RewriteIndexingVectorization.java:43): several single-cell reads X[i, j1],
+    X[i, j2], ... of one row (literal columns) become one row-segment read X[i, jmin:jmax]
+    and cell reads of that small vector (likewise for one column): one pass over X instead of
+    one per cell.  Returns the number of rewritten reads."""
+    live = getattr(bb, "live_out", None)
+    tops = list(bb.roots) + list(bb.env_out.values())
+    groups = {}
+    for h in H.walk(tops):
+        if h.op != "rix" or h.p.get("list") or len(h.inputs) != 5 or h.inputs[0].dt != "M":
+            continue
+        src, rl, ru, cl, cu = h.inputs
+        if _same_index(rl, ru) and rl.value is not None and _num_lit(cl) and _same_index(cl, cu) \
+                and isinstance(cl.value, int):
+            key = ("r", src.id, rl.id if rl.op != "lit" else ("lit", rl.value))
+            groups.setdefault(key, []).append((h, cl.value))
+        elif _same_index(cl, cu) and cl.value is not None and _num_lit(rl) and _same_index(rl, ru) \
+                and isinstance(rl.value, int):
+            key = ("c", src.id, cl.id if cl.op != "lit" else ("lit", cl.value))
+            groups.setdefault(key, []).append((h, rl.value))
+    n = 0
+    for (kind, _, _), hs in groups.items():
+        idx = {j for _, j in hs}
+        if len(idx) < 2:
+            continue
+        lo, hi = min(idx), max(idx)
+        if hi - lo + 1 > 4 * len(idx):
+            continue                      # sparse accesses: the segment would read mostly unused cells
+        h0 = hs[0][0]
+        src, rl, ru, cl, cu = h0.inputs
+        none = Hop("lit", p={"v": None, "vt": "STRING"}, dt="S", pos=h0.pos)
+        if kind == "r":
+            seg = Hop("rix", [src, rl, ru, lit(lo), lit(hi)], {}, dt="M", pos=h0.pos)
+        else:
+            seg = Hop("rix", [src, lit(lo), lit(hi), cl, cu], {}, dt="M", pos=h0.pos)
+        for h, j in hs:
+            k = lit(j - lo + 1)
+            h.inputs = [seg, none, none, k, k] if kind == "r" else [seg, k, k, none, none]
+            n += 1
+    return n
+
+
 def rewrite_block(bb, config=None):
     """Rewrite a BasicBlock's DAG in place (roots + env_out)."""
     rw = Rewriter(config)
@@ -779,6 +1017,10 @@ def rewrite_block(bb, config=None):
     roots, visit = cse(bb.roots)
     bb.roots = roots
     bb.env_out = {k: visit(v) for k, v in bb.env_out.items()}
+    if rw.enabled:
+        n = vectorize_indexing(bb)
+        if n:
+            rw.stats["indexing-vectorization"] = n
     if rw.enabled and rw.fuse:
         n = fuse_conv_bias(bb)
         if n:

@@ -151,6 +151,9 @@ def fuse_vectors(bb):
                     leaves.append(c)
         if any(c.dt not in ("M", "S") for c in leaves):
             continue
+        for c in leaves:
+            if c.dt == "M" and c.op not in ("lit", "tread"):
+                c.p["keep_dev"] = True       # the program reads it from HBM: no host demotion
         n = len(leaves)
         vid = dict((c.id, k) for k, c in enumerate(leaves))
         instrs = []

@@ -89,11 +89,18 @@ def _placed(fn, h):
     from ..ops.backend import backend
     Tensor = torch.Tensor
 
+    keep_dev = bool(h.p.get("keep_dev"))    # read by a vector program (compiler/vecgen.py)
+
     def run(ctx, a):
         small = backend.small_cells
         if small <= 0 or not backend.on_gpu:
             return fn(ctx, a)
         et = h.exec_type
+        if keep_dev:
+            if et == "CP":
+                return fn(ctx, a)
+            a = [h2d(x) if (type(x) is Tensor and not x.is_cuda) else x for x in a] if et == "GPU" else a
+            return fn(ctx, a)
         if et == "CP":
             a = [d2h(x) if (type(x) is Tensor and x.is_cuda and x.layout == torch.strided) else x for x in a]
             return fn(ctx, a)

@@ -413,3 +413,29 @@ def test_speculative_accept_gradient_fused_into_softmax_pass(icpt):
         r, _ = EX.execute(cs, {"X": X, "Y_vec": y}, out=lambda s: None)
         out[fuse] = r["B_out"].numpy()
     np.testing.assert_allclose(out[True], out[False], rtol=1e-9, atol=1e-11)
+
+
+_RW_CASES = {
+    # rule counter -> script (reference rule in the comment)
+    "empty-aggregate": "Z = matrix(0, rows=4, cols=3)\nr = sum(Z) + sum(rowSums(Z)) + sum(colMaxs(Z))",   # simplifyEmptyAggregate
+    "empty-unary": "Z = matrix(0, rows=4, cols=3)\nr = sum(abs(Z) + 1)",                                    # simplifyEmptyUnaryOperation
+    "empty-reorg": "Z = matrix(0, rows=4, cols=3)\nr = sum(t(Z) + 2)",                                       # simplifyEmptyReorgOperation
+    "empty-matrix-mult": "X = rand(rows=4, cols=5, seed=1)\nZ = matrix(0, rows=5, cols=3)\nr = sum((X %*% Z) + 1)",  # simplifyEmptyMatrixMult
+    "empty-binary": "X = rand(rows=4, cols=3, seed=1)\nZ = matrix(0, rows=nrow(X), cols=ncol(X))\nr = sum((X + Z) * 2)",  # simplifyEmptyBinaryOperation
+    "distributive-binary": "X = rand(rows=4, cols=3, seed=1)\nY = rand(rows=4, cols=3, seed=2)\nr = sum(X - Y * X)",  # simplifyDistributiveBinaryOperation
+    "emult-chain": "A = rand(rows=4, cols=3, seed=1)\nB = rand(rows=4, cols=3, seed=2)\nr = sum((B * A) * B)",  # RewriteElementwiseMultChainOptimization
+    "lix-chain-append": "X = rand(rows=4, cols=3, seed=1)\nW = matrix(0, rows=4, cols=2)\nW[,1] = X[,1]\nW[,2] = X[,3]\nr = sum(W * W)",  # fuseLeftIndexingChainToAppend
+    "indexing-vectorization": "X = rand(rows=4, cols=6, seed=1)\nr = as.scalar(X[2,1]) + as.scalar(X[2,2]) * as.scalar(X[2,4])",  # RewriteIndexingVectorization
+}
+
+
+@pytest.mark.parametrize("rule", sorted(_RW_CASES))
+def test_reference_rewrite_rules(rule):
+    from systemml_amd.api import executor as EX
+    from systemml_amd.conf import DMLConfig
+    src = _RW_CASES[rule]
+    cs = EX.compile_script(src, {}, outputs=["r"], config=DMLConfig(gpu=False))
+    assert cs.cp.rewrite_stats.get(rule, 0) >= 1, cs.cp.rewrite_stats
+    a, _ = EX.execute(cs, {})
+    b, _ = EX.execute(EX.compile_script(src, {}, outputs=["r"], config=DMLConfig(gpu=False, rewrites=False)), {})
+    assert float(a["r"]) == pytest.approx(float(b["r"]), rel=1e-12)

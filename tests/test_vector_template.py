@@ -16,8 +16,8 @@ from systemml_amd.api.mlcontext import SCRIPTS_DIR
 from systemml_amd.conf import DMLConfig
 
 SCRIPT = """
-A = rand(rows=$r, cols=$c, seed=1) - 0.5
-B = rand(rows=$r, cols=$c, seed=2) + 0.1
+A = A0 - 0.5
+B = B0 + 0.1
 k = 3
 while (k > 0) {
   s = sum(A * B)
@@ -40,9 +40,15 @@ while (k > 0) {
 OUTS = ["C2", "D", "f", "flag", "e", "cnt", "A"]
 
 
+def _inputs(r, c):
+    rng = np.random.default_rng(r * 1000 + c)
+    return {"A0": rng.uniform(0, 1, (r, c)), "B0": rng.uniform(0, 1, (r, c))}
+
+
 def _run(cfg, r, c):
-    cs = EX.compile_script(SCRIPT, {"r": r, "c": c}, outputs=OUTS, config=cfg)
-    res, _ = EX.execute(cs, {})
+    ins = _inputs(r, c)
+    cs = EX.compile_script(SCRIPT, {}, inputs=ins, outputs=OUTS, config=cfg)
+    res, _ = EX.execute(cs, ins)
     return cs, {k: (v.double().cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in res.items()}
 
 
@@ -57,7 +63,7 @@ def _check(a, b, tol):
 
 
 def test_plan_one_program_per_loop_tail():
-    cs = EX.compile_script(SCRIPT, {"r": 20, "c": 5}, outputs=OUTS, config=DMLConfig())
+    cs = EX.compile_script(SCRIPT, {}, inputs=_inputs(20, 5), outputs=OUTS, config=DMLConfig())
     assert cs.cp.rewrite_stats.get("vector-fused-ops", 0) >= 20, cs.cp.rewrite_stats
     text = EX.explain(cs.cp, "hops")
     assert sum("vprog[" in ln for ln in text.splitlines()) >= 1, text
