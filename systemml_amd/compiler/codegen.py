@@ -106,8 +106,11 @@ def _regalloc(ops, leaves):
     return code, reg[("op", ops[-1].id)]
 
 
-def fuse_cells(bb):
-    """Fuse the cellwise sub-DAGs of a basic block; returns the number of fused operators."""
+def fuse_cells(bb, single=False):
+    """Fuse the cellwise sub-DAGs of a basic block; returns the number of fused operators.
+    single: also single operators and aggregates of a plain input become generated kernels
+    (GPU plans: the reference's SystemML.cu matrix_matrix_cellwise_op / reduce_* kernels, here
+    generated per operator and operand signature instead of ATen's)."""
     live = getattr(bb, "live_out", None)
     order = walk(list(bb.roots) + list(bb.env_out.values()))
     # block outputs are materialised: statement roots and the variables read after the block
@@ -148,13 +151,18 @@ def fuse_cells(bb):
             if g is not None and ncons.get(c.id, 0) == 1 and c.id not in absorbed:
                 absorbed.add(c.id)
                 plans.append((h, g[0], g[1], (h.p["o"], h.p["dir"])))
+            elif single and g is None and c.dt == "M" and h.dt in ("M", "S"):
+                plans.append((h, [], [c], (h.p["o"], h.p["dir"])))       # aggregate of a plain input
     for h in order:
         g = groups.get(h.id)
-        if g is not None and h.id not in absorbed and len(g[0]) >= 2:
+        if g is not None and h.id not in absorbed and len(g[0]) >= (1 if single else 2):
             plans.append((h, g[0], g[1], None))
     n = 0
     built = []
     for root, ops, leaves, agg in plans:
+        if not ops:
+            built.append((root, ops, leaves, CellProgram((), 1, 0, agg)))
+            continue
         ra = _regalloc(ops, leaves)
         if ra is None:
             continue

@@ -25,6 +25,8 @@ class DMLConfig:
     lazy_scalars: bool = False          # GPU backend: aggregates return HBM-resident scalars (runtime/scalars.DevScalar);
                                         # implies every matrix lives in HBM (gpu_min_cells ignored)
     parallelism: int = 8                # parfor local workers
+    parfor_gpu_streams: int = 4         # parfor on the GPU backend: concurrent worker streams (HW queues)
+    parfor_gpus: int = 1                # parfor on the GPU backend: devices used by one process's workers
     # compiler
     rewrites: bool = True
     fusion: bool = True

@@ -11,9 +11,14 @@ import os
 import torch
 
 
+import threading
+
+_TLS = threading.local()
+
+
 class Backend:
     def __init__(self):
-        self.device = torch.device("cpu")
+        self._device = torch.device("cpu")
         self.dtype = torch.float64
         self.use_kernels = False
         self.bf16_min_cells = 0
@@ -22,8 +27,21 @@ class Backend:
         self.lazy = False           # GPU backend: HBM-resident scalars (runtime/scalars.DevScalar)
 
     @property
+    def device(self):
+        # a parfor worker thread on another GPU sees its own device (runtime/parfor.py)
+        d = getattr(_TLS, "device", None)
+        return self._device if d is None else d
+
+    @device.setter
+    def device(self, d):
+        self._device = d
+
+    def set_thread_device(self, d):
+        _TLS.device = d
+
+    @property
     def on_gpu(self):
-        return self.device.type == "cuda"
+        return self._device.type == "cuda"
 
     def configure(self, config=None):
         want_gpu = True if config is None else (config.gpu and not config.force_cpu)

@@ -12,8 +12,14 @@ Execution model:
     worker changed relative to the pre-loop value is copied into the result;
     accumulators (variables only updated by `+=`, ResultMergeLocalMemory's accumulate
     mode) are merged as the pre-loop value plus every worker's increment.
-On the GPU / SPMD backends workers run on one stream in task order (same result,
-no host thread contention); `par=1` or `mode=LOCAL` with one worker is sequential.
+On the GPU backend each worker thread issues its iterations on a stream of its own (and,
+with config.parfor_gpus > 1, on a device of its own: reference GPUContextPool.java:209
+reserves one GPU context per parfor worker), so independent iterations overlap on the
+MI355X's hardware queues; results merge on the main stream after every worker stream
+has drained into it.  `par=1` or an SPMD run of a row-partitioned body is sequential.
+The degree of parallelism, exec type and task partitioner are chosen by a rule-based
+optimizer (`optimize`, reference opt/OptimizerRuleBased.java:197) unless the script
+fixes them (par=, mode=, taskpartitioner=).
 """
 from __future__ import annotations
 
@@ -125,53 +131,209 @@ def _run_iters(wctx, b, iters, idx, fork):
         exec_blocks(wctx, b.body)
 
 
+class ParForPlan:
+    """Decisions of the parfor optimizer (reference ParForProgramBlock's opt tree after
+    OptimizerRuleBased.optimize): exec type, degree of parallelism, task partitioner and the
+    row / column access pattern of the body's matrix reads (data partitioning candidates)."""
+    __slots__ = ("exec_type", "k", "partitioner", "task_size", "partitions", "devices")
+
+    def __repr__(self):
+        return (f"ParForPlan({self.exec_type}, k={self.k}, {self.partitioner}, devices={self.devices}, "
+                f"partitions={self.partitions})")
+
+
+def _body_has(blocks, kinds):
+    from ..compiler.blocks import IfBlock, WhileBlock, ForBlock
+    for x in blocks:
+        if isinstance(x, kinds):
+            return True
+        if isinstance(x, IfBlock) and (_body_has(x.then_blocks, kinds) or _body_has(x.else_blocks, kinds)):
+            return True
+        if isinstance(x, (WhileBlock, ForBlock)) and _body_has(x.body, kinds):
+            return True
+    return False
+
+
+def data_partitions(b):
+    """Matrices the body reads only as X[i, ] or X[, i] with i the loop variable: the
+    candidates of the reference's data partitioner (DataPartitionerLocal.java:79 writes them as
+    row / column blocks so each task reads its own).  Returns {var: 'row' | 'col'}."""
+    from ..compiler.blocks import BasicBlock
+    from ..compiler import hops as H
+    acc = {}
+    bad = set()
+
+    def visit(blocks):
+        from ..compiler.blocks import IfBlock, WhileBlock, ForBlock
+        for x in blocks:
+            if isinstance(x, BasicBlock):
+                tops = list(x.roots) + list(x.env_out.values())
+                for h in H.walk(tops):
+                    for c in h.inputs:
+                        if c.op != "tread" or c.dt != "M":
+                            continue
+                        name = c.p["name"]
+                        kind = None
+                        if h.op == "rix" and h.inputs[0] is c:
+                            _, rl, ru, cl, cu = h.inputs
+                            def is_var(z):
+                                return z.op == "tread" and z.p.get("name") == b.var
+                            def empty(z):
+                                return z.op == "lit" and z.value is None
+                            if is_var(rl) and (ru is rl or is_var(ru)) and empty(cl) and empty(cu):
+                                kind = "row"
+                            elif is_var(cl) and (cu is cl or is_var(cu)) and empty(rl) and empty(ru):
+                                kind = "col"
+                        if kind is None:
+                            bad.add(name)
+                        elif acc.get(name, kind) != kind:
+                            bad.add(name)
+                        else:
+                            acc[name] = kind
+            elif isinstance(x, IfBlock):
+                visit(x.then_blocks)
+                visit(x.else_blocks)
+            elif isinstance(x, (WhileBlock, ForBlock)):
+                visit(x.body)
+    visit(b.body)
+    return {k: v for k, v in acc.items() if k not in bad}
+
+
+def optimize(ctx, b, n_iters):
+    """Rule-based parfor optimizer (reference opt/OptimizerRuleBased.java:144-197):
+      exec type  REMOTE_SPMD when the run has several ranks and the body reads no
+                 row-partitioned matrix; LOCAL_GPU (worker streams / devices) on a GPU
+                 backend; LOCAL_CPU threads otherwise;
+      k          the script's par=, else the exec type's parallelism (GPU: hardware queues
+                 = config.parfor_gpu_streams, times the devices used), capped by the iterations;
+      tasks      the script's taskpartitioner=, else STATIC for bodies of uniform cost (no
+                 branches or inner while-loops) and FACTORING otherwise;
+      data       row / column access patterns of the body's matrix reads (data_partitions)."""
+    from ..compiler.blocks import IfBlock, WhileBlock
+    cfg = ctx.config
+    pl = ParForPlan()
+    mode = str(b.params.get("mode", "")).upper()
+    par = b.params.get("par")
+    pl.devices = 1
+    if ctx.dist is not None and ctx.dist.world > 1 and mode != "LOCAL" and _spmd_ok(ctx, b):
+        pl.exec_type = "REMOTE_SPMD"
+        k = ctx.dist.world
+    elif ctx.dist is not None:
+        pl.exec_type = "SEQUENTIAL"          # every rank runs every iteration (row-partitioned body)
+        k = 1
+    elif _on_gpu() and torch.cuda.is_available():
+        pl.exec_type = "LOCAL_GPU"
+        ndev = max(1, min(int(getattr(cfg, "parfor_gpus", 1) or 1), torch.cuda.device_count()))
+        pl.devices = ndev
+        k = max(1, int(getattr(cfg, "parfor_gpu_streams", 4) or 1)) * ndev
+    else:
+        pl.exec_type = "LOCAL_CPU"
+        k = cfg.parallelism
+    if isinstance(par, (int, float)) and par and pl.exec_type not in ("REMOTE_SPMD", "SEQUENTIAL"):
+        k = int(par)
+    pl.k = max(1, min(k, n_iters))
+    if pl.k == 1 and pl.exec_type in ("LOCAL_GPU", "LOCAL_CPU"):
+        pl.exec_type = "SEQUENTIAL"
+    pl.devices = min(pl.devices, pl.k)
+    tp = b.params.get("taskpartitioner")
+    if tp is None:
+        tp = "factoring" if _body_has(b.body, (IfBlock, WhileBlock)) else "static"
+    pl.partitioner = str(tp).lower()
+    pl.task_size = b.params.get("tasksize")
+    pl.partitions = data_partitions(b)
+    return pl
+
+
 def exec_parfor(ctx, b, start, end, incr, as_int):
-    from .program import ExecutionContext
     iters = parfor_iterations(start, end, incr, as_int)
     if not iters:
         return
     fork = ctx.seeds.fork()
-    par = b.params.get("par")
-    k = int(par) if isinstance(par, (int, float)) and par else ctx.config.parallelism
-    k = max(1, min(k, len(iters)))
+    pl = optimize(ctx, b, len(iters))
+    b.last_plan = pl                       # -explain / tests
+    if ctx.stats is not None:
+        ctx.stats.count(f"parfor {pl.exec_type.lower()} k={pl.k}")
     result_vars = list(b.result_vars)
     base = {v: ctx.vars.get(v) for v in result_vars}
-    if ctx.dist is not None and ctx.dist.world > 1 and _spmd_ok(ctx, b):
+    if pl.exec_type == "REMOTE_SPMD":
         exec_parfor_spmd(ctx, b, iters, fork, result_vars, base)
         return
-    sequential = k == 1 or ctx.dist is not None or (torch.cuda.is_available() and _on_gpu())
-    if sequential:
+    if pl.exec_type == "SEQUENTIAL":
         saved = ctx.seeds
         try:
             _run_iters(ctx, b, iters, range(len(iters)), fork)
         finally:
             ctx.seeds = saved
         return
-    tasks = partition_tasks(list(enumerate(iters)), k, b.params.get("taskpartitioner", "factoring"),
-                            b.params.get("tasksize"))
+    k = pl.k
+    tasks = partition_tasks(list(enumerate(iters)), k, pl.partitioner, pl.task_size)
     lock = threading.Lock()
     queue = list(tasks)
+    gpu = pl.exec_type == "LOCAL_GPU"
+    main = torch.cuda.current_stream() if gpu else None
+    main_dev = torch.cuda.current_device() if gpu else None
 
-    def worker():
+    def worker(w):
+        from .program import ExecutionContext
         wctx = ExecutionContext(ctx.program, ctx.config, stats=ctx.stats, out=ctx._out, dist=None)
         wctx.vars = dict(ctx.vars)
         wctx.parfor_worker = True        # program.exec_block: serialise recompiling blocks
-        while True:
-            with lock:
-                if not queue:
-                    break
-                task = queue.pop(0)
-            _run_iters(wctx, b, [it for _, it in task], [i for i, _ in task], fork)
-        return {v: wctx.vars.get(v) for v in result_vars}
+
+        def run():
+            while True:
+                with lock:
+                    if not queue:
+                        break
+                    task = queue.pop(0)
+                _run_iters(wctx, b, [it for _, it in task], [i for i, _ in task], fork)
+
+        if not gpu:
+            run()
+            return {v: wctx.vars.get(v) for v in result_vars}, None
+        dev = (main_dev + w) % torch.cuda.device_count() if pl.devices > 1 and w < pl.devices else main_dev
+        from ..ops.backend import backend
+        with torch.cuda.device(dev):
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(main)              # inputs produced on the main stream
+            backend.set_thread_device(torch.device("cuda", dev))
+            try:
+                with torch.cuda.stream(s):
+                    if dev != main_dev:
+                        wctx.vars = _to_device(wctx.vars, torch.device("cuda", dev), pl.partitions)
+                    run()
+            finally:
+                backend.set_thread_device(None)
+        out = {v: wctx.vars.get(v) for v in result_vars}
+        if dev != main_dev:
+            with torch.cuda.stream(s):
+                out = _to_device(out, torch.device("cuda", main_dev), None)
+        for v in out.values():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v.record_stream(main)        # used on the main stream from now on
+        return out, s
 
     with ThreadPoolExecutor(max_workers=k) as ex:
-        futs = [ex.submit(worker) for _ in range(k)]
-        results = [f.result() for f in futs]
+        futs = [ex.submit(worker, w) for w in range(k)]
+        done = [f.result() for f in futs]
+    results = [r for r, _ in done]
+    for _, s in done:
+        if s is not None:
+            main.wait_stream(s)
     acc = set(getattr(b, "accumulators", ()))
     for v in result_vars:
         rs = [r[v] for r in results]
         ctx.vars[v] = _accumulate(base[v], rs) if v in acc else _merge(base[v], rs)
     ctx.vars[b.var] = iters[-1]
+
+
+def _to_device(vars_, dev, partitions):
+    """Copies of a worker's device-resident values on its own GPU (matrices only)."""
+    out = {}
+    for k, v in vars_.items():
+        if isinstance(v, torch.Tensor) and v.is_cuda and v.device != dev:
+            v = v.to(dev, non_blocking=True)
+        out[k] = v
+    return out
 
 
 def _accumulate(base, results):

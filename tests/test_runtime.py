@@ -446,3 +446,66 @@ def test_conv_bias_fusion_keeps_bias_add_semantics():
     from systemml_amd.parser.errors import DMLRuntimeError
     with pytest.raises(Exception):
         R(src, outputs=["d"], args={"nb": 5})
+
+
+def test_parfor_optimizer_rules():
+    """Rule-based parfor optimizer (reference OptimizerRuleBased.java:197): exec type, k,
+    task partitioner from the body's shape, row / column data-partitioning candidates."""
+    from systemml_amd.api import executor as EX
+    from systemml_amd.compiler.blocks import ForBlock
+    src = """
+    X = rand(rows=6, cols=4, seed=1)
+    Y = rand(rows=4, cols=6, seed=2)
+    R = matrix(0, rows=6, cols=1)
+    parfor (i in 1:6) {
+      R[i, 1] = sum(X[i, ] * t(Y[, i]))
+    }
+    S = matrix(0, rows=6, cols=1)
+    parfor (i in 1:6, par=2) {
+      v = 0
+      if (i > 3) { v = sum(X) }
+      S[i, 1] = v + sum(X[i, ])
+    }
+    """
+    cs = EX.compile_script(src, {}, outputs=["R", "S"], config=CFG)
+    res, _ = EX.execute(cs, {})
+    loops = [b for b in cs.cp.blocks if isinstance(b, ForBlock)]
+    p1, p2 = loops[0].last_plan, loops[1].last_plan
+    assert p1.exec_type == "LOCAL_CPU" and p1.k == 6 and p1.partitioner == "static"
+    assert p1.partitions == {"X": "row", "Y": "col"}
+    assert p2.k == 2 and p2.partitioner == "factoring" and "X" not in p2.partitions
+    X = M(res, "R")
+    assert X.shape == (6, 1)
+
+
+@pytest.mark.gpu
+def test_parfor_gpu_streams_beat_serial_loop():
+    """4 worker streams over independent products that each fill a fraction of the GPU
+    (reference GPUContextPool: one GPU context per parfor worker): same result as the
+    sequential loop, in less time."""
+    import time
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from systemml_amd.api import executor as EX
+    rng = np.random.default_rng(5)
+    ins = {"A": rng.uniform(0, 1, (512, 16384)), "B": rng.uniform(0, 1, (16384, 512))}
+    body = "{ C = (A * i) %*% B\n  R[1, i] = sum(C) }"
+    srcs = {"par": "R = matrix(0, rows=1, cols=16)\nparfor (i in 1:16, par=4) " + body,
+            "seq": "R = matrix(0, rows=1, cols=16)\nfor (i in 1:16) " + body}
+    cfg = DMLConfig(gpu=True, precision="single")
+    times, out = {}, {}
+    for k, src in srcs.items():
+        cs = EX.compile_script(src, {}, inputs=ins, outputs=["R"], config=cfg)
+        best = 1e9
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r, _ = EX.execute(cs, ins)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        times[k] = best
+        out[k] = r["R"].double().cpu().numpy()
+    np.testing.assert_allclose(out["par"], out["seq"], rtol=1e-6)
+    print("parfor gpu streams:", times)
+    assert times["par"] < times["seq"], times
