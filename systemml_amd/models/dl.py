@@ -796,7 +796,7 @@ TEST_ALGOS = ("minibatch", "batch", "allreduce")
 
 
 def generate_train_dml(layers, input_shape, solver, epochs, batch_size, seed=-1, train_algo="minibatch",
-                       parallel_batches=2):
+                       parallel_batches=2, spmd=False):
     """Training script for the network.  train_algo (reference Caffe2DML.scala):
       minibatch  -- one update per mini-batch;
       batch      -- full-batch gradient descent;
@@ -827,6 +827,30 @@ def generate_train_dml(layers, input_shape, solver, epochs, batch_size, seed=-1,
         lines += ["    " + c for c in fwd]
         lines.append(f"    loss = {gen.loss_expr()}")
         lines += ["    " + c for c in bwd]
+        lines += [f"    {a} = {b}" for a, b in bn]
+        lines += _opt_update(sc, gen, params, "    ")
+        lines += ["  }", '  print("Epoch " + e + ": loss " + loss)', "}"]
+        return "\n".join(lines), state_vars(gen.layers)
+    if spmd:
+        # synchronous data parallelism over SPMD ranks (one per GPU): every step takes W
+        # consecutive mini-batches, rank r computes the gradients of mini-batch r on its GPU,
+        # one bucketed all-reduce (_dp_allreduce: RCCL over xGMI) averages them (and the loss)
+        # and every rank applies the same update -- the reference's allreduce algorithms
+        # (Caffe2DML.scala:396-405) without the parfor's per-task gradient matrices
+        grads = [gen.grad_of(t) for t in params]
+        bs_local = 1 if train_algo == "allreduce" else None
+        lines += ["W = _dp_world()", "r = _dp_rank()"]
+        if bs_local is not None:
+            lines.append("bs = 1")
+        lines += ["gsz = W * bs", "groups = as.integer(ceil(N / gsz))", "for (e in 1:epochs) {",
+                  "  for (g in 1:groups) {", "    beg = ((g - 1) * gsz + r * bs) %% N + 1",
+                  "    end = min(N, beg + bs - 1)", "    Xb = X[beg:end, ]", "    Yb = Y[beg:end, ]"]
+        lines += ["    " + c for c in fwd]
+        lines.append(f"    loss = {gen.loss_expr()}")
+        lines += ["    " + c for c in bwd]
+        lines.append("    Lm = matrix(loss, rows = 1, cols = 1)")
+        lines.append("    [" + ", ".join(grads + ["Lm"]) + "] = _dp_allreduce(" + ", ".join(grads + ["Lm"]) + ")")
+        lines.append("    loss = as.scalar(Lm)")
         lines += [f"    {a} = {b}" for a, b in bn]
         lines += _opt_update(sc, gen, params, "    ")
         lines += ["  }", '  print("Epoch " + e + ": loss " + loss)', "}"]
@@ -1002,8 +1026,12 @@ class Caffe2DML(BaseSystemMLClassifier):
         else:
             per_step = self.batch_size * (self.parallel_batches if self.train_algo == "allreduce_parallel_batches" else 1)
             epochs = max(1, math.ceil(self.max_iter * per_step / n))
+        from ..parallel import dist as D
+        dctx = D.get_context()
+        spmd = dctx is not None and dctx.world > 1 and self.train_algo in ("allreduce", "allreduce_parallel_batches")
         src, wnames = generate_train_dml(gen_layers, self.input_shape, self.solver, epochs, self.batch_size,
-                                         train_algo=self.train_algo, parallel_batches=self.parallel_batches)
+                                         train_algo=self.train_algo, parallel_batches=self.parallel_batches,
+                                         spmd=spmd)
         self.train_script_ = src
         inputs = {"X": X, "Y": Y}
         if getattr(self, "init_weights_", None):

@@ -539,6 +539,42 @@ def b_ifelse(ctx, test, yes, no):
     return torch.where(tt != 0, yy, nn)
 
 
+# ----------------------------------------------------------------------------
+# data-parallel training across SPMD ranks (Caffe2DML allreduce algorithms, reference
+# Caffe2DML.scala:396-405; here one rank per GPU with an RCCL gradient all-reduce)
+# ----------------------------------------------------------------------------
+@builtin("_dp_world")
+def b_dp_world(ctx):
+    return int(ctx.dist.world) if ctx.dist is not None else 1
+
+
+@builtin("_dp_rank")
+def b_dp_rank(ctx):
+    return int(ctx.dist.rank) if ctx.dist is not None else 0
+
+
+@builtin("_dp_allreduce", multi=True)
+def b_dp_allreduce(ctx, *grads):
+    """Mean of every rank's gradients, as ONE bucketed all-reduce: the matrices are packed
+    into a flat fp32 / fp64 buffer in HBM (one RCCL call over xGMI instead of one per
+    parameter), reduced, scaled by 1 / world and unpacked.  Single process: identity."""
+    dist = ctx.dist
+    if dist is None or dist.world <= 1:
+        return tuple(grads)
+    mats = [_mat(g) for g in grads]
+    dev = dist._coll_device()
+    dt = torch.float64 if any(m.dtype == torch.float64 for m in mats) else torch.float32
+    flat = torch.cat([m.reshape(-1).to(device=dev, dtype=dt) for m in mats])
+    dist.allreduce_(flat, "sum")
+    flat.mul_(1.0 / dist.world)
+    out, off = [], 0
+    for m in mats:
+        n = m.numel()
+        out.append(flat[off:off + n].reshape(m.shape).to(device=m.device, dtype=m.dtype))
+        off += n
+    return tuple(out)
+
+
 @builtin("_sel")
 def b_sel(ctx, test, yes, no):
     """Select of an if-converted branch (compiler/ifconv.py): a scalar test picks one operand

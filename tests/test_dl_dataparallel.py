@@ -1,0 +1,107 @@
+"""Data-parallel Caffe2DML training across SPMD ranks (train_algo allreduce_parallel_batches /
+allreduce; reference Caffe2DML.scala:396-405): every rank trains its own mini-batch and one
+bucketed gradient all-reduce (_dp_allreduce) averages the gradients.  A 2-rank gloo run with
+local batch b must follow the same loss trajectory and end at the same weights as one
+process training mini-batch SGD with batch 2b (a network without batch statistics, so the
+two are mathematically identical)."""
+import os
+import socket
+
+import numpy as np
+
+from systemml_amd.models import dl
+
+LAYERS = None
+
+
+def _layers():
+    L = dl.Layer
+    return [L("conv", "c1", [dl.INPUT], ["c1"], F=4, kh=3, kw=3, sh=1, sw=1, ph=1, pw=1),
+            L("relu", "r1", ["c1"], ["r1"]),
+            L("pool", "p1", ["r1"], ["p1"], mode="MAX", kh=2, kw=2, sh=2, sw=2, ph=0, pw=0),
+            L("dense", "fc", ["p1"], ["fc"], M=3),
+            L("softmax_loss", "loss", ["fc"], ["prob"])]
+
+
+SOLVER = {"type": "momentum", "base_lr": 0.05, "momentum": 0.9}
+SHAPE = (1, 6, 6)
+
+
+def _data():
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((32, 36))
+    Y = np.eye(3)[rng.integers(0, 3, 32)]
+    return X, Y
+
+
+def _train(src, wnames, dist=None):
+    from systemml_amd.api import executor as EX
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.conf import DMLConfig
+    X, Y = _data()
+    cfg = DMLConfig(gpu=False, seed=3)
+    cs = EX.compile_script(src, {"X": "X", "Y": "Y"}, inputs={"X": X, "Y": Y}, outputs=wnames, config=cfg,
+                           filename=os.path.join(SCRIPTS_DIR, "dp.dml"))
+    out = []
+    res, _ = EX.execute(cs, {"X": X, "Y": Y}, out=out.append, dist=dist)
+    losses = [float(s.split("loss ")[1]) for s in out if s.startswith("Epoch")]
+    return {k: res[k].double().numpy() for k in wnames}, losses
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from systemml_amd.parallel import dist as D
+        ctx = D.init(backend="gloo")
+        src, wn = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 3, 4, train_algo="allreduce_parallel_batches",
+                                        spmd=True)
+        w, losses = _train(src, wn, ctx)
+        q.put((rank, w, losses, dict(D.stats)))
+        D.shutdown()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_single_process_dp_script_is_minibatch():
+    # W = 1: the data-parallel script is plain mini-batch SGD
+    a_src, wn = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 2, 8, train_algo="allreduce_parallel_batches",
+                                      spmd=True)
+    b_src, _ = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 2, 8, train_algo="minibatch")
+    wa, la = _train(a_src, wn)
+    wb, lb = _train(b_src, wn)
+    np.testing.assert_allclose(la, lb, rtol=1e-12)
+    for k in wn:
+        np.testing.assert_allclose(wa[k], wb[k], rtol=1e-10, atol=1e-12, err_msg=k)
+
+
+def test_two_rank_gloo_matches_double_batch():
+    import torch.multiprocessing as mp
+    ref_src, wn = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 3, 8, train_algo="minibatch")
+    ref_w, ref_l = _train(ref_src, wn)
+    world, port = 2, _free_port()
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    procs = [mctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, w, losses, st in res:
+        assert not isinstance(w, str), w
+        if rank == 0:                                # prints come from rank 0
+            np.testing.assert_allclose(losses, ref_l, rtol=1e-9)
+        for k in wn:
+            np.testing.assert_allclose(w[k], ref_w[k], rtol=1e-8, atol=1e-10, err_msg=k)
+        assert st["allreduce"] >= 12                 # one bucketed all-reduce per step (4 steps x 3 epochs)
+        assert st["fallback_gathers"] == 0
