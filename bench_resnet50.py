@@ -66,7 +66,7 @@ def resnet50_layers(classes=1000, stages=(3, 4, 6, 3), image=224):
     return L
 
 
-def build_script(layers, input_shape, steps, batch):
+def build_script(layers, input_shape, steps, batch, dp=False):
     from systemml_amd.models import dl
     gen = dl._Gen(layers, input_shape)
     params = dl.trainable(gen.layers)
@@ -86,6 +86,11 @@ def build_script(layers, input_shape, steps, batch):
     lines += ["  " + c for c in gen.forward(train=True)]
     lines.append(f"  loss = {gen.loss_expr()}")
     lines += ["  " + c for c in gen.backward()]
+    if dp:
+        # data parallelism over ranks (one per GPU): one bucketed RCCL all-reduce of every
+        # gradient per step (Caffe2DML allreduce, models/dl.py)
+        grads = [gen.grad_of(t) for t in params]
+        lines.append("  [" + ", ".join(grads) + "] = _dp_allreduce(" + ", ".join(grads) + ")")
     lines += [f"  {a} = {b}" for a, b in gen.bn_updates()]
     lines += dl._opt_update(sc, gen, params, "  ")
     lines += ["  if (i > 0) {", f"    t1 = benchSync({params[-1]})", "  }",
@@ -99,11 +104,18 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="run under torchrun with one rank per GPU: data parallel, --batch images per rank")
     ap.add_argument("--exact-fp32", action="store_true", help="convolutions on exact fp32 MFMA instead of bf16")
     ap.add_argument("--no-fusion", action="store_true", help="disable operator fusion (codegen templates)")
     a = ap.parse_args()
     import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    ctx = None
+    if world > 1:
+        from systemml_amd.parallel import dist as D
+        ctx = D.init()
+    rank = ctx.rank if ctx is not None else 0
     from systemml_amd.api.executor import compile_script, execute
     from systemml_amd.api.mlcontext import SCRIPTS_DIR
     from systemml_amd.conf import DMLConfig
@@ -119,8 +131,8 @@ def main():
     layers = resnet50_layers(image=a.image)
     shape = (3, a.image, a.image)
     total = a.steps + a.warmup
-    src = build_script(layers, shape, total, a.batch)
-    rng = np.random.default_rng(0)
+    src = build_script(layers, shape, total, a.batch, dp=world > 1)
+    rng = np.random.default_rng(rank)          # each rank trains on its own images
     n = a.batch * min(total, 2)
     X = rng.standard_normal((n, 3 * a.image * a.image)).astype(np.float32)
     Y = np.eye(1000, dtype=np.float32)[rng.integers(0, 1000, n)]
@@ -141,16 +153,33 @@ def main():
     steps = [(int(m.group(1)), float(m.group(2)), int(m.group(3))) for m in
              (re.match(r"STEP (\d+) loss (\S+) ns (\d+)", s) for s in out) if m]
     timed = [ns for i, _, ns in steps if i > a.warmup]
-    ms = sum(timed) / len(timed) / 1e6
+    ms = sum(timed) / len(timed) / 1e6 if timed else 0.0
+    n_phys = 1
+    if ctx is not None:
+        ms = ctx.allreduce_scalar(ms, "max")          # rank 0 prints; the slowest rank sets the pace
+        import torch.distributed as tdist
+        devs = [None] * world
+        tdist.all_gather_object(devs, (os.uname().nodename, torch.cuda.current_device() if torch.cuda.is_available() else -1))
+        n_phys = len(set(devs))
+    if rank != 0:
+        if ctx is not None:
+            from systemml_amd.parallel import dist as D
+            D.shutdown()
+        return
     print(json.dumps({"metric": "ResNet-50 training images/s (scripts/nn via Caffe2DML layer DAG)",
-                      "value": round(a.batch / (ms / 1e3), 2), "unit": "images/s", "n_gpus": 1,
+                      "value": round(world * a.batch / (ms / 1e3), 2), "unit": "images/s", "n_gpus": n_phys,
+                      "scaling": "weak", "parallelism": f"dp{world}",
                       "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2),
                       "higher_is_better": True, "dtype": "fp32-exact" if a.exact_fp32 else "bf16 conv MFMA / fp32",
                       "data": "synthetic N(0,1) images, random labels, random-init weights",
                       "losses": [round(l, 4) for _, l, _ in steps], "wall_s": round(wall, 1),
                       "step_ms": [round(ns / 1e6, 1) for _, _, ns in steps],
                       "kernel_counters": {k: v for k, v in K.counters.items() if k.startswith(("conv", "pool", "bias"))},
-                      "config": {"model": "ResNet-50", "batch": a.batch, "image": a.image, "classes": 1000}}))
+                      "config": {"model": "ResNet-50", "batch": a.batch, "global_batch": world * a.batch,
+                                 "image": a.image, "classes": 1000}}))
+    if ctx is not None:
+        from systemml_amd.parallel import dist as D
+        D.shutdown()
 
 
 if __name__ == "__main__":
