@@ -185,13 +185,29 @@ def main():
         return compile_lr(), compile_mlr()
 
     class _Both:
-        """The two compilations of one step, requested from the compiler process."""
+        """The two compilations of one step, requested from the compiler process; the plans
+        are received and hydrated (unpickled, instructions bound) on a host thread while this
+        step's MultiLogReg runs, whose host thread mostly waits on the device."""
 
         def __init__(self):
+            import threading
             self.p1 = svc.submit(src_lr, args_lr, {"X": X1, "y": y1}, ["B_out"], cfg, world=world)
             self.p2 = svc.submit(src_mlr, args_mlr, {"X": X2, "Y_vec": lab}, ["B_out"], cfg, world=world)
+            self.err = None
+
+            def hydrate():
+                try:
+                    self.p1.result()
+                    self.p2.result()
+                except BaseException as e:  # noqa: BLE001 - re-raised by result()
+                    self.err = e
+            self.th = threading.Thread(target=hydrate, daemon=True)
+            self.th.start()
 
         def result(self):
+            self.th.join()
+            if self.err is not None:
+                raise self.err
             r = self.p1.result(), self.p2.result()
             if a.verbose:
                 print("compile service (worker s, wait s, hydrate s):", self.p1.times, self.p2.times, file=sys.stderr)

@@ -408,8 +408,21 @@ def _chain_block(bb, env, stats):
 # ----------------------------------------------------------------------------
 # program-level pass
 # ----------------------------------------------------------------------------
+_SCALAR_TYPES = (bool, int, float, str)
+
+
+import torch as _torch
+_Tensor = _torch.Tensor
+
+
 def _shape_of(v):
-    if isinstance(v, (bool, int, float, str)) or getattr(v, "is_dev_scalar", False):
+    tv = type(v)
+    if tv is _Tensor:
+        sh = v.shape
+        return (sh[0], sh[1]) if len(sh) == 2 else UNK
+    if tv in _SCALAR_TYPES:
+        return SCALAR
+    if isinstance(v, _SCALAR_TYPES) or getattr(v, "is_dev_scalar", False):
         return SCALAR
     sh = getattr(v, "shape", None)
     if sh is not None and len(sh) == 2:

@@ -35,6 +35,7 @@ from .backend import backend
 from .cell import (_C_BIN, _C_UN, BIN_CODES, UN_CODES, _prelude, compile_source, gpu_arch, _rtc_lib, RTC)
 
 VMAX = 65536            # largest common cell count run as one workgroup
+REG = __import__("os").environ.get("SYSML_VPROG_REG", "1") != "0"   # register-resident variant for small n
 NT = 1024               # threads of the workgroup (16 wave64s)
 REDS = ("sum", "sumsq", "min", "max", "mean", "dot", "dot3")
 
@@ -299,6 +300,145 @@ extern "C" __global__ void __launch_bounds__({NT}) sysml_vprog_k(const VArgs P) 
 """), len(scratch)
 
 
+REG_CPT = (1, 2, 4, 8, 16)   # cells per thread of the register-resident variant (n <= 16 * NTR)
+NTR = 512                    # its workgroup: 8 wave64s, 256 VGPRs per lane
+
+
+def _reg_cpt(n):
+    for c in REG_CPT:
+        if n <= c * NTR:
+            return c
+    return 0
+
+
+def generate_reg(vp, T, dts, kinds, n_out_m, n_out_s, cpt):
+    """Register-resident variant for n <= cpt * NT cells: every thread owns cells
+    tid + c * NTR (c < cpt); all matrix operands are loaded once, up front (every load in
+    flight together), and each value stays in VGPRs for the whole program -- the stages
+    between aggregates cost one LDS block reduction each and no memory traffic."""
+    ct = "float" if T == torch.float32 else "double"
+    n = len(vp.leaf_dts)
+    nv = n + len(vp.instrs)
+    cls = vp.cls
+    out_m = [v for v in vp.outs if cls[v] == "M"]
+    out_s = [v for v in vp.outs if cls[v] == "S"]
+    lines = []
+    A = lines.append
+    A("  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;")
+    A("  const sysml_i64 n = P.n;")
+    for k in range(n):
+        if kinds[k] == "h":
+            A(f"  const double v{k} = P.s[{k}];")
+        elif kinds[k] == "d":
+            A(f"  const double v{k} = sysml_ld<double>(P.in[{k}], {dts[k]}, 0);")
+        else:
+            A(f"  T x{k}[{cpt}];")
+    mats = [k for k in range(n) if kinds[k] == "m"]
+    if mats:
+        A(f"  #pragma unroll")
+        A(f"  for (int c = 0; c < {cpt}; ++c) {{")
+        A(f"    const sysml_i64 i = tid + (sysml_i64)c * {NTR};")
+        A(f"    const sysml_i64 ic = i < n ? i : n - 1;")
+        for k in mats:
+            A(f"    x{k}[c] = sysml_ld<T>(P.in[{k}], {dts[k]}, ic);")
+        A("  }")
+    for v in range(n, nv):
+        if cls[v] == "M":
+            A(f"  T m{v}[{cpt}];")
+    by_stage_scalar, by_stage_loop = {}, {}
+    for k, (kind, o, srcs) in enumerate(vp.instrs):
+        v = n + k
+        if kind == "s":
+            by_stage_scalar.setdefault(vp.avail[v], []).append(v)
+        else:
+            by_stage_loop.setdefault(vp.stage[v], []).append(v)
+    kred = max([sum(1 for v in by_stage_loop.get(st, []) if vp.instrs[v - n][0] == "r")
+                for st in range(vp.nstages)] + [1])
+
+    def ref(sv):
+        if cls[sv] == "S":
+            return f"(T)v{sv}"
+        return f"x{sv}[c]" if sv < n else f"m{sv}[c]"
+
+    for st in range(vp.nstages):
+        for v in by_stage_scalar.get(st, []):
+            kind, o, srcs = vp.instrs[v - n]
+            A(f"  const double v{v} = (double){_expr(o, [f'v{x}' for x in srcs], True)};")
+        loop = by_stage_loop.get(st, [])
+        if not loop:
+            continue
+        reds = [v for v in loop if vp.instrs[v - n][0] == "r"]
+        for v in reds:
+            o = vp.instrs[v - n][1]
+            init = "__builtin_inf()" if o == "min" else ("-__builtin_inf()" if o == "max" else "0.0")
+            A(f"  double r{v} = {init};")
+        A("  #pragma unroll")
+        A(f"  for (int c = 0; c < {cpt}; ++c) {{")
+        A(f"    const sysml_i64 i = tid + (sysml_i64)c * {NTR};")
+        A("    const bool ok = i < n;")
+        for v in loop:
+            kind, o, srcs = vp.instrs[v - n]
+            args = [ref(x) for x in srcs]
+            if kind == "m":
+                A(f"    m{v}[c] = (T){_expr(o, args, False)};")
+                if v in out_m:
+                    A(f"    if (ok) static_cast<T*>(P.out[{out_m.index(v)}])[i] = m{v}[c];")
+            else:
+                if o == "dot":
+                    x = f"(double){args[0]} * (double){args[1]}"
+                elif o == "dot3":
+                    x = f"(double){args[0]} * (double){args[1]} * (double){args[2]}"
+                else:
+                    x = f"(double){args[0]}"
+                if o in ("sum", "mean", "dot", "dot3"):
+                    A(f"    if (ok) r{v} += {x};")
+                elif o == "sumsq":
+                    A(f"    if (ok) {{ const double t = {x}; r{v} += t * t; }}")
+                elif o == "min":
+                    A(f"    if (ok) {{ const double t = {x}; r{v} = (t != t || t < r{v}) ? t : r{v}; }}")
+                else:
+                    A(f"    if (ok) {{ const double t = {x}; r{v} = (t != t || t > r{v}) ? t : r{v}; }}")
+        A("  }")
+        for j, v in enumerate(reds):
+            o = vp.instrs[v - n][1]
+            cop = 1 if o == "min" else (2 if o == "max" else 0)
+            A(f"  for (int off = 32; off > 0; off >>= 1) r{v} = sysml_red_comb({cop}, r{v}, __shfl_xor(r{v}, off));")
+            A(f"  if (lane == 0) red[wid * {kred} + {j}] = r{v};")
+        if reds:
+            A("  __syncthreads();")
+        for j, v in enumerate(reds):
+            o = vp.instrs[v - n][1]
+            cop = 1 if o == "min" else (2 if o == "max" else 0)
+            A(f"  double v{v} = red[{j}];")
+            A(f"  for (int w = 1; w < {NTR // 64}; ++w) v{v} = sysml_red_comb({cop}, v{v}, red[w * {kred} + {j}]);")
+            if o == "mean":
+                A(f"  v{v} = v{v} / (double)n;")
+        if reds:
+            A("  __syncthreads();")
+    if out_s:
+        A("  if (tid == 0) {")
+        for j, v in enumerate(out_s):
+            A(f"    P.sout[{j}] = (double)v{v};")
+        A("  }")
+    body = "\n".join(lines)
+    return (_prelude() + _VPRELUDE + f"""
+// generated (register-resident, {cpt} cells / thread): {vp.describe()}
+typedef {ct} T;
+struct VArgs {{
+  const void* in[{max(n, 1)}];
+  double s[{max(n, 1)}];
+  void* out[{max(n_out_m, 1)}];
+  double* sout;
+  T* scratch;
+  sysml_i64 n;
+}};
+extern "C" __global__ void __launch_bounds__({NTR}) sysml_vprog_k(const VArgs P) {{
+  __shared__ double red[{NTR // 64} * {kred}];
+{body}
+}}
+"""), 0
+
+
 def _args_struct(n_in, n_out_m):
     class VArgs(ctypes.Structure):
         _fields_ = [("inp", ctypes.c_void_p * max(n_in, 1)), ("s", ctypes.c_double * max(n_in, 1)),
@@ -412,10 +552,10 @@ def _signature(vp, args):
 
 
 class _Plan:
-    __slots__ = ("fn", "T", "kinds", "types", "Args", "nscr", "out_m", "out_s", "dev")
+    __slots__ = ("fn", "T", "kinds", "types", "Args", "nscr", "out_m", "out_s", "dev", "cpt")
 
 
-def _make_plan(vp, sig, dev):
+def _make_plan(vp, sig, dev, cpt=0):
     kinds, dts, ltypes = [], [], []
     f64 = False
     for e in sig:
@@ -440,7 +580,10 @@ def _make_plan(vp, sig, dev):
     T = torch.float64 if (f64 or backend.dtype == torch.float64) else torch.float32
     out_m = [v for v in vp.outs if vp.cls[v] == "M"]
     out_s = [v for v in vp.outs if vp.cls[v] == "S"]
-    src, nscr = generate(vp, T, dts, kinds, len(out_m), len(out_s))
+    if cpt:
+        src, nscr = generate_reg(vp, T, dts, kinds, len(out_m), len(out_s), cpt)
+    else:
+        src, nscr = generate(vp, T, dts, kinds, len(out_m), len(out_s))
     code = compile_source(src, gpu_arch(dev))
     L = _rtc_lib()
     fn = ctypes.c_void_p()
@@ -455,10 +598,14 @@ def _make_plan(vp, sig, dev):
     pl.Args = _args_struct(len(vp.leaf_dts), len(out_m))
     pl.out_m, pl.out_s = out_m, out_s
     pl.dev = dev
+    pl.cpt = cpt
     return pl
 
 
 _raw_stream = torch._C._cuda_getCurrentRawStream if hasattr(torch._C, "_cuda_getCurrentRawStream") else None
+
+
+_PLANS = {}      # structural program key + signature + device -> plan: programs of recompiled scripts share
 
 
 def _kernel(vp, args):
@@ -470,15 +617,20 @@ def _kernel(vp, args):
         dev = backend.device
     if dev is None or getattr(dev, "type", None) != "cuda":
         return None
-    key = (sig, str(dev))
+    cpt = _reg_cpt(R * Cc) if REG else 0
+    key = (sig, str(dev), cpt)
     pl = vp._plans.get(key, False)
     if pl is False:
-        try:
-            pl = _make_plan(vp, sig, dev)
-        except RuntimeError as e:
-            import warnings
-            warnings.warn(f"vector program not compiled, running its operators one by one: {e}")
-            pl = None
+        gkey = (vp.leaf_dts, vp.instrs, vp.outs, sig, str(dev), backend.dtype, cpt)
+        pl = _PLANS.get(gkey, False)
+        if pl is False:
+            try:
+                pl = _make_plan(vp, sig, dev, cpt)
+            except RuntimeError as e:
+                import warnings
+                warnings.warn(f"vector program not compiled, running its operators one by one: {e}")
+                pl = None
+            _PLANS[gkey] = pl
         vp._plans[key] = pl
     if pl is None:
         return None
@@ -510,12 +662,12 @@ def _kernel(vp, args):
     P.n = n
     di = dev.index if dev.index is not None else torch.cuda.current_device()
     st = _raw_stream(di) if _raw_stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    rc = _rtc_lib().sysml_rtc_launch(pl.fn[0], 1, 1, NT, ctypes.byref(P), ctypes.sizeof(P), st)
+    rc = _rtc_lib().sysml_rtc_launch(pl.fn[0], 1, 1, NTR if pl.cpt else NT, ctypes.byref(P), ctypes.sizeof(P), st)
     if rc != 0:
         raise RuntimeError(f"vector program launch failed: {rc}")
     from . import kernels
     kernels._count("vprog")
-    svals = sout.tolist() if sout is not None else ()     # the one device synchronisation
+    svals = sout.cpu().tolist() if sout is not None else ()     # the one device synchronisation (GIL released)
     del keep
     res = []
     im = iter(outs_m)

@@ -111,7 +111,7 @@ class BufferPool:
         self.host_tensors = False         # tests: treat host tensors as the "device" tier
         self._total = None
         self._next_check = 0.0
-        self.check_interval = 0.005       # s between proactive HBM-usage checks (the query is not free)
+        self.check_interval = 0.05        # s between proactive HBM-usage checks (the query costs ~0.1 ms)
 
     # ------------------------------------------------------------------ access
     def touch(self, frame, name):
