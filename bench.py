@@ -259,8 +259,12 @@ def main():
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    from systemml_amd.utils import hosttrace as HT
+    HT.reset()
     run_steps(a.steps, st, cs_next)
     torch.cuda.synchronize()
+    if HT.ON and rank == 0:
+        print(HT.summary(), file=sys.stderr)
     if prof is not None:
         prof.disable()
     if sampler is not None:

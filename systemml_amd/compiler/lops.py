@@ -46,6 +46,7 @@ def _linearize(roots, tail_writes, make_impl):
             if x.id not in seen:
                 seen.add(x.id)
                 order.append(x)
+    order = _launch_first(order)
     slot_of = {}
     instrs = []
     for i, h in enumerate(order):
@@ -69,6 +70,52 @@ def _linearize(roots, tail_writes, make_impl):
             ins.free = tuple(s for s in f if s != ins.out)
     writes = [(name, slot_of[h.id]) for name, h in tail_writes]
     return instrs, writes, len(order)
+
+
+_HEAVY = {"mm", "tsmm", "mmchain", "smgrad", "smobj", "row", "wquat", "outer"}
+_SIDE = {"sink", "fcall", "fout"}
+
+
+def _launch_first(order):
+    """Issue the block's big device operators (products, fused row / chain kernels) as early
+    as their inputs allow, ahead of unrelated host scalar work: the GPU starts on the long
+    kernel while the host interprets the rest of the block (e.g. a solver loop's counter
+    updates and convergence bookkeeping).  Operators that depend on a side effect (calls,
+    prints, random generators) keep their statement order."""
+    if not any(h.op in _HEAVY for h in order):
+        return order
+    from .hops import NONDETERMINISTIC
+    pos = {h.id: i for i, h in enumerate(order)}
+    tainted = set()
+    for h in order:
+        if h.op in _SIDE or (h.op == "bi" and h.p.get("name") in NONDETERMINISTIC) or \
+                any(c.id in tainted for c in h.inputs):
+            tainted.add(h.id)
+    out, done = [], set()
+
+    def emit(h):
+        stack = [(h, False)]
+        while stack:
+            x, ready = stack.pop()
+            if x.id in done:
+                continue
+            if ready:
+                done.add(x.id)
+                out.append(x)
+                continue
+            stack.append((x, True))
+            for c in sorted(x.inputs, key=lambda c: -pos.get(c.id, 0)):
+                if c.id not in done:
+                    stack.append((c, False))
+
+    for h in order:
+        if h.op in _HEAVY and h.id not in tainted:
+            emit(h)
+    for h in order:
+        if h.id not in done:
+            done.add(h.id)
+            out.append(h)
+    return out
 
 
 _TLS = threading.local()    # .rw: rewrite counters of the program this thread compiles

@@ -15,6 +15,7 @@ import ctypes
 import os
 
 import torch
+from ..utils import hosttrace as _HT
 
 from ..parser.errors import DMLRuntimeError
 from .backend import backend
@@ -446,6 +447,7 @@ def _chain4(mode, X, kp, V, S, lds, sbc, U=None, ldu=0, obj=None):
     part = torch.empty((grid, D * kp), dtype=torch.float32, device=X.device)
     if S is None:
         S, lds = V, 0      # the kernel streams a row-side operand in every mode: any valid memory
+    _HT.mark("chain-launch")
     if _c4m(X, kp):
         ob = None
         if obj is not None:

@@ -32,6 +32,7 @@ import weakref
 import torch
 
 from .backend import backend
+from ..utils import hosttrace as _HT
 from .cell import (_C_BIN, _C_UN, BIN_CODES, UN_CODES, _prelude, compile_source, gpu_arch, _rtc_lib, RTC)
 
 VMAX = 65536            # largest common cell count run as one workgroup
@@ -668,6 +669,7 @@ def _kernel(vp, args):
     from . import kernels
     kernels._count("vprog")
     svals = sout.cpu().tolist() if sout is not None else ()     # the one device synchronisation (GIL released)
+    _HT.mark("vprog-sync")
     del keep
     res = []
     im = iter(outs_m)

@@ -20,6 +20,7 @@ from ..parser.errors import DMLRuntimeError, DMLScriptStop
 from ..compiler.blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
 from . import scalars as S
 from .bufferpool import Evicted
+from ..utils import hosttrace as _HT
 
 
 class ExecutionContext:
@@ -271,6 +272,7 @@ def exec_instrs(ctx, instrs, nslots, owner=None):
 
 
 def eval_pred(ctx, pred):
+    _HT.mark("pred")
     if pred.is_const:
         return pred.const
     slots = exec_instrs(ctx, pred.instrs, pred.nslots, pred)
@@ -308,6 +310,7 @@ def exec_block(ctx, b):
 
 
 def _exec_basic(ctx, b):
+    _HT.mark("block-start")
     if True:
         if ctx.debugger is not None:
             ctx.debugger.cur_block = b
@@ -324,6 +327,7 @@ def _exec_basic(ctx, b):
                 if ctx.config is not None and ctx.config.explain == "recompile_runtime":
                     ctx.print(f"# EXPLAIN (recompile_runtime): block at line "
                               f"{b.pos.line if b.pos else '?'}\n" + runtime_plan(b, "  "))
+        _HT.mark("block-plan")
         if getattr(b, "licm_pre", False):
             # hoisted loop invariants: a failure surfaces only if the loop reads the value
             try:
@@ -342,6 +346,7 @@ def _exec_basic(ctx, b):
             vars_.pop(name, None)
         if ctx.pool is not None:
             ctx.pool.maybe_evict(ctx.frames())
+        _HT.mark("block-end")
         return
 
 
