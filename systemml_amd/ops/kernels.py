@@ -80,6 +80,21 @@ def load(required=False):
     L.sysml_spmm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                              ctypes.c_int, ctypes.c_void_p]
+    L.sysml_spmm_bal.restype = ctypes.c_int
+    L.sysml_spmm_bal.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_void_p,
+                                                                                        ctypes.c_int64, ctypes.c_int64,
+                                                                                        ctypes.c_int, ctypes.c_int64,
+                                                                                        ctypes.c_void_p]
+    L.sysml_spgemm_count.restype = ctypes.c_int
+    L.sysml_spgemm_count.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int,
+                                                                                            ctypes.c_void_p,
+                                                                                            ctypes.c_void_p]
+    L.sysml_spgemm_fill.restype = ctypes.c_int
+    L.sysml_spgemm_fill.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.c_int] + \
+        [ctypes.c_void_p] * 4
+    L.sysml_tsmm_sparse.restype = ctypes.c_int
+    L.sysml_tsmm_sparse.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     L.sysml_sddmm.restype = ctypes.c_int
     L.sysml_sddmm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
@@ -867,6 +882,120 @@ def cumagg(op, X):
 # ----------------------------------------------------------------------------
 # CSR sparse x dense (ops/hip/spmm.hip)
 # ----------------------------------------------------------------------------
+_IDX32 = {}
+
+
+def csr_idx32(A):
+    """int32 copy of a CSR matrix's column indices (half the index bytes of every sparse
+    product), cached per pattern; None when the matrix has >= 2^31 columns."""
+    col = A.col_indices()
+    if A.shape[1] >= 2 ** 31:
+        return None
+    if col.dtype == torch.int32:
+        return col.contiguous()
+    key = (col.data_ptr(), col.numel(), A.shape[1])
+    e = _IDX32.get(key)
+    if e is None or e[0] is not col:
+        if len(_IDX32) >= 8:
+            _IDX32.pop(next(iter(_IDX32)))
+        e = (col, col.to(torch.int32).contiguous())
+        _IDX32[key] = e
+    return e[1]
+
+
+def spmm_bal(A, B):
+    """C = A %*% B for CSR A and dense B on the nnz-balanced kernel (int32 column indices,
+    skew-tolerant: ops/hip/spgemm.hip); None if unsupported."""
+    L = load(required=True)
+    if A.layout != torch.sparse_csr or B.dim() != 2 or B.shape[0] != A.shape[1]:
+        return None
+    dt = torch.promote_types(A.dtype, B.dtype)
+    if dt not in (torch.float32, torch.float64):
+        dt = torch.float32
+    m, n = A.shape
+    K = B.shape[1]
+    crow = A.crow_indices().to(torch.int64).contiguous()
+    c32 = csr_idx32(A)
+    col = c32 if c32 is not None else A.col_indices().to(torch.int64).contiguous()
+    val = A.values().to(dt).contiguous()
+    B = B.to(device=val.device, dtype=dt).contiguous()
+    C = torch.zeros((m, K), dtype=dt, device=val.device)
+    nnz = int(val.numel())
+    rc = L.sysml_spmm_bal(1 if dt == torch.float32 else 2, int(c32 is not None), crow.data_ptr(), col.data_ptr(),
+                          val.data_ptr(), B.data_ptr(), K, C.data_ptr(), K, m, K, nnz, _stream())
+    if rc == -1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"sysml_spmm_bal failed: {rc}")
+    _count("spmm_bal")
+    return C
+
+
+SPGEMM_MAXN = 32768
+
+
+def spgemm(A, B):
+    """C = A %*% B for two CSR matrices (fp32, n = ncol(B) <= 32768): Gustavson rows with an LDS
+    dense accumulator, count pass + fill pass; canonical CSR result.  None if unsupported."""
+    L = load(required=True)
+    if A.layout != torch.sparse_csr or B.layout != torch.sparse_csr or A.shape[1] != B.shape[0]:
+        return None
+    m, n = A.shape[0], B.shape[1]
+    if n > SPGEMM_MAXN or n < 1 or m < 1:
+        return None
+    dev = A.values().device
+    ac, bc = A.crow_indices().to(torch.int64).contiguous(), B.crow_indices().to(torch.int64).contiguous()
+    a32, b32 = csr_idx32(A), csr_idx32(B)
+    acol = a32 if a32 is not None else A.col_indices().to(torch.int64).contiguous()
+    bcol = b32 if b32 is not None else B.col_indices().to(torch.int64).contiguous()
+    av = A.values().to(torch.float32).contiguous()
+    bv = B.values().to(device=dev, dtype=torch.float32).contiguous()
+    cnt = torch.empty(m, dtype=torch.int64, device=dev)
+    st = _stream()
+    rc = L.sysml_spgemm_count(int(a32 is not None), int(b32 is not None), ac.data_ptr(), acol.data_ptr(),
+                              bc.data_ptr(), bcol.data_ptr(), m, n, cnt.data_ptr(), st)
+    if rc != 0:
+        return None
+    ccrow = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(cnt, 0, out=ccrow[1:])
+    nnz = int(ccrow[-1].item())
+    ccol = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
+    cval = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    rc = L.sysml_spgemm_fill(int(a32 is not None), int(b32 is not None), ac.data_ptr(), acol.data_ptr(),
+                             av.data_ptr(), bc.data_ptr(), bcol.data_ptr(), bv.data_ptr(), m, n, ccrow.data_ptr(),
+                             ccol.data_ptr(), cval.data_ptr(), _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_spgemm_fill failed: {rc}")
+    _count("spgemm")
+    return torch.sparse_csr_tensor(ccrow, ccol[:nnz], cval[:nnz], (m, n), device=dev)
+
+
+TSMM_SP_MAXD = 8192
+
+
+def tsmm_sparse(X):
+    """t(X) %*% X for CSR X (D = ncol <= 8192) as a dense D x D matrix: pair products of
+    every row's non-zeros scattered into the upper triangle, then mirrored."""
+    L = load(required=True)
+    if X.layout != torch.sparse_csr:
+        return None
+    m, D = X.shape
+    if D > TSMM_SP_MAXD or D < 1:
+        return None
+    dt = X.dtype if X.dtype in (torch.float32, torch.float64) else torch.float32
+    crow = X.crow_indices().to(torch.int64).contiguous()
+    c32 = csr_idx32(X)
+    col = c32 if c32 is not None else X.col_indices().to(torch.int64).contiguous()
+    val = X.values().to(dt).contiguous()
+    C = torch.zeros((D, D), dtype=dt, device=val.device)
+    rc = L.sysml_tsmm_sparse(1 if dt == torch.float32 else 2, int(c32 is not None), crow.data_ptr(), col.data_ptr(),
+                             val.data_ptr(), m, C.data_ptr(), D, _stream())
+    if rc != 0:
+        return None
+    _count("tsmm_sparse")
+    return C
+
+
 def spmm(A, B, transA=False):
     """A (CSR, m x n) %*% B (dense n x K), or t(A) %*% B (B: m x K) without transposing A.
     Computed in the wider of the two dtypes (fp32 / fp64); None if unsupported."""

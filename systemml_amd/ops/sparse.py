@@ -177,21 +177,35 @@ def mm(a, b, transA=False):
     a dense right operand runs the hand-written SpMM / SpMV kernel of ops/hip/spmm.hip; t(A)
     uses the cached transposed structure of A's pattern (_transpose_plan) when the product
     is wide enough to pay for the value gather, else the kernel's atomic scatter."""
+    from .backend import backend
     if is_sparse(a) and a.layout == torch.sparse_csr and a.is_cuda and not is_sparse(b):
-        from .backend import backend
         if backend.use_kernels:
             from . import kernels
             bd = densify(b)
             if transA and bd.dim() == 2 and bd.shape[1] >= 4:
-                crowT, colT, perm, _, _ = _transpose_plan(a)
-                at = torch.sparse_csr_tensor(crowT, colT, a.values()[perm], (a.shape[1], a.shape[0]),
-                                             device=a.device)
-                r = kernels.spmm(at, bd, False)
+                at = _transposed(a)
+                r = kernels.spmm_bal(at, bd)
                 if r is not None:
                     return r
-            r = kernels.spmm(a, bd, transA)
+            r = kernels.spmm_bal(a, bd) if not transA else kernels.spmm(a, bd, True)
             if r is not None:
                 return r
+    if backend.use_kernels and is_sparse(a) and is_sparse(b) and a.is_cuda and b.is_cuda and \
+            a.layout == torch.sparse_csr and b.layout == torch.sparse_csr:
+        # sparse x sparse: Gustavson SpGEMM with an LDS accumulator (ops/hip/spgemm.hip)
+        from . import kernels
+        r = kernels.spgemm(_transposed(a) if transA else a, b)
+        if r is not None:
+            return r
+    if backend.use_kernels and not is_sparse(a) and is_sparse(b) and b.layout == torch.sparse_csr and b.is_cuda \
+            and isinstance(a, torch.Tensor) and a.is_cuda and a.dim() == 2:
+        # dense x sparse: D %*% S = t(t(S) %*% t(D)), t(S) from the cached transpose plan and
+        # the nnz-balanced SpMM over it
+        from . import kernels
+        at = a.t() if transA else a
+        r = kernels.spmm_bal(_transposed(b), at.t().contiguous())
+        if r is not None:
+            return r.t().contiguous()
     if is_sparse(a):
         if transA:
             a = a.t()                                  # CSR^T = CSC, consumed by spmm
@@ -201,8 +215,26 @@ def mm(a, b, transA=False):
     return (b.t() @ at.t().contiguous().to(b.dtype)).t().contiguous() if is_sparse(b) else None
 
 
+def _transposed(a):
+    """t(A) as CSR from the cached transpose plan of A's pattern (values gathered)."""
+    crowT, colT, perm, _, _ = _transpose_plan(a)
+    return torch.sparse_csr_tensor(crowT, colT, a.values()[perm], (a.shape[1], a.shape[0]), device=a.device)
+
+
 def tsmm(x, left=True):
-    """t(X) %*% X (left) or X %*% t(X) as a sparse x sparse product; the (small) result is dense."""
+    """t(X) %*% X (left) or X %*% t(X) as a sparse x sparse product; the (small) result is dense.
+    On the MI355X the left form is the pair-scatter kernel (ops/hip/spgemm.hip), the right
+    form the SpGEMM of X and t(X) when its columns fit the LDS accumulator."""
+    from .backend import backend
+    if backend.use_kernels and x.is_cuda and x.layout == torch.sparse_csr:
+        from . import kernels
+        r = kernels.tsmm_sparse(x) if left else None
+        if r is None and not left:
+            r = kernels.spgemm(x, _transposed(x))
+            if r is not None:
+                r = r.to_dense()
+        if r is not None:
+            return r
     xt = x.t().to_sparse_csr()
     r = (xt @ x) if left else (x @ xt)
     return densify(r).contiguous()
