@@ -148,15 +148,14 @@ __global__ void __launch_bounds__(SG_T) spgemm_fill_kernel(const int64_t* __rest
                                                            const IB* __restrict__ bcol,
                                                            const float* __restrict__ bval, int64_t m, int n,
                                                            const int64_t* __restrict__ ccrow,
-                                                           int64_t* __restrict__ ccol, float* __restrict__ cval) {
+                                                           int64_t* __restrict__ ccol, float* __restrict__ cval,
+                                                           int64_t* __restrict__ fcnt) {
   extern __shared__ float acc[];                      // n floats, then the bitmap
   unsigned* bits = reinterpret_cast<unsigned*>(acc + n);
-  __shared__ unsigned wsum[SG_T];
   const int nw = (n + 31) >> 5;
+  const int lane = threadIdx.x & 63;
   for (int64_t i = blockIdx.x; i < m; i += gridDim.x) {
     const int64_t ab = acrow[i], ae = acrow[i + 1];
-    const int64_t out0 = ccrow[i];
-    if (ab == ae) continue;
     for (int x = threadIdx.x; x < n; x += SG_T) acc[x] = 0.0f;
     for (int x = threadIdx.x; x < nw; x += SG_T) bits[x] = 0u;
     __syncthreads();
@@ -171,32 +170,32 @@ __global__ void __launch_bounds__(SG_T) spgemm_fill_kernel(const int64_t* __rest
       }
     }
     __syncthreads();
-    // ordered compaction: thread t owns a contiguous range of bitmap words
-    const int per = (nw + SG_T - 1) / SG_T;
-    const int w0 = threadIdx.x * per;
-    const int w1 = w0 + per < nw ? w0 + per : nw;
-    unsigned c = 0;
-    for (int x = w0; x < w1; ++x) c += __popc(bits[x]);
-    wsum[threadIdx.x] = c;
-    __syncthreads();
-    // exclusive scan of wsum (Hillis-Steele in LDS)
-    for (int off = 1; off < SG_T; off <<= 1) {
-      const unsigned v = threadIdx.x >= off ? wsum[threadIdx.x - off] : 0u;
-      __syncthreads();
-      wsum[threadIdx.x] += v;
-      __syncthreads();
-    }
-    int64_t o = out0 + (int64_t)(wsum[threadIdx.x] - c);
-    for (int x = w0; x < w1; ++x) {
-      unsigned bw = bits[x];
-      while (bw) {
-        const int bit = __ffs(bw) - 1;
-        bw &= bw - 1;
-        const int j = (x << 5) + bit;
-        ccol[o] = j;
-        cval[o] = acc[j];
-        ++o;
+    // ordered compaction by the first wave: 64 bitmap words per step, a wave-wide exclusive
+    // scan of their popcounts places each lane's columns
+    if (threadIdx.x < 64) {
+      int64_t o = ccrow[i];
+      for (int base = 0; base < nw; base += 64) {
+        const int x = base + lane;
+        unsigned bw = x < nw ? bits[x] : 0u;
+        const int c = __popc(bw);
+        int incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int v = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += v;
+        }
+        int64_t w = o + (incl - c);
+        while (bw) {
+          const int bit = __ffs(bw) - 1;
+          bw &= bw - 1;
+          const int j = (x << 5) + bit;
+          ccol[w] = j;
+          cval[w] = acc[j];
+          ++w;
+        }
+        o += __shfl(incl, 63, 64);
       }
+      if (lane == 0) fcnt[i] = o - ccrow[i];
     }
     __syncthreads();
   }
@@ -284,10 +283,11 @@ int sysml_spgemm_count(int ia32, int ib32, const void* acrow, const void* acol, 
   return (int)hipGetLastError();
 }
 
-// pass 2 (fp32 values): C's columns (int64, sorted per row) and values at ccrow's offsets.
+// pass 2 (fp32 values): C's columns (int64, sorted per row) and values at ccrow's offsets;
+// fcnt[i] receives the entries written for row i (checked against pass 1 by the caller).
 int sysml_spgemm_fill(int ia32, int ib32, const void* acrow, const void* acol, const void* aval, const void* bcrow,
                       const void* bcol, const void* bval, int64_t m, int n, const void* ccrow, void* ccol, void* cval,
-                      void* stream) {
+                      void* fcnt, void* stream) {
   using namespace sysml_sg;
   if (n > SG_MAXN || n <= 0) return -1;
   if (m <= 0) return 0;
@@ -301,7 +301,7 @@ int sysml_spgemm_fill(int ia32, int ib32, const void* acrow, const void* acol, c
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
   hipLaunchKernelGGL((spgemm_fill_kernel<IA, IB>), dim3(blocks), dim3(SG_T), lds, s, ac, (const IA*)acol, \
                      (const float*)aval, bc, (const IB*)bcol, (const float*)bval, m, n,                    \
-                     (const int64_t*)ccrow, (int64_t*)ccol, (float*)cval)
+                     (const int64_t*)ccrow, (int64_t*)ccol, (float*)cval, (int64_t*)fcnt)
   if (ia32 && ib32) { SGF(int32_t, int32_t); }
   else if (ia32) { SGF(int32_t, int64_t); }
   else if (ib32) { SGF(int64_t, int32_t); }

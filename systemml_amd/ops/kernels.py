@@ -91,7 +91,7 @@ def load(required=False):
                                                                                             ctypes.c_void_p]
     L.sysml_spgemm_fill.restype = ctypes.c_int
     L.sysml_spgemm_fill.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.c_int] + \
-        [ctypes.c_void_p] * 4
+        [ctypes.c_void_p] * 5
     L.sysml_tsmm_sparse.restype = ctypes.c_int
     L.sysml_tsmm_sparse.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
@@ -957,15 +957,18 @@ def spgemm(A, B):
     if rc != 0:
         return None
     ccrow = torch.zeros(m + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(cnt, 0, out=ccrow[1:])
+    ccrow[1:] = torch.cumsum(cnt, 0)
     nnz = int(ccrow[-1].item())
     ccol = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
     cval = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    fcnt = torch.empty(m, dtype=torch.int64, device=dev)
     rc = L.sysml_spgemm_fill(int(a32 is not None), int(b32 is not None), ac.data_ptr(), acol.data_ptr(),
                              av.data_ptr(), bc.data_ptr(), bcol.data_ptr(), bv.data_ptr(), m, n, ccrow.data_ptr(),
-                             ccol.data_ptr(), cval.data_ptr(), _stream())
+                             ccol.data_ptr(), cval.data_ptr(), fcnt.data_ptr(), _stream())
     if rc != 0:
         raise RuntimeError(f"sysml_spgemm_fill failed: {rc}")
+    if not torch.equal(fcnt, cnt):
+        raise RuntimeError("sysml_spgemm: fill pass disagrees with the count pass")
     _count("spgemm")
     return torch.sparse_csr_tensor(ccrow, ccol[:nnz], cval[:nnz], (m, n), device=dev)
 
