@@ -416,6 +416,8 @@ def _signature(args):
     for x in args:
         tx = type(x)
         if tx is _Tensor:
+            if x.layout is not torch.strided:
+                return None               # sparse operands: the sequential operators' sparse paths
             sig.append((x.shape, x.dtype, x.device, x.layout, x.is_contiguous(), x.data_ptr() & 15))
         elif tx is DevScalar:
             sig.append(("d", x.t.dtype, x.t.device))
