@@ -33,9 +33,9 @@ __device__ __forceinline__ void load_vec(const T* p, T (&v)[NV]) {
 }
 
 // G lanes per non-zero, NV elements per lane per chunk (16 B when vectorised), NCH chunks
-template <typename T, int G, int NV, int NCH>
+template <typename T, int G, int NV, int NCH, typename I>
 __global__ __launch_bounds__(WAVES * 64) void sddmm_kernel(const int64_t* __restrict__ crow,
-                                                           const int64_t* __restrict__ col,
+                                                           const I* __restrict__ col,
                                                            const T* __restrict__ U, const T* __restrict__ V,
                                                            int64_t m, int r, T* __restrict__ out) {
   const int lane = threadIdx.x & 63;
@@ -55,37 +55,54 @@ __global__ __launch_bounds__(WAVES * 64) void sddmm_kernel(const int64_t* __rest
 #pragma unroll
         for (int j = 0; j < NV; ++j) u[c][j] = T(0);
     }
-    for (int64_t p0 = b; p0 < e; p0 += NG) {
-      const int64_t p = p0 + grp;
-      T acc = T(0);
-      if (p < e) {
-        const T* vr = V + col[p] * (int64_t)r;
+    // UN steps of NG non-zeros per iteration: the column indices first, then every V-row
+    // gather of the batch (random rows), then the dot products
+    constexpr int UN = NCH == 1 ? 4 : 1;
+    for (int64_t p0 = b; p0 < e; p0 += NG * UN) {
+      int64_t cc[UN];
+#pragma unroll
+      for (int s2 = 0; s2 < UN; ++s2) {
+        const int64_t p = p0 + s2 * NG + grp;
+        cc[s2] = p < e ? (int64_t)col[p] : 0;
+      }
+      T acc[UN];
+      T vv[UN][NCH][NV];
+#pragma unroll
+      for (int s2 = 0; s2 < UN; ++s2) {
+        const T* vr = V + cc[s2] * (int64_t)r;
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
           const int k = (c * G + gl) * NV;
-          if (k < r) {
-            T v[NV];
-            load_vec<T, NV>(vr + k, v);
+          if (k < r) load_vec<T, NV>(vr + k, vv[s2][c]);
+          else
 #pragma unroll
-            for (int j = 0; j < NV; ++j) acc += u[c][j] * v[j];
-          }
+            for (int j = 0; j < NV; ++j) vv[s2][c][j] = T(0);
         }
       }
 #pragma unroll
-      for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-      if (gl == 0 && p < e) out[p] = acc;
+      for (int s2 = 0; s2 < UN; ++s2) {
+        acc[s2] = T(0);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int j = 0; j < NV; ++j) acc[s2] += u[c][j] * vv[s2][c][j];
+#pragma unroll
+        for (int o = G / 2; o >= 1; o >>= 1) acc[s2] += __shfl_xor(acc[s2], o, 64);
+        const int64_t p = p0 + s2 * NG + grp;
+        if (gl == 0 && p < e) out[p] = acc[s2];
+      }
     }
   }
 }
 
-template <typename T, int NV>
-int launch(const int64_t* crow, const int64_t* col, const T* U, const T* V, int64_t m, int r, T* out,
+template <typename T, int NV, typename I>
+int launch(const int64_t* crow, const I* col, const T* U, const T* V, int64_t m, int r, T* out,
            hipStream_t s) {
   int64_t blocks = (m + WAVES - 1) / WAVES;
   if (blocks > 256 * 64) blocks = 256 * 64;     // 8 XCDs x 32 CUs x 64: grid-stride beyond that
   const int lanes = (r + NV - 1) / NV;          // lanes needed to cover one row once
   dim3 g((unsigned)blocks), t(WAVES * 64);
-#define SD_CASE(G_, NCH_) hipLaunchKernelGGL((sddmm_kernel<T, G_, NV, NCH_>), g, t, 0, s, crow, col, U, V, m, r, out)
+#define SD_CASE(G_, NCH_) hipLaunchKernelGGL((sddmm_kernel<T, G_, NV, NCH_, I>), g, t, 0, s, crow, col, U, V, m, r, out)
   if (lanes <= 1) SD_CASE(1, 1);
   else if (lanes <= 2) SD_CASE(2, 1);
   else if (lanes <= 4) SD_CASE(4, 1);
@@ -105,29 +122,38 @@ int launch(const int64_t* crow, const int64_t* col, const T* U, const T* V, int6
 extern "C" {
 
 // dtype 0 = fp32, 1 = fp64.  Returns 0 on success, -1 on unsupported shape, else a hipError_t.
-int sysml_sddmm(int dtype, const void* crow, const void* col, const void* U, const void* V, int64_t m, int r,
-                void* out, void* stream) {
+// idx32: the column indices are int32 (half the index bytes of the pass).
+int sysml_sddmm2(int dtype, int idx32, const void* crow, const void* col, const void* U, const void* V, int64_t m,
+                 int r, void* out, void* stream) {
   using namespace sysml_sd;
   if (r <= 0 || m <= 0) return -1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const auto* cr = static_cast<const int64_t*>(crow);
-  const auto* cl = static_cast<const int64_t*>(col);
   const bool aligned = (reinterpret_cast<uintptr_t>(U) % 16) == 0 && (reinterpret_cast<uintptr_t>(V) % 16) == 0;
+#define SD_IDX(T_, NV_, u_, v_, o_)                                                                   \
+  (idx32 ? launch<T_, NV_, int32_t>(cr, static_cast<const int32_t*>(col), u_, v_, m, r, o_, s)        \
+         : launch<T_, NV_, int64_t>(cr, static_cast<const int64_t*>(col), u_, v_, m, r, o_, s))
   if (dtype == 0) {
     const auto* u = static_cast<const float*>(U);
     const auto* v = static_cast<const float*>(V);
     auto* o = static_cast<float*>(out);
-    if (aligned && r % 4 == 0) return launch<float, 4>(cr, cl, u, v, m, r, o, s);
-    return launch<float, 1>(cr, cl, u, v, m, r, o, s);
+    if (aligned && r % 4 == 0) return SD_IDX(float, 4, u, v, o);
+    return SD_IDX(float, 1, u, v, o);
   }
   if (dtype == 1) {
     const auto* u = static_cast<const double*>(U);
     const auto* v = static_cast<const double*>(V);
     auto* o = static_cast<double*>(out);
-    if (aligned && r % 2 == 0) return launch<double, 2>(cr, cl, u, v, m, r, o, s);
-    return launch<double, 1>(cr, cl, u, v, m, r, o, s);
+    if (aligned && r % 2 == 0) return SD_IDX(double, 2, u, v, o);
+    return SD_IDX(double, 1, u, v, o);
   }
+#undef SD_IDX
   return -1;
+}
+
+int sysml_sddmm(int dtype, const void* crow, const void* col, const void* U, const void* V, int64_t m, int r,
+                void* out, void* stream) {
+  return sysml_sddmm2(dtype, 0, crow, col, U, V, m, r, out, stream);
 }
 
 }  // extern "C"

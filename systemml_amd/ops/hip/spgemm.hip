@@ -65,7 +65,23 @@ __global__ void __launch_bounds__(WAVES * 64) spmm_bal_kernel(const int64_t* __r
           const int k = k0 + gl;
           T acc = T(0);
           if (k < K) {
-            for (int64_t p = b + g; p < q; p += NG) acc += val[p] * B[(int64_t)col[p] * ldb + k];
+            // 4 non-zeros per group in flight: their indices and values first, then the 4
+            // dependent B-row gathers (random rows: latency-bound without the batching)
+            for (int64_t p0 = b + g; p0 < q; p0 += 4 * NG) {
+              int64_t c[4];
+              T v[4], bv[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int64_t p = p0 + u * NG;
+                const bool in = p < q;
+                c[u] = in ? (int64_t)col[p] : 0;
+                v[u] = in ? val[p] : T(0);
+              }
+#pragma unroll
+              for (int u = 0; u < 4; ++u) bv[u] = B[c[u] * ldb + k];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) acc += v[u] * bv[u];
+            }
           }
 #pragma unroll
           for (int o = G; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);

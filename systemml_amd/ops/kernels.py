@@ -95,6 +95,9 @@ def load(required=False):
     L.sysml_tsmm_sparse.restype = ctypes.c_int
     L.sysml_tsmm_sparse.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    L.sysml_sddmm2.restype = ctypes.c_int
+    L.sysml_sddmm2.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     L.sysml_sddmm.restype = ctypes.c_int
     L.sysml_sddmm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
@@ -715,11 +718,12 @@ def sddmm(crow, col, U, V, dtype=None):
     U = U.to(dtype).contiguous()
     V = V.to(dtype).contiguous()
     crow = crow.to(torch.int64).contiguous()
-    col = col.to(torch.int64).contiguous()
+    idx32 = col.dtype == torch.int32
+    col = col.contiguous() if idx32 else col.to(torch.int64).contiguous()
     out = torch.empty(col.numel(), dtype=dtype, device=U.device)
     st = torch.cuda.current_stream(U.device).cuda_stream
-    rc = L.sysml_sddmm(0 if dtype == torch.float32 else 1, crow.data_ptr(), col.data_ptr(), U.data_ptr(),
-                       V.data_ptr(), m, r, out.data_ptr(), st)
+    rc = L.sysml_sddmm2(0 if dtype == torch.float32 else 1, int(idx32), crow.data_ptr(), col.data_ptr(), U.data_ptr(),
+                        V.data_ptr(), m, r, out.data_ptr(), st)
     if rc == -1:
         return None
     if rc != 0:
@@ -893,9 +897,18 @@ def csr_idx32(A):
         return None
     if col.dtype == torch.int32:
         return col.contiguous()
-    key = (col.data_ptr(), col.numel(), A.shape[1])
+    return idx32_of(col)
+
+
+def idx32_of(col):
+    """int32 copy of an int64 index tensor, cached by storage address, length and version.
+    The cache holds the original tensor, so its storage (the key's address) cannot be
+    recycled for another tensor while the entry lives."""
+    if col.dtype == torch.int32:
+        return col.contiguous()
+    key = (col.data_ptr(), col.numel(), col._version)
     e = _IDX32.get(key)
-    if e is None or e[0] is not col:
+    if e is None:
         if len(_IDX32) >= 8:
             _IDX32.pop(next(iter(_IDX32)))
         e = (col, col.to(torch.int32).contiguous())

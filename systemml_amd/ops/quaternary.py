@@ -47,13 +47,23 @@ def _csr(x):
     return x.to_sparse_csr()
 
 
+_ROWS = {}
+
+
 def _coo_idx(x):
-    """(row, col, values) of a CSR matrix."""
+    """(row, col, values) of a CSR matrix; the expanded row indices are cached per pattern
+    (the cache holds the row-pointer tensor, so its address -- the key -- stays unique)."""
     x = _csr(x)
     crow, col, val = x.crow_indices(), x.col_indices(), x.values()
-    counts = crow[1:] - crow[:-1]
-    row = torch.repeat_interleave(torch.arange(x.shape[0], device=x.device), counts)
-    return row, col, val
+    key = (crow.data_ptr(), crow.numel(), crow._version, col.numel())
+    e = _ROWS.get(key)
+    if e is None:
+        counts = crow[1:] - crow[:-1]
+        row = torch.repeat_interleave(torch.arange(x.shape[0], device=x.device), counts)
+        if len(_ROWS) >= 4:
+            _ROWS.pop(next(iter(_ROWS)))
+        e = _ROWS[key] = (crow, row)
+    return e[1], col, val
 
 
 def _cdt(*xs):
@@ -75,7 +85,7 @@ def sddmm(row, col, U, V, crow=None, dtype=None):
         from . import kernels
         if crow is None:
             crow = torch.searchsorted(row, torch.arange(U.shape[0] + 1, device=row.device))
-        out = kernels.sddmm(crow, col, U, V, dt)
+        out = kernels.sddmm(crow, kernels.idx32_of(col) if V.shape[0] < 2 ** 31 else col, U, V, dt)
         if out is not None:
             return out
     U = U.to(dt)

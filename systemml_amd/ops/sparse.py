@@ -215,10 +215,23 @@ def mm(a, b, transA=False):
     return (b.t() @ at.t().contiguous().to(b.dtype)).t().contiguous() if is_sparse(b) else None
 
 
+_TVALS = {}
+
+
 def _transposed(a):
-    """t(A) as CSR from the cached transpose plan of A's pattern (values gathered)."""
+    """t(A) as CSR from the cached transpose plan of A's pattern (values gathered); the
+    gathered values are cached too while A's value storage is unchanged (a fixed input such
+    as the ratings of ALS is transposed once, not once per product)."""
     crowT, colT, perm, _, _ = _transpose_plan(a)
-    return torch.sparse_csr_tensor(crowT, colT, a.values()[perm], (a.shape[1], a.shape[0]), device=a.device)
+    v = a.values()
+    key = (v.data_ptr(), v.numel(), v._version, perm.data_ptr())
+    e = _TVALS.get(key)
+    if e is None:
+        if len(_TVALS) >= 2:
+            _TVALS.pop(next(iter(_TVALS)))
+        e = _TVALS[key] = (v, torch.sparse_csr_tensor(crowT, colT, v[perm], (a.shape[1], a.shape[0]),
+                                                      device=a.device))
+    return e[1]
 
 
 def tsmm(x, left=True):
