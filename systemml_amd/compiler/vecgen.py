@@ -70,9 +70,9 @@ def _kind(h, smemo):
             return None
         return ("m" if h.dt == "M" else "s", o)
     if op == "agg" and len(h.inputs) == 1 and h.p.get("dir") == "all" and h.p.get("o") in _AGG \
-            and h.inputs[0].dt == "M":
+            and h.inputs[0].dt == "M" and not _big(h.inputs[0]):
         return ("r", h.p["o"])
-    if op == "tak" and len(h.inputs) in (2, 3) and all(c.dt == "M" for c in h.inputs):
+    if op == "tak" and len(h.inputs) in (2, 3) and all(c.dt == "M" and not _big(c) for c in h.inputs):
         return ("r", "dot" if len(h.inputs) == 2 else "dot3")
     if op == "bi" and h.p.get("name") in ("ifelse", "_sel") and len(h.inputs) == 3 and not h.named:
         if any(c.dt not in ("M", "S") for c in h.inputs):
