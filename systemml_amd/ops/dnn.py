@@ -47,7 +47,7 @@ def conv2d(x, w, input_shape=None, filter_shape=None, stride=None, padding=None,
         raise DMLRuntimeError("conv2d: channel mismatch between input and filter")
     if w.shape[0] != Fo or w.shape[1] != C * Hf * Wf:
         raise DMLRuntimeError(f"conv2d: filter is {tuple(w.shape)}, expected {Fo}x{C * Hf * Wf}")
-    if bias is not None and tuple(bias.shape) != (Fo, 1):
+    if bias is not None and tuple(bias.shape) not in ((Fo, 1), (Fo,)):
         # the fused conv2d + bias_add epilogue (compiler/rewrites.fuse_conv_bias) reads one bias
         # per filter; any other bias shape keeps the unfused bias_add semantics (and its checks)
         out = conv2d(x, w, input_shape, filter_shape, stride, padding)

@@ -448,6 +448,23 @@ def test_conv_bias_fusion_keeps_bias_add_semantics():
         R(src, outputs=["d"], args={"nb": 5})
 
 
+def test_fused_conv_bias_skips_the_bias_pass(monkeypatch):
+    """conv2d + bias_add fused by the rewrite reaches the convolution with its bias (the
+    builtin hands over a flat F-vector): no separate bias_add pass runs."""
+    from systemml_amd.ops import dnn
+    monkeypatch.setattr(dnn, "bias_op", lambda *a, **k: (_ for _ in ()).throw(AssertionError("bias pass")))
+    src = """
+      X = rand(rows=2, cols=3*4*4, seed=1)
+      W = rand(rows=4, cols=3*2*2, seed=2)
+      b = rand(rows=4, cols=1, seed=3)
+      out = conv2d(X, W, input_shape=[2,3,4,4], filter_shape=[4,3,2,2], stride=[1,1], padding=[0,0])
+      out = bias_add(out, b)
+      s = sum(out)
+    """
+    res, _ = R(src, outputs=["s"])
+    assert float(res["s"]) > 0
+
+
 def test_parfor_optimizer_rules():
     """Rule-based parfor optimizer (reference OptimizerRuleBased.java:197): exec type, k,
     task partitioner from the body's shape, row / column data-partitioning candidates."""
