@@ -5,8 +5,9 @@ The network is built as a Caffe2DML layer DAG (models/dl.py: Convolution + Batch
 ReLU bottlenecks with Eltwise residual sums, 3x3/2 max pool, 7x7 average pool, InnerProduct,
 SoftmaxWithLoss), the generated forward / backward / SGD-momentum DML runs on the MI355X
 backend: every conv2d / conv2d_backward_* / pooling / bias op is a hand-written kernel of
-ops/hip/dnn.hip; convolutions compute on bf16 MFMA with fp32 accumulation (activations and
-the other layers stay fp32).
+ops/hip/dnn.hip; convolutions compute on bf16 MFMA with fp32 accumulation, activations and
+their gradients are stored bf16 (fp32 arithmetic in every kernel), weights, weight gradients
+and the optimizer state stay fp32 (--fp32-activations: fp32 activations too).
 
     python bench_resnet50.py [--batch 32] [--steps 3] [--warmup 1] [--image 224]
 Prints one JSON line (images/s over the timed steps).
@@ -108,6 +109,8 @@ def main():
                     help="run under torchrun with one rank per GPU: data parallel, --batch images per rank")
     ap.add_argument("--exact-fp32", action="store_true", help="convolutions on exact fp32 MFMA instead of bf16")
     ap.add_argument("--no-fusion", action="store_true", help="disable operator fusion (codegen templates)")
+    ap.add_argument("--fp32-activations", action="store_true",
+                    help="keep activations / their gradients fp32 (default: stored bf16, fp32 math)")
     a = ap.parse_args()
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,7 +139,11 @@ def main():
     n = a.batch * min(total, 2)
     X = rng.standard_normal((n, 3 * a.image * a.image)).astype(np.float32)
     Y = np.eye(1000, dtype=np.float32)[rng.integers(0, 1000, n)]
-    cfg = DMLConfig(precision="single", gpu_min_cells=0, fusion=not a.no_fusion)
+    # bf16 activations: fused cellwise results, conv outputs and pooling results of >= 4M cells
+    # are stored bf16 (fp32 math); every weight / weight-gradient matrix of ResNet-50 is smaller
+    # (largest: 512 x 4608), so parameters and the optimizer state stay fp32
+    act = 0 if (a.fp32_activations or a.exact_fp32) else 1 << 22
+    cfg = DMLConfig(precision="single", gpu_min_cells=0, fusion=not a.no_fusion, act_bf16_min_cells=act)
     cs = compile_script(src, {"X": "X", "Y": "Y"}, inputs={"X": X, "Y": Y}, config=cfg,
                         filename=os.path.join(SCRIPTS_DIR, "resnet50_bench.dml"))
     out = []
@@ -170,13 +177,19 @@ def main():
                       "value": round(world * a.batch / (ms / 1e3), 2), "unit": "images/s", "n_gpus": n_phys,
                       "scaling": "weak", "parallelism": f"dp{world}",
                       "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2),
-                      "higher_is_better": True, "dtype": "fp32-exact" if a.exact_fp32 else "bf16 conv MFMA / fp32",
+                      "higher_is_better": True, "dtype": "fp32-exact" if a.exact_fp32 else ("bf16 conv MFMA / fp32" if not act
+                                                                       else "bf16 activations + MFMA / fp32 weights"),
                       "data": "synthetic N(0,1) images, random labels, random-init weights",
                       "losses": [round(l, 4) for _, l, _ in steps], "wall_s": round(wall, 1),
                       "step_ms": [round(ns / 1e6, 1) for _, _, ns in steps],
                       "kernel_counters": {k: v for k, v in K.counters.items() if k.startswith(("conv", "pool", "bias"))},
                       "config": {"model": "ResNet-50", "batch": a.batch, "global_batch": world * a.batch,
                                  "image": a.image, "classes": 1000}}))
+    from systemml_amd.ops import cell as CE
+    if CE.TRACE:
+        print("cell stats", CE.stats, file=sys.stderr)
+        for k, v in sorted(CE.fallbacks.items(), key=lambda kv: -kv[1])[:40]:
+            print(f"  fallback x{v}: {k}", file=sys.stderr)
     if ctx is not None:
         from systemml_amd.parallel import dist as D
         D.shutdown()

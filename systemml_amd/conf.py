@@ -20,6 +20,8 @@ class DMLConfig:
     force_cpu: bool = False
     precision: str = "double"           # 'double' | 'single' : compute dtype of matrices on GPU
     bf16_storage_min_cells: int = 0     # >0: large read-only inputs stored bf16 (fp32 accumulate)
+    act_bf16_min_cells: int = 0         # >0: fused cellwise results and convolution outputs with at least
+                                        # this many cells stored bf16 (DL activations / gradients; fp32 math)
     dist_min_rows: int = 100_000        # row-partition matrices with >= rows across ranks (SPMD)
     gpu_min_cells: int = 16384          # GPU backend: smaller matrices (and their operators) stay on host
     lazy_scalars: bool = False          # GPU backend: aggregates return HBM-resident scalars (runtime/scalars.DevScalar);
@@ -52,6 +54,7 @@ class DMLConfig:
     _XML_KEYS = {
         "sysml.floating.point.precision": ("precision", str),
         "sysml.gpu.storage.bf16.mincells": ("bf16_storage_min_cells", int),
+        "sysml.gpu.activation.bf16.mincells": ("act_bf16_min_cells", int),
         "sysml.dist.minrows": ("dist_min_rows", int),
         "sysml.gpu.mincells": ("gpu_min_cells", int),
         "sysml.gpu.lazy.scalars": ("lazy_scalars", lambda v: str(v).lower() == "true"),

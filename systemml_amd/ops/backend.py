@@ -22,6 +22,7 @@ class Backend:
         self.dtype = torch.float64
         self.use_kernels = False
         self.bf16_min_cells = 0
+        self.act_bf16_min_cells = 0  # >0: fused cellwise results / conv outputs this large stored bf16
         self.stream_sync = False
         self.small_cells = 0        # GPU backend: matrices below this many cells live on the host
         self.lazy = False           # GPU backend: HBM-resident scalars (runtime/scalars.DevScalar)
@@ -54,6 +55,7 @@ class Backend:
             prec = "double" if config is None else config.precision
             self.dtype = torch.float32 if prec in ("single", "float", "fp32", "bf16") else torch.float64
             self.bf16_min_cells = 0 if config is None else config.bf16_storage_min_cells
+            self.act_bf16_min_cells = 0 if config is None else int(getattr(config, "act_bf16_min_cells", 0))
             self.small_cells = 16384 if config is None else int(config.gpu_min_cells)
             self.lazy = bool(config is not None and getattr(config, "lazy_scalars", False))
             if self.lazy:
@@ -70,6 +72,7 @@ class Backend:
             self.dtype = torch.float64
             self.use_kernels = False
             self.bf16_min_cells = 0
+            self.act_bf16_min_cells = 0
             self.small_cells = 0
             self.lazy = False
         return self

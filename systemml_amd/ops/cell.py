@@ -48,6 +48,8 @@ BIAS_OPS = {"bias+": "+", "bias*": "*"}
 stats = {"kernel": 0, "sequential": 0, "rtc_compiled": 0, "rtc_cache_hits": 0, "rtc_launches": 0,
          "interpreter_launches": 0}
 RTC = os.environ.get("SYSML_CELL_RTC", "1") != "0"
+TRACE = os.environ.get("SYSML_CELL_TRACE", "0") == "1"
+fallbacks = {}
 RTC_DIR = os.environ.get("SYSML_RTC_CACHE", os.path.join(tempfile.gettempdir(), "systemml_amd_rtc"))
 
 # C expressions of the operators ({a}, {b}: operand expressions of type T)
@@ -120,6 +122,11 @@ def evaluate(prog: CellProgram, args):
         stats["kernel"] += 1
         return r
     stats["sequential"] += 1
+    if TRACE and backend.use_kernels:
+        # SYSML_CELL_TRACE=1: which programs miss the generated kernels, on which operands
+        k = (prog.describe(), tuple((tuple(x.shape), str(x.dtype), x.device.type) if type(x) is _Tensor
+                                    else type(x).__name__ for x in args))
+        fallbacks[k] = fallbacks.get(k, 0) + 1
     return sequential(prog, args)
 
 
@@ -205,6 +212,34 @@ def out_shape(prog: CellProgram, shapes):
     return regs[prog.out]
 
 
+def chan_inputs(prog: CellProgram):
+    """Input registers read as per-channel operands of bias+ / bias*, or None when the program
+    is outside the generated kernels' scope: a channel operand that is an intermediate, or an
+    input read both per channel and cellwise.  Registers are reused once their value is dead,
+    so a register number names an input only until the first instruction writing it."""
+    f = prog._code.get("chan", False)
+    if f is not False:
+        return f
+    inputs = set(range(prog.n_in))            # registers still holding their input
+    chan, cellwise = set(), set()
+    ok = True
+    for kind, o, d, a, b in prog.ops:
+        if o in BIAS_OPS:
+            if b not in inputs:
+                ok = False
+            chan.add(b)
+            reads = (a,)
+        else:
+            reads = (a, b) if kind == "b" else (a,)
+        cellwise.update(r for r in reads if r in inputs)
+        inputs.discard(d)
+    if chan & cellwise:
+        ok = False
+    f = frozenset(chan) if ok else None
+    prog._code["chan"] = f
+    return f
+
+
 class _In(ctypes.Structure):
     _fields_ = [("p", ctypes.c_void_p), ("s", ctypes.c_double), ("mode", ctypes.c_int), ("dtype", ctypes.c_int),
                 ("vec", ctypes.c_int), ("pad", ctypes.c_int)]
@@ -245,10 +280,11 @@ def _cases(vals):
     return expr
 
 
-def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant, idx32=False):
+def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant, idx32=False, outbf=False):
     """HIP source of the fused kernel: the program as straight-line code over the cell values
     of its inputs, instantiated into the flat / row / column kernel template.  idx32: the
-    operand has < 2^31 cells (32-bit row / column arithmetic)."""
+    operand has < 2^31 cells (32-bit row / column arithmetic); outbf: the (unaggregated)
+    result is stored as bf16."""
     ct = "float" if T == torch.float32 else "double"
     var = [f"x[{k}]" for k in range(prog.n_in)] + [None] * (NR - prog.n_in)
     body = []
@@ -274,6 +310,7 @@ struct Spec {{
   static constexpr int AGGOP = {aggop};
   static constexpr int NEED_IJ = {need_ij};
   static constexpr int IDX32 = {int(bool(idx32))};
+  static constexpr int OUTBF = {int(bool(outbf))};
   static constexpr int mode(int k) {{ return {_cases(modes)}; }}
   static constexpr int dt(int k) {{ return {_cases(dts)}; }}
   static constexpr int vec(int k) {{ return {_cases(vecs)}; }}
@@ -377,13 +414,13 @@ def compile_source(src, arch):
     return code
 
 
-def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, idx32=False):
-    key = (prog.key(), T, modes, dts, vecs, mode, variant, str(dev), idx32)
+def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, idx32=False, outbf=False):
+    key = (prog.key(), T, modes, dts, vecs, mode, variant, str(dev), idx32, outbf)
     f = _rtc_funcs.get(key, False)
     if f is not False:
         return f
     try:
-        code = compile_source(generate(prog, T, modes, dts, vecs, mode, variant, idx32), gpu_arch(dev))
+        code = compile_source(generate(prog, T, modes, dts, vecs, mode, variant, idx32, outbf), gpu_arch(dev))
         L = _rtc_lib()
         fn = ctypes.c_void_p()
         cbuf = ctypes.create_string_buffer(code, len(code))
@@ -430,8 +467,8 @@ def _signature(args):
 
 class _Plan:
     """Everything a launch of one program on one operand signature needs but the pointers."""
-    __slots__ = ("prog", "fn", "interp", "mode", "nblk", "gx", "gy", "R", "Cc", "T", "out_shape", "part_shape",
-                 "kinds", "P", "dev", "dev_index", "launch", "count", "hws")
+    __slots__ = ("prog", "fn", "interp", "mode", "nblk", "gx", "gy", "R", "Cc", "T", "odt", "out_shape",
+                 "part_shape", "kinds", "P", "dev", "dev_index", "launch", "count", "hws")
 
 
 def _make_plan(prog, args):
@@ -468,14 +505,9 @@ def _make_plan(prog, args):
     if R <= 0 or Cc <= 0:
         return None
     T = torch.float64 if (f64 or (bf16 and backend.dtype == torch.float64)) else torch.float32
-    chan = {b for kind, o, d, a, b in prog.ops if o in BIAS_OPS}
-    if chan and (not RTC or any(k >= prog.n_in for k in chan)):
+    chan = chan_inputs(prog)
+    if chan is None or (chan and not RTC):
         return None                   # per-channel operands: generated kernels only, inputs only
-    if chan:
-        other = {a for kind, o, d, a, b in prog.ops} | {b for kind, o, d, a, b in prog.ops
-                                                         if kind == "b" and o not in BIAS_OPS}
-        if chan & other or prog.out in chan:
-            return None               # also read as an ordinary operand
     P = _Prog()
     kinds = []
     need_ij = 0
@@ -532,6 +564,7 @@ def _make_plan(prog, args):
     pl.out_shape = (R, Cc) if mode == 0 else ((R, 1) if mode == 2 else None)
     pl.part_shape = (nblk,) if mode == 1 else ((nblk, Cc) if mode == 3 else None)
     pl.fn = None
+    pl.odt = T
     pl.gx, pl.gy = nblk, 1
     if RTC:
         modes = tuple(P.inp[k].mode for k in range(prog.n_in))
@@ -543,9 +576,12 @@ def _make_plan(prog, args):
             variant = 8 if Cc <= 8 else 64
         else:
             variant = 0
-        f = _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, R * Cc < 2 ** 31)
+        outbf = mode == 0 and T == torch.float32 and 0 < backend.act_bf16_min_cells <= R * Cc
+        f = _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, R * Cc < 2 ** 31, outbf)
         if f is not None:
             pl.fn = f[0]
+            if outbf:
+                pl.odt = torch.bfloat16
             if mode == 3:
                 pl.gx, pl.gy = (Cc + variant - 1) // variant, nblk
     pl.interp = pl.fn is None
@@ -568,7 +604,7 @@ def _kernel(prog: CellProgram, args):
     sig = _signature(args)
     if sig is None:
         return None
-    key = (id(prog), sig, RTC)
+    key = (id(prog), sig, RTC, backend.act_bf16_min_cells)
     pl = _plans.get(key, False)
     if pl is False or (pl is not None and pl.prog is not prog):
         pl = _make_plan(prog, args)
@@ -576,7 +612,7 @@ def _kernel(prog: CellProgram, args):
     if pl is None:
         return None
     dev, T, mode = pl.dev, pl.T, pl.mode
-    out = torch.empty(pl.out_shape, dtype=T, device=dev) if pl.out_shape is not None else None
+    out = torch.empty(pl.out_shape, dtype=pl.odt, device=dev) if pl.out_shape is not None else None
     part = torch.empty(pl.part_shape, dtype=torch.float64, device=dev) if pl.part_shape is not None else None
     st = _raw_stream(pl.dev_index) if _raw_stream is not None else torch.cuda.current_stream(dev).cuda_stream
     keep = []

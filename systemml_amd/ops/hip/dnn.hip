@@ -335,10 +335,13 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
   }
   // epilogue.  C/D maps: f32 16x16: row = (lane >> 4) * 4 + reg;  f64 16x16: row = (lane >> 4) + 4 * reg
   // split-K: partial sums are added atomically into the zero-initialised output (vector
-  // global atomics, fp32 / fp64); bias / relu then run as a separate pass (host)
+  // global atomics, fp32 / fp64); bias / relu then run as a separate pass (host).  A bf16
+  // output (activations of a bf16 network) is rounded once, after bias and relu in fp32.
+  constexpr bool OBF = std::is_same<TO, __bf16>::value;
+  typedef typename std::conditional<OBF, float, TO>::type CT;
   const bool atomic = c.ksplit > 1;
   TO* out = (TO*)c.out;
-  const TO* bias = (const TO*)c.bias;
+  const CT* bias = (const CT*)c.bias;
 #pragma unroll
   for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -348,14 +351,16 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
         const int mo = m0 + wr * (TM_ / 2) + i * 16 + (PATH == 2 ? (lane >> 4) + 4 * r : (lane >> 4) * 4 + r);
         const int no = n0 + wc * (TN_ / 2) + j * 16 + (lane & 15);
         if (mo < c.M && no < c.Ncol) {
-          TO v = (TO)acc[i][j][r];
-          if (atomic) {
-            atomicAdd(out + out_index<MODE>(c, mo, no), v);
-            continue;
+          CT v = (CT)acc[i][j][r];
+          if constexpr (!OBF) {
+            if (atomic) {
+              atomicAdd(out + out_index<MODE>(c, mo, no), v);
+              continue;
+            }
           }
           if (MODE == FWD && bias) v += bias[mo];
-          if (MODE == FWD && c.relu) v = v > TO(0) ? v : TO(0);
-          out[out_index<MODE>(c, mo, no)] = v;
+          if (MODE == FWD && c.relu) v = v > CT(0) ? v : CT(0);
+          out[out_index<MODE>(c, mo, no)] = (TO)v;
         }
       }
 }
@@ -424,8 +429,13 @@ struct Pool {
 
 // I: index type of the flat cell loops (int below 2^31 cells: 32-bit divisions instead of the
 // emulated 64-bit ones)
+// storage type T, arithmetic type Acc<T>::type (bf16 activations: fp32 math, one rounding)
+template <typename T> struct Acc { typedef T type; };
+template <> struct Acc<__bf16> { typedef float type; };
+
 template <typename T, typename I>
 __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
+  typedef typename Acc<T>::type A;
   const T* __restrict__ X = (const T*)p.X;
   T* __restrict__ O = (T*)p.out;
   const I total = (I)p.N * p.C * p.Ho * p.Wo;
@@ -436,19 +446,19 @@ __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
     const int oh = (int)(q - nc * p.Ho);
     const T* x = X + (int64_t)nc * p.H * p.W;
     const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
-    T m = p.avg ? T(0) : -INFINITY;
+    A m = p.avg ? A(0) : A(-INFINITY);
     for (int a = 0; a < p.KH; ++a) {
       const int h = h0 + a;
       if (h < 0 || h >= p.H) continue;
       for (int b = 0; b < p.KW; ++b) {
         const int w = w0 + b;
         if (w < 0 || w >= p.W) continue;
-        const T v = x[h * p.W + w];
+        const A v = (A)x[h * p.W + w];
         if (p.avg) m += v;
         else m = v > m ? v : m;
       }
     }
-    O[i] = p.avg ? m / T(p.KH * p.KW) : m;
+    O[i] = (T)(p.avg ? m / A(p.KH * p.KW) : m);
   }
 }
 
@@ -456,6 +466,7 @@ __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
 // scan, as the forward pass), 255 for a window without a cell above -inf
 template <typename T, typename I>
 __global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__ idx) {
+  typedef typename Acc<T>::type A;
   const T* __restrict__ X = (const T*)p.X;
   const I total = (I)p.N * p.C * p.Ho * p.Wo;
   for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
@@ -465,7 +476,7 @@ __global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__
     const int oh = (int)(q - nc * p.Ho);
     const T* x = X + (int64_t)nc * p.H * p.W;
     const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
-    T m = -INFINITY;
+    A m = A(-INFINITY);
     int am = 255;
     for (int a = 0; a < p.KH; ++a) {
       const int h = h0 + a;
@@ -473,7 +484,7 @@ __global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__
       for (int b = 0; b < p.KW; ++b) {
         const int w = w0 + b;
         if (w < 0 || w >= p.W) continue;
-        const T v = x[h * p.W + w];
+        const A v = (A)x[h * p.W + w];
         if (v > m) {
           m = v;
           am = a * p.KW + b;
@@ -490,6 +501,7 @@ __global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__
 // band instead of once per cell; each cell sums the dout of the windows whose argmax it is
 template <typename T, typename I>
 __global__ void __launch_bounds__(256) pool_bwd_band(Pool p, const uint8_t* __restrict__ idx) {
+  typedef typename Acc<T>::type A;
   const T* __restrict__ D = (const T*)p.D;
   T* __restrict__ O = (T*)p.out;
   const int Bh = (p.H + p.ph + p.sh - 1) / p.sh, Bw = (p.W + p.pw + p.sw - 1) / p.sw;
@@ -512,13 +524,13 @@ __global__ void __launch_bounds__(256) pool_bwd_band(Pool p, const uint8_t* __re
         if (w < 0 || w >= p.W) continue;
         const int owl = dw <= p.KW - 1 ? max(0, bw - (p.KW - 1 - dw) / p.sw) : bw + 1;
         const int owh = min(bw, p.Wo - 1);
-        T g = 0;
+        A g = 0;
         for (int oh = ohl; oh <= ohh; ++oh) {
           const int rh = (bh - oh) * p.sh + dh;           // row of (h, w) inside window (oh, ow)
           for (int ow = owl; ow <= owh; ++ow)
-            if (ix[oh * p.Wo + ow] == rh * p.KW + (bw - ow) * p.sw + dw) g += d[oh * p.Wo + ow];
+            if (ix[oh * p.Wo + ow] == rh * p.KW + (bw - ow) * p.sw + dw) g += (A)d[oh * p.Wo + ow];
         }
-        o[h * p.W + w] = g;
+        o[h * p.W + w] = (T)g;
       }
     }
   }
@@ -529,6 +541,7 @@ __global__ void __launch_bounds__(256) pool_bwd_band(Pool p, const uint8_t* __re
 // when no position buffer is given) -- a gather, no atomics
 template <typename T, typename I>
 __global__ void __launch_bounds__(256) pool_bwd(Pool p, const uint8_t* __restrict__ idx) {
+  typedef typename Acc<T>::type A;
   const T* __restrict__ X = (const T*)p.X;
   const T* __restrict__ D = (const T*)p.D;
   T* __restrict__ O = (T*)p.out;
@@ -544,20 +557,20 @@ __global__ void __launch_bounds__(256) pool_bwd(Pool p, const uint8_t* __restric
     // output windows covering (h, w): oh*sh - ph <= h <= oh*sh - ph + KH - 1
     const int ohl = max(0, (h + p.ph - p.KH + p.sh) / p.sh), ohh = min(p.Ho - 1, (h + p.ph) / p.sh);
     const int owl = max(0, (w + p.pw - p.KW + p.sw) / p.sw), owh = min(p.Wo - 1, (w + p.pw) / p.sw);
-    T g = 0;
+    A g = 0;
     for (int oh = ohl; oh <= ohh; ++oh) {
       const int h0 = oh * p.sh - p.ph;
       if (h < h0 || h >= h0 + p.KH) continue;
       for (int ow = owl; ow <= owh; ++ow) {
         const int w0 = ow * p.sw - p.pw;
         if (w < w0 || w >= w0 + p.KW) continue;
-        const T dv = d[oh * p.Wo + ow];
-        if (p.avg) { g += dv / T(p.KH * p.KW); continue; }
+        const A dv = (A)d[oh * p.Wo + ow];
+        if (p.avg) { g += dv / A(p.KH * p.KW); continue; }
         if (ix) {
           if (ix[oh * p.Wo + ow] == (h - h0) * p.KW + (w - w0)) g += dv;
           continue;
         }
-        T m = -INFINITY;
+        A m = A(-INFINITY);
         int ah = -1, aw = -1;
         for (int a = 0; a < p.KH; ++a) {
           const int hh = h0 + a;
@@ -565,14 +578,14 @@ __global__ void __launch_bounds__(256) pool_bwd(Pool p, const uint8_t* __restric
           for (int b = 0; b < p.KW; ++b) {
             const int ww = w0 + b;
             if (ww < 0 || ww >= p.W) continue;
-            const T v = x[hh * p.W + ww];
+            const A v = (A)x[hh * p.W + ww];
             if (v > m) { m = v; ah = hh; aw = ww; }
           }
         }
         if (ah == h && aw == w) g += dv;
       }
     }
-    O[i] = g;
+    O[i] = (T)g;
   }
 }
 
@@ -646,7 +659,7 @@ namespace sysml_dnn {
 // 128 x 128 tiles only when they still give >= 2 workgroups per CU (256 CUs): a 256-filter
 // 14 x 14 layer at batch 64 has 196 such tiles and runs 1.5x faster on 64 x 64 ones
 inline int conv_tile(int dtype, int64_t M, int64_t Nc) {
-  if (!(dtype == 0 || dtype == 3) || M < 128 || Nc < 128) return 64;
+  if (!(dtype == 0 || dtype == 3 || dtype == 4) || M < 128 || Nc < 128) return 64;
   return ((M + 127) / 128) * ((Nc + 127) / 128) >= 512 ? 128 : 64;
 }
 }  // namespace sysml_dnn
@@ -676,7 +689,8 @@ extern "C" {
 // Output tile edge the launcher uses for a GEMM view (the host sizes split-K from it).
 int sysml_conv2d_tile(int dtype, int64_t M, int64_t Nc) { return sysml_dnn::conv_tile(dtype, M, Nc); }
 
-// dtype: 0 bf16 in (fp32 out), 1 fp32 exact, 2 fp64 exact, 3 fp32 in / bf16 MFMA / fp32 out.
+// dtype: 0 bf16 in (fp32 out), 1 fp32 exact, 2 fp64 exact, 3 fp32 in / bf16 MFMA / fp32 out,
+// 4 bf16 in / bf16 out (forward and backward data, no split-K; fp32 bias).
 // mode: 0 forward, 1 backward data, 2 backward filter.  ksplit > 1 splits the GEMM depth over
 // blocks that accumulate atomically (ws unused).
 // Returns 0, -1 (unsupported) or a hipError_t.
@@ -691,7 +705,7 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   c.Wo = (Wd + 2 * pw - KW) / sw + 1;
   c.relu = relu;
   {
-    const int es = dtype == 2 ? 8 : (dtype == 0 ? 2 : 4);
+    const int es = dtype == 2 ? 8 : ((dtype == 0 || dtype == 4) ? 2 : 4);
     const int64_t rowb = (int64_t)C * KH * KW * es;
     c.avec = (rowb % 16 == 0) && (reinterpret_cast<uintptr_t>(W) % 16 == 0);
   }
@@ -706,7 +720,8 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   if ((int64_t)N * C * H * Wd >= (1LL << 31) || (int64_t)N * F * P >= (1LL << 31) || (int64_t)F * C * KK >= (1LL << 31))
     return -1;
   c.M = (int)M; c.Ncol = (int)Nc; c.K = (int)K;
-  const bool bfmma = dtype == 0 || dtype == 3;
+  const bool bfmma = dtype == 0 || dtype == 3 || dtype == 4;
+  if (dtype == 4 && (mode == BWD_FILTER || (mode == BWD_DATA && C <= 8) || ksplit > 1)) return -1;
   const int tile = conv_tile(dtype, M, Nc);          // 128 x 128 (bf16, both dims >= 128) or 64 x 64
   c.tm = (int)((M + tile - 1) / tile);
   c.tn = (int)((Nc + tile - 1) / tile);
@@ -746,6 +761,14 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   if (dtype == 0) {
     if (tile == 128) LAUNCH(conv_kernel, __bf16, 0, float, 128, 128);
     else LAUNCH(conv_kernel, __bf16, 0, float, 64, 64);
+  } else if (dtype == 4) {
+    if (mode == FWD) {
+      if (tile == 128) hipLaunchKernelGGL((conv_kernel<FWD, __bf16, 0, __bf16, 128, 128>), g, t, 0, s, c);
+      else hipLaunchKernelGGL((conv_kernel<FWD, __bf16, 0, __bf16, 64, 64>), g, t, 0, s, c);
+    } else {
+      if (tile == 128) hipLaunchKernelGGL((conv_kernel<BWD_DATA, __bf16, 0, __bf16, 128, 128>), g, t, 0, s, c);
+      else hipLaunchKernelGGL((conv_kernel<BWD_DATA, __bf16, 0, __bf16, 64, 64>), g, t, 0, s, c);
+    }
   } else if (dtype == 3) {
     if (tile == 128) LAUNCH(conv_kernel, float, 0, float, 128, 128);
     else LAUNCH(conv_kernel, float, 0, float, 64, 64);
@@ -770,7 +793,7 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   return (int)hipGetLastError();
 }
 
-// dtype 1 fp32, 2 fp64; backward: D = dout, out = dX; ws: N*C*Ho*Wo bytes for the window argmax
+// dtype 1 fp32, 2 fp64, 3 bf16 (fp32 math); backward: D = dout, out = dX; ws: N*C*Ho*Wo bytes for the window argmax
 // positions of max-pooling backward (nullptr: recomputed per covered window)
 int sysml_pool2d_ws(int dtype, int backward, int avg, const void* X, const void* D, void* out, void* ws, int N, int C,
                     int H, int W, int KH, int KW, int sh, int sw, int ph, int pw, void* stream) {
@@ -791,6 +814,9 @@ int sysml_pool2d_ws(int dtype, int backward, int avg, const void* X, const void*
   } else if (dtype == 2) {
     if (small) pool_launch<double, int>(p, backward, w8, s);
     else pool_launch<double, int64_t>(p, backward, w8, s);
+  } else if (dtype == 3) {
+    if (small) pool_launch<__bf16, int>(p, backward, w8, s);
+    else pool_launch<__bf16, int64_t>(p, backward, w8, s);
   } else {
     return -1;
   }

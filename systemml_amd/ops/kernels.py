@@ -772,7 +772,6 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
         shape = (N, C * H * Wd)
     else:
         shape = (F, C * KH * KW)
-    out = torch.empty(shape, dtype=odt, device=dev)
     # GEMM view (M x Ncol, depth K); split K when the output tiles alone cannot fill the chip:
     # ~2k blocks in flight, each reducing >= 512 products per output (slab traffic stays small)
     M, Nc, K = {0: (F, N * Ho * Wo, C * KH * KW), 1: (C, N * H * Wd, F * KH * KW),
@@ -784,8 +783,13 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
     ksplit = 1
     if tiles < 2048:
         ksplit = max(1, min(256, 2048 // max(tiles, 1), K // 512))
+    bdt = odt
+    if code == 0 and mode != 2 and ksplit == 1 and not (mode == 1 and C <= 8) and \
+            0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+        code, odt = 4, torch.bfloat16              # bf16 activations: the output is stored bf16
+    out = torch.empty(shape, dtype=odt, device=dev)
     ws = None
-    b = None if bias is None else bias.to(device=dev, dtype=odt).contiguous().reshape(-1)
+    b = None if bias is None else bias.to(device=dev, dtype=bdt).contiguous().reshape(-1)
     rc = L.sysml_conv2d(code, mode, _ptr(X), _ptr(W), _ptr(D), _ptr(b), out.data_ptr(), _ptr(ws), ksplit,
                         N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, int(bool(relu)), _stream())
     if rc == -1:
@@ -803,7 +807,9 @@ def _ptr(t):
 def pool2d(backward, avg, X, D, N, C, H, W, KH, KW, sh, sw, ph, pw):
     L = load(required=True)
     dt = X.dtype if X.dtype in (torch.float32, torch.float64) else torch.float32
-    code = 1 if dt == torch.float32 else 2
+    if X.dtype == torch.bfloat16 and backend.act_bf16_min_cells > 0:
+        dt = torch.bfloat16                        # bf16 activations stay bf16 (fp32 math)
+    code = {torch.float32: 1, torch.float64: 2, torch.bfloat16: 3}[dt]
     X = X.to(dt).contiguous()
     D = None if D is None else D.to(device=X.device, dtype=dt).contiguous()
     Ho = (H + 2 * ph - KH) // sh + 1

@@ -87,6 +87,8 @@ def _merge(base, results):
                 raise DMLRuntimeError("parfor result merge: dimension change of a result variable")
             if out is None:
                 out = base.clone()
+            if r.device != base.device:            # a worker's result placed on the host (or another GPU)
+                r = r.to(base.device)
             same = (r == base) | (torch.isnan(r) & torch.isnan(base))
             changed = ~same
             out[changed] = r[changed].to(out.dtype)
@@ -293,7 +295,7 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
         dev = (main_dev + w) % torch.cuda.device_count() if pl.devices > 1 and w < pl.devices else main_dev
         from ..ops.backend import backend
         with torch.cuda.device(dev):
-            s = torch.cuda.Stream(device=dev)
+            s = _worker_stream(dev, w)
             s.wait_stream(main)              # inputs produced on the main stream
             backend.set_thread_device(torch.device("cuda", dev))
             try:
@@ -324,6 +326,19 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
         rs = [r[v] for r in results]
         ctx.vars[v] = _accumulate(base[v], rs) if v in acc else _merge(base[v], rs)
     ctx.vars[b.var] = iters[-1]
+
+
+_STREAMS = {}
+
+
+def _worker_stream(dev, w):
+    """Worker w's stream on device dev, kept for the process: the caching allocator serves a
+    stream from the blocks freed on it, so a fresh stream per parfor execution would pay a
+    device allocation for every temporary of its first iterations."""
+    s = _STREAMS.get((dev, w))
+    if s is None:
+        s = _STREAMS[(dev, w)] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def _to_device(vars_, dev, partitions):
