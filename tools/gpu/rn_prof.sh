@@ -7,9 +7,9 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $R
 for mode in act fp32; do
   extra=""; [ $mode = fp32 ] && extra="--fp32-activations"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rnp_${mode}_a -o run -- \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rnp_${mode}_a -o run --output-format csv -- \
       python3 bench_resnet50.py --batch 256 --steps 1 --warmup 1 $extra > gpurun_out/rnp_${mode}_a.log 2>&1 || exit $?
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rnp_${mode}_b -o run -- \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rnp_${mode}_b -o run --output-format csv -- \
       python3 bench_resnet50.py --batch 256 --steps 4 --warmup 1 $extra > gpurun_out/rnp_${mode}_b.log 2>&1 || exit $?
   python3 tools/prof_diff.py gpurun_out/rnp_${mode}_a gpurun_out/rnp_${mode}_b 3 > gpurun_out/rnp_${mode}_step.txt || exit $?
   rm -rf gpurun_out/rnp_${mode}_a gpurun_out/rnp_${mode}_b
