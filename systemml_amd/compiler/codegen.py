@@ -5,9 +5,12 @@ cplan/CNodeCell for the generated operator).
 
 Candidates are the cellwise binary / unary operators over matrices (the operator set of
 ops/cell.py).  Fusion plans follow the reference's materialisation rules:
-  * an operator is fused into its consumer only if that consumer is its ONLY consumer in the
-    basic block and the value is not a block output (variable written or statement root) --
-    a shared intermediate is materialised once instead of being recomputed per consumer;
+  * an operator is fused into its consumer if that consumer is its ONLY consumer in the basic
+    block and the value is not a block output (variable written or statement root);
+  * a shared intermediate (several consumers, not a block output) is a materialisation point:
+    the cost-based plan selection (`_select_plan`, the reference's PlanSelectionFuseCostBasedV2)
+    prices every combination of "materialise once" / "recompute inside each consumer" by HBM
+    reads + writes and operator cost and takes the cheapest;
   * a fused DAG may end in a full / row / column aggregate (sum, sumsq, mean, min, max) whose
     input it is the only consumer of (the reference's Cell template with
     CellType.FULL_AGG / ROW_AGG / COL_AGG);
@@ -106,11 +109,127 @@ def _regalloc(ops, leaves):
     return code, reg[("op", ops[-1].id)]
 
 
-def fuse_cells(bb, single=False):
+def _group(order, ncons, inline):
+    """Cell-template grouping for one materialisation plan: every cellwise hop gets the fused
+    DAG (ops in topological order, leaves) ending in it.  An operand's DAG is absorbed when the
+    hop is its only consumer, or when the plan recomputes that shared intermediate inside
+    each consumer (`inline`).  Returns (groups, times each hop was absorbed)."""
+    groups = {}                                       # hop id -> (ops in topological order, leaves)
+    absorbed = {}
+    for h in order:
+        if not _cellwise(h):
+            continue
+        ops, leaves = [], []
+        for ci, c in enumerate(_operands(h)):
+            g = groups.get(c.id)
+            if _is_bias(h) and ci == 1:
+                g = None                      # the per-channel operand is read by the kernel as is
+            if g is not None and ((ncons.get(c.id, 0) == 1 and c.id not in absorbed) or c.id in inline):
+                extra = [o for o in g[0] if all(o is not x for x in ops)]
+                nl = _merge_leaves(leaves, g[1])
+                if len(ops) + len(extra) + 1 <= MAXOPS and len(nl) <= MAXIN:
+                    ops += extra
+                    leaves = nl
+                    absorbed[c.id] = absorbed.get(c.id, 0) + 1
+                    continue
+            leaves = _merge_leaves(leaves, [c])
+        if len(leaves) > MAXIN:
+            continue
+        ops.append(h)
+        groups[h.id] = (ops, leaves)
+    return groups, absorbed
+
+
+_HEAVY_OPS = {"exp", "log", "sqrt", "^", "sigmoid", "tanh", "sin", "cos", "tan", "asin", "acos", "atan",
+              "sinh", "cosh", "%%", "%/%", "/"}
+
+
+def _cells(h, memo):
+    """Estimated cell count of a hop's value (0 for scalars; unknown matrices 1e6, cellwise
+    hops the largest of their operands)."""
+    r = memo.get(h.id)
+    if r is None:
+        if h.dt != "M":
+            r = 0.0
+        elif h.dim1 >= 0 and h.dim2 >= 0:
+            r = float(h.dim1 * h.dim2)
+        elif _cellwise(h):
+            r = max((_cells(c, memo) for c in _operands(h)), default=0.0) or 1e6
+        else:
+            r = 1e6
+        memo[h.id] = r
+    return r
+
+
+def _plan_cost(order, groups, absorbed, ncons, memo):
+    """HBM + compute cost of a Cell-template plan, in cell-reads: every materialised fused DAG
+    reads its leaves and writes its root once; its operators cost a fraction of a read per
+    cell (transcendentals more).  The reference's PlanSelectionFuseCostBasedV2 prices plans
+    the same way (memory traffic + compute of each fused operator)."""
+    cost = 0.0
+    for h in order:
+        g = groups.get(h.id)
+        if g is None or absorbed.get(h.id, 0) >= ncons.get(h.id, 0):
+            continue
+        ops, leaves = g
+        n = _cells(h, memo)
+        cost += n + sum(_cells(c, memo) for c in leaves)
+        cost += sum((0.25 if o.p.get("o") in _HEAVY_OPS else 0.05) * n for o in ops)
+    return cost
+
+
+ENUM_MAX = 8          # exhaustive plan enumeration up to this many materialisation points
+
+
+def _select_plan(order, ncons, outs):
+    """Materialisation-point selection (reference: opt/PlanSelectionFuseCostBasedV2): the
+    shared cellwise intermediates that are no block output are the interesting points; each is
+    either materialised once or recomputed inside every consumer.  Up to ENUM_MAX points every
+    combination is costed, beyond that a greedy pass flips one point at a time; a plan must be
+    >= 5 % cheaper than materialising everything to be taken.  Returns (inline set, stats)."""
+    out_ids = {h.id for h in outs}
+    cons = {}
+    for h in order:
+        for c in h.inputs:
+            cons.setdefault(c.id, []).append(h)
+    base_groups, _ = _group(order, ncons, frozenset())
+    points = [h.id for h in order if h.id in base_groups and ncons.get(h.id, 0) > 1 and h.id not in out_ids
+              and any(_cellwise(u) for u in cons.get(h.id, ()))]
+    if not points:
+        return frozenset(), None
+    memo = {}
+
+    def cost(inl):
+        g, a = _group(order, ncons, inl)
+        return _plan_cost(order, g, a, ncons, memo)
+    base = best_cost = cost(frozenset())
+    best = frozenset()
+    evaluated = 1
+    if len(points) <= ENUM_MAX:
+        for mask in range(1, 1 << len(points)):
+            inl = frozenset(p for i, p in enumerate(points) if mask >> i & 1)
+            c = cost(inl)
+            evaluated += 1
+            if c < best_cost:
+                best, best_cost = inl, c
+    else:
+        for p in points:
+            inl = best | {p}
+            c = cost(inl)
+            evaluated += 1
+            if c < best_cost:
+                best, best_cost = frozenset(inl), c
+    if best_cost > 0.95 * base:
+        best = frozenset()
+    return best, {"points": len(points), "plans": evaluated, "inlined": len(best)}
+
+
+def fuse_cells(bb, single=False, stats=None):
     """Fuse the cellwise sub-DAGs of a basic block; returns the number of fused operators.
     single: also single operators and aggregates of a plain input become generated kernels
     (GPU plans: the reference's SystemML.cu matrix_matrix_cellwise_op / reduce_* kernels, here
-    generated per operator and operand signature instead of ATen's)."""
+    generated per operator and operand signature instead of ATen's).  Shared intermediates are
+    materialised or recomputed per consumer as the cost-based plan selection decides."""
     live = getattr(bb, "live_out", None)
     order = walk(list(bb.roots) + list(bb.env_out.values()))
     # block outputs are materialised: statement roots and the variables read after the block
@@ -121,41 +240,24 @@ def fuse_cells(bb, single=False):
             ncons[c.id] = ncons.get(c.id, 0) + 1
     for h in outs:
         ncons[h.id] = ncons.get(h.id, 0) + 1
-    groups = {}                                       # hop id -> (ops in topological order, leaves)
-    absorbed = set()
-    for h in order:
-        if not _cellwise(h):
-            continue
-        ops, leaves = [], []
-        for ci, c in enumerate(_operands(h)):
-            g = groups.get(c.id)
-            if _is_bias(h) and ci == 1:
-                g = None                      # the per-channel operand is read by the kernel as is
-            if g is not None and ncons.get(c.id, 0) == 1 and c.id not in absorbed:
-                nl = _merge_leaves(leaves, g[1])
-                if len(ops) + len(g[0]) + 1 <= MAXOPS and len(nl) <= MAXIN:
-                    ops += g[0]
-                    leaves = nl
-                    absorbed.add(c.id)
-                    continue
-            leaves = _merge_leaves(leaves, [c])
-        if len(leaves) > MAXIN:
-            continue
-        ops.append(h)
-        groups[h.id] = (ops, leaves)
+    inline, st = _select_plan(order, ncons, outs)
+    if st is not None and stats is not None:
+        for k, v in st.items():
+            stats[f"cell-plan-{k}"] = stats.get(f"cell-plan-{k}", 0) + v
+    groups, absorbed = _group(order, ncons, inline)
     plans = []
     for h in order:
         if h.op == "agg" and h.p.get("o") in AGG_CODES and h.p.get("dir") in AGG_DIRS and len(h.inputs) == 1:
             c = h.inputs[0]
             g = groups.get(c.id)
-            if g is not None and ncons.get(c.id, 0) == 1 and c.id not in absorbed:
-                absorbed.add(c.id)
+            if g is not None and ((ncons.get(c.id, 0) == 1 and c.id not in absorbed) or c.id in inline):
+                absorbed[c.id] = absorbed.get(c.id, 0) + 1
                 plans.append((h, g[0], g[1], (h.p["o"], h.p["dir"])))
             elif single and g is None and c.dt == "M" and h.dt in ("M", "S"):
                 plans.append((h, [], [c], (h.p["o"], h.p["dir"])))       # aggregate of a plain input
     for h in order:
         g = groups.get(h.id)
-        if g is not None and h.id not in absorbed and len(g[0]) >= (1 if single else 2):
+        if g is not None and absorbed.get(h.id, 0) < ncons.get(h.id, 0) and len(g[0]) >= (1 if single else 2):
             plans.append((h, g[0], g[1], None))
     n = 0
     built = []

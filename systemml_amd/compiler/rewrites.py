@@ -1045,7 +1045,7 @@ def rewrite_block(bb, config=None):
             n = fuse_vectors(bb)
             if n:
                 rw.stats["vector-fused-ops"] = n
-        n = fuse_cells(bb, single=_VECGEN and (config is None or getattr(config, "gpu", True)))
+        n = fuse_cells(bb, single=_VECGEN and (config is None or getattr(config, "gpu", True)), stats=rw.stats)
         if n:
             rw.stats["cell-fused-ops"] = n
     return rw.stats

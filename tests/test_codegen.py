@@ -57,7 +57,10 @@ def test_cell_plans_and_parity_with_unfused():
             assert a == b, k
 
 
-def test_shared_intermediates_are_materialised():
+def test_shared_intermediate_recomputed_when_cheaper():
+    """Cost-based materialisation (reference PlanSelectionFuseCostBasedV2): T = exp(X) + 1 has
+    two aggregate consumers; recomputing it inside both reads X once in ONE multi-aggregate
+    pass instead of writing T and reading it twice."""
     src = """
     X = rand(rows=20, cols=4, seed=5)
     T = exp(X) + 1
@@ -67,11 +70,29 @@ def test_shared_intermediates_are_materialised():
     """
     cs = EX.compile_script(src, {}, config=DMLConfig(gpu=False))
     fused = _fused_hops(cs)
-    # T has two consumers: it is computed once; the two aggregates over T and X are one
-    # multi-aggregate pass (MAgg template)
-    assert len(fused) == 2, fused
-    assert any("cell[exp,+]" in ln for ln in fused)
-    assert any("magg[" in ln for ln in fused), fused
+    assert len(fused) == 1 and "magg[" in fused[0] and "exp" in fused[0], fused
+    assert cs.cp.rewrite_stats.get("cell-plan-inlined", 0) >= 1
+    out, ref = [], []
+    EX.run(src, config=DMLConfig(gpu=False), out=out.append)
+    EX.run(src, config=DMLConfig(gpu=False, fusion=False), out=ref.append)
+    assert abs(float(out[0]) - float(ref[0])) < 1e-12 * abs(float(ref[0]))
+
+
+def test_shared_intermediate_materialised_for_a_matrix_product():
+    """A shared intermediate that a non-cellwise consumer needs anyway is materialised once;
+    its cellwise consumer reads it instead of recomputing exp."""
+    src = """
+    X = rand(rows=20, cols=4, seed=5)
+    v = rand(rows=4, cols=1, seed=6)
+    T = exp(X) + 1
+    a = sum(T %*% v)
+    b = sum(T * 2)
+    print(a + b)
+    """
+    cs = EX.compile_script(src, {}, config=DMLConfig(gpu=False))
+    fused = _fused_hops(cs)
+    assert any("cell[exp,+]" in ln for ln in fused), fused
+    assert cs.cp.rewrite_stats.get("cell-plan-inlined", 0) == 0
 
 
 def test_sequential_fallback_errors_like_unfused():

@@ -80,10 +80,16 @@ def main():
             if C > 3:
                 fns["miopen_bwd_data"] = lambda: torch.nn.grad.conv2d_input(
                     (N, C, H, H), Wb.view(Fo, C, k, k), G.view(N, Fo, Ho, Ho), stride=s, padding=p)
+        if k == 1 and s == 1:     # 1x1 stride-1: a batched GEMM per image (hipBLASLt via torch.matmul)
+            Wb2 = W.to(torch.bfloat16)
+            fns["blas_fwd"] = lambda: torch.matmul(Wb2, X.view(N, C, H * H))
+            fns["blas_bwd_data"] = lambda: torch.matmul(Wb2.t(), G.view(N, Fo, H * H))
         for name, fn in fns.items():
             ms = timeit(fn, a.reps)
             r[name + "_ms"] = round(ms, 3)
             r[name + "_TF"] = round(flop / ms / 1e9, 1)
+            if name.startswith("blas"):
+                continue
             key = "miopen_ms" if name.startswith("miopen") else "ours_ms"
             tot[key] += ms * n
             if not name.startswith("miopen"):
