@@ -40,6 +40,7 @@ UN_CODES = {"sq": 20,               # x ^ 2 (binary '^' with the literal 2, lowe
 AGG_CODES = {"sum": 0, "sumsq": 1, "mean": 0, "min": 2, "max": 3}
 AGG_DIRS = {"all": 1, "row": 2, "col": 3}
 MAXIN, MAXOPS, NR = 8, 40, 16
+COL4 = 1000           # column-aggregate variant offset: 4 adjacent columns per lane (sysml_cell_col4)
 FULL, ROWV, COLV, HSCALAR, DSCALAR, CHAN = range(6)
 # per-channel broadcast operators (bias_add / bias_multiply: a C x 1 vector over the H*W columns
 # of each channel of an N x (C*H*W) operand); generated kernels only (mode CHAN)
@@ -300,6 +301,8 @@ def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant, idx32=False,
         call = "sysml_cell_flat<Spec, 1>(A);"
     elif mode == 2:
         call = f"sysml_cell_row<Spec, {variant}>(A);"
+    elif variant >= COL4:
+        call = f"sysml_cell_col4<Spec, {variant - COL4}>(A);"
     else:
         call = f"sysml_cell_col<Spec, {variant}>(A);"
     return (_prelude() + f"""
@@ -574,6 +577,8 @@ def _make_plan(prog, args):
             variant = 1 if Cc <= 8 else (4 if Cc <= 32 else (16 if Cc <= 128 else 64))
         elif mode == 3:
             variant = 8 if Cc <= 8 else 64
+            if Cc % 4 == 0 and Cc >= 1024:
+                variant = COL4 + 64           # 4 adjacent columns per lane, vector loads
         else:
             variant = 0
         outbf = mode == 0 and T == torch.float32 and 0 < backend.act_bf16_min_cells <= R * Cc
@@ -583,7 +588,10 @@ def _make_plan(prog, args):
             if outbf:
                 pl.odt = torch.bfloat16
             if mode == 3:
-                pl.gx, pl.gy = (Cc + variant - 1) // variant, nblk
+                cols_per_block = 4 * (variant - COL4) if variant >= COL4 else variant
+                pl.gx, pl.gy = (Cc + cols_per_block - 1) // cols_per_block, nblk
+                if nblk == 1:                 # one row block writes the column aggregate itself
+                    pl.out_shape, pl.part_shape = (1, Cc), None
     pl.interp = pl.fn is None
     pl.hws = hws
     if chan and pl.interp:
@@ -677,9 +685,12 @@ def _kernel(prog: CellProgram, args):
         return C._lazy_out(r)
     if mode == 2:
         return out / Cc if o == "mean" else out
-    r = part.sum(0, keepdim=True) if AGG_CODES[o] <= 1 else (part.amin(0, keepdim=True) if o == "min"
-                                                             else part.amax(0, keepdim=True))
-    r = r.to(T)
+    if part is None:
+        r = out
+    else:
+        r = part.sum(0, keepdim=True) if AGG_CODES[o] <= 1 else (part.amin(0, keepdim=True) if o == "min"
+                                                                 else part.amax(0, keepdim=True))
+        r = r.to(T)
     return r / R if o == "mean" else r
 
 

@@ -212,7 +212,8 @@ def test_cell_kernel_unary_ops(op, dt, tol, rtc):
 @pytest.mark.parametrize("agg", [None, ("sum", "all"), ("sumsq", "all"), ("mean", "all"), ("min", "all"),
                                  ("max", "all"), ("sum", "row"), ("mean", "row"), ("max", "row"),
                                  ("sum", "col"), ("min", "col"), ("mean", "col")])
-@pytest.mark.parametrize("shape", [(1000, 5), (3001, 7), (257, 130), (9, 1000), (4099, 1)])
+@pytest.mark.parametrize("shape", [(1000, 5), (3001, 7), (257, 130), (9, 1000), (4099, 1),
+                                   (300, 1024), (64, 2052)])   # wide: 4-column lanes, 2 / 1 row blocks
 @pytest.mark.parametrize("rtc", [True, False])
 def test_cell_kernel_broadcast_and_aggregates(shape, agg, rtc):
     from systemml_amd.ops.cell import CellProgram
@@ -320,6 +321,29 @@ def test_multi_aggregate_kernel_gpu():
             got = res[k]
             got = float(got.value()) if hasattr(got, "value") else float(got)
             assert got == pytest.approx(float(r), rel=1e-6 if dt == torch.float32 else 1e-9, abs=1e-9), (k, dt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows", [256, 1000])
+def test_cell_kernel_channel_column_sums(dt, rows):
+    """colSums((X - m per channel)^2) over an N x (C*HW) activation (the batch-norm variance
+    pass): 4-column lanes with vector loads, per-channel operand, one or several row blocks."""
+    from systemml_amd.ops.cell import CellProgram
+    from systemml_amd.ops import cell
+    from systemml_amd.ops.backend import backend
+    backend.configure(DMLConfig(gpu=True, precision="single"))
+    dev = torch.device("cuda:0")
+    C, HW = 16, 196
+    prog = CellProgram([("b", "bias+", 2, 0, 1), ("u", "sq", 2, 2, 0)], 2, 2, ("sum", "col"))
+    X = _mk((rows, C * HW), torch.float64, 21, -2, 2).to(dt)
+    m = _mk((C, 1), torch.float32, 22, -0.5, 0.5)
+    got = cell._kernel(prog, [X.to(dev), m.to(dev)])
+    torch.cuda.synchronize()
+    ref = ((X.double().reshape(rows, C, HW) + m.double().reshape(1, C, 1)) ** 2).reshape(rows, -1).sum(0, keepdim=True)
+    assert got.shape == (1, C * HW)
+    err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err
 
 
 BIAS_SCRIPT = """
