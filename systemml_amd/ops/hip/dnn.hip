@@ -635,6 +635,29 @@ __global__ void __launch_bounds__(256) bias_op_v4(const T* __restrict__ X, const
   reinterpret_cast<V*>(O)[i] = v;
 }
 
+// bf16 activations: 4 cells per thread (one 8-B load / store), fp32 bias and arithmetic, one
+// rounding to bf16; total % 4 == 0 and 8-B aligned operands (host checked)
+__global__ void __launch_bounds__(256) bias_op_bf16(const uint2* __restrict__ X, const float* __restrict__ b,
+                                                     uint2* __restrict__ O, int64_t nvec, int C, int P, int mult,
+                                                     int relu) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nvec) return;
+  const uint2 q = X[i];
+  const unsigned short h[4] = {(unsigned short)(q.x & 0xffff), (unsigned short)(q.x >> 16),
+                               (unsigned short)(q.y & 0xffff), (unsigned short)(q.y >> 16)};
+  unsigned r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float v = __uint_as_float(((unsigned)h[k]) << 16);
+    const float bv = b ? b[(int)(((i * 4 + k) / P) % C)] : (mult ? 1.f : 0.f);
+    v = mult ? v * bv : v + bv;
+    if (relu) v = v > 0.f ? v : 0.f;
+    const unsigned u = __float_as_uint(v);
+    r[k] = ((u & 0x7fffffffu) > 0x7f800000u) ? ((u >> 16) | 0x40u) : ((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  }
+  O[i] = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
+}
+
 inline dim3 bias_grid(int64_t rows_ch, int P) {
   int64_t gy = (P + 255) / 256;
   if (gy > 1024) gy = 1024;
@@ -833,6 +856,13 @@ int sysml_bias_op(int dtype, const void* X, const void* b, void* out, int64_t to
   using namespace sysml_dnn;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (P <= 0 || total % P) return -1;
+  if (dtype == 3) {                      // bf16 storage, fp32 bias (dtype 3)
+    if (total % 4 || (uintptr_t)X % 8 || (uintptr_t)out % 8) return -1;
+    const int64_t nvec = total / 4;
+    hipLaunchKernelGGL(bias_op_bf16, dim3((unsigned)((nvec + 255) / 256)), dim3(256), 0, s, (const uint2*)X,
+                       (const float*)b, (uint2*)out, nvec, C, P, mult, relu);
+    return (int)hipGetLastError();
+  }
   const bool v4 = total % 4 == 0 && (uintptr_t)X % (dtype == 1 ? 16 : 32) == 0 &&
                   (uintptr_t)out % (dtype == 1 ? 16 : 32) == 0 && total / 4 < (int64_t)0x7fffffff * 256;
   if (v4 && (dtype == 1 || dtype == 2)) {

@@ -736,6 +736,9 @@ def sddmm(crow, col, U, V, dtype=None):
 # DNN (ops/hip/dnn.hip)
 # ----------------------------------------------------------------------------
 CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) instead of exact fp32 MFMA
+# 1x1 stride-1 convolutions of bf16 activations as batched library GEMMs (SYSML_CONV1X1_GEMM=0: the
+# implicit-GEMM kernel of dnn.hip)
+CONV1X1_GEMM = os.environ.get("SYSML_CONV1X1_GEMM", "1") != "0"
 
 
 def _conv_code(dt):
@@ -772,6 +775,20 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
         shape = (N, C * H * Wd)
     else:
         shape = (F, C * KH * KW)
+    if CONV1X1_GEMM and mode != 2 and KH == 1 and KW == 1 and sh == 1 and sw == 1 and ph == 0 and pw == 0 \
+            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+        # a 1x1 stride-1 convolution of bf16 activations is a plain batched GEMM per image
+        # (forward W . X[n], backward data t(W) . dY[n]): hipBLASLt, bf16 out / fp32 accumulate
+        HW = H * Wd
+        Wm = W.view(F, C)
+        y = torch.matmul(Wm, X.view(N, C, HW)) if mode == 0 else torch.matmul(Wm.t(), D.view(N, F, HW))
+        y = y.view(shape)
+        if mode == 0 and (bias is not None or relu):
+            bb = bias if bias is not None else torch.zeros(F, device=dev)
+            bias_op(y, bb, relu=relu, out=y)
+        _count(("conv2d", "conv2d_bwd_data")[mode])
+        _count("conv1x1_gemm")
+        return y
     # GEMM view (M x Ncol, depth K); split K when the output tiles alone cannot fill the chip:
     # ~2k blocks in flight, each reducing >= 512 products per output (slab traffic stays small)
     M, Nc, K = {0: (F, N * Ho * Wo, C * KH * KW), 1: (C, N * H * Wd, F * KH * KW),
@@ -828,8 +845,21 @@ def pool2d(backward, avg, X, D, N, C, H, W, KH, KW, sh, sw, ph, pw):
     return out
 
 
-def bias_op(X, b, mult=False, relu=False):
+def bias_op(X, b, mult=False, relu=False, out=None):
     L = load(required=True)
+    if X.dtype == torch.bfloat16 and backend.act_bf16_min_cells > 0 and X.numel() % 4 == 0 and X.is_contiguous():
+        # bf16 activations stay bf16 (fp32 bias and arithmetic); out may alias X
+        bf = b.to(device=X.device, dtype=torch.float32).contiguous().reshape(-1)
+        C = bf.numel()
+        if X.shape[1] % C == 0:
+            o = torch.empty_like(X) if out is None else out
+            rc = L.sysml_bias_op(3, X.data_ptr(), bf.data_ptr(), o.data_ptr(), X.numel(), C, X.shape[1] // C,
+                                 int(bool(mult)), int(bool(relu)), _stream())
+            if rc == 0:
+                _count("bias_mult" if mult else "bias_add")
+                return o
+            if rc != -1:
+                raise RuntimeError(f"sysml_bias_op failed: {rc}")
     dt = X.dtype if X.dtype in (torch.float32, torch.float64) else torch.float32
     X = X.to(dt).contiguous()
     b = b.to(device=X.device, dtype=dt).contiguous().reshape(-1)

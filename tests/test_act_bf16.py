@@ -54,6 +54,8 @@ def test_conv_bf16_output(shape):
                        p, p)
     torch.cuda.synchronize()
     assert got.dtype == torch.bfloat16 and gx.dtype == torch.bfloat16
+    if K == 1 and s == 1 and Kn.CONV1X1_GEMM:
+        assert Kn.counters.get("conv1x1_gemm", 0) >= 2
     for name, a, r in (("fwd", got, ref_b), ("bwd_data", gx, ref_dx)):
         err = (a.double().cpu() - r).abs().max().item() / (r.abs().max().item() + 1e-30)
         assert err < 1e-2, (name, err)
@@ -131,3 +133,19 @@ s3 = sum(abs(p))
         assert abs(float(gpu[k]) - float(cpu[k])) < 3e-2 * abs(float(cpu[k])), k
     dw_g, dw_c = gpu["dw"].double().cpu().numpy(), cpu["dw"].cpu().numpy()
     assert np.abs(dw_g - dw_c).max() < 3e-2 * np.abs(dw_c).max()
+
+
+@pytest.mark.parametrize("mult,relu", [(False, False), (True, False), (False, True)])
+def test_bias_op_bf16(mult, relu):
+    from systemml_amd.ops import kernels as Kn
+    N, C, P = 6, 8, 50
+    g = torch.Generator().manual_seed(7)
+    X = _bf(torch.randn(N, C * P, generator=g, dtype=torch.float64))
+    b = torch.randn(C, 1, generator=g, dtype=torch.float64)
+    ref = X.reshape(N, C, P) * b.reshape(1, C, 1) if mult else X.reshape(N, C, P) + b.reshape(1, C, 1)
+    ref = (torch.relu(ref) if relu else ref).reshape(N, -1)
+    with _ActBf16():
+        got = Kn.bias_op(X.to("cuda", torch.bfloat16), b.to("cuda", torch.float32), mult=mult, relu=relu)
+    torch.cuda.synchronize()
+    assert got.dtype == torch.bfloat16
+    np.testing.assert_allclose(got.double().cpu().numpy(), ref.numpy(), rtol=8e-3, atol=8e-3)

@@ -5,6 +5,8 @@ R=$GRAFT_REPO_ROOT
 cd $R
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $R
+timeout -k 10 600 python -u -m pytest tests/test_codegen.py tests/test_act_bf16.py -x -q -m gpu \
+    --timeout 200 --timeout-method thread > gpurun_out/rnp_tests.log 2>&1 || exit $?
 for mode in act fp32; do
   extra=""; [ $mode = fp32 ] && extra="--fp32-activations"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rnp_${mode}_a -o run --output-format csv -- \
@@ -14,3 +16,5 @@ for mode in act fp32; do
   python3 tools/prof_diff.py gpurun_out/rnp_${mode}_a gpurun_out/rnp_${mode}_b 3 > gpurun_out/rnp_${mode}_step.txt || exit $?
   rm -rf gpurun_out/rnp_${mode}_a gpurun_out/rnp_${mode}_b
 done
+timeout -k 10 300 python tools/bench_conv_rn50.py --reps 3 > gpurun_out/conv_rn50.log 2>&1 || exit $?
+SYSML_CONV1X1_GEMM=0 timeout -k 10 300 python tools/bench_conv_rn50.py --reps 3 --no-miopen > gpurun_out/conv_rn50_nogemm.log 2>&1
