@@ -658,6 +658,40 @@ __global__ void __launch_bounds__(256) bias_op_bf16(const uint2* __restrict__ X,
   O[i] = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
 }
 
+// col2im as a gather (no atomics): dX[n][c][ih][iw] = sum over the taps (kh, kw) whose output
+// position oh = (ih + ph - kh) / sh, ow = (iw + pw - kw) / sw lies on the stride grid inside the
+// output, of cols[n][(c*KH + kh)*KW + kw][oh*Wo + ow].  With cols = t(W) . dY[n] (a batched
+// library GEMM) this is conv2d_backward_data; fp32 accumulation, one rounding.
+template <typename TI, typename TO, typename I>
+__global__ void __launch_bounds__(256) col2im_gather(const TI* __restrict__ cols, TO* __restrict__ dx, int N, int C,
+                                                      int H, int W, int KH, int KW, int sh, int sw, int ph, int pw,
+                                                      int Ho, int Wo) {
+  const I total = (I)N * C * H * W;
+  const I P = (I)Ho * Wo;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    const I q = i / W;
+    const int iw = (int)(i - q * W);
+    const I nc = q / H;
+    const int ih = (int)(q - nc * H);
+    const TI* cb = cols + nc * (I)(KH * KW) * P;       // (n, c) block of KH*KW rows of P
+    float acc = 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int th = ih + ph - kh;
+      if (th < 0) break;
+      const int oh = th / sh;
+      if (oh * sh != th || oh >= Ho) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int tw = iw + pw - kw;
+        if (tw < 0) break;
+        const int ow = tw / sw;
+        if (ow * sw != tw || ow >= Wo) continue;
+        acc += (float)cb[(I)(kh * KW + kw) * P + oh * Wo + ow];
+      }
+    }
+    dx[i] = (TO)acc;
+  }
+}
+
 inline dim3 bias_grid(int64_t rows_ch, int P) {
   int64_t gy = (P + 255) / 256;
   if (gy > 1024) gy = 1024;
@@ -891,6 +925,32 @@ int sysml_bias_op(int dtype, const void* X, const void* b, void* out, int64_t to
                        mult, relu);
   else
     return -1;
+  return (int)hipGetLastError();
+}
+
+// dtype 3: bf16 cols -> bf16 dX; 1: fp32 -> fp32.  cols: N x (C*KH*KW) x (Ho*Wo), dx: N x C*H*W.
+int sysml_col2im(int dtype, const void* cols, void* dx, int N, int C, int H, int W, int KH, int KW, int sh, int sw,
+                 int ph, int pw, void* stream) {
+  using namespace sysml_dnn;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int Ho = (H + 2 * ph - KH) / sh + 1, Wo = (W + 2 * pw - KW) / sw + 1;
+  if (Ho <= 0 || Wo <= 0 || N <= 0) return -1;
+  const int64_t total = (int64_t)N * C * H * W, ncols = (int64_t)N * C * KH * KW * Ho * Wo;
+  const bool small = total < (1LL << 31) && ncols < (1LL << 31);
+  const dim3 g(grid_for(total));
+#define SYSML_C2I(TI, TO)                                                                                        \
+  do {                                                                                                           \
+    if (small)                                                                                                   \
+      hipLaunchKernelGGL((col2im_gather<TI, TO, int>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, KH, \
+                         KW, sh, sw, ph, pw, Ho, Wo);                                                            \
+    else                                                                                                         \
+      hipLaunchKernelGGL((col2im_gather<TI, TO, int64_t>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, \
+                         KH, KW, sh, sw, ph, pw, Ho, Wo);                                                        \
+  } while (0)
+  if (dtype == 3) SYSML_C2I(__bf16, __bf16);
+  else if (dtype == 1) SYSML_C2I(float, float);
+  else return -1;
+#undef SYSML_C2I
   return (int)hipGetLastError();
 }
 

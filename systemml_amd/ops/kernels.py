@@ -739,6 +739,7 @@ CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) in
 # 1x1 stride-1 convolutions of bf16 activations as batched library GEMMs (SYSML_CONV1X1_GEMM=0: the
 # implicit-GEMM kernel of dnn.hip)
 CONV1X1_GEMM = os.environ.get("SYSML_CONV1X1_GEMM", "1") != "0"
+COL2IM_MAX_HW = int(os.environ.get("SYSML_COL2IM_MAX_HW", "0"))   # stride-1 backward data via GEMM + col2im up to this H*W
 
 
 def _conv_code(dt):
@@ -788,6 +789,23 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
             bias_op(y, bb, relu=relu, out=y)
         _count(("conv2d", "conv2d_bwd_data")[mode])
         _count("conv1x1_gemm")
+        return y
+    if CONV1X1_GEMM and mode == 1 and (sh > 1 or sw > 1 or (KH > 1 and H * Wd <= COL2IM_MAX_HW)) \
+            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+        # backward data as cols = t(W) . dY[n] (batched library GEMM, bf16) + a col2im gather: a
+        # strided convolution's taps land on the stride grid for a quarter of the (pixel, tap)
+        # pairs, which the implicit GEMM would multiply as zeros
+        CKK, P = C * KH * KW, Ho * Wo
+        cols = torch.matmul(W.view(F, CKK).t(), D.view(N, F, P))
+        y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
+        L.sysml_col2im.restype = ctypes.c_int
+        L.sysml_col2im.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 10 + \
+            [ctypes.c_void_p]
+        rc = L.sysml_col2im(3, cols.data_ptr(), y.data_ptr(), N, C, H, Wd, KH, KW, sh, sw, ph, pw, _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_col2im failed: {rc}")
+        _count("conv2d_bwd_data")
+        _count("conv_col2im")
         return y
     # GEMM view (M x Ncol, depth K); split K when the output tiles alone cannot fill the chip:
     # ~2k blocks in flight, each reducing >= 512 products per output (slab traffic stays small)

@@ -46,6 +46,14 @@ def _dt():
     return backend.dtype
 
 
+def _matk(x, what="argument"):
+    """_mat for the DNN builtins: a bf16 activation in HBM stays bf16 (the dnn.hip kernels read
+    bf16 directly; a conversion would be one more pass over it)."""
+    if isinstance(x, Tensor) and x.dtype == torch.bfloat16 and x.is_cuda and backend.use_kernels:
+        return x
+    return _mat(x, what)
+
+
 def _mat(x, what="argument"):
     if isinstance(x, Tensor):
         return C.cvt(x)
@@ -1068,20 +1076,20 @@ def b_conv2d(ctx, input=None, filter=None, bias=None, **kw):
     """conv2d; `bias` (F x 1) is set by the conv2d + bias_add fusion rewrite and added in the
     convolution kernel's epilogue (reference: DnnOp CONV2D_BIAS_ADD)."""
     from ..ops import dnn
-    b = None if bias is None else _mat(bias).reshape(-1)
-    return dnn.conv2d(_mat(input), _mat(filter), bias=b, **_conv_kw(kw))
+    b = None if bias is None else _matk(bias).reshape(-1)
+    return dnn.conv2d(_matk(input), _matk(filter), bias=b, **_conv_kw(kw))
 
 
 @builtin("conv2d_backward_filter")
 def b_conv2d_bwd_filter(ctx, input=None, dout=None, **kw):
     from ..ops import dnn
-    return dnn.conv2d_backward_filter(_mat(input), _mat(dout), **_conv_kw(kw))
+    return dnn.conv2d_backward_filter(_matk(input), _matk(dout), **_conv_kw(kw))
 
 
 @builtin("conv2d_backward_data")
 def b_conv2d_bwd_data(ctx, filter=None, dout=None, **kw):
     from ..ops import dnn
-    return dnn.conv2d_backward_data(_mat(filter), _mat(dout), **_conv_kw(kw))
+    return dnn.conv2d_backward_data(_matk(filter), _matk(dout), **_conv_kw(kw))
 
 
 def _conv_kw(kw):
@@ -1095,15 +1103,15 @@ def _conv_kw(kw):
 @builtin("max_pool", "avg_pool")
 def b_pool(ctx, input=None, **kw):
     from ..ops import dnn
-    return dnn.pool(_mat(input), kind=kw.get("__name__", "max"), **_conv_kw(kw))
+    return dnn.pool(_matk(input), kind=kw.get("__name__", "max"), **_conv_kw(kw))
 
 
 def _pool_factory(kind, backward):
     def fn(ctx, input=None, dout=None, **kw):
         from ..ops import dnn
         if backward:
-            return dnn.pool_backward(_mat(input), _mat(dout), kind=kind, **_conv_kw(kw))
-        return dnn.pool(_mat(input), kind=kind, **_conv_kw(kw))
+            return dnn.pool_backward(_matk(input), _matk(dout), kind=kind, **_conv_kw(kw))
+        return dnn.pool(_matk(input), kind=kind, **_conv_kw(kw))
     return fn
 
 
@@ -1116,13 +1124,13 @@ REGISTRY["avg_pool_backward"] = _pool_factory("avg", True)
 @builtin("bias_add")
 def b_bias_add(ctx, input, bias):
     from ..ops import dnn
-    return dnn.bias_op(_mat(input), _mat(bias), mult=False)
+    return dnn.bias_op(_matk(input), _matk(bias), mult=False)
 
 
 @builtin("bias_multiply")
 def b_bias_mult(ctx, input, bias):
     from ..ops import dnn
-    return dnn.bias_op(_mat(input), _mat(bias), mult=True)
+    return dnn.bias_op(_matk(input), _matk(bias), mult=True)
 
 
 # ============================================================================

@@ -32,7 +32,8 @@ def _bf(x):
 # output); the last shape runs the 128 x 128 tiles
 @pytest.mark.parametrize("shape", [(2, 100, 9, 11, 96, 3, 1, 1), (4, 64, 14, 14, 96, 3, 1, 1),
                                    (2, 100, 15, 15, 56, 3, 2, 1), (8, 32, 8, 8, 64, 1, 1, 0),
-                                   (64, 64, 28, 28, 256, 1, 1, 0)])
+                                   (64, 64, 28, 28, 256, 1, 1, 0), (4, 64, 14, 14, 128, 1, 2, 0),
+                                   (3, 40, 13, 13, 24, 3, 2, 1)])
 def test_conv_bf16_output(shape):
     from systemml_amd.ops import kernels as Kn
     N, C, H, Wd, F_, K, s, p = shape
@@ -56,6 +57,8 @@ def test_conv_bf16_output(shape):
     assert got.dtype == torch.bfloat16 and gx.dtype == torch.bfloat16
     if K == 1 and s == 1 and Kn.CONV1X1_GEMM:
         assert Kn.counters.get("conv1x1_gemm", 0) >= 2
+    if s > 1 and Kn.CONV1X1_GEMM:
+        assert Kn.counters.get("conv_col2im", 0) >= 1          # backward data: GEMM + col2im
     for name, a, r in (("fwd", got, ref_b), ("bwd_data", gx, ref_dx)):
         err = (a.double().cpu() - r).abs().max().item() / (r.abs().max().item() + 1e-30)
         assert err < 1e-2, (name, err)
