@@ -137,7 +137,19 @@ def _group(order, ncons, inline):
             continue
         ops.append(h)
         groups[h.id] = (ops, leaves)
-    return groups, absorbed
+    aggs = []                                         # (aggregate hop, fused DAG it absorbs)
+    for h in order:
+        if _is_cell_agg(h):
+            c = h.inputs[0]
+            g = groups.get(c.id)
+            if g is not None and ((ncons.get(c.id, 0) == 1 and c.id not in absorbed) or c.id in inline):
+                absorbed[c.id] = absorbed.get(c.id, 0) + 1
+                aggs.append((h, g))
+    return groups, absorbed, aggs
+
+
+def _is_cell_agg(h):
+    return h.op == "agg" and h.p.get("o") in AGG_CODES and h.p.get("dir") in AGG_DIRS and len(h.inputs) == 1
 
 
 _HEAVY_OPS = {"exp", "log", "sqrt", "^", "sigmoid", "tanh", "sin", "cos", "tan", "asin", "acos", "atan",
@@ -153,6 +165,8 @@ def _cells(h, memo):
             r = 0.0
         elif h.dim1 >= 0 and h.dim2 >= 0:
             r = float(h.dim1 * h.dim2)
+        elif h.op == "agg" and h.p.get("dir") in ("row", "col"):
+            r = 1e3                                   # a row / column aggregate: a vector
         elif _cellwise(h):
             r = max((_cells(c, memo) for c in _operands(h)), default=0.0) or 1e6
         else:
@@ -161,7 +175,7 @@ def _cells(h, memo):
     return r
 
 
-def _plan_cost(order, groups, absorbed, ncons, memo):
+def _plan_cost(order, groups, absorbed, aggs, ncons, memo):
     """HBM + compute cost of a Cell-template plan, in cell-reads: every materialised fused DAG
     reads its leaves and writes its root once; its operators cost a fraction of a read per
     cell (transcendentals more).  The reference's PlanSelectionFuseCostBasedV2 prices plans
@@ -175,6 +189,10 @@ def _plan_cost(order, groups, absorbed, ncons, memo):
         n = _cells(h, memo)
         cost += n + sum(_cells(c, memo) for c in leaves)
         cost += sum((0.25 if o.p.get("o") in _HEAVY_OPS else 0.05) * n for o in ops)
+    for h, (ops, leaves) in aggs:                     # fused aggregates: read the leaves once
+        n = _cells(h.inputs[0], memo)
+        cost += sum(_cells(c, memo) for c in leaves)
+        cost += sum((0.25 if o.p.get("o") in _HEAVY_OPS else 0.05) * n for o in ops)
     return cost
 
 
@@ -185,42 +203,42 @@ def _select_plan(order, ncons, outs):
     """Materialisation-point selection (reference: opt/PlanSelectionFuseCostBasedV2): the
     shared cellwise intermediates that are no block output are the interesting points; each is
     either materialised once or recomputed inside every consumer.  Up to ENUM_MAX points every
-    combination is costed, beyond that a greedy pass flips one point at a time; a plan must be
-    >= 5 % cheaper than materialising everything to be taken.  Returns (inline set, stats)."""
+    combination is costed, beyond that a greedy pass flips one point at a time; recomputing a
+    point must save >= 5 % of a pass over it to be taken.  Returns (inline set, stats)."""
     out_ids = {h.id for h in outs}
     cons = {}
     for h in order:
         for c in h.inputs:
             cons.setdefault(c.id, []).append(h)
-    base_groups, _ = _group(order, ncons, frozenset())
+    base_groups, _, _ = _group(order, ncons, frozenset())
     points = [h.id for h in order if h.id in base_groups and ncons.get(h.id, 0) > 1 and h.id not in out_ids
-              and any(_cellwise(u) for u in cons.get(h.id, ()))]
+              and any(_cellwise(u) or _is_cell_agg(u) for u in cons.get(h.id, ()))]
     if not points:
         return frozenset(), None
     memo = {}
 
     def cost(inl):
-        g, a = _group(order, ncons, inl)
-        return _plan_cost(order, g, a, ncons, memo)
-    base = best_cost = cost(frozenset())
+        g, a, ag = _group(order, ncons, inl)
+        return _plan_cost(order, g, a, ag, ncons, memo)
+    size = {h.id: _cells(h, memo) for h in order if h.id in set(points)}
+    best_cost = cost(frozenset())
     best = frozenset()
     evaluated = 1
+    # a plan must save at least 5 % of one pass over the values it stops materialising
     if len(points) <= ENUM_MAX:
         for mask in range(1, 1 << len(points)):
             inl = frozenset(p for i, p in enumerate(points) if mask >> i & 1)
             c = cost(inl)
             evaluated += 1
-            if c < best_cost:
+            if c < best_cost - 0.05 * sum(size[p] for p in inl - best):
                 best, best_cost = inl, c
     else:
         for p in points:
             inl = best | {p}
             c = cost(inl)
             evaluated += 1
-            if c < best_cost:
+            if c < best_cost - 0.05 * size[p]:
                 best, best_cost = frozenset(inl), c
-    if best_cost > 0.95 * base:
-        best = frozenset()
     return best, {"points": len(points), "plans": evaluated, "inlined": len(best)}
 
 
@@ -244,17 +262,14 @@ def fuse_cells(bb, single=False, stats=None):
     if st is not None and stats is not None:
         for k, v in st.items():
             stats[f"cell-plan-{k}"] = stats.get(f"cell-plan-{k}", 0) + v
-    groups, absorbed = _group(order, ncons, inline)
-    plans = []
-    for h in order:
-        if h.op == "agg" and h.p.get("o") in AGG_CODES and h.p.get("dir") in AGG_DIRS and len(h.inputs) == 1:
-            c = h.inputs[0]
-            g = groups.get(c.id)
-            if g is not None and ((ncons.get(c.id, 0) == 1 and c.id not in absorbed) or c.id in inline):
-                absorbed[c.id] = absorbed.get(c.id, 0) + 1
-                plans.append((h, g[0], g[1], (h.p["o"], h.p["dir"])))
-            elif single and g is None and c.dt == "M" and h.dt in ("M", "S"):
-                plans.append((h, [], [c], (h.p["o"], h.p["dir"])))       # aggregate of a plain input
+    groups, absorbed, aggs = _group(order, ncons, inline)
+    plans = [(h, g[0], g[1], (h.p["o"], h.p["dir"])) for h, g in aggs]
+    fused_aggs = {h.id for h, _ in aggs}
+    if single:
+        for h in order:
+            if _is_cell_agg(h) and h.id not in fused_aggs and h.inputs[0].dt == "M" and h.dt in ("M", "S"):
+                # aggregate of a plain or materialised input
+                plans.append((h, [], [h.inputs[0]], (h.p["o"], h.p["dir"])))
     for h in order:
         g = groups.get(h.id)
         if g is not None and absorbed.get(h.id, 0) < ncons.get(h.id, 0) and len(g[0]) >= (1 if single else 2):

@@ -225,13 +225,16 @@ def _assigned(blocks):
     return assigned_in(blocks)
 
 
-def propagate_literals(cp, stats):
+def literal_params(cp):
+    """{function key: {scalar parameter: literal}} for the parameters every call site passes as
+    the same literal and the body never reassigns."""
     sites = {}
     units = [cp.blocks] + [fb.body for fb in cp.functions.values() if fb.body is not None]
     for blocks in units:
         calls, _, _ = _calls(blocks)
         for h in calls:
             sites.setdefault(h.p["fkey"], []).append(h)
+    out = {}
     for k, fb in cp.functions.items():
         if fb.body is None or fb.external or k not in sites:
             continue
@@ -256,8 +259,14 @@ def propagate_literals(cp, stats):
                 if p.vtype == "DOUBLE" and isinstance(v, int) and not isinstance(v, bool):
                     v = float(v)
                 consts[p.name] = v
-        if not consts:
-            continue
+        if consts:
+            out[k] = consts
+    return out
+
+
+def propagate_literals(cp, stats):
+    for k, consts in literal_params(cp).items():
+        fb = cp.functions[k]
         for owner, roots in _block_dags(fb.body):
             for h in H.walk(roots):
                 h.inputs = [lit(consts[c.p["name"]], c.pos) if (c.op == "tread" and c.p["name"] in consts) else c

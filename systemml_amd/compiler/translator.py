@@ -144,6 +144,7 @@ class Translator:
         cp = CompiledProgram(blocks, self.functions, prog.source_path)
         if self.config is None or getattr(self.config, "rewrites", True):
             from . import ipa
+            self._specialise_functions(cp)
             ipa.run(cp, self.config)                # inter-procedural analysis (inlining, ...)
             from .loops import hoist_program
             cp.licm_stats = hoist_program(cp)      # before liveness: adds blocks / variables
@@ -171,6 +172,32 @@ class Translator:
             pass  # reported at runtime with position info (variables may be defined conditionally)
         cp.outputs = set(outputs)
         return cp
+
+    def _specialise_functions(self, cp, rounds=3):
+        """Rebuild the body of every function whose scalar parameters are the same literal at
+        every call site with those literals as constants (reference
+        IPAPassPropagateReplaceLiterals + RewriteRemoveUnnecessaryBranches +
+        RewriteMergeBlockSequence): constant branches such as the nn layers'
+        `if (mode == "train")` disappear at translation and the remaining statements merge into
+        one basic block, so operator fusion sees across them.  Repeated while a rebuilt body
+        passes new literals on to its callees."""
+        from . import ipa
+        applied = {}
+        for _ in range(rounds):
+            changed = False
+            for k, consts in ipa.literal_params(cp).items():
+                if k not in self.func_defs or applied.get(k) == consts:
+                    continue
+                fd, ctx = self.func_defs[k]
+                fb = cp.functions[k]
+                types = {p.name: p.dtype[0] if p.dtype in ("MATRIX", "SCALAR", "FRAME", "LIST") else "U"
+                         for p in fd.inputs}
+                fb.body = self.build_stmts(fd.body, ctx, dict(consts), params=fd.inputs, types=types)
+                applied[k] = consts
+                changed = True
+            if not changed:
+                break
+        cp.specialised = len(applied)
 
     # ------------------------------------------------------------------ blocks
     def build_stmts(self, stmts, ctx, consts, params=None, types=None):

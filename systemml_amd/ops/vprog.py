@@ -493,7 +493,7 @@ def fallback(vp, ctx, args):
         tmp = BasicBlock()
         tmp.env_out = {f"__vp_o{k}": h for k, h in enumerate(outs)}
         tmp.live_out = None
-        fuse_cells(tmp)
+        fuse_cells(tmp, single=backend.use_kernels)     # on the GPU every operator a generated kernel
         instrs, writes, nslots = _linearize([], list(tmp.env_out.items()), make_impl)
         argpos = {nm: k for k, nm in enumerate(names)}
         reads = [(ins.out, argpos[ins.hop.p["name"]]) for ins in instrs if ins.opcode == "tread"]
