@@ -150,7 +150,10 @@ def test_vprog_kernel_matches_cpu(rc):
     if r * c <= vprog.VMAX:
         assert kernels.counters.get("vprog", 0) > before, kernels.counters
     else:
-        assert vprog.stats["fallback"] > fb
+        # matrices above the single-workgroup limit: known at compile time here, so the Cell /
+        # MAgg templates take the region (no vector program); a region sized only at run time
+        # would take the guarded fallback instead
+        assert kernels.counters.get("vprog", 0) == before or vprog.stats["fallback"] > fb
 
 
 @pytest.mark.gpu
