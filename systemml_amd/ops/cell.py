@@ -323,8 +323,21 @@ struct Spec {{
   }}
 }};
 
-extern "C" __global__ void __launch_bounds__(256) sysml_cell_k(const SysmlCellArgs A) {{ {call} }}
+extern "C" __global__ void __launch_bounds__(256) {kernel_name(prog, mode, outbf)}(const SysmlCellArgs A) {{ {call} }}
 """)
+
+
+_OPNAME = {"+": "add", "-": "sub", "*": "mul", "/": "div", "^": "pow", "%%": "mod", "%/%": "idiv", "==": "eq",
+           "!=": "ne", "<": "lt", "<=": "le", ">": "gt", ">=": "ge", "&": "and", "|": "or", "bias+": "badd",
+           "bias*": "bmul"}
+
+
+def kernel_name(prog, mode, outbf=False):
+    """Symbol of a generated kernel: its operators, aggregate and output type, so rocprofv3's
+    per-kernel statistics tell the fused programs apart (sysml_cell_<ops>[_<agg>][_bf])."""
+    ops = "_".join(_OPNAME.get(o, o) for _, o, _, _, _ in prog.ops)[:80] or "copy"
+    agg = f"_{prog.agg[0]}{prog.agg[1]}" if prog.agg else ""
+    return f"sysml_cell_{ops}{agg}{'_bf' if outbf else ''}"
 
 
 _PRELUDE = []
@@ -427,7 +440,7 @@ def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, idx32=False, outbf=
         L = _rtc_lib()
         fn = ctypes.c_void_p()
         cbuf = ctypes.create_string_buffer(code, len(code))
-        rc = L.sysml_rtc_load(cbuf, b"sysml_cell_k", ctypes.byref(fn))
+        rc = L.sysml_rtc_load(cbuf, kernel_name(prog, mode, outbf).encode(), ctypes.byref(fn))
         if rc != 0:
             raise RuntimeError(f"hipModuleLoadData failed ({rc})")
         f = (fn, cbuf)
