@@ -233,12 +233,29 @@ def _select_plan(order, ncons, outs):
             if c < best_cost - 0.05 * sum(size[p] for p in inl - best):
                 best, best_cost = inl, c
     else:
+        # many points (e.g. a whole network's layers inlined into one block): each flip is
+        # priced on its neighbourhood only -- the point's fused DAG and the downstream
+        # cellwise / aggregate consumers it could be recomputed in, with their fused DAGs
         for p in points:
-            inl = best | {p}
-            c = cost(inl)
+            region = {o.id for o in base_groups[p][0]}
+            stack = [p]
+            while stack:
+                u = stack.pop()
+                for v in cons.get(u, ()):
+                    if v.id in region or not (_cellwise(v) or _is_cell_agg(v)):
+                        continue
+                    region.add(v.id)
+                    g = base_groups.get(v.id)
+                    if g is not None:
+                        region.update(o.id for o in g[0])
+                    if len(region) < 256:
+                        stack.append(v.id)
+            sub = [h for h in order if h.id in region]
+            g0, a0, ag0 = _group(sub, ncons, best)
+            g1, a1, ag1 = _group(sub, ncons, best | {p})
             evaluated += 1
-            if c < best_cost - 0.05 * size[p]:
-                best, best_cost = frozenset(inl), c
+            if _plan_cost(sub, g1, a1, ag1, ncons, memo) < _plan_cost(sub, g0, a0, ag0, ncons, memo) - 0.05 * size[p]:
+                best = frozenset(best | {p})
     return best, {"points": len(points), "plans": evaluated, "inlined": len(best)}
 
 

@@ -158,20 +158,27 @@ def _copy_dag(outs, binding):
     return [cp_(o) for o in outs]
 
 
-def inline_functions(cp, graph, stats):
-    candidates = {k: fb for k, fb in cp.functions.items() if _inlineable(fb)}
-    if not candidates:
-        return
+def inline_functions(cp, graph, stats, rounds=4):
+    """Inline bottom-up: a function whose body calls a small function becomes inlineable itself
+    once that call is inlined (nn layers calling util::channel_sums), so candidates are
+    recomputed until a round inlines nothing."""
     ncalls = {}
     for edges in graph.values():
         for k in edges:
             ncalls[k] = ncalls.get(k, 0) + 1
-    units = [cp.blocks] + [fb.body for fb in cp.functions.values() if fb.body is not None]
-    for blocks in units:
-        for owner, _ in list(_block_dags(blocks)):
-            if not isinstance(owner, BasicBlock):
-                continue
-            _inline_in_block(owner, candidates, ncalls, stats)
+    for _ in range(rounds):
+        candidates = {k: fb for k, fb in cp.functions.items() if _inlineable(fb)}
+        if not candidates:
+            return
+        before = stats.get("inlined", 0)
+        units = [cp.blocks] + [fb.body for fb in cp.functions.values() if fb.body is not None]
+        for blocks in units:
+            for owner, _ in list(_block_dags(blocks)):
+                if not isinstance(owner, BasicBlock):
+                    continue
+                _inline_in_block(owner, candidates, ncalls, stats)
+        if stats.get("inlined", 0) == before:
+            return
 
 
 def _inline_in_block(bb, candidates, ncalls, stats):

@@ -662,10 +662,11 @@ __global__ void __launch_bounds__(256) bias_op_bf16(const uint2* __restrict__ X,
 // position oh = (ih + ph - kh) / sh, ow = (iw + pw - kw) / sw lies on the stride grid inside the
 // output, of cols[n][(c*KH + kh)*KW + kw][oh*Wo + ow].  With cols = t(W) . dY[n] (a batched
 // library GEMM) this is conv2d_backward_data; fp32 accumulation, one rounding.
-template <typename TI, typename TO, typename I>
+template <typename TI, typename TO, typename I, int S2>
 __global__ void __launch_bounds__(256) col2im_gather(const TI* __restrict__ cols, TO* __restrict__ dx, int N, int C,
                                                       int H, int W, int KH, int KW, int sh, int sw, int ph, int pw,
                                                       int Ho, int Wo) {
+  if (S2) { sh = 2; sw = 2; }                         // stride 2: shifts instead of divisions
   const I total = (I)N * C * H * W;
   const I P = (I)Ho * Wo;
   for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
@@ -678,13 +679,13 @@ __global__ void __launch_bounds__(256) col2im_gather(const TI* __restrict__ cols
     for (int kh = 0; kh < KH; ++kh) {
       const int th = ih + ph - kh;
       if (th < 0) break;
-      const int oh = th / sh;
-      if (oh * sh != th || oh >= Ho) continue;
+      const int oh = S2 ? (th >> 1) : th / sh;
+      if ((S2 ? (th & 1) != 0 : oh * sh != th) || oh >= Ho) continue;
       for (int kw = 0; kw < KW; ++kw) {
         const int tw = iw + pw - kw;
         if (tw < 0) break;
-        const int ow = tw / sw;
-        if (ow * sw != tw || ow >= Wo) continue;
+        const int ow = S2 ? (tw >> 1) : tw / sw;
+        if ((S2 ? (tw & 1) != 0 : ow * sw != tw) || ow >= Wo) continue;
         acc += (float)cb[(I)(kh * KW + kw) * P + oh * Wo + ow];
       }
     }
@@ -715,8 +716,11 @@ inline unsigned grid_for(int64_t n) {
 namespace sysml_dnn {
 // 128 x 128 tiles only when they still give >= 2 workgroups per CU (256 CUs): a 256-filter
 // 14 x 14 layer at batch 64 has 196 such tiles and runs 1.5x faster on 64 x 64 ones
-inline int conv_tile(int dtype, int64_t M, int64_t Nc) {
+inline int conv_tile(int dtype, int64_t M, int64_t Nc, int mode = 0) {
   if (!(dtype == 0 || dtype == 3 || dtype == 4) || M < 128 || Nc < 128) return 64;
+  // backward filter fills the chip by splitting its deep K: the larger tile halves the
+  // gathered operand loads per MFMA
+  if (mode == 2) return 128;
   return ((M + 127) / 128) * ((Nc + 127) / 128) >= 512 ? 128 : 64;
 }
 }  // namespace sysml_dnn
@@ -745,6 +749,9 @@ extern "C" {
 
 // Output tile edge the launcher uses for a GEMM view (the host sizes split-K from it).
 int sysml_conv2d_tile(int dtype, int64_t M, int64_t Nc) { return sysml_dnn::conv_tile(dtype, M, Nc); }
+int sysml_conv2d_tile_mode(int dtype, int mode, int64_t M, int64_t Nc) {
+  return sysml_dnn::conv_tile(dtype, M, Nc, mode);
+}
 
 // dtype: 0 bf16 in (fp32 out), 1 fp32 exact, 2 fp64 exact, 3 fp32 in / bf16 MFMA / fp32 out,
 // 4 bf16 in / bf16 out (forward and backward data, no split-K; fp32 bias).
@@ -779,7 +786,7 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
   c.M = (int)M; c.Ncol = (int)Nc; c.K = (int)K;
   const bool bfmma = dtype == 0 || dtype == 3 || dtype == 4;
   if (dtype == 4 && (mode == BWD_FILTER || (mode == BWD_DATA && C <= 8) || ksplit > 1)) return -1;
-  const int tile = conv_tile(dtype, M, Nc);          // 128 x 128 (bf16, both dims >= 128) or 64 x 64
+  const int tile = conv_tile(dtype, M, Nc, mode);    // 128 x 128 (bf16, both dims >= 128) or 64 x 64
   c.tm = (int)((M + tile - 1) / tile);
   c.tn = (int)((Nc + tile - 1) / tile);
   const int BK = bfmma ? 32 : 16;
@@ -938,14 +945,18 @@ int sysml_col2im(int dtype, const void* cols, void* dx, int N, int C, int H, int
   const int64_t total = (int64_t)N * C * H * W, ncols = (int64_t)N * C * KH * KW * Ho * Wo;
   const bool small = total < (1LL << 31) && ncols < (1LL << 31);
   const dim3 g(grid_for(total));
+  const bool s2 = sh == 2 && sw == 2;
 #define SYSML_C2I(TI, TO)                                                                                        \
   do {                                                                                                           \
-    if (small)                                                                                                   \
-      hipLaunchKernelGGL((col2im_gather<TI, TO, int>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, KH, \
-                         KW, sh, sw, ph, pw, Ho, Wo);                                                            \
-    else                                                                                                         \
-      hipLaunchKernelGGL((col2im_gather<TI, TO, int64_t>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, \
+    if (small && s2)                                                                                             \
+      hipLaunchKernelGGL((col2im_gather<TI, TO, int, 1>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, \
                          KH, KW, sh, sw, ph, pw, Ho, Wo);                                                        \
+    else if (small)                                                                                              \
+      hipLaunchKernelGGL((col2im_gather<TI, TO, int, 0>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, \
+                         KH, KW, sh, sw, ph, pw, Ho, Wo);                                                        \
+    else                                                                                                         \
+      hipLaunchKernelGGL((col2im_gather<TI, TO, int64_t, 0>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, \
+                         W, KH, KW, sh, sw, ph, pw, Ho, Wo);                                                     \
   } while (0)
   if (dtype == 3) SYSML_C2I(__bf16, __bf16);
   else if (dtype == 1) SYSML_C2I(float, float);

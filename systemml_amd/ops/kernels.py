@@ -811,9 +811,9 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
     # ~2k blocks in flight, each reducing >= 512 products per output (slab traffic stays small)
     M, Nc, K = {0: (F, N * Ho * Wo, C * KH * KW), 1: (C, N * H * Wd, F * KH * KW),
                 2: (F, C * KH * KW, N * Ho * Wo)}[mode]
-    L.sysml_conv2d_tile.restype = ctypes.c_int
-    L.sysml_conv2d_tile.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
-    te = L.sysml_conv2d_tile(code, M, Nc)           # the launcher's output tile edge
+    L.sysml_conv2d_tile_mode.restype = ctypes.c_int
+    L.sysml_conv2d_tile_mode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
+    te = L.sysml_conv2d_tile_mode(code, mode, M, Nc)   # the launcher's output tile edge
     tiles = ((M + te - 1) // te) * ((Nc + te - 1) // te)
     ksplit = 1
     if tiles < 2048:
