@@ -947,11 +947,12 @@ def _conv_gemm_path(c, config):
     base = len(c.inputs) - len(named)
 
     def vals(name):
+        """literal entries of a shape-list argument (None where not a literal)"""
         if name not in named:
             return None
         h = c.inputs[base + named.index(name)]
-        if h.op == "bi" and h.p.get("name") == "list" and all(x.op == "lit" for x in h.inputs):
-            return [x.value for x in h.inputs]
+        if h.op == "bi" and h.p.get("name") == "list":
+            return [x.value if x.op == "lit" else None for x in h.inputs]
         return None
     f, st, pd = vals("filter_shape"), vals("stride"), vals("padding")
     return f is not None and len(f) == 4 and f[2] == 1 and f[3] == 1 and st == [1, 1] and pd == [0, 0]
