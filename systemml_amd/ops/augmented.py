@@ -24,11 +24,12 @@ from ..runtime import scalars as S
 
 
 class ConstCol:
-    __slots__ = ("X", "c")
+    __slots__ = ("X", "c", "_pad")
 
     def __init__(self, X, c):
         self.X = X
         self.c = float(c)
+        self._pad = None
 
     @property
     def shape(self):
@@ -78,6 +79,49 @@ def make(X, c):
     return torch.cat([X, torch.full((X.shape[0], 1), c, dtype=X.dtype, device=X.device)], 1)
 
 
+PAD_MIN_CELLS = 1 << 24      # below this the two-pass view products are cheap enough
+stats = {"padded": 0}
+
+
+def padded(a):
+    """HBM copy of cbind(X, c) with the row length rounded up to 16 B and zeros beyond the
+    constant column, made once per view (the intercept scripts build the view once, outside
+    their loops) when the device has room for it: the fused chain / softmax kernels then take
+    one pass over it per product, where the view costs two passes plus glue.  None when X is
+    not a large bf16 / fp32 HBM matrix or memory is short."""
+    if a._pad is not None:
+        return a._pad
+    X = a.X
+    from .backend import backend
+    if not (backend.use_kernels and isinstance(X, torch.Tensor) and X.is_cuda and X.layout == torch.strided
+            and X.dtype in (torch.bfloat16, torch.float32) and X.numel() >= PAD_MIN_CELLS):
+        return None
+    N, D = X.shape
+    m = 8 if X.dtype == torch.bfloat16 else 4
+    Dp = (D + 1 + m - 1) // m * m
+    need = N * Dp * X.element_size()
+    free, _ = torch.cuda.mem_get_info(X.device)
+    if need * 1.5 > free:
+        return None
+    Xp = torch.empty((N, Dp), dtype=X.dtype, device=X.device)
+    Xp[:, :D].copy_(X)
+    Xp[:, D].fill_(a.c)
+    if Dp > D + 1:
+        Xp[:, D + 1:].zero_()
+    a._pad = Xp
+    stats["padded"] += 1
+    return Xp
+
+
+def padv(v, Dp):
+    """(D+1) x K operand zero-extended to the padded row length."""
+    C = _C()
+    v = C.cvt(v)
+    if v.shape[0] == Dp:
+        return v
+    return torch.cat([v, torch.zeros((Dp - v.shape[0], v.shape[1]), dtype=v.dtype, device=v.device)], 0)
+
+
 def _split(v):
     """v (D+1 x K) -> (v[1:D], v[D+1] as 1 x K)."""
     return v[:-1], v[-1:]
@@ -88,6 +132,12 @@ def mm(a, b, transA=False):
     if is_cc(b):
         b = b.materialize()
         return C.mm(a, b, transA)
+    Xp = padded(a)
+    if Xp is not None and isinstance(b, torch.Tensor):
+        D1 = a.X.shape[1] + 1
+        if transA:
+            return C.mm(Xp, b, True)[:D1]
+        return C.mm(Xp, padv(b.to(Xp.device), Xp.shape[1]))
     if transA:                                      # t(A) %*% y
         y = C.cvt(b) if isinstance(b, torch.Tensor) else b
         top = C.mm(a.X, y, True)
@@ -112,9 +162,13 @@ def tsmm(a, left=True):
 
 
 def mmchain(ctype, X, v, w=None):
-    """t(A) %*% g(A %*% v) for A = ConstCol: the product A v and the final t(A) g each run on
-    X with the streaming kernels, the constant column is added / reduced on the side."""
+    """t(A) %*% g(A %*% v) for A = ConstCol: one fused pass over the padded copy when it
+    exists (`padded`); else the product A v and the final t(A) g each run on X with the
+    streaming kernels, the constant column added / reduced on the side."""
     C = _C()
+    Xp = padded(X)
+    if Xp is not None and isinstance(v, torch.Tensor):
+        return C.mmchain(ctype, Xp, padv(v.to(Xp.device), Xp.shape[1]), w)[:X.X.shape[1] + 1]
     u = mm(X, v)
     if ctype == "XtXv":
         g = u
@@ -132,6 +186,10 @@ def mmchain(ctype, X, v, w=None):
 
 def smgrad(X, V, Y, kc):
     C = _C()
+    Xp = padded(X)
+    if Xp is not None and isinstance(V, torch.Tensor):
+        u, g = C.smgrad(Xp, padv(V.to(Xp.device), Xp.shape[1]), Y, kc)
+        return u, g[:X.X.shape[1] + 1]
     u = C.cvt(mm(X, V))
     lt = torch.cat([u, torch.zeros((u.shape[0], 1), dtype=u.dtype, device=u.device)], dim=1)
     lt = lt - lt.max(dim=1, keepdim=True).values

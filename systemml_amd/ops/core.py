@@ -683,6 +683,10 @@ def mm(a, b, transA=False):
 
 def tsmm(x, left=True):
     if type(x) is _CC:
+        Xp = AUG.padded(x) if left else None
+        if Xp is not None:
+            D1 = x.X.shape[1] + 1
+            return tsmm(Xp, True)[:D1, :D1]
         return AUG.tsmm(x, left)
     if is_dist(x):
         return _dist().tsmm(x, left)
@@ -743,6 +747,11 @@ def smobj(X, V, Y, cu=None):
     kc = K if cu is None else int(S.as_double(cu))
     if is_dist(X):
         return _dist().smobj(X, V, Y, kc)
+    if type(X) is _CC and isinstance(V, Tensor):
+        Xp = AUG.padded(X)            # cbind(X, 1) copy with 16-B rows: the one-pass kernel applies
+        if Xp is not None:
+            p, g, s1, s2 = smobj(Xp, AUG.padv(V.to(Xp.device), Xp.shape[1]), Y, cu)
+            return p, g[:X.X.shape[1] + 1], s1, s2
     if type(X) is not _CC and backend.use_kernels and isinstance(X, Tensor) and X.is_cuda \
             and not SP.is_sparse(X) and kc == K and isinstance(V, Tensor) and isinstance(Y, Tensor) \
             and not SP.is_sparse(Y):
