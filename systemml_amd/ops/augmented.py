@@ -73,12 +73,13 @@ def make(X, c):
     if C.is_dist(X):
         loc = C.cvt(SP.densify(X.local))
         return X.like(torch.cat([loc, torch.full((loc.shape[0], 1), c, dtype=loc.dtype, device=loc.device)], 1))
-    if isinstance(X, torch.Tensor) and X.layout == torch.strided and X.numel() >= (1 << 20):
+    if isinstance(X, torch.Tensor) and X.layout == torch.strided and X.numel() >= VIEW_MIN_CELLS:
         return ConstCol(X, c)
     X = C.cvt(SP.densify(X))
     return torch.cat([X, torch.full((X.shape[0], 1), c, dtype=X.dtype, device=X.device)], 1)
 
 
+VIEW_MIN_CELLS = 1 << 20     # smaller matrices are simply concatenated
 PAD_MIN_CELLS = 1 << 24      # below this the two-pass view products are cheap enough
 stats = {"padded": 0}
 

@@ -25,6 +25,7 @@ def _data(n=4000, d=30, k=3, seed=11):
 def test_multilogreg_intercept_on_padded_copy(icpt, monkeypatch):
     from systemml_amd.ops import augmented as AUG
     monkeypatch.setattr(AUG, "PAD_MIN_CELLS", 0)
+    monkeypatch.setattr(AUG, "VIEW_MIN_CELLS", 0)
     X, y = _data()
     args = dict(X="X", Y="Y", B="B", icpt=icpt, reg=0.01, tol=1e-8, moi=8, mii=6)
     src = open(SCRIPTS_DIR + "/algorithms/MultiLogReg.dml").read()
@@ -43,6 +44,7 @@ def test_multilogreg_intercept_on_padded_copy(icpt, monkeypatch):
 def test_linreg_cg_intercept_on_padded_copy(monkeypatch):
     from systemml_amd.ops import augmented as AUG
     monkeypatch.setattr(AUG, "PAD_MIN_CELLS", 0)
+    monkeypatch.setattr(AUG, "VIEW_MIN_CELLS", 0)
     g = torch.Generator().manual_seed(5)
     X = torch.rand(3000, 24, dtype=torch.float64, generator=g)
     y = X @ torch.rand(24, 1, dtype=torch.float64, generator=g) + 0.5
