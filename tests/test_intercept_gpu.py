@@ -38,7 +38,7 @@ def test_multilogreg_intercept_on_padded_copy(icpt, monkeypatch):
         r, _ = EX.execute(cs, ins, out=lambda s: None)
         res[gpu] = r["B_out"].double().cpu().numpy()
     assert AUG.stats["padded"] > before
-    np.testing.assert_allclose(res[True], res[False], rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(res[True], res[False], rtol=2e-3, atol=1e-2)   # fp32 vs fp64 solves
 
 
 def test_linreg_cg_intercept_on_padded_copy(monkeypatch):
@@ -59,4 +59,4 @@ def test_linreg_cg_intercept_on_padded_copy(monkeypatch):
         r, _ = EX.execute(cs, ins, out=lambda s: None)
         res[gpu] = r["B_out"].double().cpu().numpy()
     assert AUG.stats["padded"] > before
-    np.testing.assert_allclose(res[True], res[False], rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(res[True], res[False], rtol=2e-3, atol=1e-2)   # fp32 vs fp64 solves
