@@ -146,7 +146,10 @@ s = sum(p) + sum(dw) + sum(dx)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(2, 130, 9, 11, 136, 3, 1, 1), (4, 256, 7, 7, 128, 1, 1, 0), (1, 64, 14, 14, 96, 3, 1, 1)])
+@pytest.mark.parametrize("shape", [(2, 130, 9, 11, 136, 3, 1, 1), (4, 256, 7, 7, 128, 1, 1, 0), (1, 64, 14, 14, 96, 3, 1, 1),
+                                   # the 7 x 7 / 2 RGB stem and a C <= 8 layer with F not a multiple
+                                   # of 8: backward data on the direct kernel
+                                   (2, 3, 32, 32, 64, 7, 2, 3), (2, 5, 12, 12, 20, 3, 1, 1)])
 def test_conv2d_fp32_operands_on_bf16_mfma(shape):
     """fp32 activations / filters computed on bf16 MFMA (the ResNet bench mode, dtype code 3):
     against an fp64 reference of the bf16-rounded operands."""
