@@ -119,7 +119,7 @@ def _group(order, ncons, inline):
     for h in order:
         if not _cellwise(h):
             continue
-        ops, leaves = [], []
+        ops, leaves, took = [], [], []
         for ci, c in enumerate(_operands(h)):
             g = groups.get(c.id)
             if _is_bias(h) and ci == 1:
@@ -131,10 +131,19 @@ def _group(order, ncons, inline):
                     ops += extra
                     leaves = nl
                     absorbed[c.id] = absorbed.get(c.id, 0) + 1
+                    took.append(c.id)
                     continue
             leaves = _merge_leaves(leaves, [c])
         if len(leaves) > MAXIN:
-            continue
+            # a later operand overflowed the input limit: the absorbed operands stay
+            # materialised (their own plans) and h reads them
+            for cid in took:
+                absorbed[cid] -= 1
+                if not absorbed[cid]:
+                    del absorbed[cid]
+            ops, leaves = [], _merge_leaves([], _operands(h))
+            if len(leaves) > MAXIN:
+                continue
         ops.append(h)
         groups[h.id] = (ops, leaves)
     aggs = []                                         # (aggregate hop, fused DAG it absorbs)

@@ -30,9 +30,30 @@ _AGG = ("sum", "sumsq", "min", "max", "mean")
 _SCALAR_BIN_OK = set(BIN_CODES) - {"%%", "%/%"}
 
 
-def _big(h):
+_DNN = {"conv2d", "conv2d_backward_data", "conv2d_backward_filter", "max_pool", "avg_pool", "max_pool_backward",
+        "avg_pool_backward", "bias_add", "bias_multiply", "relu_backward"}
+
+
+def _big(h, act=frozenset()):
     d1, d2 = h.dim1, h.dim2
-    return (d1 > VMAX) or (d2 > VMAX) or (d1 >= 0 and d2 >= 0 and d1 * d2 > VMAX)
+    return (d1 > VMAX) or (d2 > VMAX) or (d1 >= 0 and d2 >= 0 and d1 * d2 > VMAX) or h.id in act
+
+
+def _activations(order):
+    """Ids of the block's DL activations / gradients: the values of DNN builtins and the
+    cellwise operators over them.  Their sizes are only known at run time, but they are never
+    single-workgroup vectors, so they stay with the Cell template (which fuses them with their
+    neighbours) instead of joining a vector program whose run-time guard would send them to
+    the one-region fallback."""
+    act = set()
+    for h in order:
+        if h.dt != "M":
+            continue
+        if h.op == "bi" and h.p.get("name") in _DNN:
+            act.add(h.id)
+        elif h.op in ("b", "u") and any(c.id in act and c.dt == "M" for c in h.inputs):
+            act.add(h.id)
+    return frozenset(act)
 
 
 def _stringy(h, memo):
@@ -54,7 +75,8 @@ def _stringy(h, memo):
 
 def _kind(h, smemo):
     """('m' | 's' | 'r', op) when h can join a vector program, else None."""
-    if h.dt not in ("M", "S") or _big(h):
+    act = smemo.get("__act", frozenset())
+    if h.dt not in ("M", "S") or _big(h, act):
         return None
     op = h.op
     if op == "b" and len(h.inputs) == 2:
@@ -70,9 +92,9 @@ def _kind(h, smemo):
             return None
         return ("m" if h.dt == "M" else "s", o)
     if op == "agg" and len(h.inputs) == 1 and h.p.get("dir") == "all" and h.p.get("o") in _AGG \
-            and h.inputs[0].dt == "M" and not _big(h.inputs[0]):
+            and h.inputs[0].dt == "M" and not _big(h.inputs[0], act):
         return ("r", h.p["o"])
-    if op == "tak" and len(h.inputs) in (2, 3) and all(c.dt == "M" and not _big(c) for c in h.inputs):
+    if op == "tak" and len(h.inputs) in (2, 3) and all(c.dt == "M" and not _big(c, act) for c in h.inputs):
         return ("r", "dot" if len(h.inputs) == 2 else "dot3")
     if op == "bi" and h.p.get("name") in ("ifelse", "_sel") and len(h.inputs) == 3 and not h.named:
         if any(c.dt not in ("M", "S") for c in h.inputs):
@@ -92,7 +114,7 @@ def fuse_vectors(bb):
     live = getattr(bb, "live_out", None)
     tops = list(bb.roots) + [h for k, h in bb.env_out.items() if live is None or k in live]
     order = H.walk(tops)
-    smemo = {}
+    smemo = {"__act": _activations(order)}
     kinds = {h.id: _kind(h, smemo) for h in order}
     # epochs
     ep = {}
