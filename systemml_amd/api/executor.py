@@ -45,13 +45,45 @@ class CompiledScript:
 _REC_LIMIT = 50000
 
 
+_STACK_BYTES = 1 << 29       # 512 MiB: room for _REC_LIMIT Python frames on CPython 3.10's C stack
+
+
+def _on_big_stack(fn):
+    """Run fn in a thread with a stack sized for the raised recursion limit (a deep DAG on the
+    8 MiB main-thread stack would overflow it -- a segfault, not a RecursionError)."""
+    import threading
+    box = {}
+
+    def run():
+        try:
+            box["r"] = fn()
+        except BaseException as e:     # re-raised in the caller
+            box["e"] = e
+    old = threading.stack_size()
+    threading.stack_size(_STACK_BYTES)
+    try:
+        t = threading.Thread(target=run, name="sysml-compile")
+        t.start()
+    finally:
+        threading.stack_size(old)
+    t.join()
+    if "e" in box:
+        raise box["e"]
+    return box["r"]
+
+
 def compile_script(source, args=None, inputs=(), outputs=(), config=None, pydml=False, filename="",
                    base_dir=None):
-    config = config or get_default_config()
-    # inlined layer libraries make one basic block of a whole training step (thousands of HOPs
-    # deep); the recursive DAG passes need more than Python's default 1000 frames
+    """Parse, translate and plan a DML / PyDML script (on a large-stack thread: inlined layer
+    libraries make one basic block of a whole training step, thousands of HOPs deep, and the
+    recursive DAG passes need more than Python's default 1000 frames)."""
     if sys.getrecursionlimit() < _REC_LIMIT:
         sys.setrecursionlimit(_REC_LIMIT)
+    return _on_big_stack(lambda: _compile_script(source, args, inputs, outputs, config, pydml, filename, base_dir))
+
+
+def _compile_script(source, args, inputs, outputs, config, pydml, filename, base_dir):
+    config = config or get_default_config()
     t0 = time.perf_counter()
     prog = parse(source, pydml=pydml, filename=filename)
     t1 = time.perf_counter()
