@@ -302,12 +302,31 @@ def fuse_cells(bb, single=False, stats=None):
             plans.append((h, g[0], g[1], None))
     n = 0
     built = []
+    planned = set()
     for root, ops, leaves, agg in plans:
         if not ops:
             built.append((root, ops, leaves, CellProgram((), 1, 0, agg)))
             continue
         ra = _regalloc(ops, leaves)
         if ra is None:
+            # more live values than registers: the DAG's operators become one-operator
+            # programs (on the GPU: generated kernels, not the unfused fallback)
+            if single:
+                for o in ops:
+                    if o.id in planned or (o is root and agg is None):
+                        continue
+                    planned.add(o.id)
+                    lv = _merge_leaves([], _operands(o))
+                    r1 = _regalloc([o], lv)
+                    if r1 is not None:
+                        built.append((o, [o], lv, CellProgram(r1[0], len(lv), r1[1], None)))
+                if agg is not None:
+                    built.append((root, [], [root.inputs[0]], CellProgram((), 1, 0, agg)))
+                elif root.id not in planned:
+                    lv = _merge_leaves([], _operands(root))
+                    r1 = _regalloc([root], lv)
+                    if r1 is not None:
+                        built.append((root, [root], lv, CellProgram(r1[0], len(lv), r1[1], None)))
             continue
         code, out = ra
         built.append((root, ops, leaves, CellProgram(code, len(leaves), out, agg)))
