@@ -693,6 +693,28 @@ __global__ void __launch_bounds__(256) col2im_gather(const TI* __restrict__ cols
   }
 }
 
+// im2col: cols[n][(c*KH + kh)*KW + kw][oh*Wo + ow] = X[n][c][oh*sh - ph + kh][ow*sw - pw + kw]
+// (0 outside the image); one thread per cols cell, consecutive threads along the output row
+// (coalesced writes, near-coalesced reads).  Feeds the batched-GEMM forward convolution.
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) im2col_kernel(const T* __restrict__ X, T* __restrict__ cols, int N, int C,
+                                                      int H, int W, int KH, int KW, int sh, int sw, int ph, int pw,
+                                                      int Ho, int Wo) {
+  const I P = (I)Ho * Wo, KK = (I)KH * KW;
+  const I total = (I)N * C * KK * P;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    const I r = i / P;                         // (n, c, kh, kw) row of cols
+    const I p = i - r * P;
+    const I nc = r / KK;
+    const int t = (int)(r - nc * KK), kh = t / KW, kw = t - kh * KW;
+    const int oh = (int)(p / Wo), ow = (int)(p - (I)oh * Wo);
+    const int ih = oh * sh - ph + kh, iw = ow * sw - pw + kw;
+    T v = T(0);
+    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = X[nc * (I)H * W + (I)ih * W + iw];
+    cols[i] = v;
+  }
+}
+
 inline dim3 bias_grid(int64_t rows_ch, int P) {
   int64_t gy = (P + 255) / 256;
   if (gy > 1024) gy = 1024;
@@ -932,6 +954,28 @@ int sysml_bias_op(int dtype, const void* X, const void* b, void* out, int64_t to
                        mult, relu);
   else
     return -1;
+  return (int)hipGetLastError();
+}
+
+// dtype 3: bf16, 1: fp32.  X: N x C*H*W -> cols: N x (C*KH*KW) x (Ho*Wo).
+int sysml_im2col(int dtype, const void* X, void* cols, int N, int C, int H, int W, int KH, int KW, int sh, int sw,
+                 int ph, int pw, void* stream) {
+  using namespace sysml_dnn;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int Ho = (H + 2 * ph - KH) / sh + 1, Wo = (W + 2 * pw - KW) / sw + 1;
+  if (Ho <= 0 || Wo <= 0 || N <= 0) return -1;
+  const int64_t total = (int64_t)N * C * KH * KW * Ho * Wo;
+  const bool small = total < (1LL << 31) && (int64_t)N * C * H * W < (1LL << 31);
+  const dim3 g(grid_for(total));
+  if (dtype == 3) {
+    if (small) hipLaunchKernelGGL((im2col_kernel<__bf16, int>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo);
+    else hipLaunchKernelGGL((im2col_kernel<__bf16, int64_t>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo);
+  } else if (dtype == 1) {
+    if (small) hipLaunchKernelGGL((im2col_kernel<float, int>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo);
+    else hipLaunchKernelGGL((im2col_kernel<float, int64_t>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo);
+  } else {
+    return -1;
+  }
   return (int)hipGetLastError();
 }
 

@@ -739,6 +739,7 @@ CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) in
 # 1x1 stride-1 convolutions of bf16 activations as batched library GEMMs (SYSML_CONV1X1_GEMM=0: the
 # implicit-GEMM kernel of dnn.hip)
 CONV1X1_GEMM = os.environ.get("SYSML_CONV1X1_GEMM", "1") != "0"
+IM2COL_MAX_HW = int(os.environ.get("SYSML_IM2COL_MAX_HW", "196"))   # forward k x k convolutions via im2col + GEMM up to this Ho*Wo
 COL2IM_MAX_HW = int(os.environ.get("SYSML_COL2IM_MAX_HW", "196"))   # stride-1 backward data via GEMM + col2im up to this H*W (measured: faster at 14 x 14 and 7 x 7, slower at 28 x 28 and 56 x 56)
 
 
@@ -789,6 +790,24 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
             bias_op(y, bb, relu=relu, out=y)
         _count(("conv2d", "conv2d_bwd_data")[mode])
         _count("conv1x1_gemm")
+        return y
+    if CONV1X1_GEMM and mode == 0 and KH * KW > 1 and Ho * Wo <= IM2COL_MAX_HW and C > 8 \
+            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+        # small-image convolutions: an im2col gather and one batched library GEMM per image
+        CKK, P = C * KH * KW, Ho * Wo
+        cols = torch.empty((N, CKK, P), dtype=torch.bfloat16, device=dev)
+        L.sysml_im2col.restype = ctypes.c_int
+        L.sysml_im2col.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 10 + \
+            [ctypes.c_void_p]
+        rc = L.sysml_im2col(3, X.data_ptr(), cols.data_ptr(), N, C, H, Wd, KH, KW, sh, sw, ph, pw, _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_im2col failed: {rc}")
+        y = torch.matmul(W.view(F, CKK), cols).view(shape)
+        if bias is not None or relu:
+            bb = bias if bias is not None else torch.zeros(F, device=dev)
+            bias_op(y, bb, relu=relu, out=y)
+        _count("conv2d")
+        _count("conv_im2col")
         return y
     if CONV1X1_GEMM and mode == 1 and (sh > 1 or sw > 1 or (KH > 1 and H * Wd <= COL2IM_MAX_HW)) \
             and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:

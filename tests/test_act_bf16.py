@@ -59,6 +59,8 @@ def test_conv_bf16_output(shape):
         assert Kn.counters.get("conv1x1_gemm", 0) >= 2
     if s > 1 and Kn.CONV1X1_GEMM:
         assert Kn.counters.get("conv_col2im", 0) >= 1          # backward data: GEMM + col2im
+    if K > 1 and Ho * Wo <= Kn.IM2COL_MAX_HW and C > 8 and Kn.CONV1X1_GEMM:
+        assert Kn.counters.get("conv_im2col", 0) >= 1          # forward: im2col + GEMM
     for name, a, r in (("fwd", got, ref_b), ("bwd_data", gx, ref_dx)):
         err = (a.double().cpu() - r).abs().max().item() / (r.abs().max().item() + 1e-30)
         assert err < 1e-2, (name, err)
