@@ -439,3 +439,67 @@ def test_reference_rewrite_rules(rule):
     a, _ = EX.execute(cs, {})
     b, _ = EX.execute(EX.compile_script(src, {}, outputs=["r"], config=DMLConfig(gpu=False, rewrites=False)), {})
     assert float(a["r"]) == pytest.approx(float(b["r"]), rel=1e-12)
+
+
+def test_functions_specialised_on_literal_arguments_and_inlined():
+    """A function called with the same literal everywhere is rebuilt with it as a constant
+    (its `if (mode == "train")` disappears and the body is one block), then inlined -- also
+    when it calls another small function (inlining runs to a fixpoint)."""
+    src = """
+    helper = function(matrix[double] A) return (matrix[double] B) {
+      B = A * 2
+    }
+    layer = function(matrix[double] X, string mode) return (matrix[double] out) {
+      if (mode == "train") {
+        Y = helper(X) + 1
+      } else {
+        Y = X
+      }
+      out = Y * 3
+    }
+    X = rand(rows=4, cols=3, seed=1)
+    O1 = layer(X, "train")
+    O2 = layer(X + 1, "train")
+    s = sum(O1) + sum(O2)
+    print(s)
+    """
+    cs = compile_script(src, {}, config=DMLConfig(gpu=False))
+    assert getattr(cs.cp, "specialised", 0) >= 1
+    rt = explain(cs.cp, "runtime")
+    main = rt[rt.find("MAIN PROGRAM"):]
+    assert "fcall" not in main, main
+    out = []
+    run(src, config=DMLConfig(gpu=False), out=out.append)
+    ref = []
+    run(src, config=DMLConfig(gpu=False, rewrites=False), out=ref.append)
+    assert abs(float(out[0]) - float(ref[0])) < 1e-9 * abs(float(ref[0]))
+
+
+def test_cell_group_overflowing_inputs_keeps_operands_fused():
+    """A cellwise chain whose last operand would push the fused DAG past the 8-input limit:
+    the operands already absorbed stay materialised as their own fused kernels (no operator
+    left to run unfused)."""
+    src = """
+    X = rand(rows=10, cols=6, seed=1)
+    a = rand(rows=10, cols=6, seed=2)
+    b = rand(rows=10, cols=6, seed=3)
+    c = rand(rows=10, cols=6, seed=4)
+    d = rand(rows=10, cols=6, seed=5)
+    e = rand(rows=10, cols=6, seed=6)
+    f = rand(rows=10, cols=6, seed=7)
+    g = rand(rows=10, cols=6, seed=8)
+    h = rand(rows=10, cols=6, seed=9)
+    T = ((((((X * a + b) * c - d) * e + f) * g) - h) > 0.5)
+    U = T * X
+    V = U + T
+    print(sum(V))
+    """
+    cs = compile_script(src, {}, config=DMLConfig(gpu=False))
+    rt = explain(cs.cp, "runtime")
+    main = rt[rt.find("MAIN PROGRAM"):]
+    plain = [ln.strip().split(" ")[0] for ln in main.splitlines() if ln.startswith("    ")]
+    assert not any(op in ("*", "+", "-", ">") for op in plain), plain
+    out, ref = [], []
+    run(src, config=DMLConfig(gpu=False), out=out.append)
+    run(src, config=DMLConfig(gpu=False, fusion=False), out=ref.append)
+    assert abs(float(out[0]) - float(ref[0])) < 1e-9 * max(1.0, abs(float(ref[0])))
