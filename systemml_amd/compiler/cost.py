@@ -602,7 +602,13 @@ def recompile_exec_types(bb, vars_, config):
     the shape signature; returns True when the plan changed."""
     names = getattr(bb, "_et_names", None)
     if names is None:
-        names = bb._et_names = tuple(sorted(bb.reads))
+        # scalar-typed reads carry no shape: leaving them out of the signature keeps the per-
+        # execution check to the block's matrices (it runs once per block execution)
+        dts = {}
+        for h in H.walk(list(bb.roots) + list(bb.env_out.values())):
+            if h.op == "tread":
+                dts.setdefault(h.p.get("name"), set()).add(h.dt)
+        names = bb._et_names = tuple(n for n in sorted(bb.reads) if dts.get(n) != {"S"})
     get = vars_.get
     sig = tuple(_shape_of(get(n)) for n in names)
     if getattr(bb, "_et_sig", None) == sig:
