@@ -693,6 +693,46 @@ __global__ void __launch_bounds__(256) col2im_gather(const TI* __restrict__ cols
   }
 }
 
+// Stride-2 col2im of bf16 with even W: one thread per input-column pair (iw = 2j, 2j + 1).  A tap
+// (kh, kw) lands on the stride grid for exactly one of the two columns (the one with
+// iw + pw - kw even), so each tap is one load instead of two half-masked ones, and the pair is
+// one 4-byte store -- half the threads and index divisions of the per-cell gather.
+struct __attribute__((aligned(4))) bf16x2 { __bf16 a, b; };
+
+__global__ void __launch_bounds__(256) col2im_s2_pair(const __bf16* __restrict__ cols, bf16x2* __restrict__ dx, int N,
+                                                      int C, int H, int W, int KH, int KW, int ph, int pw, int Ho,
+                                                      int Wo) {
+  const int W2 = W >> 1;
+  const int total = N * C * H * W2;
+  const int P = Ho * Wo;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int q = i / W2;
+    const int j = i - q * W2;
+    const int nc = q / H;
+    const int ih = q - nc * H;
+    const __bf16* cb = cols + (int64_t)nc * (KH * KW) * P;
+    float a0 = 0.f, a1 = 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int th = ih + ph - kh;
+      if (th < 0) break;
+      const int oh = th >> 1;
+      if ((th & 1) != 0 || oh >= Ho) continue;
+      const __bf16* row = cb + (kh * KW) * P + oh * Wo;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int e = (pw - kw) & 1;                  // the column of the pair this tap lands on
+        const int tw = 2 * j + e + pw - kw;
+        if (tw < 0) continue;
+        const int ow = tw >> 1;
+        if (ow >= Wo) continue;
+        const float v = (float)row[kw * P + ow];
+        if (e) a1 += v;
+        else a0 += v;
+      }
+    }
+    dx[i] = bf16x2{(__bf16)a0, (__bf16)a1};
+  }
+}
+
 // im2col: cols[n][(c*KH + kh)*KW + kw][oh*Wo + ow] = X[n][c][oh*sh - ph + kh][ow*sw - pw + kw]
 // (0 outside the image); one thread per cols cell, consecutive threads along the output row
 // (coalesced writes, near-coalesced reads).  Feeds the batched-GEMM forward convolution.
@@ -1002,7 +1042,10 @@ int sysml_col2im(int dtype, const void* cols, void* dx, int N, int C, int H, int
       hipLaunchKernelGGL((col2im_gather<TI, TO, int64_t, 0>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, \
                          W, KH, KW, sh, sw, ph, pw, Ho, Wo);                                                     \
   } while (0)
-  if (dtype == 3) SYSML_C2I(__bf16, __bf16);
+  if (dtype == 3 && small && s2 && W % 2 == 0)
+    hipLaunchKernelGGL(col2im_s2_pair, dim3(grid_for(total / 2)), dim3(256), 0, s, (const __bf16*)cols, (bf16x2*)dx, N,
+                       C, H, W, KH, KW, ph, pw, Ho, Wo);
+  else if (dtype == 3) SYSML_C2I(__bf16, __bf16);
   else if (dtype == 1) SYSML_C2I(float, float);
   else return -1;
 #undef SYSML_C2I

@@ -741,6 +741,8 @@ CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) in
 CONV1X1_GEMM = os.environ.get("SYSML_CONV1X1_GEMM", "1") != "0"
 IM2COL_MAX_HW = int(os.environ.get("SYSML_IM2COL_MAX_HW", "196"))   # forward k x k convolutions via im2col + GEMM up to this Ho*Wo
 COL2IM_MAX_HW = int(os.environ.get("SYSML_COL2IM_MAX_HW", "196"))   # stride-1 backward data via GEMM + col2im up to this H*W (measured: faster at 14 x 14 and 7 x 7, slower at 28 x 28 and 56 x 56)
+CONV_SPLIT_BLOCKS = int(os.environ.get("SYSML_CONV_SPLIT_BLOCKS", "2048"))   # split K until ~this many blocks
+CONV_SPLIT_MINK = int(os.environ.get("SYSML_CONV_SPLIT_MINK", "1536"))       # ... each reducing >= this many products (sweep: profiles/conv_split_sweep_r4.txt)
 
 
 def _conv_code(dt):
@@ -827,7 +829,7 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
         _count("conv_col2im")
         return y
     # GEMM view (M x Ncol, depth K); split K when the output tiles alone cannot fill the chip:
-    # ~2k blocks in flight, each reducing >= 512 products per output (slab traffic stays small)
+    # ~2k blocks in flight, each reducing >= CONV_SPLIT_MINK products per output (slab traffic stays small)
     M, Nc, K = {0: (F, N * Ho * Wo, C * KH * KW), 1: (C, N * H * Wd, F * KH * KW),
                 2: (F, C * KH * KW, N * Ho * Wo)}[mode]
     L.sysml_conv2d_tile_mode.restype = ctypes.c_int
@@ -835,8 +837,8 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
     te = L.sysml_conv2d_tile_mode(code, mode, M, Nc)   # the launcher's output tile edge
     tiles = ((M + te - 1) // te) * ((Nc + te - 1) // te)
     ksplit = 1
-    if tiles < 2048:
-        ksplit = max(1, min(256, 2048 // max(tiles, 1), K // 512))
+    if tiles < CONV_SPLIT_BLOCKS:
+        ksplit = max(1, min(256, CONV_SPLIT_BLOCKS // max(tiles, 1), K // CONV_SPLIT_MINK))
     bdt = odt
     if code == 0 and mode != 2 and ksplit == 1 and not (mode == 1 and C <= 8) and \
             0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:

@@ -33,7 +33,10 @@ def _bf(x):
 @pytest.mark.parametrize("shape", [(2, 100, 9, 11, 96, 3, 1, 1), (4, 64, 14, 14, 96, 3, 1, 1),
                                    (2, 100, 15, 15, 56, 3, 2, 1), (8, 32, 8, 8, 64, 1, 1, 0),
                                    (64, 64, 28, 28, 256, 1, 1, 0), (4, 64, 14, 14, 128, 1, 2, 0),
-                                   (3, 40, 13, 13, 24, 3, 2, 1)])
+                                   (3, 40, 13, 13, 24, 3, 2, 1),
+                                   # even widths: the stride-2 paired col2im
+                                   (2, 64, 16, 16, 32, 3, 2, 1), (2, 48, 14, 14, 40, 3, 2, 1),
+                                   (2, 32, 12, 12, 16, 3, 2, 0), (2, 3, 32, 32, 16, 7, 2, 3)])
 def test_conv_bf16_output(shape):
     from systemml_amd.ops import kernels as Kn
     N, C, H, Wd, F_, K, s, p = shape
