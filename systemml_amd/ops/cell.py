@@ -281,11 +281,12 @@ def _cases(vals):
     return expr
 
 
-def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant, idx32=False, outbf=False):
+def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant, idx32=False, outbf=False, ch4=False):
     """HIP source of the fused kernel: the program as straight-line code over the cell values
     of its inputs, instantiated into the flat / row / column kernel template.  idx32: the
     operand has < 2^31 cells (32-bit row / column arithmetic); outbf: the (unaggregated)
-    result is stored as bf16."""
+    result is stored as bf16; ch4: every per-channel operand's H*W and the column count are
+    multiples of 4 (a 4-cell group lies in one channel: one load instead of four)."""
     ct = "float" if T == torch.float32 else "double"
     var = [f"x[{k}]" for k in range(prog.n_in)] + [None] * (NR - prog.n_in)
     body = []
@@ -314,6 +315,7 @@ struct Spec {{
   static constexpr int NEED_IJ = {need_ij};
   static constexpr int IDX32 = {int(bool(idx32))};
   static constexpr int OUTBF = {int(bool(outbf))};
+  static constexpr int CH4 = {int(bool(ch4))};
   static constexpr int mode(int k) {{ return {_cases(modes)}; }}
   static constexpr int dt(int k) {{ return {_cases(dts)}; }}
   static constexpr int vec(int k) {{ return {_cases(vecs)}; }}
@@ -430,13 +432,13 @@ def compile_source(src, arch):
     return code
 
 
-def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, idx32=False, outbf=False):
-    key = (prog.key(), T, modes, dts, vecs, mode, variant, str(dev), idx32, outbf)
+def _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, idx32=False, outbf=False, ch4=False):
+    key = (prog.key(), T, modes, dts, vecs, mode, variant, str(dev), idx32, outbf, ch4)
     f = _rtc_funcs.get(key, False)
     if f is not False:
         return f
     try:
-        code = compile_source(generate(prog, T, modes, dts, vecs, mode, variant, idx32, outbf), gpu_arch(dev))
+        code = compile_source(generate(prog, T, modes, dts, vecs, mode, variant, idx32, outbf, ch4), gpu_arch(dev))
         L = _rtc_lib()
         fn = ctypes.c_void_p()
         cbuf = ctypes.create_string_buffer(code, len(code))
@@ -595,7 +597,8 @@ def _make_plan(prog, args):
         else:
             variant = 0
         outbf = mode == 0 and T == torch.float32 and 0 < backend.act_bf16_min_cells <= R * Cc
-        f = _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, R * Cc < 2 ** 31, outbf)
+        ch4 = bool(hws) and Cc % 4 == 0 and all(h % 4 == 0 for h in hws.values())
+        f = _rtc_func(prog, T, modes, dts, vecs, mode, variant, dev, R * Cc < 2 ** 31, outbf, ch4)
         if f is not None:
             pl.fn = f[0]
             if outbf:
@@ -762,6 +765,7 @@ struct Spec {{
   static constexpr int NOUT = {len(m.progs)};
   static constexpr int NEED_IJ = {need_ij};
   static constexpr int IDX32 = 0;
+  static constexpr int CH4 = 0;
   static constexpr int mode(int k) {{ return {_cases(modes)}; }}
   static constexpr int dt(int k) {{ return {_cases(dts)}; }}
   static constexpr int vec(int k) {{ return {_cases(vecs)}; }}
