@@ -378,7 +378,8 @@ def test_bias_ops_fuse_with_cellwise_chains():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(6, 10, 9), (32, 64, 3136), (3, 7, 1), (5, 3, 2), (7, 1, 1), (3, 5, 6)])
+@pytest.mark.parametrize("shape", [(6, 10, 9), (32, 64, 3136), (3, 7, 1), (5, 3, 2), (7, 1, 1), (3, 5, 6),
+                                   (2, 3, 8), (4, 6, 4), (3, 5, 12)])          # last three: one channel per 4-cell group
 def test_bias_ops_cell_kernel_gpu(shape):
     from systemml_amd.ops import kernels
     N, C, HW = shape
