@@ -418,6 +418,19 @@ __global__ void __launch_bounds__(256) conv_bwd_data_direct(Conv c, TA* __restri
   }
 }
 
+// n / d for 0 <= n < 2^31 by multiply-high and shift (d fixed per launch): the flat index
+// kernels below spend most of their instructions on 32-bit divisions otherwise
+struct FastDiv {
+  unsigned d, m, l;
+};
+inline FastDiv fastdiv(unsigned d) {
+  unsigned l = 0;
+  while ((1ull << l) < d) ++l;
+  const unsigned long long m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return FastDiv{d, (unsigned)m, l};
+}
+__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.l; }
+
 // ---- pooling ----------------------------------------------------------------------------
 struct Pool {
   const void* X;
@@ -425,6 +438,7 @@ struct Pool {
   void* out;
   int N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo;
   int avg;
+  FastDiv fWo, fHo, fBw, fBh;     // divisions of the 32-bit index kernels
 };
 
 // I: index type of the flat cell loops (int below 2^31 cells: 32-bit divisions instead of the
@@ -440,9 +454,15 @@ __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
   T* __restrict__ O = (T*)p.out;
   const I total = (I)p.N * p.C * p.Ho * p.Wo;
   for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
-    const I q = i / p.Wo;
+    I q, nc;
+    if constexpr (sizeof(I) == 4) {
+      q = (I)fdiv((unsigned)i, p.fWo);
+      nc = (I)fdiv((unsigned)q, p.fHo);
+    } else {
+      q = i / p.Wo;
+      nc = q / p.Ho;
+    }
     const int ow = (int)(i - q * p.Wo);
-    const I nc = q / p.Ho;
     const int oh = (int)(q - nc * p.Ho);
     const T* x = X + (int64_t)nc * p.H * p.W;
     const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
@@ -470,9 +490,15 @@ __global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__
   const T* __restrict__ X = (const T*)p.X;
   const I total = (I)p.N * p.C * p.Ho * p.Wo;
   for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
-    const I q = i / p.Wo;
+    I q, nc;
+    if constexpr (sizeof(I) == 4) {
+      q = (I)fdiv((unsigned)i, p.fWo);
+      nc = (I)fdiv((unsigned)q, p.fHo);
+    } else {
+      q = i / p.Wo;
+      nc = q / p.Ho;
+    }
     const int ow = (int)(i - q * p.Wo);
-    const I nc = q / p.Ho;
     const int oh = (int)(q - nc * p.Ho);
     const T* x = X + (int64_t)nc * p.H * p.W;
     const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
@@ -507,9 +533,15 @@ __global__ void __launch_bounds__(256) pool_bwd_band(Pool p, const uint8_t* __re
   const int Bh = (p.H + p.ph + p.sh - 1) / p.sh, Bw = (p.W + p.pw + p.sw - 1) / p.sw;
   const I total = (I)p.N * p.C * Bh * Bw;
   for (I t = (I)blockIdx.x * 256 + threadIdx.x; t < total; t += (I)gridDim.x * 256) {
-    const I q = t / Bw;
+    I q, nc;
+    if constexpr (sizeof(I) == 4) {
+      q = (I)fdiv((unsigned)t, p.fBw);
+      nc = (I)fdiv((unsigned)q, p.fBh);
+    } else {
+      q = t / Bw;
+      nc = q / Bh;
+    }
     const int bw = (int)(t - q * Bw);
-    const I nc = q / Bh;
     const int bh = (int)(q - nc * Bh);
     const T* d = D + (int64_t)nc * p.Ho * p.Wo;
     const uint8_t* ix = idx + (int64_t)nc * p.Ho * p.Wo;
@@ -665,27 +697,34 @@ __global__ void __launch_bounds__(256) bias_op_bf16(const uint2* __restrict__ X,
 template <typename TI, typename TO, typename I, int S2>
 __global__ void __launch_bounds__(256) col2im_gather(const TI* __restrict__ cols, TO* __restrict__ dx, int N, int C,
                                                       int H, int W, int KH, int KW, int sh, int sw, int ph, int pw,
-                                                      int Ho, int Wo) {
-  if (S2) { sh = 2; sw = 2; }                         // stride 2: shifts instead of divisions
+                                                      int Ho, int Wo, FastDiv fW, FastDiv fH) {
+  if (S2 == 1) { sh = 2; sw = 2; }                    // stride 2: shifts instead of divisions
+  if (S2 == 2) { sh = 1; sw = 1; }                    // stride 1: no divisions
   const I total = (I)N * C * H * W;
   const I P = (I)Ho * Wo;
   for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
-    const I q = i / W;
+    I q, nc;
+    if constexpr (sizeof(I) == 4) {
+      q = (I)fdiv((unsigned)i, fW);
+      nc = (I)fdiv((unsigned)q, fH);
+    } else {
+      q = i / W;
+      nc = q / H;
+    }
     const int iw = (int)(i - q * W);
-    const I nc = q / H;
     const int ih = (int)(q - nc * H);
     const TI* cb = cols + nc * (I)(KH * KW) * P;       // (n, c) block of KH*KW rows of P
     float acc = 0.f;
     for (int kh = 0; kh < KH; ++kh) {
       const int th = ih + ph - kh;
       if (th < 0) break;
-      const int oh = S2 ? (th >> 1) : th / sh;
-      if ((S2 ? (th & 1) != 0 : oh * sh != th) || oh >= Ho) continue;
+      const int oh = S2 == 1 ? (th >> 1) : th / sh;
+      if ((S2 == 1 ? (th & 1) != 0 : oh * sh != th) || oh >= Ho) continue;
       for (int kw = 0; kw < KW; ++kw) {
         const int tw = iw + pw - kw;
         if (tw < 0) break;
-        const int ow = S2 ? (tw >> 1) : tw / sw;
-        if ((S2 ? (tw & 1) != 0 : ow * sw != tw) || ow >= Wo) continue;
+        const int ow = S2 == 1 ? (tw >> 1) : tw / sw;
+        if ((S2 == 1 ? (tw & 1) != 0 : ow * sw != tw) || ow >= Wo) continue;
         acc += (float)cb[(I)(kh * KW + kw) * P + oh * Wo + ow];
       }
     }
@@ -739,15 +778,30 @@ __global__ void __launch_bounds__(256) col2im_s2_pair(const __bf16* __restrict__
 template <typename T, typename I>
 __global__ void __launch_bounds__(256) im2col_kernel(const T* __restrict__ X, T* __restrict__ cols, int N, int C,
                                                       int H, int W, int KH, int KW, int sh, int sw, int ph, int pw,
-                                                      int Ho, int Wo) {
+                                                      int Ho, int Wo, FastDiv fP, FastDiv fKK, FastDiv fKW,
+                                                      FastDiv fWo) {
   const I P = (I)Ho * Wo, KK = (I)KH * KW;
   const I total = (I)N * C * KK * P;
   for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
-    const I r = i / P;                         // (n, c, kh, kw) row of cols
-    const I p = i - r * P;
-    const I nc = r / KK;
-    const int t = (int)(r - nc * KK), kh = t / KW, kw = t - kh * KW;
-    const int oh = (int)(p / Wo), ow = (int)(p - (I)oh * Wo);
+    I r, nc, p;
+    int t, kh, kw, oh, ow;
+    if constexpr (sizeof(I) == 4) {
+      r = (I)fdiv((unsigned)i, fP);                  // (n, c, kh, kw) row of cols
+      p = i - r * P;
+      nc = (I)fdiv((unsigned)r, fKK);
+      t = (int)(r - nc * KK);
+      kh = (int)fdiv((unsigned)t, fKW);
+      oh = (int)fdiv((unsigned)p, fWo);
+    } else {
+      r = i / P;
+      p = i - r * P;
+      nc = r / KK;
+      t = (int)(r - nc * KK);
+      kh = t / KW;
+      oh = (int)(p / Wo);
+    }
+    kw = t - kh * KW;
+    ow = (int)(p - (I)oh * Wo);
     const int ih = oh * sh - ph + kh, iw = ow * sw - pw + kw;
     T v = T(0);
     if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = X[nc * (I)H * W + (I)ih * W + iw];
@@ -930,6 +984,10 @@ int sysml_pool2d_ws(int dtype, int backward, int avg, const void* X, const void*
   p.Ho = (H + 2 * ph - KH) / sh + 1;
   p.Wo = (W + 2 * pw - KW) / sw + 1;
   if (p.Ho <= 0 || p.Wo <= 0) return -1;
+  p.fWo = fastdiv(p.Wo);
+  p.fHo = fastdiv(p.Ho);
+  p.fBw = fastdiv((W + pw + sw - 1) / sw);
+  p.fBh = fastdiv((H + ph + sh - 1) / sh);
   if (KH * KW > 255) ws = nullptr;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bool small = (int64_t)N * C * H * W < (1LL << 31) && (int64_t)N * C * p.Ho * p.Wo < (1LL << 31);
@@ -1007,12 +1065,13 @@ int sysml_im2col(int dtype, const void* X, void* cols, int N, int C, int H, int 
   const int64_t total = (int64_t)N * C * KH * KW * Ho * Wo;
   const bool small = total < (1LL << 31) && (int64_t)N * C * H * W < (1LL << 31);
   const dim3 g(grid_for(total));
+  const FastDiv fP = fastdiv(Ho * Wo), fKK = fastdiv(KH * KW), fKW = fastdiv(KW), fWo = fastdiv(Wo);
   if (dtype == 3) {
-    if (small) hipLaunchKernelGGL((im2col_kernel<__bf16, int>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo);
-    else hipLaunchKernelGGL((im2col_kernel<__bf16, int64_t>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo);
+    if (small) hipLaunchKernelGGL((im2col_kernel<__bf16, int>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo);
+    else hipLaunchKernelGGL((im2col_kernel<__bf16, int64_t>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo);
   } else if (dtype == 1) {
-    if (small) hipLaunchKernelGGL((im2col_kernel<float, int>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo);
-    else hipLaunchKernelGGL((im2col_kernel<float, int64_t>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo);
+    if (small) hipLaunchKernelGGL((im2col_kernel<float, int>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo);
+    else hipLaunchKernelGGL((im2col_kernel<float, int64_t>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo);
   } else {
     return -1;
   }
@@ -1030,17 +1089,21 @@ int sysml_col2im(int dtype, const void* cols, void* dx, int N, int C, int H, int
   const bool small = total < (1LL << 31) && ncols < (1LL << 31);
   const dim3 g(grid_for(total));
   const bool s2 = sh == 2 && sw == 2;
+  const FastDiv fW = fastdiv(W), fH = fastdiv(H);
 #define SYSML_C2I(TI, TO)                                                                                        \
   do {                                                                                                           \
     if (small && s2)                                                                                             \
       hipLaunchKernelGGL((col2im_gather<TI, TO, int, 1>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, \
-                         KH, KW, sh, sw, ph, pw, Ho, Wo);                                                        \
+                         KH, KW, sh, sw, ph, pw, Ho, Wo, fW, fH);                                                        \
+    else if (small && sh == 1 && sw == 1)                                                                        \
+      hipLaunchKernelGGL((col2im_gather<TI, TO, int, 2>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, \
+                         KH, KW, sh, sw, ph, pw, Ho, Wo, fW, fH);                                                \
     else if (small)                                                                                              \
       hipLaunchKernelGGL((col2im_gather<TI, TO, int, 0>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, W, \
-                         KH, KW, sh, sw, ph, pw, Ho, Wo);                                                        \
+                         KH, KW, sh, sw, ph, pw, Ho, Wo, fW, fH);                                                        \
     else                                                                                                         \
       hipLaunchKernelGGL((col2im_gather<TI, TO, int64_t, 0>), g, dim3(256), 0, s, (const TI*)cols, (TO*)dx, N, C, H, \
-                         W, KH, KW, sh, sw, ph, pw, Ho, Wo);                                                     \
+                         W, KH, KW, sh, sw, ph, pw, Ho, Wo, fW, fH);                                                     \
   } while (0)
   if (dtype == 3 && small && s2 && W % 2 == 0)
     hipLaunchKernelGGL(col2im_s2_pair, dim3(grid_for(total / 2)), dim3(256), 0, s, (const __bf16*)cols, (bf16x2*)dx, N,
