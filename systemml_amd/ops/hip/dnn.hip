@@ -447,7 +447,10 @@ struct Pool {
 template <typename T> struct Acc { typedef T type; };
 template <> struct Acc<__bf16> { typedef float type; };
 
-template <typename T, typename I>
+// K > 0: K x K windows, fully unrolled with every tap loaded unconditionally (out-of-image taps
+// read cell 0 and are replaced by the neutral value) so all loads of a window are in flight at
+// once; K == 0: any window, taps outside the image skipped
+template <typename T, typename I, int K>
 __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
   typedef typename Acc<T>::type A;
   const T* __restrict__ X = (const T*)p.X;
@@ -467,13 +470,23 @@ __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
     const T* x = X + (int64_t)nc * p.H * p.W;
     const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
     A m = p.avg ? A(0) : A(-INFINITY);
-    for (int a = 0; a < p.KH; ++a) {
+    const int KH = K ? K : p.KH, KW = K ? K : p.KW;
+#pragma unroll
+    for (int a = 0; a < KH; ++a) {
       const int h = h0 + a;
-      if (h < 0 || h >= p.H) continue;
-      for (int b = 0; b < p.KW; ++b) {
+      if (!K && (h < 0 || h >= p.H)) continue;
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
         const int w = w0 + b;
-        if (w < 0 || w >= p.W) continue;
-        const A v = (A)x[h * p.W + w];
+        if (!K && (w < 0 || w >= p.W)) continue;
+        A v;
+        if (K) {
+          const bool ok = (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+          const A t = (A)x[ok ? h * p.W + w : 0];
+          v = ok ? t : (p.avg ? A(0) : A(-INFINITY));
+        } else {
+          v = (A)x[h * p.W + w];
+        }
         if (p.avg) m += v;
         else m = v > m ? v : m;
       }
@@ -484,7 +497,7 @@ __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
 
 // max pooling backward, pass 1: position (a * KW + b) of each window's first maximum (row-major
 // scan, as the forward pass), 255 for a window without a cell above -inf
-template <typename T, typename I>
+template <typename T, typename I, int K>
 __global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__ idx) {
   typedef typename Acc<T>::type A;
   const T* __restrict__ X = (const T*)p.X;
@@ -504,16 +517,26 @@ __global__ void __launch_bounds__(256) pool_argmax(Pool p, uint8_t* __restrict__
     const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
     A m = A(-INFINITY);
     int am = 255;
-    for (int a = 0; a < p.KH; ++a) {
+    const int KH = K ? K : p.KH, KW = K ? K : p.KW;
+#pragma unroll
+    for (int a = 0; a < KH; ++a) {
       const int h = h0 + a;
-      if (h < 0 || h >= p.H) continue;
-      for (int b = 0; b < p.KW; ++b) {
+      if (!K && (h < 0 || h >= p.H)) continue;
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
         const int w = w0 + b;
-        if (w < 0 || w >= p.W) continue;
-        const A v = (A)x[h * p.W + w];
+        if (!K && (w < 0 || w >= p.W)) continue;
+        A v;
+        if (K) {
+          const bool ok = (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+          const A t = (A)x[ok ? h * p.W + w : 0];
+          v = ok ? t : A(-INFINITY);
+        } else {
+          v = (A)x[h * p.W + w];
+        }
         if (v > m) {
           m = v;
-          am = a * p.KW + b;
+          am = a * KW + b;
         }
       }
     }
@@ -846,13 +869,16 @@ namespace sysml_dnn {
 template <typename T, typename I>
 void pool_launch(const Pool& p, int backward, uint8_t* ws, hipStream_t s) {
   const int64_t nin = (int64_t)p.N * p.C * p.H * p.W, nout = (int64_t)p.N * p.C * p.Ho * p.Wo;
+  const bool k3 = p.KH == 3 && p.KW == 3;
   if (!backward) {
-    hipLaunchKernelGGL((pool_fwd<T, I>), dim3(grid_for(nout)), dim3(256), 0, s, p);
+    if (k3) hipLaunchKernelGGL((pool_fwd<T, I, 3>), dim3(grid_for(nout)), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((pool_fwd<T, I, 0>), dim3(grid_for(nout)), dim3(256), 0, s, p);
     return;
   }
   if (ws && !p.avg) {
     const int64_t bands = (int64_t)p.N * p.C * ((p.H + p.ph + p.sh - 1) / p.sh) * ((p.W + p.pw + p.sw - 1) / p.sw);
-    hipLaunchKernelGGL((pool_argmax<T, I>), dim3(grid_for(nout)), dim3(256), 0, s, p, ws);
+    if (k3) hipLaunchKernelGGL((pool_argmax<T, I, 3>), dim3(grid_for(nout)), dim3(256), 0, s, p, ws);
+    else hipLaunchKernelGGL((pool_argmax<T, I, 0>), dim3(grid_for(nout)), dim3(256), 0, s, p, ws);
     hipLaunchKernelGGL((pool_bwd_band<T, I>), dim3(grid_for(bands)), dim3(256), 0, s, p, ws);
     return;
   }
