@@ -745,6 +745,29 @@ CONV_SPLIT_BLOCKS = int(os.environ.get("SYSML_CONV_SPLIT_BLOCKS", "2048"))   # s
 CONV_SPLIT_MINK = int(os.environ.get("SYSML_CONV_SPLIT_MINK", "1536"))       # ... each reducing >= this many products (sweep: profiles/conv_split_sweep_r4.txt)
 
 
+class _WeightCasts:
+    """bf16 copies of fp32 filters, keyed by tensor identity and version and dropped with the
+    tensor: a training step reads each filter twice (forward, backward data) but casts it once."""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, t, dev, dt):
+        import weakref
+        k = id(t)
+        e = self._d.get(k)
+        if e is not None and e[0]() is t and e[1] == t._version and e[2].device == dev and e[2].dtype == dt:
+            return e[2]
+        c = t.to(device=dev, dtype=dt).contiguous()
+        dd = self._d
+        ref = weakref.ref(t, lambda _r, k=k: dd.pop(k, None) if dd.get(k, (None,))[0] is _r else None)
+        dd[k] = (ref, t._version, c)
+        return c
+
+
+_wcast = _WeightCasts()
+
+
 def _conv_code(dt):
     if dt == torch.bfloat16:
         return 0
@@ -770,7 +793,8 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
 
     def prep(t):
         return None if t is None else t.to(device=dev, dtype=dt).contiguous()
-    X, W, D = prep(X), prep(W), prep(D)
+    X, D = prep(X), prep(D)
+    W = _wcast.get(W, dev, dt) if W is not None and W.dtype != dt and dt == torch.bfloat16 else prep(W)
     Ho = (H + 2 * ph - KH) // sh + 1
     Wo = (Wd + 2 * pw - KW) // sw + 1
     if mode == 0:
