@@ -495,6 +495,27 @@ __global__ void __launch_bounds__(256) pool_fwd(Pool p) {
   }
 }
 
+// average pooling over the whole image (global pooling, Ho = Wo = 1): one wave per (n, c)
+// plane, lanes strided along the plane (coalesced), a wave reduction and one store -- the
+// per-output kernel above would read each plane with one lane
+template <typename T>
+__global__ void __launch_bounds__(256) pool_global_avg(Pool p) {
+  typedef typename Acc<T>::type A;
+  const T* __restrict__ X = (const T*)p.X;
+  T* __restrict__ O = (T*)p.out;
+  const int64_t planes = (int64_t)p.N * p.C;
+  const int HW = p.H * p.W;
+  const int lane = threadIdx.x & 63;
+  for (int64_t nc = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); nc < planes; nc += (int64_t)gridDim.x * 4) {
+    const T* x = X + nc * HW;
+    A acc = A(0);
+    for (int k = lane; k < HW; k += 64) acc += (A)x[k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) O[nc] = (T)(acc / A(HW));
+  }
+}
+
 // max pooling backward, pass 1: position (a * KW + b) of each window's first maximum (row-major
 // scan, as the forward pass), 255 for a window without a cell above -inf
 template <typename T, typename I, int K>
@@ -871,6 +892,11 @@ void pool_launch(const Pool& p, int backward, uint8_t* ws, hipStream_t s) {
   const int64_t nin = (int64_t)p.N * p.C * p.H * p.W, nout = (int64_t)p.N * p.C * p.Ho * p.Wo;
   const bool k3 = p.KH == 3 && p.KW == 3;
   if (!backward) {
+    if (p.avg && p.KH == p.H && p.KW == p.W && p.ph == 0 && p.pw == 0 && p.Ho == 1 && p.Wo == 1) {
+      const int64_t planes = (int64_t)p.N * p.C;
+      hipLaunchKernelGGL((pool_global_avg<T>), dim3(grid_for(planes * 64)), dim3(256), 0, s, p);
+      return;
+    }
     if (k3) hipLaunchKernelGGL((pool_fwd<T, I, 3>), dim3(grid_for(nout)), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((pool_fwd<T, I, 0>), dim3(grid_for(nout)), dim3(256), 0, s, p);
     return;

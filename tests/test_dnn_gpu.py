@@ -75,7 +75,8 @@ def test_conv2d_bias_relu_epilogue():
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
-@pytest.mark.parametrize("cfg", [(2, 3, 8, 8, 2, 2, 0), (3, 4, 9, 7, 3, 2, 1), (1, 2, 6, 6, 3, 1, 1)])
+@pytest.mark.parametrize("cfg", [(2, 3, 8, 8, 2, 2, 0), (3, 4, 9, 7, 3, 2, 1), (1, 2, 6, 6, 3, 1, 1),
+                                 (5, 9, 7, 7, 7, 1, 0), (2, 3, 11, 11, 11, 2, 0)])    # last two: global windows
 def test_pooling_kernels(cfg, dt):
     from systemml_amd.ops import kernels as Kn
     N, C, H, W, k, s, p = cfg
