@@ -612,6 +612,71 @@ __global__ void __launch_bounds__(256) pool_bwd_band(Pool p, const uint8_t* __re
   }
 }
 
+// 3 x 3 / stride-2 bands (the ResNet stem pooling): a band's four cells share the windows
+// oh in {bh - 1, bh} x ow in {bw - 1, bw}; their positions and dout are loaded once per band
+// (4 + 4 loads instead of 9 + 9 per-cell re-reads) and each cell takes the windows whose
+// argmax it is (row rh = 2 (bh - oh) + dh < 3, column likewise)
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) pool_bwd_band_k3s2(Pool p, const uint8_t* __restrict__ idx) {
+  typedef typename Acc<T>::type A;
+  const T* __restrict__ D = (const T*)p.D;
+  T* __restrict__ O = (T*)p.out;
+  const int Bh = (p.H + p.ph + 1) / 2, Bw = (p.W + p.pw + 1) / 2;
+  const I total = (I)p.N * p.C * Bh * Bw;
+  for (I t = (I)blockIdx.x * 256 + threadIdx.x; t < total; t += (I)gridDim.x * 256) {
+    I q, nc;
+    if constexpr (sizeof(I) == 4) {
+      q = (I)fdiv((unsigned)t, p.fBw);
+      nc = (I)fdiv((unsigned)q, p.fBh);
+    } else {
+      q = t / Bw;
+      nc = q / Bh;
+    }
+    const int bw = (int)(t - q * Bw);
+    const int bh = (int)(q - nc * Bh);
+    const T* d = D + (int64_t)nc * p.Ho * p.Wo;
+    const uint8_t* ix = idx + (int64_t)nc * p.Ho * p.Wo;
+    T* o = O + (int64_t)nc * p.H * p.W;
+    int wi[2][2];
+    A wd[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = bh - 1 + a, ow = bw - 1 + b;
+        const bool ok = (unsigned)oh < (unsigned)p.Ho && (unsigned)ow < (unsigned)p.Wo;
+        const int off = ok ? oh * p.Wo + ow : 0;
+        const int iv = (int)ix[off];
+        const A dv = (A)d[off];
+        wi[a][b] = ok ? iv : 255;
+        wd[a][b] = ok ? dv : A(0);
+      }
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const int h = bh * 2 + dh - p.ph;
+      if (h < 0 || h >= p.H) continue;
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int w = bw * 2 + dw - p.pw;
+        if (w < 0 || w >= p.W) continue;
+        A g = 0;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int rh = 2 * (1 - a) + dh;                  // row of (h, w) in window (bh - 1 + a, .)
+          if (rh > 2) continue;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int rw = 2 * (1 - b) + dw;
+            if (rw > 2) continue;
+            if (wi[a][b] == rh * 3 + rw) g += wd[a][b];
+          }
+        }
+        o[h * p.W + w] = (T)g;
+      }
+    }
+  }
+}
+
 // dX[n,c,h,w] = sum over windows containing (h,w) of dout / (KH*KW) (avg) or of dout where
 // (h,w) is the window's first maximum (max: from pass 1's positions, or recomputed per window
 // when no position buffer is given) -- a gather, no atomics
@@ -905,7 +970,10 @@ void pool_launch(const Pool& p, int backward, uint8_t* ws, hipStream_t s) {
     const int64_t bands = (int64_t)p.N * p.C * ((p.H + p.ph + p.sh - 1) / p.sh) * ((p.W + p.pw + p.sw - 1) / p.sw);
     if (k3) hipLaunchKernelGGL((pool_argmax<T, I, 3>), dim3(grid_for(nout)), dim3(256), 0, s, p, ws);
     else hipLaunchKernelGGL((pool_argmax<T, I, 0>), dim3(grid_for(nout)), dim3(256), 0, s, p, ws);
-    hipLaunchKernelGGL((pool_bwd_band<T, I>), dim3(grid_for(bands)), dim3(256), 0, s, p, ws);
+    if (k3 && p.sh == 2 && p.sw == 2)
+      hipLaunchKernelGGL((pool_bwd_band_k3s2<T, I>), dim3(grid_for(bands)), dim3(256), 0, s, p, ws);
+    else
+      hipLaunchKernelGGL((pool_bwd_band<T, I>), dim3(grid_for(bands)), dim3(256), 0, s, p, ws);
     return;
   }
   hipLaunchKernelGGL((pool_bwd<T, I>), dim3(grid_for(nin)), dim3(256), 0, s, p, nullptr);
