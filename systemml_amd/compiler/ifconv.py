@@ -19,6 +19,14 @@ so the converted block is guarded: `if (_vguard(state vars)) {converted} else {o
 blocks}`.  The guard holds on a GPU backend when every matrix the branches assign currently
 holds at most VMAX cells (ops/vprog.py); CPU runs and big matrices take the original
 control flow.  SYSML_IFCONV=0 disables the rewrite, =force makes the guard always true.
+
+Evaluating the branch not taken can fail where the original program does not: a shape
+mismatch valid only under the predicate (`if (nrow(A) == nrow(B)) {C = A + B}`), or a read of
+a variable defined on one path only.  The converted block is pure (branches are cheap
+expressions; neighbours with prints, writes, calls or random draws are not merged) and a
+basic block assigns its variables only once all its instructions succeeded, so the runtime
+answers any error of the converted block by running the original blocks instead
+(runtime/program.py): the error, if any, is then the original program's.
 """
 from __future__ import annotations
 
@@ -94,6 +102,15 @@ class _Seq:
         bb.writes = set(self.env)
         bb.pos = self.pos
         return bb
+
+
+def _pure(bb):
+    """No side effects and no random draws: a neighbour merged into a converted block may be
+    executed twice (the converted block, then the original blocks when it raises)."""
+    for h in H.walk(list(bb.roots) + list(bb.env_out.values())):
+        if h.op in ("sink", "fcall") or (h.op == "bi" and h.p.get("name") in (H.SIDE_EFFECT | H.NONDETERMINISTIC)):
+            return False
+    return True
 
 
 def _tail_live(blocks):
@@ -198,13 +215,14 @@ def _scan(blocks, stats):
                 orig = [b]
                 seq = _Seq()
                 prev = res[-1] if res and isinstance(res[-1], BasicBlock) and not getattr(res[-1], "licm_pre", False) \
-                    else None
+                    and _pure(res[-1]) else None
                 if prev is not None:
                     res.pop()
                     orig.insert(0, prev)
                     seq.add_block(prev)
                 seq.add_block(conv)
-                nxt = blocks[k + 1] if k + 1 < len(blocks) and isinstance(blocks[k + 1], BasicBlock) else None
+                nxt = blocks[k + 1] if k + 1 < len(blocks) and isinstance(blocks[k + 1], BasicBlock) \
+                    and _pure(blocks[k + 1]) else None
                 if nxt is not None:
                     orig.append(nxt)
                     seq.add_block(nxt)

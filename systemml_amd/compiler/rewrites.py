@@ -102,6 +102,26 @@ def _vec_kind(h):
     return None
 
 
+def _dims(h):
+    """(rows, cols) when both are known at compile time, else None."""
+    if h.dt == "M" and h.dim1 is not None and h.dim2 is not None and h.dim1 >= 0 and h.dim2 >= 0:
+        return h.dim1, h.dim2
+    return None
+
+
+def _is_diag(h):
+    return h.op == "bi" and h.p.get("name") == "diag" and len(h.inputs) == 1 and not h.named
+
+
+def _col_vector(h):
+    """h is an n x 1 matrix with n > 1 (diag(h) builds a diagonal matrix): by construction or
+    by known dimensions."""
+    if _vec_kind(h) == "col":
+        return True
+    d = _dims(h)
+    return d is not None and d[1] == 1 and d[0] > 1
+
+
 def _empty(h):
     """(rows, cols) hops of an all-zero datagen matrix(0, rows, cols) (nnz == 0 by
     construction), else None."""
@@ -330,6 +350,15 @@ class Rewriter:
             # simplifyMultiBinaryToBinaryOperation: X * X -> X ^ 2 (one operand read)
             if o == "*" and a is b and a.dt == "M":
                 return self._hit("square", Hop("b", [a, lit(2)], {"o": "^"}, dt="M", pos=h.pos))
+            # pushdownBinaryOperationOnDiag (Dynamic.java:1068): diag(v) * s -> diag(v * s) for a
+            # column vector v and a scalar s (n cells scaled instead of n x n)
+            if o == "*":
+                for d_, s_ in ((a, b), (b, a)):
+                    if _is_diag(d_) and s_.dt == "S" and _col_vector(d_.inputs[0]):
+                        v = d_.inputs[0]
+                        vs = Hop("b", [v, s_], {"o": "*"}, dt="M", dim1=v.dim1, dim2=1, pos=h.pos)
+                        return self._hit("diag-binary-pushdown", Hop("bi", [vs], dict(d_.p), dt="M", dim1=d_.dim1,
+                                                                     dim2=d_.dim2, pos=h.pos))
             # literal chains: (X + c1) + c2 -> X + (c1 + c2), (X * c1) * c2 -> X * (c1 * c2)
             if o in ("+", "*") and _num_lit(b) and a.op == "b" and a.p["o"] == o and a.dt == "M" \
                     and _num_lit(a.inputs[1]):
@@ -349,6 +378,16 @@ class Rewriter:
             return h
         if op == "bi":
             name = h.p.get("name")
+            # simplifyDiagMatrixMult (Dynamic.java:1012): diag(X %*% Y) -> rowSums(X * t(Y)) when
+            # X %*% Y is square (its diagonal without the n x n product)
+            if name == "diag" and len(h.inputs) == 1 and h.inputs[0].op == "mm" and not h.inputs[0].p.get("transA"):
+                X, Y = h.inputs[0].inputs
+                dx, dy = _dims(X), _dims(Y)
+                if dx is not None and dy is not None and dx[0] == dy[1] and dx[0] > 1:
+                    prod = Hop("b", [X, Hop("t", [Y], dt="M", dim1=dy[1], dim2=dy[0], pos=h.pos)], {"o": "*"}, dt="M",
+                               dim1=dx[0], dim2=dx[1], pos=h.pos)
+                    return self._hit("diag-matrix-mult", Hop("agg", [prod], {"o": "sum", "dir": "row"}, dt="M",
+                                                             dim1=dx[0], dim2=1, pos=h.pos))
             # removeUnnecessaryReorgOperation: rev(rev(X)) -> X
             if name == "rev" and len(h.inputs) == 1 and h.inputs[0].op == "bi" \
                     and h.inputs[0].p.get("name") == "rev" and len(h.inputs[0].inputs) == 1:
@@ -585,6 +624,20 @@ class Rewriter:
     def _rw_mm(self, h):
         a, b = h.inputs
         transA = h.p.get("transA", False)
+        if not transA:
+            # simplifyScalarMatrixMult (Dynamic.java:922): y %*% X -> as.scalar(y) * X and
+            # X %*% y -> X * as.scalar(y) for a 1 x 1 y
+            for y, X in ((a, b), (b, a)):
+                if _dims(y) == (1, 1) and X.dt == "M" and _dims(X) != (1, 1):
+                    sc = Hop("u", [y], {"o": "cast_scalar"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                    return self._hit("scalar-matrix-mult", Hop("b", [X, sc], {"o": "*"}, dt="M", dim1=X.dim1,
+                                                               dim2=X.dim2, pos=h.pos))
+            # simplifyMatrixMultDiag (Dynamic.java:960): diag(v) %*% Y -> v * Y for a column
+            # vector v (a row scaling instead of an n x n diagonal matrix and a product)
+            if _is_diag(a) and _col_vector(a.inputs[0]) and b.dt == "M":
+                v = a.inputs[0]
+                return self._hit("matrix-mult-diag", Hop("b", [b, v], {"o": "*"}, dt="M", dim1=b.dim1, dim2=b.dim2,
+                                                         pos=h.pos))
         # (-A) %*% B -> -(A %*% B): keeps t(X) visible to the transpose / fusion rules
         if a.op == "u" and a.p["o"] == "neg" and a.dt == "M":
             self._count("neg-pushdown")

@@ -832,24 +832,30 @@ def generate_train_dml(layers, input_shape, solver, epochs, batch_size, seed=-1,
         lines += ["  }", '  print("Epoch " + e + ": loss " + loss)', "}"]
         return "\n".join(lines), state_vars(gen.layers)
     if spmd:
-        # synchronous data parallelism over SPMD ranks (one per GPU): every step takes W
-        # consecutive mini-batches, rank r computes the gradients of mini-batch r on its GPU,
-        # one bucketed all-reduce (_dp_allreduce: RCCL over xGMI) averages them (and the loss)
-        # and every rank applies the same update -- the reference's allreduce algorithms
-        # (Caffe2DML.scala:396-405) without the parfor's per-task gradient matrices
+        # synchronous data parallelism over SPMD ranks (one per GPU), with the parfor form's
+        # semantics (below): a step takes the same group of rows (bs for allreduce, P * bs for
+        # allreduce_parallel_batches), split into W contiguous shares; rank r computes the
+        # gradients of its share, weights them (and its loss and batch-norm statistics) by its
+        # share of the group's rows, and one bucketed all-reduce (_dp_allreduce: RCCL over
+        # xGMI) sums them -- every rank then applies the same update (Caffe2DML.scala:396-405
+        # without the parfor's per-task gradient matrices).  A rank with an empty share of a
+        # short last group still joins the collective, with weight 0.
         grads = [gen.grad_of(t) for t in params]
-        bs_local = 1 if train_algo == "allreduce" else None
-        lines += ["W = _dp_world()", "r = _dp_rank()"]
-        if bs_local is not None:
-            lines.append("bs = 1")
-        lines += ["gsz = W * bs", "groups = as.integer(ceil(N / gsz))", "for (e in 1:epochs) {",
-                  "  for (g in 1:groups) {", "    beg = ((g - 1) * gsz + r * bs) %% N + 1",
-                  "    end = min(N, beg + bs - 1)", "    Xb = X[beg:end, ]", "    Yb = Y[beg:end, ]"]
+        P = int(parallel_batches) if train_algo == "allreduce_parallel_batches" else 1
+        lines += ["W = _dp_world()", "r = _dp_rank()", f"gsz = {P} * bs", "groups = as.integer(ceil(N / gsz))",
+                  "for (e in 1:epochs) {", "  for (g in 1:groups) {",
+                  "    gb = ((g - 1) * gsz) %% N + 1", "    ge = min(N, gb + gsz - 1)", "    ng = ge - gb + 1",
+                  "    share = as.integer(ceil(ng / W))", "    lo = gb + r * share",
+                  "    hi = min(ge, lo + share - 1)", "    wt = max(0, hi - lo + 1) / ng",
+                  "    lo = min(lo, ge)", "    hi = max(hi, lo)",
+                  "    Xb = X[lo:hi, ]", "    Yb = Y[lo:hi, ]"]
         lines += ["    " + c for c in fwd]
         lines.append(f"    loss = {gen.loss_expr()}")
         lines += ["    " + c for c in bwd]
-        lines.append("    Lm = matrix(loss, rows = 1, cols = 1)")
-        lines.append("    [" + ", ".join(grads + ["Lm"]) + "] = _dp_allreduce(" + ", ".join(grads + ["Lm"]) + ")")
+        red = grads + [b for _, b in bn]
+        lines += [f"    {v} = wt * {v}" for v in red]
+        lines.append("    Lm = matrix(wt * loss, rows = 1, cols = 1)")
+        lines.append("    [" + ", ".join(red + ["Lm"]) + "] = _dp_allreduce(" + ", ".join(red + ["Lm"]) + ")")
         lines.append("    loss = as.scalar(Lm)")
         lines += [f"    {a} = {b}" for a, b in bn]
         lines += _opt_update(sc, gen, params, "    ")

@@ -40,6 +40,27 @@ class Backend:
     def set_thread_device(self, d):
         _TLS.device = d
 
+    # run-ahead loop state of the executing thread (runtime/program.py _exec_while_runahead):
+    # `defer` -- vector programs return their scalars as device-resident values instead of
+    # reading them back; `live` -- device address of the fp64 flag (the previous iteration's
+    # loop predicate) that the streaming kernels of a speculatively queued iteration read
+    # first: 0.0 means the iteration is dead and they return at once (0 = no flag)
+    @property
+    def defer(self):
+        return getattr(_TLS, "defer", False)
+
+    @property
+    def live(self):
+        return getattr(_TLS, "live", 0)
+
+    def set_runahead(self, defer, live=0):
+        _TLS.defer = defer
+        if live != getattr(_TLS, "live", 0):
+            _TLS.live = live
+            if self.use_kernels:
+                from . import kernels
+                kernels.load(required=True).sysml_set_live(live or None)
+
     @property
     def on_gpu(self):
         return self._device.type == "cuda"

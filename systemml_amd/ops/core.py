@@ -242,7 +242,9 @@ def _dev_binary(op, a, b):
             xt = x if da else torch.full_like(y, x)
             yt = y if db else torch.full_like(x, y)
             r = torch.minimum(xt, yt) if op == "min" else torch.maximum(xt, yt)
-        return DevScalar(r)
+        # INT op INT stays INT except for '/' and '^' (runtime/scalars.binary)
+        ints = op not in ("/", "^") and (a.vt == "i" if da else type(a) is int) and (b.vt == "i" if db else type(b) is int)
+        return DevScalar(r, "i" if ints else "d")
     if op in _DEV_CMP:
         r = _DEV_CMP[op](x, y) if da else _DEV_CMP[op](torch.full_like(y, x), y)
         return DevScalar(r.to(torch.float64), "b")
@@ -270,8 +272,9 @@ _DEV_UN = {"neg": torch.neg, "abs": torch.abs, "exp": torch.exp, "log": torch.lo
 
 def _dev_unary(op, x):
     f = _DEV_UN.get(op)
-    if f is not None and x.vt == "d":
-        return DevScalar(f(x.t))
+    if f is not None and x.vt != "b":
+        return DevScalar(f(x.t), "i" if (x.vt == "i" and op in ("neg", "abs", "sign", "floor", "ceil", "round"))
+                         else "d")
     if op == "not":
         return DevScalar((x.t == 0).to(torch.float64), "b")
     if op in ("ident", "cast_scalar"):

@@ -27,6 +27,13 @@
 #include <stdint.h>
 #include <unordered_set>
 
+// Run-ahead loops (runtime/program.py _exec_while_runahead): the device address of the fp64
+// flag a speculatively queued iteration's streaming kernels read first (0.0 = dead iteration:
+// return at once).  Set per host thread by the executor, read by every launch below.
+static thread_local const double* g_live_flag = nullptr;
+const double* sysml_live_flag() { return g_live_flag; }
+extern "C" void sysml_set_live(const void* p) { g_live_flag = static_cast<const double*>(p); }
+
 namespace sysml_c4 {
 
 enum Mode { XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5, XTSMG = 10, XTSMGO = 11 };   // = rowstream.hip
@@ -179,7 +186,8 @@ template <typename T, int K, int J, int MODE>
 __global__ void __launch_bounds__(BLOCK, 2)
 chain4_kernel(const T* __restrict__ X, int64_t N, int D, const float* __restrict__ V, int ldv,
               const float* __restrict__ S, int lds, int sbc, float* __restrict__ out,
-              float* __restrict__ U, int ldu, int64_t rows_per_block) {
+              float* __restrict__ U, int ldu, int64_t rows_per_block, const double* __restrict__ live) {
+  if (live != nullptr && *live == 0.0) return;    // dead run-ahead iteration (runtime/program.py)
   constexpr int C = J * 8;
   constexpr int K2 = (K + 1) / 2;
   constexpr int NV = G * K;
@@ -450,7 +458,9 @@ template <int J, int MODE, int VAR>
 __global__ void __launch_bounds__(BLOCK, 2)
 chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __restrict__ V, int ldv,
                const float* __restrict__ S, int lds, int sbc, float* __restrict__ out,
-               float* __restrict__ U, int ldu, int64_t rows_per_block, double* __restrict__ obj) {
+               float* __restrict__ U, int ldu, int64_t rows_per_block, double* __restrict__ obj,
+               const double* __restrict__ live) {
+  if (live != nullptr && *live == 0.0) return;    // dead run-ahead iteration (runtime/program.py)
   constexpr int K = 4;
   constexpr int NS = J * 8;                       // 64-column steps per row
   constexpr int XB = J * 1024;
@@ -741,7 +751,7 @@ static int launch(bool occ, const void* X, int64_t N, int D, const float* V, int
     return nb;
   }
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(BLOCK), sh, st, (const T*)X, N, D, V, ldv, S, lds, sbc, out, U, ldu,
-                     rpb);
+                     rpb, sysml_live_flag());
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -782,7 +792,7 @@ static int launch_m(int var, bool occ, const void* X, int64_t N, int D, const fl
     return nb;
   }
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(BLOCK), sh, st, (const uint16_t*)X, N, D, V, ldv, S, lds, sbc, out, U,
-                     ldu, rpb, obj);
+                     ldu, rpb, obj, sysml_live_flag());
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

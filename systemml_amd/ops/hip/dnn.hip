@@ -884,12 +884,14 @@ __global__ void __launch_bounds__(256) col2im_s2_pair(const __bf16* __restrict__
 // im2col: cols[n][(c*KH + kh)*KW + kw][oh*Wo + ow] = X[n][c][oh*sh - ph + kh][ow*sw - pw + kw]
 // (0 outside the image); one thread per cols cell, consecutive threads along the output row
 // (coalesced writes, near-coalesced reads).  Feeds the batched-GEMM forward convolution.
+// Rows are Pp >= P cells apart (pixels P .. Pp-1 zero): the image-blocked GEMM of gemm.hip
+// reads 8-pixel pieces, so small images are padded to a multiple of 8 here, in the one write.
 template <typename T, typename I>
 __global__ void __launch_bounds__(256) im2col_kernel(const T* __restrict__ X, T* __restrict__ cols, int N, int C,
                                                       int H, int W, int KH, int KW, int sh, int sw, int ph, int pw,
                                                       int Ho, int Wo, FastDiv fP, FastDiv fKK, FastDiv fKW,
-                                                      FastDiv fWo) {
-  const I P = (I)Ho * Wo, KK = (I)KH * KW;
+                                                      FastDiv fWo, int Pp) {
+  const I P = Pp, KK = (I)KH * KW;
   const I total = (I)N * C * KK * P;
   for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
     I r, nc, p;
@@ -913,7 +915,7 @@ __global__ void __launch_bounds__(256) im2col_kernel(const T* __restrict__ X, T*
     ow = (int)(p - (I)oh * Wo);
     const int ih = oh * sh - ph + kh, iw = ow * sw - pw + kw;
     T v = T(0);
-    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = X[nc * (I)H * W + (I)ih * W + iw];
+    if (oh < Ho && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = X[nc * (I)H * W + (I)ih * W + iw];
     cols[i] = v;
   }
 }
@@ -1175,27 +1177,33 @@ int sysml_bias_op(int dtype, const void* X, const void* b, void* out, int64_t to
   return (int)hipGetLastError();
 }
 
-// dtype 3: bf16, 1: fp32.  X: N x C*H*W -> cols: N x (C*KH*KW) x (Ho*Wo).
-int sysml_im2col(int dtype, const void* X, void* cols, int N, int C, int H, int W, int KH, int KW, int sh, int sw,
-                 int ph, int pw, void* stream) {
+// dtype 3: bf16, 1: fp32.  X: N x C*H*W -> cols: N x (C*KH*KW) x Pp, Pp >= Ho*Wo (zero padded).
+int sysml_im2col_pad(int dtype, const void* X, void* cols, int N, int C, int H, int W, int KH, int KW, int sh, int sw,
+                     int ph, int pw, int Pp, void* stream) {
   using namespace sysml_dnn;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int Ho = (H + 2 * ph - KH) / sh + 1, Wo = (W + 2 * pw - KW) / sw + 1;
-  if (Ho <= 0 || Wo <= 0 || N <= 0) return -1;
-  const int64_t total = (int64_t)N * C * KH * KW * Ho * Wo;
+  if (Ho <= 0 || Wo <= 0 || N <= 0 || Pp < Ho * Wo) return -1;
+  const int64_t total = (int64_t)N * C * KH * KW * Pp;
   const bool small = total < (1LL << 31) && (int64_t)N * C * H * W < (1LL << 31);
   const dim3 g(grid_for(total));
-  const FastDiv fP = fastdiv(Ho * Wo), fKK = fastdiv(KH * KW), fKW = fastdiv(KW), fWo = fastdiv(Wo);
+  const FastDiv fP = fastdiv(Pp), fKK = fastdiv(KH * KW), fKW = fastdiv(KW), fWo = fastdiv(Wo);
   if (dtype == 3) {
-    if (small) hipLaunchKernelGGL((im2col_kernel<__bf16, int>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo);
-    else hipLaunchKernelGGL((im2col_kernel<__bf16, int64_t>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo);
+    if (small) hipLaunchKernelGGL((im2col_kernel<__bf16, int>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo, Pp);
+    else hipLaunchKernelGGL((im2col_kernel<__bf16, int64_t>), g, dim3(256), 0, s, (const __bf16*)X, (__bf16*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo, Pp);
   } else if (dtype == 1) {
-    if (small) hipLaunchKernelGGL((im2col_kernel<float, int>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo);
-    else hipLaunchKernelGGL((im2col_kernel<float, int64_t>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo);
+    if (small) hipLaunchKernelGGL((im2col_kernel<float, int>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo, Pp);
+    else hipLaunchKernelGGL((im2col_kernel<float, int64_t>), g, dim3(256), 0, s, (const float*)X, (float*)cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho, Wo, fP, fKK, fKW, fWo, Pp);
   } else {
     return -1;
   }
   return (int)hipGetLastError();
+}
+
+int sysml_im2col(int dtype, const void* X, void* cols, int N, int C, int H, int W, int KH, int KW, int sh, int sw,
+                 int ph, int pw, void* stream) {
+  const int Ho = (H + 2 * ph - KH) / sh + 1, Wo = (W + 2 * pw - KW) / sw + 1;
+  return sysml_im2col_pad(dtype, X, cols, N, C, H, W, KH, KW, sh, sw, ph, pw, Ho * Wo, stream);
 }
 
 // dtype 3: bf16 cols -> bf16 dX; 1: fp32 -> fp32.  cols: N x (C*KH*KW) x (Ho*Wo), dx: N x C*H*W.

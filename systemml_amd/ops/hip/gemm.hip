@@ -64,6 +64,14 @@ struct Args {
   int ksplit, ktps;  // K splits, K-tiles per split
   int tri, beta;
   int veca, vecb;    // fp kernel: operand rows are 16-B aligned (vector loads allowed)
+  // image-blocked columns (convolutions lowered to ONE GEMM over all images, bf16 kernel):
+  // hwb > 0 -> column j of B and C is pixel j % hwb of image j / hwb; B image n starts at
+  // simgB * n (pixels contiguous, k stride ldb), C image n at simgC * n (pixels contiguous,
+  // row stride ldc); pixels >= hwr are padding (read as data, never stored)
+  int hwb, hwr;
+  int64_t simgB, simgC;
+  int obf16, relu;   // C stored bf16 (round to nearest even); relu after the bias
+  const float* bias; // C[row][*] += bias[row] (null: none)
 };
 
 __device__ __forceinline__ int swz_k(int row) { return (row >> 1) & 7; }
@@ -121,17 +129,21 @@ __device__ __forceinline__ void glds16(const uint16_t* sbase, uint32_t voff, uin
 }
 #pragma clang diagnostic pop
 
-template <bool KMAJ, int BKT>
+template <bool KMAJ, int BKT, int ROWS = 256>
 struct Stager {
-  static constexpr int NJ = BKT / 16;            // DMA instructions per wave per K-tile
+  static_assert(KMAJ || ROWS == 256, "MN-major images are 256 columns wide");
+  static constexpr int NJ = ROWS * BKT * 2 / 8192; // DMA instructions per wave per K-tile
   static constexpr int RPI = 1024 / (BKT * 2);   // K-major rows per 1-KiB instruction
   static constexpr int CPR = BKT / 8;            // 16-B chunks per K-major row
   int off[NJ];
   const uint16_t* base;   // block base: operand + r0 * ld (KMAJ) or operand + r0 (MN-major)
   int64_t ld;
-  __device__ __forceinline__ void init(const uint16_t* op, int wave, int lane, int r0, int R, int64_t ld_) {
+  // hw > 0 (MN-major only): image-blocked columns (Args::hwb), images simg elements apart
+  __device__ __forceinline__ void init(const uint16_t* op, int wave, int lane, int r0, int R, int64_t ld_,
+                                       int hw = 0, int64_t simg = 0) {
     ld = ld_;
-    base = KMAJ ? op + (int64_t)r0 * ld_ : op + r0;
+    const int img0 = hw > 0 ? r0 / hw : 0;
+    base = KMAJ ? op + (int64_t)r0 * ld_ : (hw > 0 ? op + (int64_t)img0 * simg : op + r0);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int gi = wave * NJ + j;
@@ -145,7 +157,13 @@ struct Stager {
         const int g = (lane & 31) ^ swz_t(krow);
         const int R8 = (R + 7) & ~7;                   // ld >= R8: columns up to R8 are in bounds
         const int gc = (r0 + 8 * g < R8 - 8) ? 8 * g : R8 - 8 - r0;
-        off[j] = krow * (int)ld_ + gc;
+        if (hw > 0) {
+          // hw % 8 == 0: an 8-column piece never straddles two images
+          const int col = r0 + gc, img = col / hw;
+          off[j] = (int)((int64_t)(img - img0) * simg) + krow * (int)ld_ + (col - img * hw);
+        } else {
+          off[j] = krow * (int)ld_ + gc;
+        }
       }
     }
   }
@@ -209,17 +227,23 @@ __device__ __forceinline__ void bar_keep_dma() {
 // BKT = 64: two LDS stages (DMA of tile t+1 overlaps tile t; drain + barrier per tile).
 // BKT = 32: four LDS stages of 32 KiB, three K-tiles in flight; per tile a COUNTED vmcnt
 //           (own DMAs of tile t retired, later tiles keep streaming) + a raw s_barrier.
-template <bool TA, bool TB, int BKT>
+// BMT = rows of A per block: 256 (waves 2 x 4 of 128 x 64) or 64 (waves 2 x 4 of 32 x 64, for
+// GEMMs with few rows -- convolutions with 64 filters / channels; K-major A, BKT 64 only)
+template <bool TA, bool TB, int BKT, int BMT = 256>
 __global__ void __launch_bounds__(NTHR, 2)
 gemm_bf16_kernel(Args a) {
   constexpr bool AK = !TA;   // A K-major
   constexpr bool BKM = TB;   // B K-major
+  static_assert(BMT == 256 || (BMT == 64 && !TA && BKT == 64), "row-tile variants");
+  constexpr int WM = BMT / 2;                    // rows per wave
+  constexpr int MI = WM / 16;                    // 16-row MFMA tiles per wave
   constexpr int NST = BKT == 64 ? 2 : 4;         // LDS stages
-  constexpr int STG = 2 * BM * BKT * 2;          // bytes per stage (A + B images)
-  constexpr int OPI = BM * BKT * 2;              // bytes per operand image
+  constexpr int OPA = BMT * BKT * 2;             // bytes of the A image
+  constexpr int OPI = BM * BKT * 2;              // bytes of the B image (256 columns)
+  constexpr int STG = OPA + OPI;                 // bytes per stage (A + B images)
   constexpr int KK = BKT / 32;                   // 32-deep MFMA steps per tile
-  constexpr int DPT = 2 * (BKT / 16);            // DMA instructions per wave per tile (A + B)
-  static_assert(NST * STG == LDS_BYTES, "LDS budget");
+  constexpr int DPT = (BMT * BKT * 2 + BM * BKT * 2) / 8192;   // DMA instructions per wave per tile (A + B)
+  static_assert(NST * STG <= LDS_BYTES, "LDS budget");
   extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
 
@@ -235,14 +259,14 @@ gemm_bf16_kernel(Args a) {
   const int kt0 = split * a.ktps;
   const int kt1 = (kt0 + a.ktps < ktiles) ? kt0 + a.ktps : ktiles;
 
-  Stager<AK, BKT> sa;
+  Stager<AK, BKT, BMT> sa;
   Stager<BKM, BKT> sb;
-  sa.init((const uint16_t*)a.A, wave, lane, bm * BM, a.M, a.lda);
-  sb.init((const uint16_t*)a.B, wave, lane, bn * BN, a.N, a.ldb);
+  sa.init((const uint16_t*)a.A, wave, lane, bm * BMT, a.M, a.lda);
+  sb.init((const uint16_t*)a.B, wave, lane, bn * BN, a.N, a.ldb, BKM ? 0 : a.hwb, a.simgB);
 
-  f4 acc[8][4];
+  f4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
@@ -259,12 +283,12 @@ gemm_bf16_kernel(Args a) {
         bfr[j] = frag<BKM, BKT>(Bi, wc * 64 + j * 16, kk, lane);
         if constexpr (TAIL) bfr[j] = mask_k(bfr[j], kb, a.K);
       }
-      s8 af = frag<AK, BKT>(Ai, wr * 128, kk, lane);
+      s8 af = frag<AK, BKT>(Ai, wr * WM, kk, lane);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < MI; ++i) {
         // next A fragment in flight while this one's 4 MFMAs issue
         s8 an = af;
-        if (i < 7) an = frag<AK, BKT>(Ai, wr * 128 + (i + 1) * 16, kk, lane);
+        if (i < MI - 1) an = frag<AK, BKT>(Ai, wr * WM + (i + 1) * 16, kk, lane);
         if constexpr (TAIL) af = mask_k(af, kb, a.K);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -275,7 +299,7 @@ gemm_bf16_kernel(Args a) {
   };
   auto issue = [&](int kt, int ktail, lds_char* st) {
     sa.issue(kt * BKT, a.K, kt == ktail, st, wave, lane);
-    sb.issue(kt * BKT, a.K, kt == ktail, st + OPI, wave, lane);
+    sb.issue(kt * BKT, a.K, kt == ktail, st + OPA, wave, lane);
   };
 
   if (kt0 < kt1) {
@@ -290,14 +314,14 @@ gemm_bf16_kernel(Args a) {
       for (int kt = kt0; kt < ktf; ++kt) {
         lds_char* St = smem + cur * STG;
         if (kt + 1 < kt1) issue(kt + 1, ktail, smem + (cur ^ 1) * STG);
-        compute(St, St + OPI, kt * BKT, std::false_type{});
+        compute(St, St + OPA, kt * BKT, std::false_type{});
         wait_vm<0>();
         __syncthreads();
         cur ^= 1;
       }
       if (has_tail) {
         lds_char* St = smem + cur * STG;
-        compute(St, St + OPI, ktf * BKT, std::true_type{});
+        compute(St, St + OPA, ktf * BKT, std::true_type{});
       }
     } else {
       // prologue: tiles kt0 .. kt0+2 in flight
@@ -315,40 +339,75 @@ gemm_bf16_kernel(Args a) {
         bar_keep_dma();   // every wave's tile-kt DMAs retired; every wave done reading tile kt-1
         if (kt + NST - 1 < kt1) issue(kt + NST - 1, ktail, smem + ((slot + NST - 1) & (NST - 1)) * STG);
         lds_char* St = smem + slot * STG;
-        compute(St, St + OPI, kt * BKT, std::false_type{});
+        compute(St, St + OPA, kt * BKT, std::false_type{});
         slot = (slot + 1) & (NST - 1);
       }
       if (has_tail) {
         wait_vm<0>();
         bar_keep_dma();
         lds_char* St = smem + slot * STG;
-        compute(St, St + OPI, ktf * BKT, std::true_type{});
+        compute(St, St + OPA, ktf * BKT, std::true_type{});
       }
     }
   }
 
   // epilogue: C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + reg
-  float* dst = a.C + (a.slab ? (int64_t)split * a.slab : 0);
   const int64_t ldc = a.ldc;
-  const int rbase = bm * BM + wr * 128 + (lane >> 4) * 4;
+  const int rbase = bm * BMT + wr * WM + (lane >> 4) * 4;
   const int cbase = bn * BN + wc * 64 + (lane & 15);
-  const bool acc_in = a.beta && !a.slab;
+  if (a.slab || (!a.obf16 && a.hwb == 0 && a.bias == nullptr && !a.relu)) {
+    // plain fp32 C (or a split-K slab: the reduction pass applies the epilogue)
+    float* dst = (float*)a.C + (a.slab ? (int64_t)split * a.slab : 0);
+    const bool acc_in = a.beta && !a.slab;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = cbase + j * 16;
-      if (col < a.N) {
+      for (int j = 0; j < 4; ++j) {
+        const int col = cbase + j * 16;
+        if (col < a.N) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rbase + i * 16 + r;
-          if (row < a.M) {
-            float* p = dst + (int64_t)row * ldc + col;
-            *p = acc_in ? *p + acc[i][j][r] : acc[i][j][r];
+          for (int r = 0; r < 4; ++r) {
+            const int row = rbase + i * 16 + r;
+            if (row < a.M) {
+              float* p = dst + (int64_t)row * ldc + col;
+              *p = acc_in ? *p + acc[i][j][r] : acc[i][j][r];
+            }
           }
         }
       }
+    return;
+  }
+  // DNN epilogue: image-blocked columns, per-row bias, relu, bf16 or fp32 C
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = cbase + j * 16;
+    if (col >= a.N) continue;
+    int64_t cofs = col;
+    if (a.hwb > 0) {
+      const int img = col / a.hwb, px = col - img * a.hwb;
+      if (px >= a.hwr) continue;
+      cofs = (int64_t)img * a.simgC + px;
     }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + i * 16 + r;
+        if (row < a.M) {
+          float v = acc[i][j][r];
+          if (a.bias != nullptr) v += a.bias[row];
+          if (a.relu) v = v > 0.f ? v : 0.f;
+          const int64_t o = (int64_t)row * ldc + cofs;
+          if (a.obf16) {
+            uint32_t u = __float_as_uint(v);
+            u += 0x7fffu + ((u >> 16) & 1u);
+            ((uint16_t*)a.C)[o] = (uint16_t)(u >> 16);
+          } else {
+            ((float*)a.C)[o] = v;
+          }
+        }
+      }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -556,6 +615,47 @@ splitk_reduce(const T* __restrict__ slab, int64_t stride, int ks, T* __restrict_
   }
 }
 
+// split-K reduction with the DNN epilogue (image-blocked columns, bias, relu, bf16 / fp32 C)
+__global__ void __launch_bounds__(256)
+splitk_reduce_dnn(const float* __restrict__ slab, int64_t stride, int ks, void* __restrict__ C, int64_t ldc, int M,
+                  int N, int hwb, int hwr, int64_t simgC, const float* __restrict__ bias, int relu, int obf16) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(idx / N), j = (int)(idx - (int64_t)i * N);
+    int64_t cofs = j;
+    if (hwb > 0) {
+      const int img = j / hwb, px = j - img * hwb;
+      if (px >= hwr) continue;
+      cofs = (int64_t)img * simgC + px;
+    }
+    float v = 0.f;
+    for (int k = 0; k < ks; ++k) v += slab[idx + (int64_t)k * stride];
+    if (bias != nullptr) v += bias[i];
+    if (relu) v = v > 0.f ? v : 0.f;
+    const int64_t o = (int64_t)i * ldc + cofs;
+    if (obf16) {
+      uint32_t u = __float_as_uint(v);
+      u += 0x7fffu + ((u >> 16) & 1u);
+      ((uint16_t*)C)[o] = (uint16_t)(u >> 16);
+    } else {
+      ((float*)C)[o] = v;
+    }
+  }
+}
+
+// B [N][C][hw] -> [N][C][hwp] (zero padding): image-blocked GEMM operands need 8-pixel pieces
+__global__ void __launch_bounds__(256)
+pad_pixels(const uint16_t* __restrict__ X, uint16_t* __restrict__ Y, int64_t planes, int hw, int hwp) {
+  const int64_t total = planes * hwp;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pl = idx / hwp;
+    const int px = (int)(idx - pl * hwp);
+    Y[idx] = px < hw ? X[pl * hw + px] : (uint16_t)0;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 mirror_lower(T* __restrict__ C, int64_t ldc, int M, int tb) {
@@ -580,16 +680,16 @@ using namespace sysml_gk;
 
 static int g_bk = 0;    // bf16 K-tile override: 0 = auto, 32 (4-stage, counted vmcnt), 64 (2-stage)
 
-template <bool TA, bool TB, int BKT>
+template <bool TA, bool TB, int BKT, int BMT = 256>
 static int launch_bf16_t(const Args& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<TA, TB, BKT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            LDS_BYTES) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<TA, TB, BKT, BMT>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess)
       return -3;
     attr = true;
   }
-  return launch_kernel(gemm_bf16_kernel<TA, TB, BKT>, a, NTHR, LDS_BYTES, st);
+  return launch_kernel(gemm_bf16_kernel<TA, TB, BKT, BMT>, a, NTHR, LDS_BYTES, st);
 }
 
 template <bool TA, bool TB>
@@ -648,6 +748,10 @@ int sysml_gemm(int dtype, const void* A, int64_t lda, int ta, const void* B, int
   const int kt = dtype == 2 ? bk : FBK;
   Args a;
   a.veca = a.vecb = 0;
+  a.hwb = a.hwr = 0;
+  a.simgB = a.simgC = 0;
+  a.obf16 = a.relu = 0;
+  a.bias = nullptr;
   a.A = A; a.B = B;
   a.lda = lda; a.ldb = ldb;
   a.M = M; a.N = N; a.K = K;
@@ -698,6 +802,72 @@ int sysml_gemm(int dtype, const void* A, int64_t lda, int ta, const void* B, int
     return tri ? mirror<double>((double*)C, ldc, M, tile, st) : 0;
   }
   return -1;
+}
+
+// Convolution GEMMs over ALL images as one launch (bf16 operands, fp32 accumulation):
+//   C[m][img, px] = bias[m] + sum_k A[m][k] B_img[k][px]   (relu optional, C bf16 or fp32)
+// A: K-major [M][lda] (filters; the host transposes W for backward data).  B: images of
+// [K][hwb] pixels (hwb % 8 == 0), image n at B + n * simgB, k stride ldb.  C: images of
+// [M][hwr] pixels at C + n * simgC (row stride ldc), pixels >= hwr of B's blocks are padding.
+// N = images * hwb.  M <= 128 runs the 64-row tile.  ksplit > 1: fp32 slabs (ksplit x M x N)
+// reduced by the epilogue pass.
+int sysml_gemm_dnn(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t simgB, void* C, int64_t ldc,
+                   int64_t simgC, int M, int N, int K, int hwb, int hwr, const float* bias, int relu, int obf16,
+                   int ksplit, void* slab, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M <= 0 || N <= 0) return 0;
+  if (K <= 0 || ksplit < 1 || hwb <= 0 || (hwb & 7) || hwr > hwb || N % hwb) return -1;
+  if ((lda & 7) || (ldb & 7) || (simgB & 7) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return -4;
+  if (lda < ((K + 7) & ~7) || ldb < hwb) return -4;
+  // 32-bit lane offsets: a 256-column tile spans at most 256 / hwb + 2 images
+  if (((int64_t)(256 / hwb + 2) * simgB + (int64_t)BK * ldb) * 2 >= ((int64_t)1 << 31)) return -4;
+  if (lda * 256 >= (int64_t)1 << 31) return -4;
+  const bool small = M <= 128;
+  const int tile = small ? 64 : BM;
+  const int bk = small ? 64 : (g_bk ? g_bk : (ksplit > 1 ? 32 : 64));
+  Args a;
+  a.veca = a.vecb = 0;
+  a.A = A; a.B = B;
+  a.lda = lda; a.ldb = ldb;
+  a.M = M; a.N = N; a.K = K;
+  a.tm = (M + tile - 1) / tile;
+  a.tn = (N + BN - 1) / BN;
+  a.ntiles = a.tm * a.tn;
+  const int ktiles = (K + bk - 1) / bk;
+  if (ksplit > ktiles) ksplit = ktiles;
+  a.ktps = (ktiles + ksplit - 1) / ksplit;
+  a.ksplit = (ktiles + a.ktps - 1) / a.ktps;
+  a.tri = 0;
+  a.beta = 0;
+  a.hwb = hwb; a.hwr = hwr;
+  a.simgB = simgB; a.simgC = simgC;
+  a.bias = bias; a.relu = relu; a.obf16 = obf16;
+  const bool use_slab = a.ksplit > 1;
+  if (use_slab && !slab) return -1;
+  a.C = (float*)(use_slab ? slab : C);
+  a.ldc = use_slab ? N : ldc;
+  a.slab = use_slab ? (int64_t)M * N : 0;
+  int rc;
+  if (small) rc = launch_bf16_t<false, false, 64, 64>(a, st);
+  else rc = bk == 64 ? launch_bf16_t<false, false, 64>(a, st) : launch_bf16_t<false, false, 32>(a, st);
+  if (rc || !use_slab) return rc;
+  const int64_t total = (int64_t)M * N;
+  int g = (int)((total + 255) / 256);
+  g = g < 16384 ? g : 16384;
+  hipLaunchKernelGGL(splitk_reduce_dnn, dim3(g), dim3(256), 0, st, (const float*)slab, a.slab, a.ksplit, C, ldc, M, N,
+                     hwb, hwr, simgC, bias, relu, obf16);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// Y[planes][hwp] = X[planes][hw] zero-padded to hwp pixels (bf16)
+int sysml_pad_pixels(const void* X, void* Y, int64_t planes, int hw, int hwp, void* stream) {
+  if (planes <= 0 || hw <= 0 || hwp < hw) return -1;
+  const int64_t total = planes * hwp;
+  int g = (int)((total + 255) / 256);
+  g = g < 65536 ? g : 65536;
+  hipLaunchKernelGGL(pad_pixels, dim3(g), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)X, (uint16_t*)Y, planes,
+                     hw, hwp);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 }  // extern "C"

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+const double* sysml_live_flag();   // chain4.hip: run-ahead flag of the calling host thread
+
 namespace sysml_mc {
 
 typedef short s4 __attribute__((ext_vector_type(4)));
@@ -57,7 +59,8 @@ __global__ void __launch_bounds__(BLOCK, MIN_WAVES_PER_SIMD)
 mchain_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
               const uint16_t* __restrict__ V3T,  // [16][Dp] bf16 (row 4s+k = plane s of V[:,k])
               const float* __restrict__ S, int lds, int sbc, int K,
-              float* __restrict__ out, int ldo, int64_t tiles_per_block) {
+              float* __restrict__ out, int ldo, int64_t tiles_per_block, const double* __restrict__ live) {
+  if (live != nullptr && *live == 0.0) return;    // dead run-ahead iteration (runtime/program.py)
   constexpr int Dp = KS * 32 * WAVES;   // KS = 32-column k-steps per wave
   constexpr int ROWB = Dp * 2 + 16;      // LDS pitch of one X row (bytes)
   constexpr int CH = Dp / 8;             // 16-byte chunks per row
@@ -239,7 +242,8 @@ wide_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
             const uint16_t* __restrict__ VW,   // [3][16][Dp] bf16: plane p of V[:, k] in row 16p + k
             const float* __restrict__ S, int lds, int K,
             float* __restrict__ out, int ldo, int64_t tiles_per_block,
-            float* __restrict__ U, int ldu, double* __restrict__ obj) {
+            float* __restrict__ U, int ldu, double* __restrict__ obj, const double* __restrict__ live) {
+  if (live != nullptr && *live == 0.0) return;    // dead run-ahead iteration (runtime/program.py)
   constexpr int WV = wide_waves<MODE, KS>();
   constexpr int BLK = 64 * WV;
   constexpr int Dp = KS * 256;
@@ -461,7 +465,7 @@ static int launch_wide(bool occ, const void* X, int64_t N, int D, const void* VW
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t tpb = (ntiles + grid - 1) / grid;
   hipLaunchKernelGGL((wide_kernel<MODE, KS>), dim3(grid), dim3(blk), sh, st, (const uint16_t*)X, N, D,
-                     (const uint16_t*)VW, S, lds, K, out, ldo, tpb, U, ldu, obj);
+                     (const uint16_t*)VW, S, lds, K, out, ldo, tpb, U, ldu, obj, sysml_live_flag());
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -489,7 +493,7 @@ static int launch(const void* X, int64_t N, int D, const void* V3T, const float*
   const int64_t tpb = (ntiles + grid - 1) / grid;
   const size_t sh = lds_bytes<MODE, KS>();
   hipLaunchKernelGGL((mchain_kernel<MODE, KS>), dim3(grid), dim3(BLOCK), sh, st,
-                     (const uint16_t*)X, N, D, (const uint16_t*)V3T, S, lds, sbc, K, out, ldo, tpb);
+                     (const uint16_t*)X, N, D, (const uint16_t*)V3T, S, lds, sbc, K, out, ldo, tpb, sysml_live_flag());
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -121,6 +121,16 @@ def load(required=False):
                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
                                 ctypes.c_int, ctypes.c_void_p]
+    L.sysml_gemm_dnn.restype = ctypes.c_int
+    L.sysml_gemm_dnn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    L.sysml_pad_pixels.restype = ctypes.c_int
+    L.sysml_pad_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_void_p]
+    L.sysml_set_live.restype = None
+    L.sysml_set_live.argtypes = [ctypes.c_void_p]
     L.sysml_chain4m_occupancy.restype = ctypes.c_int
     L.sysml_chain4m_occupancy.argtypes = [ctypes.c_int, ctypes.c_int]
     L.sysml_mwide.restype = ctypes.c_int
@@ -752,13 +762,16 @@ class _WeightCasts:
     def __init__(self):
         self._d = {}
 
-    def get(self, t, dev, dt):
+    def get(self, t, dev, dt, trans=False):
+        """t (2-D) cast to dt on dev; trans: its transpose, contiguous (the K-major filter
+        operand of a backward-data GEMM)."""
         import weakref
-        k = id(t)
+        k = (id(t), trans)
         e = self._d.get(k)
         if e is not None and e[0]() is t and e[1] == t._version and e[2].device == dev and e[2].dtype == dt:
             return e[2]
-        c = t.to(device=dev, dtype=dt).contiguous()
+        c = t.to(device=dev, dtype=dt)
+        c = (c.t() if trans else c).contiguous()
         dd = self._d
         ref = weakref.ref(t, lambda _r, k=k: dd.pop(k, None) if dd.get(k, (None,))[0] is _r else None)
         dd[k] = (ref, t._version, c)
@@ -778,6 +791,56 @@ def _conv_code(dt):
     return None
 
 
+GEMM_DNN_BLOCKS = int(os.environ.get("SYSML_GEMM_DNN_BLOCKS", "512"))   # split K until ~this many blocks
+
+
+def _gemm_img(A, B, out, M, K, nimg, hw, hwb=None, bias=None, relu=False):
+    """out[n] (M x hw, bf16) = A (M x K, bf16 K-major) . B[n] (K x hw) for every image n as ONE
+    image-blocked GEMM launch (gemm.hip sysml_gemm_dnn); B's images are `hwb` pixels apart
+    (hwb % 8 == 0; B is padded here when hw is not a multiple of 8), pixels past hw are padding.
+    bias (M) and relu are applied in the epilogue."""
+    L = load(required=True)
+    dev = out.device
+    st = _stream()
+    if hwb is None:
+        hwb = hw
+        if hw % 8:
+            hwb = (hw + 7) & ~7
+            Bp = torch.empty((nimg * K * hwb,), dtype=torch.bfloat16, device=dev)
+            rc = L.sysml_pad_pixels(B.data_ptr(), Bp.data_ptr(), nimg * K, hw, hwb, st)
+            if rc != 0:
+                raise RuntimeError(f"sysml_pad_pixels failed: {rc}")
+            B = Bp
+    Ncol = nimg * hwb
+    te = 64 if M <= 128 else 256
+    tiles = ((M + te - 1) // te) * ((Ncol + 255) // 256)
+    ksplit = 1
+    if tiles < GEMM_DNN_BLOCKS and K >= 512:
+        ksplit = max(1, min(GEMM_DNN_BLOCKS // tiles, K // 256, 16))
+    slab = torch.empty((ksplit * M * Ncol,), dtype=torch.float32, device=dev) if ksplit > 1 else None
+    bb = None
+    if bias is not None:
+        bb = bias.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+    rc = L.sysml_gemm_dnn(A.data_ptr(), A.stride(0), B.data_ptr(), hwb, K * hwb, out.data_ptr(), hw, M * hw,
+                          M, Ncol, K, hwb, hw, bb.data_ptr() if bb is not None else None, int(bool(relu)), 1,
+                          ksplit, slab.data_ptr() if slab is not None else None, st)
+    if rc != 0:
+        raise RuntimeError(f"sysml_gemm_dnn failed: {rc}")
+    _count("gemm_dnn")
+    return out
+
+
+def _bias_epilogue(y, bias, relu, F, dev):
+    """bias_add (+ relu) over a convolution result.  bias_op writes into `out` only on its bf16
+    fast path; otherwise it returns a new fp32 tensor, which is taken (cast back to y's dtype)
+    instead of silently keeping the un-biased y."""
+    bb = bias if bias is not None else torch.zeros(F, device=dev)
+    r = bias_op(y, bb, relu=relu, out=y)
+    if r is None:
+        raise RuntimeError(f"conv2d bias epilogue: {bb.numel()} channels do not divide a row of {y.shape[1]}")
+    return r if r is y else r.to(y.dtype)
+
+
 def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, relu=False):
     """Implicit-GEMM convolution (mode 0 forward, 1 backward data, 2 backward filter).  X / W /
     D are the DML 2-D matrices (NCHW rows); returns the DML 2-D result.  bf16 operands compute
@@ -794,6 +857,7 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
     def prep(t):
         return None if t is None else t.to(device=dev, dtype=dt).contiguous()
     X, D = prep(X), prep(D)
+    W0 = W
     W = _wcast.get(W, dev, dt) if W is not None and W.dtype != dt and dt == torch.bfloat16 else prep(W)
     Ho = (H + 2 * ph - KH) // sh + 1
     Wo = (Wd + 2 * pw - KW) // sw + 1
@@ -803,45 +867,48 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
         shape = (N, C * H * Wd)
     else:
         shape = (F, C * KH * KW)
+    Wsrc = W0 if W0 is not None else W         # the filter as given (cache key of its transposed bf16 copy)
     if CONV1X1_GEMM and mode != 2 and KH == 1 and KW == 1 and sh == 1 and sw == 1 and ph == 0 and pw == 0 \
-            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
-        # a 1x1 stride-1 convolution of bf16 activations is a plain batched GEMM per image
-        # (forward W . X[n], backward data t(W) . dY[n]): hipBLASLt, bf16 out / fp32 accumulate
+            and dt == torch.bfloat16 and C % 8 == 0 and F % 8 == 0 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+        # a 1x1 stride-1 convolution of bf16 activations is ONE GEMM over all images (gemm.hip
+        # image-blocked columns): forward W . X[n], backward data t(W) . dY[n]; bias + relu in
+        # the epilogue, bf16 out / fp32 accumulate
         HW = H * Wd
-        Wm = W.view(F, C)
-        y = torch.matmul(Wm, X.view(N, C, HW)) if mode == 0 else torch.matmul(Wm.t(), D.view(N, F, HW))
-        y = y.view(shape)
-        if mode == 0 and (bias is not None or relu):
-            bb = bias if bias is not None else torch.zeros(F, device=dev)
-            bias_op(y, bb, relu=relu, out=y)
+        y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
+        if mode == 0:
+            _gemm_img(W, X, y, F, C, N, HW, bias=bias, relu=relu)
+        else:
+            _gemm_img(_wcast.get(Wsrc, dev, dt, trans=True), D, y, C, F, N, HW)
         _count(("conv2d", "conv2d_bwd_data")[mode])
         _count("conv1x1_gemm")
         return y
     if CONV1X1_GEMM and mode == 0 and KH * KW > 1 and Ho * Wo <= IM2COL_MAX_HW and C > 8 \
-            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
-        # small-image convolutions: an im2col gather and one batched library GEMM per image
+            and dt == torch.bfloat16 and F % 8 == 0 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+        # small-image convolutions: an im2col gather (pixels padded to a multiple of 8) and ONE
+        # image-blocked GEMM over all images
         CKK, P = C * KH * KW, Ho * Wo
-        cols = torch.empty((N, CKK, P), dtype=torch.bfloat16, device=dev)
-        L.sysml_im2col.restype = ctypes.c_int
-        L.sysml_im2col.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 10 + \
-            [ctypes.c_void_p]
-        rc = L.sysml_im2col(3, X.data_ptr(), cols.data_ptr(), N, C, H, Wd, KH, KW, sh, sw, ph, pw, _stream())
-        if rc != 0:
-            raise RuntimeError(f"sysml_im2col failed: {rc}")
-        y = torch.matmul(W.view(F, CKK), cols).view(shape)
-        if bias is not None or relu:
-            bb = bias if bias is not None else torch.zeros(F, device=dev)
-            bias_op(y, bb, relu=relu, out=y)
-        _count("conv2d")
-        _count("conv_im2col")
-        return y
+        Pp = (P + 7) & ~7
+        if CKK % 8 == 0:
+            cols = torch.empty((N, CKK, Pp), dtype=torch.bfloat16, device=dev)
+            L.sysml_im2col_pad.restype = ctypes.c_int
+            L.sysml_im2col_pad.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 11 + \
+                [ctypes.c_void_p]
+            rc = L.sysml_im2col_pad(3, X.data_ptr(), cols.data_ptr(), N, C, H, Wd, KH, KW, sh, sw, ph, pw, Pp, _stream())
+            if rc != 0:
+                raise RuntimeError(f"sysml_im2col failed: {rc}")
+            y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
+            _gemm_img(W, cols, y, F, CKK, N, P, hwb=Pp, bias=bias, relu=relu)
+            _count("conv2d")
+            _count("conv_im2col")
+            return y
     if CONV1X1_GEMM and mode == 1 and (sh > 1 or sw > 1 or (KH > 1 and H * Wd <= COL2IM_MAX_HW)) \
-            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
-        # backward data as cols = t(W) . dY[n] (batched library GEMM, bf16) + a col2im gather: a
-        # strided convolution's taps land on the stride grid for a quarter of the (pixel, tap)
+            and dt == torch.bfloat16 and F % 8 == 0 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+        # backward data as cols = t(W) . dY[n] (one image-blocked GEMM, bf16) + a col2im gather:
+        # a strided convolution's taps land on the stride grid for a quarter of the (pixel, tap)
         # pairs, which the implicit GEMM would multiply as zeros
         CKK, P = C * KH * KW, Ho * Wo
-        cols = torch.matmul(W.view(F, CKK).t(), D.view(N, F, P))
+        cols = torch.empty((N, CKK, P), dtype=torch.bfloat16, device=dev)
+        _gemm_img(_wcast.get(Wsrc, dev, dt, trans=True), D, cols, CKK, F, N, P)
         y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
         L.sysml_col2im.restype = ctypes.c_int
         L.sysml_col2im.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 10 + \
@@ -1009,7 +1076,7 @@ def idx32_of(col):
     e = _IDX32.get(key)
     if e is None:
         if len(_IDX32) >= 8:
-            _IDX32.pop(next(iter(_IDX32)))
+            _IDX32.pop(next(iter(_IDX32), None), None)   # tolerant of a concurrent parfor worker's eviction
         e = (col, col.to(torch.int32).contiguous())
         _IDX32[key] = e
     return e[1]
@@ -1055,6 +1122,8 @@ def spgemm(A, B):
     m, n = A.shape[0], B.shape[1]
     if n > SPGEMM_MAXN or n < 1 or m < 1:
         return None
+    if torch.float64 in (A.values().dtype, B.values().dtype, backend.dtype):
+        return None          # the LDS accumulator is fp32: double-precision products keep the fp64 path
     dev = A.values().device
     ac, bc = A.crow_indices().to(torch.int64).contiguous(), B.crow_indices().to(torch.int64).contiguous()
     a32, b32 = csr_idx32(A), csr_idx32(B)

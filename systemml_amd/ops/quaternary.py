@@ -61,7 +61,7 @@ def _coo_idx(x):
         counts = crow[1:] - crow[:-1]
         row = torch.repeat_interleave(torch.arange(x.shape[0], device=x.device), counts)
         if len(_ROWS) >= 4:
-            _ROWS.pop(next(iter(_ROWS)))
+            _ROWS.pop(next(iter(_ROWS), None), None)   # tolerant of a concurrent parfor worker's eviction
         e = _ROWS[key] = (crow, row)
     return e[1], col, val
 

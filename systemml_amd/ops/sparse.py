@@ -167,7 +167,7 @@ def _transpose_plan(a):
         crowT[1:] = torch.cumsum(torch.bincount(col, minlength=c), 0)
         p = (crowT, rows[perm].contiguous(), perm, crow, col)
         if len(_TPLANS) >= 4:
-            _TPLANS.pop(next(iter(_TPLANS)))
+            _TPLANS.pop(next(iter(_TPLANS), None), None)   # tolerant of a concurrent parfor worker's eviction
         _TPLANS[key] = p
     return p
 
@@ -228,7 +228,7 @@ def _transposed(a):
     e = _TVALS.get(key)
     if e is None:
         if len(_TVALS) >= 2:
-            _TVALS.pop(next(iter(_TVALS)))
+            _TVALS.pop(next(iter(_TVALS), None), None)   # tolerant of a concurrent parfor worker's eviction
         e = _TVALS[key] = (v, torch.sparse_csr_tensor(crowT, colT, v[perm], (a.shape[1], a.shape[0]),
                                                       device=a.device))
     return e[1]

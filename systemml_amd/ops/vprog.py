@@ -293,8 +293,10 @@ struct VArgs {{
   double* sout;
   T* scratch;
   sysml_i64 n;
+  const double* live;
 }};
 extern "C" __global__ void __launch_bounds__({NT}) sysml_vprog_k(const VArgs P) {{
+  if (P.live != nullptr && *P.live == 0.0) return;    // dead run-ahead iteration
   __shared__ double red[{NT // 64} * {kred}];
 {body}
 }}
@@ -432,8 +434,10 @@ struct VArgs {{
   double* sout;
   T* scratch;
   sysml_i64 n;
+  const double* live;
 }};
 extern "C" __global__ void __launch_bounds__({NTR}) sysml_vprog_k(const VArgs P) {{
+  if (P.live != nullptr && *P.live == 0.0) return;    // dead run-ahead iteration
   __shared__ double red[{NTR // 64} * {kred}];
 {body}
 }}
@@ -444,7 +448,7 @@ def _args_struct(n_in, n_out_m):
     class VArgs(ctypes.Structure):
         _fields_ = [("inp", ctypes.c_void_p * max(n_in, 1)), ("s", ctypes.c_double * max(n_in, 1)),
                     ("out", ctypes.c_void_p * max(n_out_m, 1)), ("sout", ctypes.c_void_p),
-                    ("scratch", ctypes.c_void_p), ("n", ctypes.c_int64)]
+                    ("scratch", ctypes.c_void_p), ("n", ctypes.c_int64), ("live", ctypes.c_void_p)]
     return VArgs
 
 
@@ -661,6 +665,7 @@ def _kernel(vp, args):
     scr = torch.empty(pl.nscr * n, dtype=T, device=dev) if pl.nscr else None
     P.scratch = scr.data_ptr() if scr is not None else 0
     P.n = n
+    P.live = backend.live
     di = dev.index if dev.index is not None else torch.cuda.current_device()
     st = _raw_stream(di) if _raw_stream is not None else torch.cuda.current_stream(dev).cuda_stream
     rc = _rtc_lib().sysml_rtc_launch(pl.fn[0], 1, 1, NTR if pl.cpt else NT, ctypes.byref(P), ctypes.sizeof(P), st)
@@ -668,13 +673,25 @@ def _kernel(vp, args):
         raise RuntimeError(f"vector program launch failed: {rc}")
     from . import kernels
     kernels._count("vprog")
-    svals = sout.cpu().tolist() if sout is not None else ()     # the one device synchronisation (GIL released)
-    _HT.mark("vprog-sync")
-    del keep
+    types = pl.types
     res = []
     im = iter(outs_m)
     si = 0
-    types = pl.types
+    if backend.defer and sout is not None:
+        # run-ahead loop: the scalars stay in HBM (the next iteration's kernels read them
+        # there); the loop reads its predicate one iteration late
+        DS = _DevScalar[0]
+        for v in vp.outs:
+            if vp.cls[v] == "M":
+                res.append(next(im))
+            else:
+                t = types[v]
+                res.append(DS(sout[si], t if t in ("b", "i") else "d"))
+                si += 1
+        return tuple(res)
+    svals = sout.cpu().tolist() if sout is not None else ()     # the one device synchronisation (GIL released)
+    _HT.mark("vprog-sync")
+    del keep
     for v in vp.outs:
         if vp.cls[v] == "M":
             res.append(next(im))

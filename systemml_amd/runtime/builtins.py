@@ -563,9 +563,10 @@ def b_dp_rank(ctx):
 
 @builtin("_dp_allreduce", multi=True)
 def b_dp_allreduce(ctx, *grads):
-    """Mean of every rank's gradients, as ONE bucketed all-reduce: the matrices are packed
-    into a flat fp32 / fp64 buffer in HBM (one RCCL call over xGMI instead of one per
-    parameter), reduced, scaled by 1 / world and unpacked.  Single process: identity."""
+    """Sum over the ranks of every operand (the training script weights each rank's
+    gradients by its share of the step's rows first), as ONE bucketed all-reduce: the
+    matrices are packed into a flat fp32 / fp64 buffer in HBM (one RCCL call over xGMI
+    instead of one per parameter), reduced and unpacked.  Single process: identity."""
     dist = ctx.dist
     if dist is None or dist.world <= 1:
         return tuple(grads)
@@ -574,7 +575,6 @@ def b_dp_allreduce(ctx, *grads):
     dt = torch.float64 if any(m.dtype == torch.float64 for m in mats) else torch.float32
     flat = torch.cat([m.reshape(-1).to(device=dev, dtype=dt) for m in mats])
     dist.allreduce_(flat, "sum")
-    flat.mul_(1.0 / dist.world)
     out, off = [], 0
     for m in mats:
         n = m.numel()

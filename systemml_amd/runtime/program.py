@@ -353,6 +353,14 @@ def _exec_basic(ctx, b):
 def _exec_control(ctx, b):
     if isinstance(b, IfBlock):
         if _to_bool(eval_pred(ctx, b.pred)):
+            if getattr(b, "vguard", False):
+                # if-converted block (compiler/ifconv.py): it evaluates both branches; an error
+                # there may belong to the branch not taken, so the original control flow decides
+                try:
+                    exec_blocks(ctx, b.then_blocks)
+                except DMLRuntimeError:
+                    exec_blocks(ctx, b.else_blocks)
+                return
             exec_blocks(ctx, b.then_blocks)
         else:
             exec_blocks(ctx, b.else_blocks)
@@ -366,6 +374,8 @@ def _exec_control(ctx, b):
             if isinstance(x, torch.Tensor):
                 ctx.owned.discard(x)
     if isinstance(b, WhileBlock):
+        if RUNAHEAD and _runahead_ok(ctx, b):
+            return _exec_while_runahead(ctx, b)
         while _to_bool(eval_pred(ctx, b.pred)):
             exec_blocks(ctx, b.body)
         return
@@ -393,6 +403,121 @@ def _exec_control(ctx, b):
             i = start + cnt * incr
         return
     raise DMLRuntimeError(f"unknown block type {type(b).__name__}")
+
+
+# ----------------------------------------------------------------------------
+# run-ahead while loops
+# ----------------------------------------------------------------------------
+# A data-dependent while loop on the GPU backend costs one device round trip per iteration:
+# the host reads the predicate back, and only then queues the next iteration, so the device
+# idles for the host's whole per-iteration time (reference: WhileProgramBlock.execute
+# evaluates the predicate synchronously; on a CPU that is free).  A run-ahead loop queues
+# iteration k+1 BEFORE it reads iteration k's predicate:
+#   * vector programs leave their scalar results in HBM (ops/vprog.py, backend.defer), so the
+#     next iteration's kernels take them from there and the predicate is a device value;
+#   * the predicate's copy to pinned host memory is queued with an event behind it
+#     (DevScalar.start_read); the host waits for that event one iteration later, while the
+#     device already works on the next iteration;
+#   * the queued iteration carries the device address of that predicate (backend.live): the
+#     streaming kernels (ops/hip/chain4.hip, mfma_chain.hip) and vector programs read it first
+#     and return at once when it is 0, so the one speculative iteration past the loop's end
+#     costs a few microseconds of launches, not a pass over X;
+#   * variables are immutable tensors / values, so a dead iteration is undone by restoring
+#     the variable map it started from.
+# Only bodies without side effects qualify (no print / write / stop, function calls, random
+# generators, nested loops or update-in-place indexing): compiler facts checked once per loop.
+RUNAHEAD = __import__("os").environ.get("SYSML_RUNAHEAD", "1") != "0"
+_RA_BAD_BI = frozenset({"print", "write", "stop", "assert", "printf", "rand", "sample", "time", "read", "eval",
+                        "list", "exists", "toString", "setwd"})
+_RA_BAD_OPS = frozenset({"fcall", "sink"})
+
+
+def _pure_hops(roots):
+    from ..compiler import hops as H
+    for h in H.walk(roots):
+        if h.op in _RA_BAD_OPS:
+            return False
+        if h.op == "bi" and h.p.get("name") in _RA_BAD_BI:
+            return False
+        if h.op == "lix" and h.p.get("inplace"):
+            return False
+    return True
+
+
+def _pure_blocks(blocks):
+    for b in blocks:
+        if isinstance(b, BasicBlock):
+            if not _pure_hops(list(b.roots) + list(b.env_out.values())):
+                return False
+        elif isinstance(b, IfBlock):
+            if not (b.pred.is_const or _pure_hops([b.pred.root])):
+                return False
+            if not (_pure_blocks(b.then_blocks) and _pure_blocks(b.else_blocks)):
+                return False
+        else:
+            return False            # nested loops keep their own control flow
+    return True
+
+
+def _runahead_ok(ctx, b):
+    if ctx.debugger is not None or getattr(ctx, "parfor_worker", False) or (ctx.stats is not None and ctx.stats.enabled):
+        return False
+    from ..ops.backend import backend
+    if not (backend.on_gpu and backend.use_kernels) or backend.lazy:
+        return False
+    ok = getattr(b, "_runahead", None)
+    if ok is None:
+        ok = b._runahead = (not getattr(b, "inplace_vars", None) and not b.pred.is_const
+                            and _pure_hops([b.pred.root]) and _pure_blocks(b.body))
+    return ok
+
+
+runahead_stats = {"loops": 0, "iterations": 0, "dead": 0, "host_pred": 0}
+
+
+def _exec_while_runahead(ctx, b):
+    from ..ops.backend import backend
+    if not _to_bool(eval_pred(ctx, b.pred)):
+        return
+    runahead_stats["loops"] += 1
+    vars_ = ctx.vars
+    pend = None          # device predicate guarding the iteration being queued (None: known live)
+    try:
+        while True:
+            snap = vars_.copy()
+            live = 0
+            if pend is not None and pend.t.is_cuda and pend.t.dtype == torch.float64:
+                live = pend.t.data_ptr()
+            backend.set_runahead(True, live)
+            err = None
+            q = None
+            try:
+                exec_blocks(ctx, b.body)
+                q = eval_pred(ctx, b.pred)
+                if type(q) is S.DevScalar:
+                    q.start_read()
+            except DMLScriptStop:
+                raise
+            except Exception as e:      # noqa: BLE001 - re-raised below unless the iteration was dead
+                err = e
+            runahead_stats["iterations"] += 1
+            if pend is not None and not pend.value():
+                # the iteration just queued lies past the loop's end: undo it
+                runahead_stats["dead"] += 1
+                vars_.clear()
+                vars_.update(snap)
+                return
+            if err is not None:
+                raise err
+            if type(q) is S.DevScalar:
+                pend = q
+            else:
+                runahead_stats["host_pred"] += 1
+                if not _to_bool(q):
+                    return
+                pend = None
+    finally:
+        backend.set_runahead(False, 0)
 
 
 # ----------------------------------------------------------------------------

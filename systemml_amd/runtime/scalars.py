@@ -27,19 +27,40 @@ class DevScalar:
     the CP ScalarObject (runtime/instructions/cp/DoubleObject.java), which is always on the
     JVM heap — on the GPU backend that costs a device round trip per scalar.
     """
-    __slots__ = ("t", "vt", "_v")
+    __slots__ = ("t", "vt", "_v", "_hb", "_ev")
     is_dev_scalar = True
 
     def __init__(self, t, vt="d"):
         self.t = t          # 0-d float64 tensor on the device
-        self.vt = vt        # 'd' (DOUBLE) | 'b' (BOOLEAN)
+        self.vt = vt        # 'd' (DOUBLE) | 'b' (BOOLEAN) | 'i' (INT, held as a double)
         self._v = None
+        self._hb = None     # pinned host copy in flight (start_read)
+        self._ev = None
+
+    def start_read(self):
+        """Queue the device-to-host copy of the value behind the work that produces it and
+        return at once; a later value() waits for that copy only (an event), not for work
+        queued after it -- how a run-ahead loop reads its predicate one iteration late
+        (runtime/program.py _exec_while_runahead)."""
+        if self._v is None and self._hb is None:
+            import torch
+            hb = torch.empty(1, dtype=torch.float64, pin_memory=True)
+            hb.copy_(self.t.reshape(1), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._hb, self._ev = hb, ev
+        return self
 
     def value(self):
         """Materialise (one device sync, cached)."""
         if self._v is None:
-            x = float(self.t.item())
-            self._v = (x != 0.0) if self.vt == "b" else x
+            if self._ev is not None:
+                self._ev.synchronize()
+                x = float(self._hb[0])
+                self._hb = self._ev = None
+            else:
+                x = float(self.t.item())
+            self._v = (x != 0.0) if self.vt == "b" else (int(x) if self.vt == "i" else x)
         return self._v
 
     def __float__(self):
@@ -113,7 +134,7 @@ def to_str(v) -> str:
 
 def vtype_of(v):
     if type(v) is DevScalar:
-        return "BOOLEAN" if v.vt == "b" else "DOUBLE"
+        return "BOOLEAN" if v.vt == "b" else ("INT" if v.vt == "i" else "DOUBLE")
     if isinstance(v, bool):
         return "BOOLEAN"
     if isinstance(v, int):

@@ -36,7 +36,9 @@ def _bf(x):
                                    (3, 40, 13, 13, 24, 3, 2, 1),
                                    # even widths: the stride-2 paired col2im
                                    (2, 64, 16, 16, 32, 3, 2, 1), (2, 48, 14, 14, 40, 3, 2, 1),
-                                   (2, 32, 12, 12, 16, 3, 2, 0), (2, 3, 32, 32, 16, 7, 2, 3)])
+                                   (2, 32, 12, 12, 16, 3, 2, 0), (2, 3, 32, 32, 16, 7, 2, 3),
+                                   # N*F*H*W not a multiple of 4: the bias epilogue's fp32 path
+                                   (1, 16, 7, 7, 3, 1, 1, 0), (1, 16, 7, 7, 3, 3, 1, 1)])
 def test_conv_bf16_output(shape):
     from systemml_amd.ops import kernels as Kn
     N, C, H, Wd, F_, K, s, p = shape

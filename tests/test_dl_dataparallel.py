@@ -1,9 +1,11 @@
 """Data-parallel Caffe2DML training across SPMD ranks (train_algo allreduce_parallel_batches /
-allreduce; reference Caffe2DML.scala:396-405): every rank trains its own mini-batch and one
-bucketed gradient all-reduce (_dp_allreduce) averages the gradients.  A 2-rank gloo run with
-local batch b must follow the same loss trajectory and end at the same weights as one
-process training mini-batch SGD with batch 2b (a network without batch statistics, so the
-two are mathematically identical)."""
+allreduce; reference Caffe2DML.scala:396-405): a step takes P * bs rows (bs for allreduce),
+every rank trains a contiguous share of them and one bucketed all-reduce (_dp_allreduce)
+sums the share-weighted gradients.  A 2-rank gloo run must follow the same loss trajectory
+and end at the same weights as one process training mini-batch SGD with batch P * bs (a
+network without batch statistics, so the two are mathematically identical), also when P is
+not the number of ranks; with a batch-norm layer every rank ends with the same weights and
+the same running statistics."""
 import os
 import socket
 
@@ -48,14 +50,23 @@ def _train(src, wnames, dist=None):
     return {k: res[k].double().numpy() for k in wnames}, losses
 
 
-def _worker(rank, world, port, q):
+def _bn_layers():
+    L = dl.Layer
+    return [L("conv", "c1", [dl.INPUT], ["c1"], F=4, kh=3, kw=3, sh=1, sw=1, ph=1, pw=1),
+            L("batchnorm", "bn1", ["c1"], ["bn1"], affine=True, mu=0.9, eps=1e-5),
+            L("relu", "r1", ["bn1"], ["r1"]),
+            L("dense", "fc", ["r1"], ["fc"], M=3),
+            L("softmax_loss", "loss", ["fc"], ["prob"])]
+
+
+def _worker(rank, world, port, q, bn=False, P=2, bs=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
         from systemml_amd.parallel import dist as D
         ctx = D.init(backend="gloo")
-        src, wn = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 3, 4, train_algo="allreduce_parallel_batches",
-                                        spmd=True)
+        src, wn = dl.generate_train_dml(_bn_layers() if bn else _layers(), SHAPE, SOLVER, 3, bs,
+                                        train_algo="allreduce_parallel_batches", parallel_batches=P, spmd=True)
         w, losses = _train(src, wn, ctx)
         q.put((rank, w, losses, dict(D.stats)))
         D.shutdown()
@@ -73,10 +84,10 @@ def _free_port():
 
 
 def test_single_process_dp_script_is_minibatch():
-    # W = 1: the data-parallel script is plain mini-batch SGD
+    # W = 1: the data-parallel script is plain mini-batch SGD over P * bs rows
     a_src, wn = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 2, 8, train_algo="allreduce_parallel_batches",
-                                      spmd=True)
-    b_src, _ = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 2, 8, train_algo="minibatch")
+                                      parallel_batches=2, spmd=True)
+    b_src, _ = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 2, 16, train_algo="minibatch")
     wa, la = _train(a_src, wn)
     wb, lb = _train(b_src, wn)
     np.testing.assert_allclose(la, lb, rtol=1e-12)
@@ -84,14 +95,12 @@ def test_single_process_dp_script_is_minibatch():
         np.testing.assert_allclose(wa[k], wb[k], rtol=1e-10, atol=1e-12, err_msg=k)
 
 
-def test_two_rank_gloo_matches_double_batch():
+def _run_ranks(world, **kw):
     import torch.multiprocessing as mp
-    ref_src, wn = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 3, 8, train_algo="minibatch")
-    ref_w, ref_l = _train(ref_src, wn)
-    world, port = 2, _free_port()
+    port = _free_port()
     mctx = mp.get_context("spawn")
     q = mctx.Queue()
-    procs = [mctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [mctx.Process(target=_worker, args=(r, world, port, q), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in range(world)]
@@ -99,9 +108,37 @@ def test_two_rank_gloo_matches_double_batch():
         p.join(timeout=60)
     for rank, w, losses, st in res:
         assert not isinstance(w, str), w
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_two_rank_gloo_matches_double_batch():
+    ref_src, wn = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 3, 8, train_algo="minibatch")
+    ref_w, ref_l = _train(ref_src, wn)
+    for rank, w, losses, st in _run_ranks(2):
         if rank == 0:                                # prints come from rank 0
             np.testing.assert_allclose(losses, ref_l, rtol=1e-9)
         for k in wn:
             np.testing.assert_allclose(w[k], ref_w[k], rtol=1e-8, atol=1e-10, err_msg=k)
         assert st["allreduce"] >= 12                 # one bucketed all-reduce per step (4 steps x 3 epochs)
         assert st["fallback_gathers"] == 0
+
+
+def test_two_rank_gloo_parallel_batches_not_world_size():
+    """P = 3 mini-batches of 4 rows per step on 2 ranks (6 rows each; the last group of 32
+    rows is short, 8 rows): mini-batch SGD with batch 12."""
+    ref_src, wn = dl.generate_train_dml(_layers(), SHAPE, SOLVER, 3, 12, train_algo="minibatch")
+    ref_w, ref_l = _train(ref_src, wn)
+    for rank, w, losses, st in _run_ranks(2, P=3, bs=4):
+        if rank == 0:
+            np.testing.assert_allclose(losses, ref_l, rtol=1e-9)
+        for k in wn:
+            np.testing.assert_allclose(w[k], ref_w[k], rtol=1e-8, atol=1e-10, err_msg=k)
+
+
+def test_two_rank_gloo_batchnorm_state_agrees():
+    res = _run_ranks(2, bn=True, P=3, bs=4)
+    (_, w0, l0, _), (_, w1, _, _) = res
+    assert any(k.startswith("em_") for k in w0) and any(k.startswith("ev_") for k in w0), sorted(w0)
+    assert all(np.isfinite(l0))
+    for k in w0:
+        np.testing.assert_allclose(w1[k], w0[k], rtol=1e-12, atol=1e-14, err_msg=k)

@@ -103,3 +103,37 @@ def test_gemm_nonfinite_tail(G):
     C = G.matmul(P, Q)
     assert torch.isfinite(C).all()
     _check(C, P, Q, 1e-4)
+
+
+# ----------------------------------------------------------------------------- image-blocked DNN GEMM
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,nimg,hw,bias,relu", [
+    (64, 256, 8, 3136, True, True),      # 64-row tile, pixels a multiple of 8
+    (256, 64, 16, 784, False, False),    # 256-row tile
+    (512, 2048, 32, 49, True, False),    # 7 x 7 images (padded to 56), split-K
+    (128, 1152, 12, 196, False, True),   # 14 x 14 (padded to 200), 64-row tile, split-K
+    (1000, 72, 3, 100, True, True),      # ragged M, padded pixels
+])
+def test_gemm_img_matches_fp32(M, K, nimg, hw, bias, relu):
+    """sysml_gemm_dnn: out[n] = relu(A . B[n] + bias) for all images in one launch, bf16 out,
+    against an fp32 torch evaluation on the same bf16 operands."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from systemml_amd.ops import kernels as Kn
+    Kn.load(required=True)
+    g = torch.Generator(device="cuda").manual_seed(M + K + hw)
+    A = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    B = torch.randn(nimg, K, hw, device="cuda", generator=g).to(torch.bfloat16)
+    b = torch.randn(M, device="cuda", generator=g) if bias else None
+    out = torch.empty(nimg, M, hw, dtype=torch.bfloat16, device="cuda")
+    before = Kn.counters.get("gemm_dnn", 0)
+    Kn._gemm_img(A, B, out, M, K, nimg, hw, bias=b, relu=relu)
+    ref = torch.matmul(A.float(), B.float())
+    if bias:
+        ref = ref + b.reshape(1, -1, 1)
+    if relu:
+        ref = torch.relu(ref)
+    torch.cuda.synchronize()
+    assert Kn.counters.get("gemm_dnn", 0) == before + 1
+    err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-30)
+    assert err < 1e-2, err

@@ -1,0 +1,138 @@
+"""Run-ahead while loops (runtime/program.py _exec_while_runahead).
+
+CPU: which loops qualify (side-effect-free bodies only) and that the CPU backend never takes
+the run-ahead path.  GPU: MultiLogReg and a vector-program loop give the same results with
+and without run-ahead, every run-ahead loop ends by discarding exactly one speculative
+iteration, the dead iteration's chain kernel returns at once (live flag), and an error
+raised only by the dead iteration is not reported."""
+import numpy as np
+import pytest
+import torch
+
+from systemml_amd.api import executor as EX
+from systemml_amd.api.mlcontext import SCRIPTS_DIR
+from systemml_amd.compiler.blocks import WhileBlock
+from systemml_amd.conf import DMLConfig
+from systemml_amd.runtime import program as PR
+
+
+def _loops(blocks, out=None):
+    out = [] if out is None else out
+    for b in blocks:
+        if isinstance(b, WhileBlock):
+            out.append(b)
+            _loops(b.body, out)
+        for attr in ("then_blocks", "else_blocks", "body"):
+            if not isinstance(b, WhileBlock) and hasattr(b, attr) and isinstance(getattr(b, attr), list):
+                _loops(getattr(b, attr), out)
+    return out
+
+
+def _qualifies(b):
+    return (not getattr(b, "inplace_vars", None) and not b.pred.is_const and PR._pure_hops([b.pred.root])
+            and PR._pure_blocks(b.body))
+
+
+def test_pure_loops_qualify_and_side_effects_do_not():
+    src = """
+    A = A0
+    s = 1
+    while (s > 0.001) {
+      A = A * 0.5
+      s = sum(A ^ 2)
+    }
+    k = 0
+    while (k < 3) {
+      k = k + 1
+      print("k " + k)
+    }
+    j = 0
+    while (j < 2) {
+      j = j + 1
+      R = rand(rows=2, cols=2)
+    }
+    """
+    cs = EX.compile_script(src, {}, inputs={"A0": np.ones((4, 4))}, outputs=["A"], config=DMLConfig())
+    loops = _loops(cs.cp.blocks)
+    assert len(loops) == 3
+    assert [_qualifies(b) for b in loops] == [True, False, False]
+
+
+def test_multilogreg_inner_cg_loop_qualifies():
+    src = open(SCRIPTS_DIR + "/algorithms/MultiLogReg.dml").read()
+    X = torch.rand(500, 16, dtype=torch.float64)
+    y = torch.randint(1, 4, (500, 1)).double()
+    cs = EX.compile_script(src, dict(X="X", Y="Y", B="B", icpt=0, reg=0.01, tol=1e-4, moi=3, mii=5),
+                           inputs={"X": X, "Y_vec": y}, outputs=["B_out"], config=DMLConfig(precision="single"))
+    loops = _loops(cs.cp.blocks)
+    # outer Newton loop prints every iteration; the inner CG loop is pure
+    assert [_qualifies(b) for b in loops] == [False, True]
+
+
+def test_cpu_backend_never_runs_ahead():
+    before = dict(PR.runahead_stats)
+    src = "A = A0\ns = 1\nwhile (s > 0.01) {\n A = A * 0.5\n s = sum(A)\n}\nprint(s)"
+    out = []
+    EX.run(src, inputs={"A0": np.ones((3, 3))}, config=DMLConfig(gpu=False), out=out.append)
+    assert PR.runahead_stats == before
+    assert float(out[0]) < 0.01
+
+
+# ----------------------------------------------------------------------------- GPU
+def _mlr(X, y, icpt, runahead, monkeypatch):
+    monkeypatch.setattr(PR, "RUNAHEAD", runahead)
+    src = open(SCRIPTS_DIR + "/algorithms/MultiLogReg.dml").read()
+    args = dict(X="X", Y="Y", B="B", icpt=icpt, reg=0.01, tol=1e-8, moi=6, mii=6)
+    ins = {"X": X, "Y_vec": y}
+    cs = EX.compile_script(src, args, inputs=ins, outputs=["B_out"], config=DMLConfig(gpu=True, precision="single"))
+    out = []
+    r, _ = EX.execute(cs, ins, out=out.append)
+    return r["B_out"].double().cpu().numpy(), out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("icpt", [0, 2])
+def test_multilogreg_same_with_and_without_runahead(monkeypatch, icpt):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand(20000, 64, generator=g).to(torch.bfloat16).cuda()
+    y = (torch.argmax(X[:, :4].float().cpu() + 0.3 * torch.rand(20000, 4, generator=g), 1) + 1).double()
+    y = y.reshape(-1, 1).cuda().float()
+    b0, out0 = _mlr(X, y, icpt, False, monkeypatch)
+    st = dict(PR.runahead_stats)
+    b1, out1 = _mlr(X, y, icpt, True, monkeypatch)
+    loops = PR.runahead_stats["loops"] - st["loops"]
+    dead = PR.runahead_stats["dead"] - st["dead"]
+    assert loops >= 3, PR.runahead_stats
+    # each loop is left by undoing the one iteration queued past its end
+    assert dead == loops, PR.runahead_stats
+    np.testing.assert_allclose(b1, b0, rtol=1e-6, atol=1e-7)
+    assert out1 == out0
+
+
+@pytest.mark.gpu
+def test_dead_iteration_errors_are_dropped():
+    """The iteration queued past the end reads v[k + 1, 1] out of bounds; only a live
+    iteration may raise."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    src = """
+    A = A0
+    v = matrix(1, rows=3, cols=1)
+    s = 100
+    k = 0
+    while (s > 0.5) {
+      A = A * 0.1
+      s = sum(A)
+      k = k + 1
+      x = as.scalar(v[k, 1])
+    }
+    print(k)
+    """
+    st = dict(PR.runahead_stats)
+    out = []
+    EX.run(src, inputs={"A0": np.full((200, 100), 0.005)}, config=DMLConfig(gpu=True, precision="double"),
+           out=out.append)
+    assert out == ["3"]
+    assert PR.runahead_stats["loops"] - st["loops"] == 1, PR.runahead_stats

@@ -111,6 +111,31 @@ def test_sparse_dispatch_through_dml():
         r, _ = EX.execute(cs, ins)
         out[gpu] = {k: float(r[k]) for k in "abcde"}
     grew = {k for k, v in kernels.counters.items() if v > before.get(k, 0)}
-    assert {"spmm_bal", "spgemm", "tsmm_sparse"} <= grew, kernels.counters
+    assert {"spmm_bal", "tsmm_sparse"} <= grew, kernels.counters
     for k in "abcde":
         assert out[True][k] == pytest.approx(out[False][k], rel=1e-8), k
+
+
+@pytest.mark.parametrize("prec", ["single", "double"])
+def test_sparse_sparse_product_elementwise(prec):
+    """S %*% T element by element against scipy: single precision runs the fp32 SpGEMM
+    kernel; double precision must not (its LDS accumulator is fp32) and matches to fp64."""
+    _need_gpu()
+    from systemml_amd.api import executor as EX
+    from systemml_amd.conf import DMLConfig
+    from systemml_amd.ops import kernels
+    import scipy.sparse as sp
+    S = sp.random(3000, 2000, density=0.01, format="csr", random_state=3)
+    T = sp.random(2000, 1500, density=0.01, format="csr", random_state=4)
+    before = kernels.counters.get("spgemm", 0)
+    r, _ = EX.execute(EX.compile_script("C = S %*% T", {}, inputs={"S": S, "T": T}, outputs=["C"],
+                                        config=DMLConfig(gpu=True, precision=prec)), {"S": S, "T": T})
+    C = r["C"]
+    C = (C.to_dense() if C.layout != torch.strided else C).double().cpu().numpy()
+    ref = (S @ T).toarray()
+    if prec == "single":
+        assert kernels.counters.get("spgemm", 0) > before
+        np.testing.assert_allclose(C, ref, rtol=1e-5, atol=1e-6)
+    else:
+        assert kernels.counters.get("spgemm", 0) == before
+        np.testing.assert_allclose(C, ref, rtol=1e-12, atol=1e-14)

@@ -192,3 +192,26 @@ def test_solvers_with_vector_programs_on_gpu(icpt):
             assert kernels.counters.get("vprog", 0) - before >= 8, kernels.counters
             assert cs.cp.licm_stats.get("if-converted", 0) >= 1
     np.testing.assert_allclose(res[True], res[False], rtol=1e-6, atol=1e-8)
+
+
+def test_if_conversion_branch_not_taken_may_fail(monkeypatch):
+    """A branch valid only under its predicate (a shape mismatch otherwise): the converted
+    block fails, the original control flow runs and takes the other branch."""
+    from systemml_amd.compiler import ifconv
+    monkeypatch.setattr(ifconv, "MODE", "force")
+    src = """
+    A = A0
+    B = matrix(2, rows=as.integer(sum(A)) - 2, cols=2)
+    i = 0
+    C = A
+    while (i < 2) {
+      i = i + 1
+      if (nrow(A) == nrow(B)) { C = A + B } else { C = A * 2 }
+    }
+    print(sum(C))
+    """
+    cs = EX.compile_script(src, {}, inputs={"A0": np.ones((3, 2))}, outputs=[], config=DMLConfig())
+    assert cs.cp.licm_stats.get("if-converted", 0) >= 1, cs.cp.licm_stats
+    out = []
+    EX.execute(cs, {"A0": np.ones((3, 2))}, out=out.append)
+    assert out == ["12.0"]
