@@ -102,11 +102,16 @@ def _vec_kind(h):
     return None
 
 
-def _dims(h):
-    """(rows, cols) when both are known at compile time, else None."""
-    if h.dt == "M" and h.dim1 is not None and h.dim2 is not None and h.dim1 >= 0 and h.dim2 >= 0:
-        return h.dim1, h.dim2
-    return None
+def _one_by_one(h):
+    """h is a 1 x 1 matrix by construction: matrix(x, rows=1, cols=1) or as.matrix(scalar).
+    (Propagated hop dimensions are not trusted for rewrites that change the operator: a
+    variable's size can differ between the iterations of a loop or the calls of a function.)"""
+    if h.op == "u" and h.p.get("o") == "cast_matrix" and h.inputs and h.inputs[0].dt == "S":
+        return True
+    if h.op == "bi" and h.p.get("name") == "matrix" and h.inputs and h.inputs[0].dt == "S":
+        args = _bi_args(h)
+        return set(args) == {"data", "rows", "cols"} and _is_lit(args["rows"], 1) and _is_lit(args["cols"], 1)
+    return False
 
 
 def _is_diag(h):
@@ -114,12 +119,49 @@ def _is_diag(h):
 
 
 def _col_vector(h):
-    """h is an n x 1 matrix with n > 1 (diag(h) builds a diagonal matrix): by construction or
-    by known dimensions."""
-    if _vec_kind(h) == "col":
-        return True
-    d = _dims(h)
-    return d is not None and d[1] == 1 and d[0] > 1
+    """h is an n x 1 matrix by construction (diag(h) builds a diagonal matrix)."""
+    return _vec_kind(h) == "col"
+
+
+def _square_product(X, Y):
+    """X %*% Y is square by construction: X %*% t(X) or t(Y) %*% Y."""
+    return (Y.op == "t" and Y.inputs[0] is X) or (X.op == "t" and X.inputs[0] is Y)
+
+
+def _fuse_rand(R, sc, o):
+    """rand(rows, cols, min=a, max=b) op s as one rand with shifted / scaled bounds (uniform
+    pdf, sparsity 1, literal bounds and a literal non-negative factor), else None."""
+    if R.op != "bi" or R.p.get("name") != "rand" or not _num_lit(sc):
+        return None
+    npos = R.p.get("npos", len(R.inputs) - len(R.named))
+    if npos:
+        return None
+    args = dict(zip(R.named, R.inputs[npos:]))
+    if set(args) - {"rows", "cols", "min", "max", "seed", "pdf", "sparsity"}:
+        return None
+    pdf = args.get("pdf")
+    if pdf is not None and not (pdf.op == "lit" and str(pdf.value).lower() == "uniform"):
+        return None
+    sp = args.get("sparsity")
+    if sp is not None and not _is_lit(sp, 1):
+        return None
+    lo, hi = args.get("min", lit(0.0)), args.get("max", lit(1.0))
+    if not (_num_lit(lo) and _num_lit(hi)):
+        return None
+    v = sc.value
+    if o == "*":
+        if v < 0:
+            return None
+        lo2, hi2 = lo.value * v, hi.value * v
+    elif o == "+":
+        lo2, hi2 = lo.value + v, hi.value + v
+    else:
+        lo2, hi2 = lo.value - v, hi.value - v
+    args = dict(args)
+    args["min"], args["max"] = lit(float(lo2)), lit(float(hi2))
+    names = list(args)
+    return Hop("bi", [args[k] for k in names], {"name": "rand", "npos": 0}, named=names, dt="M", dim1=R.dim1,
+               dim2=R.dim2, pos=R.pos)
 
 
 def _empty(h):
@@ -212,6 +254,9 @@ class Rewriter:
                 if m is not h:
                     return m
         m = self._rw_algebraic(h)
+        if m is not h:
+            return m
+        m = self._rw_more(h)
         if m is not h:
             return m
         op = h.op
@@ -380,14 +425,19 @@ class Rewriter:
             name = h.p.get("name")
             # simplifyDiagMatrixMult (Dynamic.java:1012): diag(X %*% Y) -> rowSums(X * t(Y)) when
             # X %*% Y is square (its diagonal without the n x n product)
+            if name == "diag" and len(h.inputs) == 1 and h.inputs[0].op == "tsmm":
+                # the same for an already fused tsmm: diag(X %*% t(X)) = rowSums(X ^ 2),
+                # diag(t(X) %*% X) = t(colSums(X ^ 2))
+                X = h.inputs[0].inputs[0]
+                left = h.inputs[0].p.get("left", True)
+                sq = Hop("agg", [X], {"o": "sumsq", "dir": "col" if left else "row"}, dt="M", pos=h.pos)
+                return self._hit("diag-matrix-mult", Hop("t", [sq], dt="M", pos=h.pos) if left else sq)
             if name == "diag" and len(h.inputs) == 1 and h.inputs[0].op == "mm" and not h.inputs[0].p.get("transA"):
                 X, Y = h.inputs[0].inputs
-                dx, dy = _dims(X), _dims(Y)
-                if dx is not None and dy is not None and dx[0] == dy[1] and dx[0] > 1:
-                    prod = Hop("b", [X, Hop("t", [Y], dt="M", dim1=dy[1], dim2=dy[0], pos=h.pos)], {"o": "*"}, dt="M",
-                               dim1=dx[0], dim2=dx[1], pos=h.pos)
+                if _square_product(X, Y):
+                    prod = Hop("b", [X, Hop("t", [Y], dt="M", pos=h.pos)], {"o": "*"}, dt="M", pos=h.pos)
                     return self._hit("diag-matrix-mult", Hop("agg", [prod], {"o": "sum", "dir": "row"}, dt="M",
-                                                             dim1=dx[0], dim2=1, pos=h.pos))
+                                                             pos=h.pos))
             # removeUnnecessaryReorgOperation: rev(rev(X)) -> X
             if name == "rev" and len(h.inputs) == 1 and h.inputs[0].op == "bi" \
                     and h.inputs[0].p.get("name") == "rev" and len(h.inputs[0].inputs) == 1:
@@ -409,6 +459,180 @@ class Rewriter:
             return h
         if op == "lix" and not h.p.get("list") and not h.p.get("inplace"):
             return self._rw_lix_chain(h)
+        return h
+
+    # ------------------------------------------------------------------ round-5 rules
+    def _rw_more(self, h):
+        """Further rules of RewriteAlgebraicSimplification{Static,Dynamic}.java (line numbers
+        in each comment).  Rules that look through an intermediate require this hop to be its
+        sole consumer, as the reference's parent-count checks do."""
+        op = h.op
+        sole = not any(c.id in self.multi for c in h.inputs if c.op not in ("lit", "tread"))
+        if op == "agg" and len(h.inputs) == 1:
+            x = h.inputs[0]
+            o, d = h.p["o"], h.p["dir"]
+            # simplifyNnzComputation (Dynamic:2469): sum(X != 0) -> nnz(X) (no boolean matrix)
+            if d == "all" and o == "sum" and sole and x.op == "b" and x.p["o"] == "!=" and x.dt == "M":
+                a, b = x.inputs
+                X = a if _is_lit(b, 0) else (b if _is_lit(a, 0) else None)
+                if X is not None and X.dt == "M":
+                    return self._hit("nnz", Hop("bi", [X], {"name": "_nnz", "npos": 1}, dt="S", dim1=0, dim2=0,
+                                                pos=h.pos))
+            # simplifyColwiseAggregate (Dynamic:525) / simplifyRowwiseAggregate (:581):
+            # colSums(X) of a row vector is X; of a column vector it is sum(X) (1 x 1);
+            # rowSums likewise with rows and columns swapped
+            if d in ("row", "col") and o in ("sum", "mean", "min", "max"):
+                kind = _vec_kind(x)
+                if (d == "col" and kind == "row") or (d == "row" and kind == "col"):
+                    return self._hit("colwise-aggregate", x)
+                if (d == "col" and kind == "col") or (d == "row" and kind == "row"):
+                    full = Hop("agg", [x], {"o": o, "dir": "all"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                    return self._hit("colwise-aggregate", Hop("u", [full], {"o": "cast_matrix"}, dt="M", dim1=1,
+                                                              dim2=1, pos=h.pos))
+            return h
+        if op == "u" and h.p["o"] in ("cumsum", "cumprod", "cummin", "cummax"):
+            # removeUnnecessaryCumulativeOp (Dynamic:346): a cumulative aggregate of one row is the row
+            x = h.inputs[0]
+            if _vec_kind(x) == "row":
+                return self._hit("unnecessary-cumulative", x)
+            return h
+        if op == "t":
+            x = h.inputs[0]
+            # fuseDatagenAndReorgOperation (Dynamic:487): t(matrix(s, rows=r, cols=c)) -> matrix(s, c, r)
+            if x.op == "bi" and x.p.get("name") == "matrix" and x.inputs and x.inputs[0].dt == "S" and sole:
+                args = _bi_args(x)
+                if set(args) == {"data", "rows", "cols"}:
+                    return self._hit("datagen-reorg", Hop("bi", [args["data"], args["cols"], args["rows"]],
+                                                          {"name": "matrix", "npos": 1}, named=["rows", "cols"],
+                                                          dt="M", dim1=x.dim2, dim2=x.dim1, pos=h.pos))
+            # simplifyTransposedAppend (Static:1117): t(cbind(t(A), t(B))) -> rbind(A, B) (and rbind -> cbind)
+            if x.op == "bi" and x.p.get("name") in ("cbind", "append", "rbind") and sole and not x.named \
+                    and len(x.inputs) >= 2 and all(c.op == "t" for c in x.inputs) \
+                    and x.id not in self.multi:
+                name = "rbind" if x.p["name"] in ("cbind", "append") else "cbind"
+                return self._hit("transposed-append", Hop("bi", [c.inputs[0] for c in x.inputs],
+                                                          {"name": name, "npos": len(x.inputs)}, dt="M", pos=h.pos))
+            return h
+        if op == "bi":
+            name = h.p.get("name")
+            # foldMultipleAppendOperations (Static:523): cbind(cbind(A, B), C) -> cbind(A, B, C)
+            if name in ("cbind", "rbind") and not h.named and h.inputs and all(c.dt == "M" for c in h.inputs):
+                flat, changed = [], False
+                for c in h.inputs:
+                    if c.op == "bi" and c.p.get("name") == name and not c.named and c.id not in self.multi \
+                            and all(g.dt == "M" for g in c.inputs):
+                        flat.extend(c.inputs)
+                        changed = True
+                    else:
+                        flat.append(c)
+                if changed:
+                    return self._hit("fold-append", Hop("bi", flat, {"name": name, "npos": len(flat)}, dt="M",
+                                                        pos=h.pos))
+            if name == "order":
+                return self._rw_order(h)
+            if name == "rand" and sole:
+                return h
+            return h
+        if op == "b" and len(h.inputs) == 2 and h.dt == "M":
+            a, b = h.inputs
+            o = h.p["o"]
+            # fuseMinusNzBinaryOperation (Static:1670): X - s * (X != 0) -> X -nz s (sparse-safe)
+            if o == "-" and b.op == "b" and b.p["o"] == "*" and b.id not in self.multi and a.dt == "M":
+                for sc, nz in ((b.inputs[0], b.inputs[1]), (b.inputs[1], b.inputs[0])):
+                    if sc.dt == "S" and nz.op == "b" and nz.p["o"] == "!=" and nz.id not in self.multi \
+                            and ((nz.inputs[0] is a and _is_lit(nz.inputs[1], 0)) or
+                                 (nz.inputs[1] is a and _is_lit(nz.inputs[0], 0))):
+                        return self._hit("minus-nz", Hop("bi", [a, sc], {"name": "_minus_nz", "npos": 2}, dt="M",
+                                                         dim1=a.dim1, dim2=a.dim2, pos=h.pos))
+            # fuseLogNzBinaryOperation (Static:1734): (X != 0) * log(X) -> log_nz(X) (sparse-safe)
+            if o == "*":
+                for nz, lg in ((a, b), (b, a)):
+                    if nz.op == "b" and nz.p["o"] == "!=" and lg.op in ("u", "b") and lg.p.get("o") == "log" \
+                            and nz.id not in self.multi and lg.id not in self.multi:
+                        X = lg.inputs[0]
+                        if (nz.inputs[0] is X and _is_lit(nz.inputs[1], 0)) or \
+                                (nz.inputs[1] is X and _is_lit(nz.inputs[0], 0)):
+                            args = [X] + (list(lg.inputs[1:]) if lg.op == "b" else [])
+                            return self._hit("log-nz", Hop("bi", args, {"name": "_log_nz", "npos": len(args)},
+                                                           dt="M", dim1=X.dim1, dim2=X.dim2, pos=h.pos))
+            # fuseDatagenAndBinaryOperation (Static:347): rand(min=a, max=b) * s -> rand(min=a*s,
+            # max=b*s) for s >= 0, rand(...) + s -> rand(min=a+s, max=b+s) (uniform, dense)
+            if o in ("*", "+", "-") and sole:
+                for R, sc, left in ((a, b, True), (b, a, False)):
+                    if o == "-" and not left:
+                        continue
+                    g = _fuse_rand(R, sc, o)
+                    if g is not None and R.id not in self.multi:
+                        return self._hit("datagen-binary", g)
+            # simplifyBushyBinaryOperation (Static:838): X * (Y * (Z %*% v)) -> (X * Y) * (Z %*% v)
+            # for equal-sized X, Y (the cellwise product of the two matrices first; the mv
+            # product broadcasts once)
+            # (cellwise * with matrix-vector broadcasting is associative for every valid
+            # operand shape combination, so no size checks are needed)
+            if o == "*" and b.op == "b" and b.p["o"] == "*" and b.id not in self.multi and a.dt == "M" \
+                    and a.op != "mm":
+                Y, mv = b.inputs
+                if mv.op != "mm":
+                    Y, mv = mv, Y
+                if mv.op == "mm" and _vec_kind(mv.inputs[1]) == "col" and Y.dt == "M" and Y.op != "mm":
+                    xy = Hop("b", [a, Y], {"o": "*"}, dt="M", pos=h.pos)
+                    return self._hit("bushy-binary", Hop("b", [xy, mv], {"o": "*"}, dt="M", pos=h.pos))
+            return h
+        if op == "rix" and not h.p.get("list"):
+            # simplifySlicedMatrixMult (Static:1343): (X %*% Y)[i, j] -> X[i, ] %*% Y[, j]
+            src, rl, ru, cl, cu = h.inputs
+
+            def single(lo, hi):
+                if lo.op == "lit" and lo.value is None:
+                    return False
+                return lo is hi or (_num_lit(lo) and _num_lit(hi) and lo.value == hi.value)
+            if src.op == "mm" and not src.p.get("transA") and src.id not in self.multi and single(rl, ru) \
+                    and single(cl, cu):
+                X, Y = src.inputs
+                none = lit(None)
+                xr = Hop("rix", [X, rl, ru, none, none], {}, dt="M", dim1=1, dim2=X.dim2, pos=h.pos)
+                yc = Hop("rix", [Y, none, none, cl, cu], {}, dt="M", dim1=Y.dim1, dim2=1, pos=h.pos)
+                return self._hit("sliced-matrix-mult", Hop("mm", [xr, yc], {}, dt="M", dim1=1, dim2=1, pos=h.pos))
+            return h
+        return h
+
+    def _rw_order(self, h):
+        """simplifyConstantSort (Static:1383): order of a constant matrix is the matrix (its
+        index is 1..n); simplifyOrderedSort (Static:1421): order of an ascending seq is the seq
+        (decreasing: rev(seq); index.return: 1..n or n..1)."""
+        npos = h.p.get("npos", len(h.inputs) - len(h.named))
+        args = {n: h.inputs[npos + j] for j, n in enumerate(h.named)}
+        pos_names = ["target", "by", "decreasing", "index.return"]
+        for i in range(npos):
+            args[pos_names[i]] = h.inputs[i]
+        X = args.get("target")
+        if X is None or set(args) - set(pos_names):
+            return h
+        dec = args.get("decreasing")
+        ixr = args.get("index.return")
+        if (dec is not None and not (dec.op == "lit" and isinstance(dec.value, bool))) or \
+                (ixr is not None and not (ixr.op == "lit" and isinstance(ixr.value, bool))):
+            return h
+        dec = bool(dec.value) if dec is not None else False
+        ixr = bool(ixr.value) if ixr is not None else False
+        n = _nrow(X, h.pos)
+
+        def seq(a, b, step):
+            return Hop("bi", [a, b, lit(step)], {"name": "seq", "npos": 3}, dt="M", pos=h.pos)
+        if X.op == "bi" and X.p.get("name") == "matrix" and X.inputs and _num_lit(X.inputs[0]) \
+                and set(_bi_args(X)) == {"data", "rows", "cols"}:
+            # stable sort of equal keys: the identity permutation
+            return self._hit("constant-sort", seq(lit(1), n, 1) if ixr else X)
+        if X.op == "bi" and X.p.get("name") == "seq" and not X.named and X.p.get("npos", 0) in (2, 3):
+            sa = X.inputs
+            step = sa[2] if len(sa) == 3 else lit(1)
+            if not (_num_lit(step) and step.value > 0 and _num_lit(sa[0]) and _num_lit(sa[1])
+                    and sa[0].value <= sa[1].value) or (args.get("by") is not None and not _is_lit(args["by"], 1)):
+                return h
+            if ixr:
+                return self._hit("ordered-sort", seq(n, lit(1), -1) if dec else seq(lit(1), n, 1))
+            return self._hit("ordered-sort", Hop("bi", [X], {"name": "rev", "npos": 1}, dt="M", pos=h.pos) if dec
+                             else X)
         return h
 
     def _rw_lix_chain(self, h):
@@ -628,7 +852,7 @@ class Rewriter:
             # simplifyScalarMatrixMult (Dynamic.java:922): y %*% X -> as.scalar(y) * X and
             # X %*% y -> X * as.scalar(y) for a 1 x 1 y
             for y, X in ((a, b), (b, a)):
-                if _dims(y) == (1, 1) and X.dt == "M" and _dims(X) != (1, 1):
+                if _one_by_one(y) and X.dt == "M":
                     sc = Hop("u", [y], {"o": "cast_scalar"}, dt="S", dim1=0, dim2=0, pos=h.pos)
                     return self._hit("scalar-matrix-mult", Hop("b", [X, sc], {"o": "*"}, dt="M", dim1=X.dim1,
                                                                dim2=X.dim2, pos=h.pos))

@@ -146,8 +146,13 @@ class Translator:
             from . import ipa
             self._specialise_functions(cp)
             ipa.run(cp, self.config)                # inter-procedural analysis (inlining, ...)
+            from .forvec import run as forvec
+            fv = forvec(cp, self.config)           # for-loop vectorization (whole-range operations)
+            from .splitdag import run as splitdag
+            fv.update(splitdag(cp, self.config))   # cut blocks after data-dependent operators
             from .loops import hoist_program
             cp.licm_stats = hoist_program(cp)      # before liveness: adds blocks / variables
+            cp.licm_stats.update(fv)
             from .loops import mark_program
             cp.licm_stats.update(mark_program(cp))
             from .speculate import run as speculate

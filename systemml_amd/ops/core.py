@@ -504,6 +504,9 @@ def _colsum_kernel(x):
     return cell._kernel(_COLSUM[0], [x])
 
 
+_KAGG = {"sum", "sumsq", "mean", "min", "max", "prod", "var", "sd", "imax", "imin"}
+
+
 def agg(o, d, x):
     # fast path: dense host tensors (the CP backend's solver state) -- no representation checks
     if type(x) is Tensor and x.layout is _STRIDED and not x.is_cuda and x.dtype is not torch.bfloat16 \
@@ -555,6 +558,13 @@ def agg(o, d, x):
         r = _colsum_kernel(x)
         if r is not None:
             return r
+    if backend.use_kernels and x.is_cuda and x.layout is _STRIDED and x.numel() > 0 and o in _KAGG \
+            and x.dim() == 2 and (d != "all" or o not in ("sum", "sumsq")):
+        # the eager long tail on agg.hip (sum / sumsq over all cells mostly arrive fused)
+        from . import kernels
+        r = kernels.agg(o, d, x)
+        if r is not None:
+            return _lazy_out(r) if d == "all" else r
     x = cvt(x)
     if d == "all":
         if x.numel() == 0:
@@ -908,8 +918,27 @@ def lix(x, y, rl, ru, cl, cu, list_mode=False, owned=None):
     r0, r1 = _bound(rl, 1), _bound(ru, nr)
     c0, c1 = _bound(cl, 1), _bound(cu, nc)
     _check_range(r0, r1, c0, c1, nr, nc)
-    if owned is not None and type(x) is Tensor and x.layout == torch.strided and x in owned \
-            and cvt(x) is x:
+    inplace = owned is not None and type(x) is Tensor and x.layout == torch.strided and x in owned and cvt(x) is x
+    if backend.use_kernels and type(x) is Tensor and x.is_cuda and x.layout == torch.strided and x.dim() == 2:
+        # one pass on reorg.hip: every output cell written once (or only the window, in place)
+        xc = cvt(x).contiguous()
+        yv = y
+        if isinstance(y, Tensor):
+            yv = cvt(y)
+            if tuple(yv.shape) != (r1 - r0 + 1, c1 - c0 + 1):
+                if yv.numel() != 1:
+                    raise DMLRuntimeError(f"left indexing dimension mismatch: target [{r0}:{r1},{c0}:{c1}] "
+                                          f"vs source {yv.shape[0]}x{yv.shape[1]}")
+                yv = float(yv.reshape(-1)[0].item())
+        else:
+            yv = float(_num(y))
+        out = xc if (inplace and xc is x) else torch.empty_like(xc)
+        from . import kernels
+        if kernels.lix(xc, yv, out, r0 - 1, r1, c0 - 1, c1):
+            if owned is not None and out is not x:
+                owned.add(out)
+            return out
+    if inplace:
         out = x
     else:
         out = cvt(x).clone()

@@ -129,6 +129,18 @@ def load(required=False):
     L.sysml_pad_pixels.restype = ctypes.c_int
     L.sysml_pad_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
+    L.sysml_agg.restype = ctypes.c_int
+    L.sysml_agg.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+    L.sysml_agg_scratch.restype = ctypes.c_int64
+    L.sysml_agg_scratch.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int]
+    L.sysml_cat.restype = ctypes.c_int
+    L.sysml_cat.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+    L.sysml_lix.restype = ctypes.c_int
+    L.sysml_lix.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                            ctypes.c_uint64, ctypes.c_void_p]
     L.sysml_set_live.restype = None
     L.sysml_set_live.argtypes = [ctypes.c_void_p]
     L.sysml_chain4m_occupancy.restype = ctypes.c_int
@@ -762,16 +774,21 @@ class _WeightCasts:
     def __init__(self):
         self._d = {}
 
-    def get(self, t, dev, dt, trans=False):
+    def get(self, t, dev, dt, trans=False, pad8=False):
         """t (2-D) cast to dt on dev; trans: its transpose, contiguous (the K-major filter
-        operand of a backward-data GEMM)."""
+        operand of a backward-data GEMM); pad8: rows zero-padded to a multiple of 8 columns (a
+        16-B aligned row pitch for the GEMM's LDS-DMA staging; the padding is never read as data)."""
         import weakref
-        k = (id(t), trans)
+        k = (id(t), trans, pad8)
         e = self._d.get(k)
         if e is not None and e[0]() is t and e[1] == t._version and e[2].device == dev and e[2].dtype == dt:
             return e[2]
         c = t.to(device=dev, dtype=dt)
         c = (c.t() if trans else c).contiguous()
+        if pad8 and c.shape[1] % 8:
+            p = torch.zeros((c.shape[0], (c.shape[1] + 7) & ~7), dtype=c.dtype, device=c.device)
+            p[:, :c.shape[1]] = c
+            c = p
         dd = self._d
         ref = weakref.ref(t, lambda _r, k=k: dd.pop(k, None) if dd.get(k, (None,))[0] is _r else None)
         dd[k] = (ref, t._version, c)
@@ -869,46 +886,45 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
         shape = (F, C * KH * KW)
     Wsrc = W0 if W0 is not None else W         # the filter as given (cache key of its transposed bf16 copy)
     if CONV1X1_GEMM and mode != 2 and KH == 1 and KW == 1 and sh == 1 and sw == 1 and ph == 0 and pw == 0 \
-            and dt == torch.bfloat16 and C % 8 == 0 and F % 8 == 0 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
         # a 1x1 stride-1 convolution of bf16 activations is ONE GEMM over all images (gemm.hip
         # image-blocked columns): forward W . X[n], backward data t(W) . dY[n]; bias + relu in
         # the epilogue, bf16 out / fp32 accumulate
         HW = H * Wd
         y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
         if mode == 0:
-            _gemm_img(W, X, y, F, C, N, HW, bias=bias, relu=relu)
+            _gemm_img(_wcast.get(Wsrc, dev, dt, pad8=True), X, y, F, C, N, HW, bias=bias, relu=relu)
         else:
-            _gemm_img(_wcast.get(Wsrc, dev, dt, trans=True), D, y, C, F, N, HW)
+            _gemm_img(_wcast.get(Wsrc, dev, dt, trans=True, pad8=True), D, y, C, F, N, HW)
         _count(("conv2d", "conv2d_bwd_data")[mode])
         _count("conv1x1_gemm")
         return y
     if CONV1X1_GEMM and mode == 0 and KH * KW > 1 and Ho * Wo <= IM2COL_MAX_HW and C > 8 \
-            and dt == torch.bfloat16 and F % 8 == 0 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
         # small-image convolutions: an im2col gather (pixels padded to a multiple of 8) and ONE
         # image-blocked GEMM over all images
         CKK, P = C * KH * KW, Ho * Wo
         Pp = (P + 7) & ~7
-        if CKK % 8 == 0:
-            cols = torch.empty((N, CKK, Pp), dtype=torch.bfloat16, device=dev)
-            L.sysml_im2col_pad.restype = ctypes.c_int
-            L.sysml_im2col_pad.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 11 + \
-                [ctypes.c_void_p]
-            rc = L.sysml_im2col_pad(3, X.data_ptr(), cols.data_ptr(), N, C, H, Wd, KH, KW, sh, sw, ph, pw, Pp, _stream())
-            if rc != 0:
-                raise RuntimeError(f"sysml_im2col failed: {rc}")
-            y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
-            _gemm_img(W, cols, y, F, CKK, N, P, hwb=Pp, bias=bias, relu=relu)
-            _count("conv2d")
-            _count("conv_im2col")
-            return y
+        cols = torch.empty((N, CKK, Pp), dtype=torch.bfloat16, device=dev)
+        L.sysml_im2col_pad.restype = ctypes.c_int
+        L.sysml_im2col_pad.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 11 + \
+            [ctypes.c_void_p]
+        rc = L.sysml_im2col_pad(3, X.data_ptr(), cols.data_ptr(), N, C, H, Wd, KH, KW, sh, sw, ph, pw, Pp, _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_im2col failed: {rc}")
+        y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
+        _gemm_img(_wcast.get(Wsrc, dev, dt, pad8=True), cols, y, F, CKK, N, P, hwb=Pp, bias=bias, relu=relu)
+        _count("conv2d")
+        _count("conv_im2col")
+        return y
     if CONV1X1_GEMM and mode == 1 and (sh > 1 or sw > 1 or (KH > 1 and H * Wd <= COL2IM_MAX_HW)) \
-            and dt == torch.bfloat16 and F % 8 == 0 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+            and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
         # backward data as cols = t(W) . dY[n] (one image-blocked GEMM, bf16) + a col2im gather:
         # a strided convolution's taps land on the stride grid for a quarter of the (pixel, tap)
         # pairs, which the implicit GEMM would multiply as zeros
         CKK, P = C * KH * KW, Ho * Wo
         cols = torch.empty((N, CKK, P), dtype=torch.bfloat16, device=dev)
-        _gemm_img(_wcast.get(Wsrc, dev, dt, trans=True), D, cols, CKK, F, N, P)
+        _gemm_img(_wcast.get(Wsrc, dev, dt, trans=True, pad8=True), D, cols, CKK, F, N, P)
         y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
         L.sysml_col2im.restype = ctypes.c_int
         L.sysml_col2im.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 10 + \
@@ -1025,6 +1041,113 @@ def relu_backward(X, D):
 # Column-wise cumulative aggregates (ops/hip/scan.hip)
 # ----------------------------------------------------------------------------
 _CUM = {"cumsum": 0, "cumprod": 1, "cummin": 2, "cummax": 3}
+
+
+_AGG_OPS = {"sum": 0, "sumsq": 1, "mean": 2, "min": 3, "max": 4, "prod": 5, "var": 6, "sd": 7, "imax": 8, "imin": 9}
+_AGG_DIR = {"all": 0, "row": 1, "col": 2}
+_AGG_XDT = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2}
+
+
+def agg(o, d, X):
+    """Unary aggregate of a dense device matrix on ops/hip/agg.hip (fp64 accumulation, bf16 /
+    fp32 / fp64 read as stored).  d = 'all' -> 0-d fp64 tensor; 'row' -> N x 1; 'col' -> 1 x D.
+    None when the operator / layout is not covered."""
+    op, dr, xdt = _AGG_OPS.get(o), _AGG_DIR.get(d), _AGG_XDT.get(X.dtype)
+    if op is None or dr is None or xdt is None or X.dim() != 2 or (op >= 8 and dr != 1):
+        return None
+    L = load(required=True)
+    N, D = X.shape
+    if N == 0 or D == 0:
+        return None
+    X = X.contiguous()
+    ydt = torch.float64 if (X.dtype == torch.float64 or (X.dtype == torch.bfloat16 and backend.dtype == torch.float64)) \
+        else torch.float32
+    if dr == 0:
+        Y = torch.empty((), dtype=torch.float64, device=X.device)
+    elif dr == 1:
+        Y = torch.empty((N, 1), dtype=ydt, device=X.device)
+    else:
+        Y = torch.empty((1, D), dtype=ydt, device=X.device)
+    nscr = L.sysml_agg_scratch(dr, N, D)
+    scr = torch.empty((max(nscr, 8),), dtype=torch.uint8, device=X.device)
+    rc = L.sysml_agg(op, dr, xdt, 2 if (dr == 0 or ydt == torch.float64) else 1, X.data_ptr(), Y.data_ptr(),
+                     scr.data_ptr(), N, D, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_agg failed: {rc}")
+    _count("agg." + o)
+    return Y
+
+
+_ESIZE = {torch.bfloat16: 2, torch.float32: 4, torch.float64: 8}
+
+
+def cat(rows, mats):
+    """cbind (rows=False) / rbind (rows=True) of dense device matrices of one dtype in one pass
+    (ops/hip/reorg.hip); None when not covered (mixed dtypes / devices, > 16 operands)."""
+    if not mats or len(mats) > 16:
+        return None
+    dt, dev = mats[0].dtype, mats[0].device
+    if dt not in _ESIZE or any(m.dtype != dt or m.device != dev or not m.is_cuda or m.dim() != 2
+                               or m.layout != torch.strided for m in mats):
+        return None
+    L = load(required=True)
+    mats = [m.contiguous() for m in mats]
+    if rows:
+        N, D = sum(m.shape[0] for m in mats), mats[0].shape[1]
+        sizes = [m.shape[0] for m in mats]
+    else:
+        N, D = mats[0].shape[0], sum(m.shape[1] for m in mats)
+        sizes = [m.shape[1] for m in mats]
+    out = torch.empty((N, D), dtype=dt, device=dev)
+    if N == 0 or D == 0:
+        return out
+    keep = [m for m in mats if m.numel() > 0]
+    n = len(keep)
+    srcs = (ctypes.c_void_p * n)(*[m.data_ptr() for m in keep])
+    offs, acc = [], 0
+    for m in keep:
+        offs.append(acc)
+        acc += m.shape[0] if rows else m.shape[1]
+    offs.append(acc)
+    off = (ctypes.c_int64 * (n + 1))(*offs)
+    ld = (ctypes.c_int64 * n)(*[m.shape[1] for m in keep])
+    del sizes
+    rc = L.sysml_cat(int(bool(rows)), _ESIZE[dt], n, srcs, off, ld, out.data_ptr(), N, D, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_cat failed: {rc}")
+    _count("rbind" if rows else "cbind")
+    return out
+
+
+def lix(X, Y, out, r0, r1, c0, c1):
+    """out = X with out[r0:r1, c0:c1] = Y (0-based, half-open; Y a wr x wc tensor or a Python
+    number) in one pass; out may be X itself (only the window is written).  False when not
+    covered."""
+    if X.dtype not in _ESIZE or not X.is_cuda or X.dim() != 2 or not X.is_contiguous() or out.dtype != X.dtype \
+            or not out.is_contiguous():
+        return False
+    L = load(required=True)
+    import struct
+    scalar = not isinstance(Y, torch.Tensor)
+    sbits = 0
+    yp = None
+    if scalar:
+        v = float(Y)
+        if X.dtype == torch.float64:
+            sbits = struct.unpack("<Q", struct.pack("<d", v))[0]
+        elif X.dtype == torch.float32:
+            sbits = struct.unpack("<I", struct.pack("<f", v))[0]
+        else:
+            sbits = int(torch.tensor([v], dtype=torch.bfloat16).view(torch.int16).item()) & 0xFFFF
+    else:
+        Y = Y.to(device=X.device, dtype=X.dtype).contiguous()
+        yp = Y.data_ptr()
+    rc = L.sysml_lix(_ESIZE[X.dtype], X.data_ptr(), yp, out.data_ptr(), X.shape[0], X.shape[1], r0, r1, c0, c1,
+                     int(scalar), sbits, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_lix failed: {rc}")
+    _count("lix")
+    return True
 
 
 def cumagg(op, X):

@@ -420,6 +420,11 @@ def b_cbind(ctx, *args, **kw):
     for m in ms[1:]:
         if m.shape[0] != r:
             raise DMLRuntimeError(f"cbind: number of rows do not match ({r} vs {m.shape[0]})")
+    if backend.use_kernels and ms[0].is_cuda:
+        from ..ops import kernels
+        out = kernels.cat(False, ms)
+        if out is not None:
+            return out
     return torch.cat(ms, dim=1)
 
 
@@ -448,6 +453,11 @@ def b_rbind(ctx, *args, **kw):
     for m in ms[1:]:
         if m.shape[1] != c:
             raise DMLRuntimeError(f"rbind: number of columns do not match ({c} vs {m.shape[1]})")
+    if backend.use_kernels and ms[0].is_cuda:
+        from ..ops import kernels
+        out = kernels.cat(True, ms)
+        if out is not None:
+            return out
     return torch.cat(ms, dim=0)
 
 
@@ -581,6 +591,48 @@ def b_dp_allreduce(ctx, *grads):
         out.append(flat[off:off + n].reshape(m.shape).to(device=m.device, dtype=m.dtype))
         off += n
     return tuple(out)
+
+
+# sparse-safe fused operators of compiler/rewrites.py (reference: the nnz / minus-nz / log-nz
+# fusions of RewriteAlgebraicSimplification{Dynamic,Static}.java): on CSR operands they touch the
+# stored values only, so a sparse X stays sparse
+def _nz_apply(x, fn):
+    if isinstance(x, Tensor) and x.layout == torch.sparse_csr:
+        v = fn(x.values())
+        return torch.sparse_csr_tensor(x.crow_indices(), x.col_indices(), v, x.shape, device=v.device)
+    m = _mat(x)
+    return torch.where(m != 0, fn(m), torch.zeros((), dtype=m.dtype, device=m.device))
+
+
+@builtin("_nnz")
+def b_nnz(ctx, x):
+    """sum(X != 0) without the boolean matrix."""
+    if isinstance(x, Tensor) and x.layout == torch.sparse_csr:
+        return float(torch.count_nonzero(x.values()).item())     # a sum: DOUBLE, as before the rewrite
+    if C.is_dist(x):
+        return C.agg("sum", "all", C.binary("!=", x, 0))
+    return float(torch.count_nonzero(_mat(x)).item())
+
+
+@builtin("_minus_nz")
+def b_minus_nz(ctx, x, s):
+    """X - s * (X != 0)."""
+    if C.is_dist(x):
+        return C.binary("-", x, C.binary("*", s, C.binary("!=", x, 0)))
+    sv = _float(s)
+    return _nz_apply(x, lambda v: v - sv)
+
+
+@builtin("_log_nz")
+def b_log_nz(ctx, x, base=None):
+    """(X != 0) * log(X [, base])."""
+    if C.is_dist(x):
+        lg = C.unary("log", x) if base is None else C.binary("log", x, base)
+        return C.binary("*", C.binary("!=", x, 0), lg)
+    if base is None:
+        return _nz_apply(x, torch.log)
+    lb = float(np.log(_float(base)))
+    return _nz_apply(x, lambda v: torch.log(v) / lb)
 
 
 @builtin("_sel")

@@ -21,6 +21,8 @@ from .scalars import DevScalar
 
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell",
                   "magg", "row", "outer", "vprog"}
+# builtins with their own CSR paths (the sparse-safe fused operators of compiler/rewrites.py)
+_SPARSE_OK_BI = {"_nnz", "_minus_nz", "_log_nz"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
 _CC_OK_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "rix", "t", "cell", "magg", "row"}
 _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "round", "floor", "ceil", "sign",
@@ -44,7 +46,8 @@ def make_impl(h):
     fn, code = _make_impl(h)
     if h.op in _COMPUTE_OPS and not (h.op == "bi" and h.p.get("name") in _NO_PLACE_BI):
         fn = _placed(fn, h)
-    sparse_ok = h.op in _SPARSE_OK_OPS or (h.op == "u" and h.p.get("o") in _SPARSE_OK_UNARY)
+    sparse_ok = h.op in _SPARSE_OK_OPS or (h.op == "u" and h.p.get("o") in _SPARSE_OK_UNARY) or \
+        (h.op == "bi" and h.p.get("name") in _SPARSE_OK_BI)
     lazy_ok = h.op in _LAZY_OK_OPS
     if sparse_ok and lazy_ok:
         return fn, code

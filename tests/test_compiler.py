@@ -231,7 +231,9 @@ ALGEBRAIC_CASES = [
     ("R = matrix(X, rows=nrow(X), cols=ncol(X)) + 1", "unnecessary-reshape"),
     ("R = X[1:nrow(X), 1:ncol(X)] + 1", "unnecessary-indexing"),
     ("R = X[, ] * 2", "unnecessary-indexing"),
-    ("s = sum(diag(t(X) %*% X))", "sum-diag-trace"),
+    # diag(t(X) %*% X) = t(colSums(X ^ 2)) (simplifyDiagMatrixMult on the fused tsmm) comes
+    # first bottom-up; the sum of it then folds to one sum of squares
+    ("s = sum(diag(t(X) %*% X))", "diag-matrix-mult"),
 ]
 
 

@@ -1,16 +1,19 @@
 #!/bin/bash
-# Run-ahead while loops + image-blocked DNN GEMM: GPU tests, the headline at the 8-GPU per-rank
-# size (1.25M rows) and at 10M rows with run-ahead off / on, a kernel trace with idle-gap
-# attribution, then ResNet-50 b256.
+# Round-5 validation A: new-kernel GPU tests (run-ahead, DNN GEMM, aggregates, reorg), the
+# headline at 1.25M / 10M rows with run-ahead off / on, ResNet-50 b256, and a 1.25M-row kernel
+# trace with idle-gap attribution.
 R=$GRAFT_REPO_ROOT
 cd $R
 mkdir -p gpurun_out
 P=$R/gpurun_out/ra_progress.txt
 echo "start $(date)" > $P
-timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+timeout -k 10 600 python -u -m pytest -q --timeout 120 --timeout-method thread -m gpu \
     tests/test_runahead.py tests/test_vector_template.py tests/test_headline_fusion.py tests/test_gemm_gpu.py \
-    tests/test_act_bf16.py tests/test_sparse_gpu.py > gpurun_out/ra_tests.log 2>&1
-rc=$?; echo "tests rc=$rc $(date)" >> $P; [ $rc -ne 0 ] && exit $rc
+    tests/test_act_bf16.py tests/test_sparse_gpu.py tests/test_agg_gpu.py tests/test_reorg_gpu.py \
+    > gpurun_out/ra_tests.log 2>&1
+rc=$?; echo "tests rc=$rc $(date)" >> $P
+# keep going after ordinary test failures (rc 1); stop on crashes / timeouts
+[ $rc -gt 1 ] && exit $rc
 for ra in 0 1; do
   SYSML_RUNAHEAD=$ra timeout -k 10 300 python -u bench.py --rows 1250000 --steps 10 --warmup 3 > gpurun_out/ra_1250k_$ra.log 2>&1
   rc=$?; echo "1250k ra=$ra rc=$rc $(date)" >> $P; [ $rc -ne 0 ] && exit $rc
