@@ -11,6 +11,7 @@ which `Caffe2DML.load(dir)` reads back.
 from __future__ import annotations
 
 import os
+import struct
 
 import numpy as np
 
@@ -119,13 +120,135 @@ def convertImageToNumPyArr(im, img_shape=None, add_rotated_images=False, add_mir
 
 
 def convert_lmdb_to_jpeg(lmdb_img_file, output_dir):
-    """Needs the lmdb, caffe and cv2 packages (not part of this framework's dependencies)."""
+    """Saves the images of a caffe LMDB database as output_dir/file_<i>.jpg (reference
+    converters.py:111, which needs caffe, lmdb and cv2).  Here the caffe Datum records are
+    decoded by this module's protobuf reader, the database is read with the `lmdb` package when
+    it is installed and otherwise by a read-only reader of the LMDB file format (_lmdb_records),
+    and the images are written with PIL.  Datum pixels are stored BGR (caffe); they are written
+    as the colours they encode."""
+    from PIL import Image
+    os.makedirs(output_dir, exist_ok=True)
+    i = 1
+    for _, value in _lmdb_records(lmdb_img_file):
+        arr, _label = decode_datum(value)
+        img = np.transpose(arr, (1, 2, 0))                  # C x H x W -> H x W x C
+        if img.shape[2] == 3:
+            img = img[:, :, ::-1]                            # BGR -> RGB for PIL
+        img = np.clip(img, 0, 255).astype(np.uint8)
+        Image.fromarray(img[:, :, 0] if img.shape[2] == 1 else img).save(
+            os.path.join(output_dir, "file_" + str(i) + ".jpg"), format="JPEG", quality=95)
+        i += 1
+    return i - 1
+
+
+def decode_datum(buf):
+    """caffe.proto Datum (channels 1, height 2, width 3, data 4, label 5, float_data 6, encoded 7)
+    -> (C x H x W float array, label)."""
+    c = h = w = 1
+    data, fdata, label, encoded = None, [], 0, False
+    for fno, wt, v in _fields(bytes(buf)):
+        if fno == 1:
+            c = v
+        elif fno == 2:
+            h = v
+        elif fno == 3:
+            w = v
+        elif fno == 4:
+            data = v
+        elif fno == 5:
+            label = v
+        elif fno == 6:
+            fdata.extend(np.frombuffer(v, dtype="<f4") if wt == 2 else [struct.unpack("<f", v)[0]])
+        elif fno == 7:
+            encoded = bool(v)
+    if encoded:
+        import io
+        from PIL import Image
+        im = np.asarray(Image.open(io.BytesIO(data)))
+        im = im[:, :, None] if im.ndim == 2 else im[:, :, ::-1]      # decoded RGB -> stored BGR
+        return np.transpose(im, (2, 0, 1)).astype(np.float64), label
+    if data is not None and len(data):
+        arr = np.frombuffer(data, dtype=np.uint8).astype(np.float64)
+    else:
+        arr = np.asarray(fdata, dtype=np.float64)
+    return arr.reshape(c, h, w), label
+
+
+def _lmdb_records(path):
     try:
-        import lmdb  # noqa: F401
-        import cv2  # noqa: F401
-    except ImportError as e:
-        raise ImportError("convert_lmdb_to_jpeg needs the 'lmdb' and 'cv2' packages") from e
-    raise NotImplementedError("LMDB image export requires caffe's Datum protobuf")
+        import lmdb
+    except ImportError:
+        yield from read_lmdb(path)
+        return
+    env = lmdb.open(path, readonly=True, lock=False)
+    with env.begin() as txn:
+        for k, v in txn.cursor():
+            yield bytes(k), bytes(v)
+
+
+# LMDB on-disk format (read-only, 64-bit): meta pages 0 / 1 (the newer transaction wins), a
+# B+tree of branch / leaf pages from the main database's root, values larger than a node in
+# overflow pages.
+_P_BRANCH, _P_LEAF, _P_OVERFLOW, _P_LEAF2 = 0x01, 0x02, 0x04, 0x20
+_F_BIGDATA, _F_SUBDATA, _F_DUPDATA = 0x01, 0x02, 0x04
+_MDB_MAGIC = 0xBEEFC0DE
+
+
+def read_lmdb(path):
+    """Key / value pairs of an LMDB database (a directory with data.mdb, or the file), in key
+    order, without the lmdb package."""
+    import mmap
+    fn = os.path.join(path, "data.mdb") if os.path.isdir(path) else path
+    with open(fn, "rb") as f:
+        mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+    try:
+        # page 0: header (16 B) + MDB_meta {magic, version, address, mapsize, dbs[2] (48 B each),
+        # last_pg, txnid}; the page size is the free DB's md_pad of meta 0
+        magic, _version = struct.unpack_from("<II", mm, 16)
+        if magic != _MDB_MAGIC:
+            raise ValueError(f"{fn}: not an LMDB file (magic {magic:#x})")
+        psize = struct.unpack_from("<I", mm, 16 + 24)[0]          # dbs[0].md_pad = page size
+
+        def meta(pg):
+            o = pg * psize + 16
+            main = o + 24 + 48                                   # mm_dbs[1]
+            root = struct.unpack_from("<Q", mm, main + 40)[0]
+            entries = struct.unpack_from("<Q", mm, main + 32)[0]
+            txnid = struct.unpack_from("<Q", mm, o + 24 + 96 + 8)[0]
+            flags = struct.unpack_from("<H", mm, main + 4)[0]
+            return txnid, root, entries, flags
+        m = max(meta(0), meta(1))
+        _, root, entries, dbflags = m
+        if entries == 0 or root == 0xFFFFFFFFFFFFFFFF:
+            return
+        if dbflags & 0x04:                                       # MDB_DUPSORT
+            raise ValueError("LMDB databases with duplicate keys are not supported")
+
+        def walk(pg):
+            o = pg * psize
+            flags = struct.unpack_from("<H", mm, o + 10)[0]
+            lower = struct.unpack_from("<H", mm, o + 12)[0]
+            n = (lower - 16) // 2
+            ptrs = struct.unpack_from(f"<{n}H", mm, o + 16)
+            for p in ptrs:
+                no = o + p
+                lo, hi, nflags, ksize = struct.unpack_from("<HHHH", mm, no)
+                key = bytes(mm[no + 8:no + 8 + ksize])
+                if flags & _P_BRANCH:
+                    child = lo | (hi << 16) | (nflags << 32)
+                    yield from walk(child)
+                elif flags & _P_LEAF:
+                    dsize = lo | (hi << 16)
+                    d = no + 8 + ksize
+                    if nflags & _F_BIGDATA:
+                        opg = struct.unpack_from("<Q", mm, d)[0]
+                        start = opg * psize + 16
+                        yield key, bytes(mm[start:start + dsize])
+                    else:
+                        yield key, bytes(mm[d:d + dsize])
+        yield from walk(root)
+    finally:
+        mm.close()
 
 
 # ----------------------------------------------------------------------------

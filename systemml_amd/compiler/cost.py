@@ -445,33 +445,63 @@ def _deep_copy(roots, env_out):
 
 
 def _walk_program(cp, env, visit_bb):
+    """Size propagation over the program: each basic block is visited with the shapes of the
+    variables live into it; loops and branches merge shapes (unknown when they differ).
+    Function bodies are visited with their parameters' shapes when every call site agrees on
+    them (reference hops/ipa/FunctionCallSizeInfo.java): call sites in the main program outside
+    loops, where the argument shapes are exact; otherwise the parameters are unknown and the
+    body is planned at run time."""
     from .loops import assigned_in
+    sites = {}           # function key -> list of {param: shape} (None: a site we cannot size)
 
-    def blocks(bl, env):
+    def record_calls(b, dims, exact):
+        for h in H.walk(list(b.roots) + list(b.env_out.values())):
+            if h.op != "fcall":
+                continue
+            k = h.p.get("fkey")
+            given = list(h.p.get("given", ()))
+            if not exact or len(given) != len(h.inputs):
+                sites.setdefault(k, []).append(None)
+            else:
+                sites.setdefault(k, []).append({n: dims.get(a.id, UNK) for n, a in zip(given, h.inputs)})
+
+    def blocks(bl, env, exact):
         for b in bl:
             if isinstance(b, BasicBlock):
                 dims = visit_bb(b, env)
+                record_calls(b, dims, exact)
                 for k, h in b.env_out.items():
                     env[k] = dims.get(h.id, UNK)
             elif isinstance(b, IfBlock):
                 e1, e2 = dict(env), dict(env)
-                blocks(b.then_blocks, e1)
-                blocks(b.else_blocks, e2)
+                blocks(b.then_blocks, e1, exact)
+                blocks(b.else_blocks, e2, exact)
                 for k in set(e1) | set(e2):
                     env[k] = e1.get(k, UNK) if e1.get(k, UNK) == e2.get(k, UNK) else UNK
             elif isinstance(b, (WhileBlock, ForBlock)):
                 if isinstance(b, ForBlock):
                     env[b.var] = SCALAR
                 body_env = dict(env)
-                blocks(b.body, body_env)
+                blocks(b.body, body_env, False)
                 for k in assigned_in(b.body):
                     if body_env.get(k, UNK) != env.get(k, UNK):
                         env[k] = UNK
-    blocks(cp.blocks, env)
-    for fb in cp.functions.values():
+    blocks(cp.blocks, env, True)
+    for key, fb in cp.functions.items():
         if fb.body is not None:
             fenv = {p.name: (SCALAR if p.dtype == "SCALAR" else UNK) for p in fb.inputs}
-            blocks(fb.body, fenv)
+            ss = sites.get(key)
+            if ss and all(x is not None for x in ss) and not getattr(fb, "recursive", False):
+                for p in fb.inputs:
+                    shapes = {x.get(p.name, UNK) for x in ss}
+                    if p.dtype != "SCALAR" and len(shapes) == 1:
+                        sh = shapes.pop()
+                        if _known(sh) and sh != SCALAR:
+                            fenv[p.name] = sh
+                            if not hasattr(cp, "fcall_sized"):
+                                cp.fcall_sized = set()
+                            cp.fcall_sized.add((key, p.name))
+            blocks(fb.body, fenv, False)
 
 
 def reorder_chains(cp, inputs=None):

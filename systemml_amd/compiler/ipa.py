@@ -15,7 +15,11 @@ instruction generation):
      enforced by casts) — the caller's rewrites then see through the call (e.g. fused
      operators across nn layer boundaries), and the call frame disappears;
   4. literal propagation: a scalar parameter that every call site passes as the same
-     literal (and the body never reassigns) is replaced by that literal in the body.
+     literal (and the body never reassigns) is replaced by that literal in the body;
+  5. constant binary operations (IPAPassRemoveConstantBinaryOps): products with a main-program
+     matrix of ones become products with the literal 1.
+Static size propagation into function bodies (FunctionCallSizeInfo) is part of the program
+walk of compiler/cost.py.
 """
 from __future__ import annotations
 
@@ -287,6 +291,50 @@ def propagate_literals(cp, stats):
         stats["literals"] = stats.get("literals", 0) + len(consts)
 
 
+def _is_ones(h):
+    """matrix(1, rows=.., cols=..): a constant datagen of ones."""
+    if h.op != "bi" or h.p.get("name") != "matrix" or not h.inputs:
+        return False
+    d = h.inputs[0]
+    return d.op == "lit" and isinstance(d.value, (int, float)) and not isinstance(d.value, bool) and d.value == 1
+
+
+def remove_constant_binary_ops(cp, stats):
+    """IPAPassRemoveConstantBinaryOps (reference hops/ipa/IPAPassRemoveConstantBinaryOps.java):
+    a main-program variable assigned matrix(1, ...) in a basic block and not reassigned later
+    makes every later `M * ones` (and `ones * M`, M a matrix) a `M * 1`, which the algebraic
+    rewrites then drop -- e.g. the all-ones weight vectors scripts default to."""
+    from .loops import assigned_in
+    ones = {}
+    n = [0]
+
+    def rewrite(blocks):
+        for owner, roots in _block_dags(blocks):
+            for h in H.walk(roots):
+                if h.op == "b" and h.p.get("o") == "*" and len(h.inputs) == 2:
+                    a, b = h.inputs
+                    for i, (x, y) in enumerate(((a, b), (b, a))):
+                        if y.op == "tread" and y.p.get("name") in ones and x.dt == "M":
+                            ins = list(h.inputs)
+                            ins[1 - i] = lit(1)
+                            h.inputs = ins
+                            n[0] += 1
+                            break
+
+    for b in cp.blocks:
+        upd = b.writes if isinstance(b, BasicBlock) else assigned_in([b])
+        for v in upd:
+            ones.pop(v, None)
+        if ones:
+            rewrite([b])
+        if isinstance(b, BasicBlock):
+            for v, h in b.env_out.items():
+                if _is_ones(h):
+                    ones[v] = h
+    if n[0]:
+        stats["constant-binary-ops"] = n[0]
+
+
 # ----------------------------------------------------------------------------
 def run(cp, config=None):
     """Apply the IPA passes in place; returns a stats dict (also kept as cp.ipa_stats)."""
@@ -302,5 +350,6 @@ def run(cp, config=None):
     if config is None or getattr(config, "inline_functions", True):
         inline_functions(cp, graph, stats)
     propagate_literals(cp, stats)
+    remove_constant_binary_ops(cp, stats)
     cp.ipa_stats = stats
     return stats

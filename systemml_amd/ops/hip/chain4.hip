@@ -30,9 +30,19 @@
 // Run-ahead loops (runtime/program.py _exec_while_runahead): the device address of the fp64
 // flag a speculatively queued iteration's streaming kernels read first (0.0 = dead iteration:
 // return at once).  Set per host thread by the executor, read by every launch below.
+// Bit 0 of the address selects the sense: clear -> live while the flag is non-zero (a `while (p)`
+// predicate), set -> live while it is zero (`while (!p)`: the flag is p itself, no negation op).
 static thread_local const double* g_live_flag = nullptr;
 const double* sysml_live_flag() { return g_live_flag; }
 extern "C" void sysml_set_live(const void* p) { g_live_flag = static_cast<const double*>(p); }
+
+// run-ahead live flag (see chain4.hip sysml_set_live): true when the queued iteration is dead
+__device__ __forceinline__ bool sysml_dead(const double* live) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(live);
+  if (a == 0) return false;
+  const double f = *reinterpret_cast<const double*>(a & ~(uintptr_t)1);
+  return (f == 0.0) != ((a & 1) != 0);
+}
 
 namespace sysml_c4 {
 
@@ -187,7 +197,7 @@ __global__ void __launch_bounds__(BLOCK, 2)
 chain4_kernel(const T* __restrict__ X, int64_t N, int D, const float* __restrict__ V, int ldv,
               const float* __restrict__ S, int lds, int sbc, float* __restrict__ out,
               float* __restrict__ U, int ldu, int64_t rows_per_block, const double* __restrict__ live) {
-  if (live != nullptr && *live == 0.0) return;    // dead run-ahead iteration (runtime/program.py)
+  if (sysml_dead(live)) return;    // dead run-ahead iteration (runtime/program.py)
   constexpr int C = J * 8;
   constexpr int K2 = (K + 1) / 2;
   constexpr int NV = G * K;
@@ -460,7 +470,7 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
                const float* __restrict__ S, int lds, int sbc, float* __restrict__ out,
                float* __restrict__ U, int ldu, int64_t rows_per_block, double* __restrict__ obj,
                const double* __restrict__ live) {
-  if (live != nullptr && *live == 0.0) return;    // dead run-ahead iteration (runtime/program.py)
+  if (sysml_dead(live)) return;    // dead run-ahead iteration (runtime/program.py)
   constexpr int K = 4;
   constexpr int NS = J * 8;                       // 64-column steps per row
   constexpr int XB = J * 1024;

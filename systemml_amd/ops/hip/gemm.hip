@@ -72,6 +72,7 @@ struct Args {
   int64_t simgB, simgC;
   int obf16, relu;   // C stored bf16 (round to nearest even); relu after the bias
   const float* bias; // C[row][*] += bias[row] (null: none)
+  int vec;           // 4-column vector stores are aligned (C / slab rows, image strides, base)
 };
 
 __device__ __forceinline__ int swz_k(int row) { return (row >> 1) & 7; }
@@ -292,7 +293,9 @@ gemm_bf16_kernel(Args a) {
         if constexpr (TAIL) af = mask_k(af, kb, a.K);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf8)af, (bf8)bfr[j], acc[i][j], 0, 0, 0);
+          // operands swapped: the accumulator holds C^T, so a lane's 4 values are 4 consecutive
+          // C columns of one row (vector stores in the epilogue)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf8)bfr[j], (bf8)af, acc[i][j], 0, 0, 0);
         af = an;
       }
     }
@@ -351,62 +354,83 @@ gemm_bf16_kernel(Args a) {
     }
   }
 
-  // epilogue: C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + reg
+  // epilogue.  C^T map of 16x16x32 with swapped operands: C row = lane & 15 (+ 16 i), C columns
+  // (lane >> 4) * 4 + reg (+ 16 j) -- four consecutive columns per lane
   const int64_t ldc = a.ldc;
-  const int rbase = bm * BMT + wr * WM + (lane >> 4) * 4;
-  const int cbase = bn * BN + wc * 64 + (lane & 15);
+  const int rbase = bm * BMT + wr * WM + (lane & 15);
+  const int cbase = bn * BN + wc * 64 + (lane >> 4) * 4;
   if (a.slab || (!a.obf16 && a.hwb == 0 && a.bias == nullptr && !a.relu)) {
     // plain fp32 C (or a split-K slab: the reduction pass applies the epilogue)
     float* dst = (float*)a.C + (a.slab ? (int64_t)split * a.slab : 0);
     const bool acc_in = a.beta && !a.slab;
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i) {
+      const int row = rbase + i * 16;
+      if (row >= a.M) continue;
+      float* prow = dst + (int64_t)row * ldc;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = cbase + j * 16;
-        if (col < a.N) {
+        if (a.vec && col + 3 < a.N) {
+          f4 v = acc[i][j];
+          if (acc_in) v += *(const f4*)(prow + col);
+          *(f4*)(prow + col) = v;
+        } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = rbase + i * 16 + r;
-            if (row < a.M) {
-              float* p = dst + (int64_t)row * ldc + col;
-              *p = acc_in ? *p + acc[i][j][r] : acc[i][j][r];
-            }
-          }
+          for (int r = 0; r < 4; ++r)
+            if (col + r < a.N) prow[col + r] = acc_in ? prow[col + r] + acc[i][j][r] : acc[i][j][r];
         }
       }
+    }
     return;
   }
-  // DNN epilogue: image-blocked columns, per-row bias, relu, bf16 or fp32 C
+  // DNN epilogue: image-blocked columns (4 consecutive columns never straddle two images: hwb %
+  // 8 == 0), per-row bias, relu, bf16 or fp32 C
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = cbase + j * 16;
-    if (col >= a.N) continue;
-    int64_t cofs = col;
-    if (a.hwb > 0) {
-      const int img = col / a.hwb, px = col - img * a.hwb;
-      if (px >= a.hwr) continue;
-      cofs = (int64_t)img * a.simgC + px;
-    }
+  for (int i = 0; i < MI; ++i) {
+    const int row = rbase + i * 16;
+    if (row >= a.M) continue;
+    const float bv = a.bias != nullptr ? a.bias[row] : 0.f;
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int j = 0; j < 4; ++j) {
+      const int col = cbase + j * 16;
+      if (col >= a.N) continue;
+      int64_t cofs = col;
+      int nv = a.N - col < 4 ? a.N - col : 4;
+      if (a.hwb > 0) {
+        const int img = col / a.hwb, px = col - img * a.hwb;
+        nv = a.hwr - px < nv ? a.hwr - px : nv;
+        cofs = (int64_t)img * a.simgC + px;
+      }
+      if (nv <= 0) continue;
+      float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rbase + i * 16 + r;
-        if (row < a.M) {
-          float v = acc[i][j][r];
-          if (a.bias != nullptr) v += a.bias[row];
-          if (a.relu) v = v > 0.f ? v : 0.f;
-          const int64_t o = (int64_t)row * ldc + cofs;
-          if (a.obf16) {
-            uint32_t u = __float_as_uint(v);
-            u += 0x7fffu + ((u >> 16) & 1u);
-            ((uint16_t*)a.C)[o] = (uint16_t)(u >> 16);
-          } else {
-            ((float*)a.C)[o] = v;
-          }
-        }
+        v[r] = acc[i][j][r] + bv;
+        if (a.relu) v[r] = v[r] > 0.f ? v[r] : 0.f;
       }
+      const int64_t o = (int64_t)row * ldc + cofs;
+      if (a.obf16) {
+        uint16_t h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          uint32_t u = __float_as_uint(v[r]);
+          u += 0x7fffu + ((u >> 16) & 1u);
+          h[r] = (uint16_t)(u >> 16);
+        }
+        uint16_t* p = (uint16_t*)a.C + o;
+        if (a.vec && nv == 4) {
+          *(uint2*)p = uint2{(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+        } else {
+          for (int r = 0; r < nv; ++r) p[r] = h[r];
+        }
+      } else {
+        float* p = (float*)a.C + o;
+        if (a.vec && nv == 4) *(f4*)p = f4{v[0], v[1], v[2], v[3]};
+        else
+          for (int r = 0; r < nv; ++r) p[r] = v[r];
+      }
+    }
   }
 }
 
@@ -752,6 +776,7 @@ int sysml_gemm(int dtype, const void* A, int64_t lda, int ta, const void* B, int
   a.simgB = a.simgC = 0;
   a.obf16 = a.relu = 0;
   a.bias = nullptr;
+  a.vec = 0;
   a.A = A; a.B = B;
   a.lda = lda; a.ldb = ldb;
   a.M = M; a.N = N; a.K = K;
@@ -770,6 +795,7 @@ int sysml_gemm(int dtype, const void* A, int64_t lda, int ta, const void* B, int
   a.ldc = use_slab ? N : ldc;
   a.slab = use_slab ? (int64_t)M * N : 0;
   if (use_slab) a.beta = 0;
+  a.vec = (a.ldc % 4 == 0) && (((uintptr_t)a.C & 15) == 0) && (!use_slab || (a.slab % 4 == 0));
   int rc;
   if (dtype == 2) {
     if ((lda & 7) || (ldb & 7) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return -4;
@@ -809,11 +835,11 @@ int sysml_gemm(int dtype, const void* A, int64_t lda, int ta, const void* B, int
 // A: K-major [M][lda] (filters; the host transposes W for backward data).  B: images of
 // [K][hwb] pixels (hwb % 8 == 0), image n at B + n * simgB, k stride ldb.  C: images of
 // [M][hwr] pixels at C + n * simgC (row stride ldc), pixels >= hwr of B's blocks are padding.
-// N = images * hwb.  M <= 128 runs the 64-row tile.  ksplit > 1: fp32 slabs (ksplit x M x N)
-// reduced by the epilogue pass.
+// N = images * hwb.  rowtile: 64 or 256 rows of A per workgroup.  ksplit > 1: fp32 slabs
+// (ksplit x M x N) reduced by the epilogue pass.
 int sysml_gemm_dnn(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t simgB, void* C, int64_t ldc,
                    int64_t simgC, int M, int N, int K, int hwb, int hwr, const float* bias, int relu, int obf16,
-                   int ksplit, void* slab, void* stream) {
+                   int ksplit, void* slab, int rowtile, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || ksplit < 1 || hwb <= 0 || (hwb & 7) || hwr > hwb || N % hwb) return -1;
@@ -822,7 +848,7 @@ int sysml_gemm_dnn(const void* A, int64_t lda, const void* B, int64_t ldb, int64
   // 32-bit lane offsets: a 256-column tile spans at most 256 / hwb + 2 images
   if (((int64_t)(256 / hwb + 2) * simgB + (int64_t)BK * ldb) * 2 >= ((int64_t)1 << 31)) return -4;
   if (lda * 256 >= (int64_t)1 << 31) return -4;
-  const bool small = M <= 128;
+  const bool small = rowtile == 64;       // the host picks the row tile (ops/kernels.py _gemm_img)
   const int tile = small ? 64 : BM;
   const int bk = small ? 64 : (g_bk ? g_bk : (ksplit > 1 ? 32 : 64));
   Args a;
@@ -847,6 +873,8 @@ int sysml_gemm_dnn(const void* A, int64_t lda, const void* B, int64_t ldb, int64
   a.C = (float*)(use_slab ? slab : C);
   a.ldc = use_slab ? N : ldc;
   a.slab = use_slab ? (int64_t)M * N : 0;
+  a.vec = use_slab ? ((N % 4 == 0) && (((uintptr_t)slab & 15) == 0) && (a.slab % 4 == 0))
+                   : ((ldc % 4 == 0) && (simgC % 4 == 0) && (((uintptr_t)C & (obf16 ? 7 : 15)) == 0));
   int rc;
   if (small) rc = launch_bf16_t<false, false, 64, 64>(a, st);
   else rc = bk == 64 ? launch_bf16_t<false, false, 64>(a, st) : launch_bf16_t<false, false, 32>(a, st);

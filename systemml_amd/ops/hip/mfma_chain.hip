@@ -27,6 +27,14 @@
 
 const double* sysml_live_flag();   // chain4.hip: run-ahead flag of the calling host thread
 
+// run-ahead live flag (see chain4.hip sysml_set_live): true when the queued iteration is dead
+__device__ __forceinline__ bool sysml_dead(const double* live) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(live);
+  if (a == 0) return false;
+  const double f = *reinterpret_cast<const double*>(a & ~(uintptr_t)1);
+  return (f == 0.0) != ((a & 1) != 0);
+}
+
 namespace sysml_mc {
 
 typedef short s4 __attribute__((ext_vector_type(4)));
@@ -60,7 +68,7 @@ mchain_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
               const uint16_t* __restrict__ V3T,  // [16][Dp] bf16 (row 4s+k = plane s of V[:,k])
               const float* __restrict__ S, int lds, int sbc, int K,
               float* __restrict__ out, int ldo, int64_t tiles_per_block, const double* __restrict__ live) {
-  if (live != nullptr && *live == 0.0) return;    // dead run-ahead iteration (runtime/program.py)
+  if (sysml_dead(live)) return;    // dead run-ahead iteration (runtime/program.py)
   constexpr int Dp = KS * 32 * WAVES;   // KS = 32-column k-steps per wave
   constexpr int ROWB = Dp * 2 + 16;      // LDS pitch of one X row (bytes)
   constexpr int CH = Dp / 8;             // 16-byte chunks per row
@@ -243,7 +251,7 @@ wide_kernel(const uint16_t* __restrict__ X, int64_t N, int D,
             const float* __restrict__ S, int lds, int K,
             float* __restrict__ out, int ldo, int64_t tiles_per_block,
             float* __restrict__ U, int ldu, double* __restrict__ obj, const double* __restrict__ live) {
-  if (live != nullptr && *live == 0.0) return;    // dead run-ahead iteration (runtime/program.py)
+  if (sysml_dead(live)) return;    // dead run-ahead iteration (runtime/program.py)
   constexpr int WV = wide_waves<MODE, KS>();
   constexpr int BLK = 64 * WV;
   constexpr int Dp = KS * 256;

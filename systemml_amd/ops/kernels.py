@@ -125,7 +125,7 @@ def load(required=False):
     L.sysml_gemm_dnn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     L.sysml_pad_pixels.restype = ctypes.c_int
     L.sysml_pad_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
@@ -808,7 +808,7 @@ def _conv_code(dt):
     return None
 
 
-GEMM_DNN_BLOCKS = int(os.environ.get("SYSML_GEMM_DNN_BLOCKS", "512"))   # split K until ~this many blocks
+GEMM_DNN_FILL = int(os.environ.get("SYSML_GEMM_DNN_FILL", "240"))   # workgroups that count as a full chip
 
 
 def _gemm_img(A, B, out, M, K, nimg, hw, hwb=None, bias=None, relu=False):
@@ -829,18 +829,23 @@ def _gemm_img(A, B, out, M, K, nimg, hw, hwb=None, bias=None, relu=False):
                 raise RuntimeError(f"sysml_pad_pixels failed: {rc}")
             B = Bp
     Ncol = nimg * hwb
+    # row tile: 64 rows for M <= 128 (a 256-row tile would be mostly padding), else 256; split K
+    # only when fewer than half the CUs would get a workgroup
+    # (measured, tools/bench_gemm_dnn.py: a 256-row tile on 200 workgroups beats the 64-row tile
+    # on 800 for deep K -- the 64-row tile is LDS-bound)
+    nt = (Ncol + 255) // 256
     te = 64 if M <= 128 else 256
-    tiles = ((M + te - 1) // te) * ((Ncol + 255) // 256)
+    tiles = ((M + te - 1) // te) * nt
     ksplit = 1
-    if tiles < GEMM_DNN_BLOCKS and K >= 512:
-        ksplit = max(1, min(GEMM_DNN_BLOCKS // tiles, K // 256, 16))
+    if tiles < GEMM_DNN_FILL // 2 and K >= 1024:
+        ksplit = max(1, min((GEMM_DNN_FILL + tiles - 1) // tiles, K // 512, 4))
     slab = torch.empty((ksplit * M * Ncol,), dtype=torch.float32, device=dev) if ksplit > 1 else None
     bb = None
     if bias is not None:
         bb = bias.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
     rc = L.sysml_gemm_dnn(A.data_ptr(), A.stride(0), B.data_ptr(), hwb, K * hwb, out.data_ptr(), hw, M * hw,
                           M, Ncol, K, hwb, hw, bb.data_ptr() if bb is not None else None, int(bool(relu)), 1,
-                          ksplit, slab.data_ptr() if slab is not None else None, st)
+                          ksplit, slab.data_ptr() if slab is not None else None, te, st)
     if rc != 0:
         raise RuntimeError(f"sysml_gemm_dnn failed: {rc}")
     _count("gemm_dnn")

@@ -296,7 +296,10 @@ struct VArgs {{
   const double* live;
 }};
 extern "C" __global__ void __launch_bounds__({NT}) sysml_vprog_k(const VArgs P) {{
-  if (P.live != nullptr && *P.live == 0.0) return;    // dead run-ahead iteration
+  {{  // dead run-ahead iteration (runtime/program.py; bit 0 of the address inverts the sense)
+    const unsigned long long la = (unsigned long long)P.live;
+    if (la != 0ull && ((*(const double*)(la & ~1ull) == 0.0) != ((la & 1ull) != 0ull))) return;
+  }}
   __shared__ double red[{NT // 64} * {kred}];
 {body}
 }}
@@ -437,7 +440,10 @@ struct VArgs {{
   const double* live;
 }};
 extern "C" __global__ void __launch_bounds__({NTR}) sysml_vprog_k(const VArgs P) {{
-  if (P.live != nullptr && *P.live == 0.0) return;    // dead run-ahead iteration
+  {{  // dead run-ahead iteration (runtime/program.py; bit 0 of the address inverts the sense)
+    const unsigned long long la = (unsigned long long)P.live;
+    if (la != 0ull && ((*(const double*)(la & ~1ull) == 0.0) != ((la & 1ull) != 0ull))) return;
+  }}
   __shared__ double red[{NTR // 64} * {kred}];
 {body}
 }}

@@ -874,7 +874,20 @@ def b_iqm(ctx, x, w=None):
         s += (lo - q1) * vals[lo - 1].item() if lo > 0 else 0.0
         s -= (hi - q3) * vals[hi - 1].item() if hi > 0 else 0.0
         return float(s / (q3 - q1))
-    raise DMLRuntimeError("weighted interQuartileMean not supported")
+    # weighted (reference MatrixBlock.interQuartileMean, weights as frequencies): walk the sorted
+    # values by cumulative weight to the 25% / 75% marks, sum value * weight in between and
+    # correct for the fractional weight of the two boundary values
+    cw = torch.cumsum(wts.double(), 0)
+    v = vals.double()
+    sum_wt = float(cw[-1].item())
+    q25d, q75d = 0.25 * sum_wt, 0.75 * sum_wt
+    q25i, q75i = math.ceil(q25d), math.ceil(q75d)
+    i25 = min(int(torch.searchsorted(cw, torch.tensor(float(q25i), dtype=cw.dtype, device=cw.device)).item()), n - 1)
+    i75 = min(int(torch.searchsorted(cw, torch.tensor(float(q75i), dtype=cw.dtype, device=cw.device)).item()), n - 1)
+    mid = (v[i25 + 1:i75 + 1] * wts.double()[i25 + 1:i75 + 1]).sum().item() if i75 > i25 else 0.0
+    q25part, q25val = float(cw[i25].item()) - q25d, float(v[i25].item())
+    q75part, q75val = float(cw[i75].item()) - q75d, float(v[i75].item())
+    return float((mid + q25part * q25val - q75part * q75val) / (sum_wt * 0.5))
 
 
 @builtin("aggregate")

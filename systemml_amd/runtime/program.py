@@ -475,25 +475,48 @@ def _runahead_ok(ctx, b):
 runahead_stats = {"loops": 0, "iterations": 0, "dead": 0, "host_pred": 0}
 
 
+def _pred_var(b):
+    """(variable, inverted) when the loop predicate is `v` or `!v` for a variable v, else None:
+    then a device-resident v serves as the live flag itself (inverted: bit 0 of its address,
+    ops/hip/chain4.hip sysml_dead) and no negation is queued per iteration."""
+    r = getattr(b, "_pred_var", False)
+    if r is False:
+        h = b.pred.root
+        r = None
+        if h.op == "tread":
+            r = (h.p["name"], False)
+        elif h.op == "u" and h.p.get("o") == "not" and h.inputs[0].op == "tread":
+            r = (h.inputs[0].p["name"], True)
+        b._pred_var = r
+    return r
+
+
 def _exec_while_runahead(ctx, b):
     from ..ops.backend import backend
     if not _to_bool(eval_pred(ctx, b.pred)):
         return
     runahead_stats["loops"] += 1
     vars_ = ctx.vars
+    pv = _pred_var(b)
     pend = None          # device predicate guarding the iteration being queued (None: known live)
+    pinv = False         # pend is the negation of the loop predicate
     try:
         while True:
             snap = vars_.copy()
             live = 0
             if pend is not None and pend.t.is_cuda and pend.t.dtype == torch.float64:
-                live = pend.t.data_ptr()
+                live = pend.t.data_ptr() | (1 if pinv else 0)
             backend.set_runahead(True, live)
             err = None
             q = None
+            qinv = False
             try:
                 exec_blocks(ctx, b.body)
-                q = eval_pred(ctx, b.pred)
+                v = vars_.get(pv[0]) if pv is not None else None
+                if type(v) is S.DevScalar and v.t.is_cuda and v.t.dtype == torch.float64:
+                    q, qinv = v, pv[1]              # the variable itself, read back late
+                else:
+                    q = eval_pred(ctx, b.pred)
                 if type(q) is S.DevScalar:
                     q.start_read()
             except DMLScriptStop:
@@ -501,7 +524,7 @@ def _exec_while_runahead(ctx, b):
             except Exception as e:      # noqa: BLE001 - re-raised below unless the iteration was dead
                 err = e
             runahead_stats["iterations"] += 1
-            if pend is not None and not pend.value():
+            if pend is not None and bool(pend.value()) == pinv:
                 # the iteration just queued lies past the loop's end: undo it
                 runahead_stats["dead"] += 1
                 vars_.clear()
@@ -510,12 +533,12 @@ def _exec_while_runahead(ctx, b):
             if err is not None:
                 raise err
             if type(q) is S.DevScalar:
-                pend = q
+                pend, pinv = q, qinv
             else:
                 runahead_stats["host_pred"] += 1
                 if not _to_bool(q):
                     return
-                pend = None
+                pend, pinv = None, False
     finally:
         backend.set_runahead(False, 0)
 

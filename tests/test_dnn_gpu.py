@@ -182,3 +182,19 @@ def test_conv2d_fp32_operands_on_bf16_mfma(shape):
         a = a.double().cpu()
         err = (a - b).abs().max().item() / (b.abs().max().item() + 1e-30)
         assert err < 2e-2, (name, err)
+
+
+def test_compare_backends_harness_quick():
+    """The nn/test/compare_backends harness (CPU fp64 vs GPU backend for every DNN builtin,
+    reference scripts/nn/test/compare_backends/run_tests.sh) in its quick sweep."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import importlib.util
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "systemml_amd/scripts/nn/test/compare_backends/run_tests.py")
+    spec = importlib.util.spec_from_file_location("cmp_backends", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.main(["--quick"]) == 0

@@ -218,3 +218,41 @@ def test_split_dag_after_data_dependent_operators():
     EX.execute(cs, ins, out=o1.append)
     EX.run(src, inputs=ins, config=DMLConfig(gpu=False, rewrites=False), out=o0.append)
     assert float(o1[0]) == pytest.approx(float(o0[0]), rel=1e-12)
+
+
+def test_ipa_constant_binary_ops():
+    src = """
+    w = matrix(1, rows=nrow(X), cols=1)
+    if (ncol(X) > 2) { print("wide") }
+    Z = X * w
+    s = sum(Z)
+    """
+    X = RNG.random((6, 4))
+    cs = EX.compile_script(src, {}, inputs={"X": X}, outputs=["Z", "s"], config=DMLConfig(gpu=False))
+    assert cs.cp.ipa_stats.get("constant-binary-ops", 0) == 1, cs.cp.ipa_stats
+    r, _ = EX.execute(cs, {"X": X}, out=lambda s: None)
+    np.testing.assert_allclose(r["Z"].numpy(), X)
+
+
+def test_ipa_function_call_sizes():
+    """FunctionCallSizeInfo: a function called from the main program with the same argument
+    shapes at every site is planned with those shapes (its body's hops are sized)."""
+    src = """
+    f = function(matrix[double] A, matrix[double] B) return (matrix[double] C) {
+      C = A %*% B %*% t(B)
+      if (sum(C) > 1e9) { print("big") }
+    }
+    X = rand(rows=50, cols=20, seed=1)
+    Y = rand(rows=20, cols=30, seed=2)
+    C1 = f(X, Y)
+    C2 = f(X, Y)
+    """
+    cfg = DMLConfig(gpu=False)          # the body has an if: not inlined
+    cs = EX.compile_script(src, {}, outputs=["C1"], config=cfg)
+    sized = getattr(cs.cp, "fcall_sized", set())
+    assert {p for _, p in sized} >= {"A", "B"}, sized
+    text = EX.explain(cs.cp, "hops")
+    body = text.split("MAIN PROGRAM")[0]
+    assert "M[50x30]" in body or "M[50x20]" in body, body
+    r, _ = EX.execute(cs, {}, out=lambda s: None)
+    assert tuple(r["C1"].shape) == (50, 20)
