@@ -4,8 +4,11 @@
 The network is built as a Caffe2DML layer DAG (models/dl.py: Convolution + BatchNorm + Scale +
 ReLU bottlenecks with Eltwise residual sums, 3x3/2 max pool, 7x7 average pool, InnerProduct,
 SoftmaxWithLoss), the generated forward / backward / SGD-momentum DML runs on the MI355X
-backend: every conv2d / conv2d_backward_* / pooling / bias op is a hand-written kernel of
-ops/hip/dnn.hip; convolutions compute on bf16 MFMA with fp32 accumulation, activations and
+backend: every conv2d / conv2d_backward_* / pooling / bias op is a hand-written kernel --
+implicit-GEMM convolutions of ops/hip/dnn.hip, and for 1x1 stride-1 convolutions, small-image
+im2col forward and col2im backward-data the image-blocked MFMA GEMM of ops/hip/gemm.hip
+(no library GEMM kernel runs in a step: profiles/resnet50_step_kernels_b256_r5.txt);
+convolutions compute on bf16 MFMA with fp32 accumulation, activations and
 their gradients are stored bf16 (fp32 arithmetic in every kernel), weights, weight gradients
 and the optimizer state stay fp32 (--fp32-activations: fp32 activations too).
 

@@ -2,11 +2,14 @@
 src/main/cpp/libmatrixdnn.cpp; DML signatures in parser/BuiltinFunctionExpression.java).
 
 DML keeps images as 2-D matrices: input  N x (C*H*W)  (row-major C,H,W per row),
-filter F x (C*Hf*Wf).  On the MI355X every operator runs a hand-written kernel of
-ops/hip/dnn.hip (implicit-GEMM convolutions on MFMA -- bf16 operands on bf16 MFMA, fp32 /
-fp64 on exact MFMA --, pooling and its backward pass, channel-wise bias add / multiply and
-relu backward) directly on the 2-D matrices; on the host the same operators run through
-ATen on NCHW views.
+filter F x (C*Hf*Wf).  On the MI355X every operator runs a hand-written kernel directly on
+the 2-D matrices: ops/hip/dnn.hip (implicit-GEMM convolutions on MFMA -- bf16 operands on
+bf16 MFMA, fp32 / fp64 on exact MFMA --, im2col / col2im, pooling and its backward pass,
+channel-wise bias add / multiply and relu backward) and the image-blocked MFMA GEMM of
+ops/hip/gemm.hip for 1x1 stride-1 convolutions, im2col forward and col2im backward data
+(ops/kernels.py:_gemm_img; bias and relu in its epilogue).  No library GEMM (hipBLASLt /
+rocBLAS) is called on this path.  On the host the same operators run through ATen on NCHW
+views.
 """
 from __future__ import annotations
 

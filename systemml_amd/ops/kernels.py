@@ -758,8 +758,8 @@ def sddmm(crow, col, U, V, dtype=None):
 # DNN (ops/hip/dnn.hip)
 # ----------------------------------------------------------------------------
 CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) instead of exact fp32 MFMA
-# 1x1 stride-1 convolutions of bf16 activations as batched library GEMMs (SYSML_CONV1X1_GEMM=0: the
-# implicit-GEMM kernel of dnn.hip)
+# 1x1 stride-1 convolutions of bf16 activations as image-blocked gemm.hip GEMMs (_gemm_img;
+# SYSML_CONV1X1_GEMM=0: the implicit-GEMM kernel of dnn.hip)
 CONV1X1_GEMM = os.environ.get("SYSML_CONV1X1_GEMM", "1") != "0"
 IM2COL_MAX_HW = int(os.environ.get("SYSML_IM2COL_MAX_HW", "196"))   # forward k x k convolutions via im2col + GEMM up to this Ho*Wo
 COL2IM_MAX_HW = int(os.environ.get("SYSML_COL2IM_MAX_HW", "196"))   # stride-1 backward data via GEMM + col2im up to this H*W (measured: faster at 14 x 14 and 7 x 7, slower at 28 x 28 and 56 x 56)
