@@ -247,8 +247,8 @@ def _bb_update_in_place_ok(bb, v):
             return False
     # everything computed inside the chain's inputs must be consumed only there (no escaping views)
     for hid, h in inner.items():
-        if h.op == "tread":
-            continue
+        if h.op in ("tread", "lit") or h.dt == "S":
+            continue                              # scalars hold no view of v's buffer
         for c, i in cons.get(hid, []):
             if isinstance(c, str) or not (c.id in inner or c.id in chain_ids):
                 return False
@@ -339,6 +339,7 @@ def mark_update_in_place(blocks, stats=None):
             mark_update_in_place(b.body, stats)           # inner loops first
             b.inplace_vars = []
             if isinstance(b, ForBlock) and b.parfor:
+                _mark_parfor_inplace(b, stats)
                 continue
             cand = sorted(assigned_in(b.body) - ({b.var} if isinstance(b, ForBlock) else set()))
             for v in cand:
@@ -353,6 +354,30 @@ def mark_update_in_place(blocks, stats=None):
                         h.p["inplace"] = True
                     stats["update-in-place"] = stats.get("update-in-place", 0) + 1
     return stats
+
+
+def _mark_parfor_inplace(b, stats):
+    """In-place result indexing of a parfor (reference OptimizerRuleBased.
+    rewriteSetInPlaceResultIndexing, :1642, and rewriteRemoveUnnecessaryCompareMatrix, :2021):
+    a variable the body modifies only by left indexing -- and otherwise reads at most for its
+    shape -- has disjoint per-iteration writes once the dependency analysis accepted the loop
+    (compiler/parfor_deps.py).  Its writes are marked in place; at run time all workers then
+    update ONE private copy of the pre-loop matrix and no result merge with a compare matrix
+    is needed (runtime/parfor.py).  `check=0` switches the analysis off, and with it this."""
+    chk = b.params.get("check")
+    if chk is not None and str(chk) in ("0", "0.0", "False", "false", "FALSE"):
+        b.parfor_inplace = []
+        return
+    acc = set(getattr(b, "accumulators", ()))
+    out = []
+    for v in sorted(assigned_in(b.body) - {b.var} - acc):
+        lixes = _lix_in(b.body, v, [])
+        if lixes and all(h.dt == "M" for h in lixes) and _uip_ok(b.body, v):
+            out.append(v)
+            for h in lixes:
+                h.p["inplace"] = True
+            stats["parfor-inplace-result"] = stats.get("parfor-inplace-result", 0) + 1
+    b.parfor_inplace = out
 
 
 def mark_program(cp):

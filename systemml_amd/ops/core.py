@@ -865,6 +865,8 @@ def rix(x, rl, ru, cl, cu, list_mode=False):
         _check_range(r0, r1, c0, c1, nr, nc)
         return x.slice(r0 - 1, r1, c0 - 1, c1)
     if not isinstance(x, Tensor):
+        if getattr(x, "is_part_view", False):           # parfor data partition (runtime/parfor.py)
+            return x.part_rix(rl, ru, cl, cu)
         raise DMLRuntimeError("indexing requires a matrix, frame or list")
     nr, nc = x.shape
     r0, r1 = _bound(rl, 1), _bound(ru, nr)
@@ -913,6 +915,8 @@ def lix(x, y, rl, ru, cl, cu, list_mode=False, owned=None):
         _check_range(r0, r1, c0, c1, nr, nc)
         return x.set_slice(r0 - 1, r1, c0 - 1, c1, y.cpu() if isinstance(y, Tensor) else y)
     if not isinstance(x, Tensor):
+        if getattr(x, "is_part_view", False):           # parfor data partition (runtime/parfor.py)
+            return x.part_lix(y, rl, ru, cl, cu, owned=owned)
         raise DMLRuntimeError("left indexing requires a matrix target")
     nr, nc = x.shape
     r0, r1 = _bound(rl, 1), _bound(ru, nr)

@@ -680,6 +680,25 @@ pad_pixels(const uint16_t* __restrict__ X, uint16_t* __restrict__ Y, int64_t pla
   }
 }
 
+// fp32 M x K filter -> bf16 (round to nearest even) R x Cp, R x C = W or t(W), columns C..Cp-1
+// zero: the GEMM's A operand (16-B aligned rows) in ONE pass instead of cast + transpose + pad
+__global__ void __launch_bounds__(256)
+cast_weight(const float* __restrict__ W, uint16_t* __restrict__ Y, int M, int K, int trans, int cp) {
+  const int R = trans ? K : M, C = trans ? M : K;
+  const int64_t total = (int64_t)R * cp;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(idx / cp), c = (int)(idx - (int64_t)r * cp);
+    uint16_t h = 0;
+    if (c < C) {
+      uint32_t u = __float_as_uint(trans ? W[(int64_t)c * K + r] : W[(int64_t)r * K + c]);
+      u += 0x7fffu + ((u >> 16) & 1u);
+      h = (uint16_t)(u >> 16);
+    }
+    Y[idx] = h;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 mirror_lower(T* __restrict__ C, int64_t ldc, int M, int tb) {
@@ -895,6 +914,17 @@ int sysml_pad_pixels(const void* X, void* Y, int64_t planes, int hw, int hwp, vo
   g = g < 65536 ? g : 65536;
   hipLaunchKernelGGL(pad_pixels, dim3(g), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)X, (uint16_t*)Y, planes,
                      hw, hwp);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// Y (bf16, (trans ? K : M) x cp) = W (fp32 M x K) or its transpose, zero-padded to cp columns
+int sysml_cast_weight(const void* W, void* Y, int M, int K, int trans, int cp, void* stream) {
+  if (M <= 0 || K <= 0 || cp < (trans ? M : K)) return -1;
+  const int64_t total = (int64_t)(trans ? K : M) * cp;
+  int g = (int)((total + 255) / 256);
+  g = g < 65536 ? g : 65536;
+  hipLaunchKernelGGL(cast_weight, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)W, (uint16_t*)Y, M, K,
+                     trans, cp);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -126,6 +126,9 @@ def load(required=False):
                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    L.sysml_cast_weight.restype = ctypes.c_int
+    L.sysml_cast_weight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_void_p]
     L.sysml_pad_pixels.restype = ctypes.c_int
     L.sysml_pad_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
@@ -783,8 +786,22 @@ class _WeightCasts:
         e = self._d.get(k)
         if e is not None and e[0]() is t and e[1] == t._version and e[2].device == dev and e[2].dtype == dt:
             return e[2]
-        c = t.to(device=dev, dtype=dt)
-        c = (c.t() if trans else c).contiguous()
+        L = _lib
+        if dt == torch.bfloat16 and t.dtype == torch.float32 and t.is_cuda and t.device == dev and t.dim() == 2 \
+                and t.is_contiguous() and L is not None:
+            # one pass: cast, transpose and pad (gemm.hip cast_weight)
+            M, K = t.shape
+            C = M if trans else K
+            cp = (C + 7) & ~7 if pad8 else C
+            c = torch.empty(((K if trans else M), cp), dtype=dt, device=dev)
+            rc = L.sysml_cast_weight(t.data_ptr(), c.data_ptr(), M, K, int(trans), cp, _stream())
+            if rc != 0:
+                raise RuntimeError(f"sysml_cast_weight failed: {rc}")
+            counters["cast_weight"] = counters.get("cast_weight", 0) + 1
+            pad8 = False
+        else:
+            c = t.to(device=dev, dtype=dt)
+            c = (c.t() if trans else c).contiguous()
         if pad8 and c.shape[1] % 8:
             p = torch.zeros((c.shape[0], (c.shape[1] + 7) & ~7), dtype=c.dtype, device=c.device)
             p[:, :c.shape[1]] = c

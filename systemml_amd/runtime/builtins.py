@@ -399,6 +399,16 @@ def b_sample(ctx, range_=None, size=None, replace=False, seed=-1, **kw):
 # ============================================================================
 # append / reorg
 # ============================================================================
+def _one_device(ms):
+    """Operands of an append on one device: a small host operand (e.g. the 1 x 1 constant of
+    GLM's rbind(t(X) %*% w, matrix(sw, 1, 1))) joins the device of the largest operand."""
+    dev = ms[0].device
+    if all(m.device == dev for m in ms):
+        return ms
+    big = max(ms, key=lambda m: m.numel()).device
+    return [m if m.device == big else m.to(big) for m in ms]
+
+
 @builtin("cbind", "append")
 def b_cbind(ctx, *args, **kw):
     if any(C.is_dist(a) for a in args):
@@ -415,7 +425,7 @@ def b_cbind(ctx, *args, **kw):
         return out
     if isinstance(args[0], FrameBlock):
         return FrameBlock.cbind([a if isinstance(a, FrameBlock) else C.unary("cast_frame", a) for a in args])
-    ms = [_mat(a) for a in args]
+    ms = _one_device([_mat(a) for a in args])
     r = ms[0].shape[0]
     for m in ms[1:]:
         if m.shape[0] != r:
@@ -448,7 +458,7 @@ def b_rbind(ctx, *args, **kw):
             for j, c in enumerate(a.columns):
                 cols[j] += c
         return FrameBlock(cols, args[0].schema, args[0].names)
-    ms = [_mat(a) for a in args]
+    ms = _one_device([_mat(a) for a in args])
     c = ms[0].shape[1]
     for m in ms[1:]:
         if m.shape[1] != c:

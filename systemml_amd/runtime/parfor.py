@@ -104,6 +104,62 @@ def _eq(a, b):
         return False
 
 
+class PartView:
+    """One worker's (or rank's) block of a partitioned matrix: rows (axis 0) or columns
+    (axis 1) [start, start + extent) of a matrix of `shape`.  A parfor body reads and writes
+    such a variable only as X[i, ] / X[, i] with i the loop variable (data_partitions), so
+    indexing is all it supports (ops/core.py rix / lix dispatch here): the index is moved
+    into the block, and an index outside it is an error instead of a silent wrong row."""
+    __slots__ = ("local", "start", "axis", "shape")
+    is_part_view = True
+
+    def __init__(self, local, start, axis, shape):
+        self.local = local
+        self.start = int(start)
+        self.axis = int(axis)
+        self.shape = (int(shape[0]), int(shape[1]))
+
+    def _move(self, lo, hi):
+        from ..ops.core import _bound
+        n = self.shape[self.axis]
+        a, z = _bound(lo, 1), _bound(hi, n)
+        ext = self.local.shape[self.axis]
+        if a - 1 < self.start or z > self.start + ext:
+            raise DMLRuntimeError(f"parfor data partition: {'row' if self.axis == 0 else 'column'} "
+                                  f"range [{a}:{z}] outside this worker's block "
+                                  f"[{self.start + 1}:{self.start + ext}]")
+        return a - self.start, z - self.start
+
+    def part_rix(self, rl, ru, cl, cu):
+        from ..ops import core as C
+        if self.axis == 0:
+            a, z = self._move(rl, ru)
+            return C.rix(self.local, a, z, cl, cu)
+        a, z = self._move(cl, cu)
+        return C.rix(self.local, rl, ru, a, z)
+
+    def part_lix(self, y, rl, ru, cl, cu, owned=None):
+        from ..ops import core as C
+        if self.axis == 0:
+            a, z = self._move(rl, ru)
+            out = C.lix(self.local, y, a, z, cl, cu, owned=owned)
+        else:
+            a, z = self._move(cl, cu)
+            out = C.lix(self.local, y, rl, ru, a, z, owned=owned)
+        return self if out is self.local else PartView(out, self.start, self.axis, self.shape)
+
+    def __repr__(self):
+        return f"PartView({'rows' if self.axis == 0 else 'cols'} [{self.start},{self.start + self.local.shape[self.axis]}) of {self.shape})"
+
+
+def _part_view(x, axis, lo, hi, dev=None):
+    """Block [lo, hi) of matrix x along axis as a PartView (copied to `dev` when given)."""
+    blk = x[lo:hi] if axis == 0 else x[:, lo:hi]
+    if dev is not None and blk.device != dev:
+        blk = blk.to(dev, non_blocking=True)
+    return PartView(blk, lo, axis, x.shape)
+
+
 def _body_reads(blocks, out=None):
     from ..compiler.blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
     out = set() if out is None else out
@@ -137,11 +193,12 @@ class ParForPlan:
     """Decisions of the parfor optimizer (reference ParForProgramBlock's opt tree after
     OptimizerRuleBased.optimize): exec type, degree of parallelism, task partitioner and the
     row / column access pattern of the body's matrix reads (data partitioning candidates)."""
-    __slots__ = ("exec_type", "k", "partitioner", "task_size", "partitions", "devices")
+    __slots__ = ("exec_type", "k", "partitioner", "task_size", "partitions", "devices", "part_writes",
+                 "inplace", "mem_worker", "mem_budget", "dist_parts")
 
     def __repr__(self):
         return (f"ParForPlan({self.exec_type}, k={self.k}, {self.partitioner}, devices={self.devices}, "
-                f"partitions={self.partitions})")
+                f"partitions={self.partitions}, inplace={self.inplace})")
 
 
 def _body_has(blocks, kinds):
@@ -156,14 +213,35 @@ def _body_has(blocks, kinds):
     return False
 
 
-def data_partitions(b):
+def data_partitions(b, writes=None):
     """Matrices the body reads only as X[i, ] or X[, i] with i the loop variable: the
     candidates of the reference's data partitioner (DataPartitionerLocal.java:79 writes them as
-    row / column blocks so each task reads its own).  Returns {var: 'row' | 'col'}."""
+    row / column blocks so each task reads its own).  Returns {var: 'row' | 'col'}.  Left-
+    indexing targets written only as R[i, ] = ... (or R[, i]) qualify too; `writes` (a set)
+    collects their names.  A variable also read by a predicate, passed whole to any operator
+    or indexed with anything but the loop variable is not a candidate."""
     from ..compiler.blocks import BasicBlock
     from ..compiler import hops as H
     acc = {}
     bad = set()
+    wr = set() if writes is None else writes
+
+    def is_var(z):
+        return z.op == "tread" and z.p.get("name") == b.var
+
+    def kind_of(rl, ru, cl, cu):
+        # row i (any columns) / column i (any rows): the block owning row / column i holds it
+        if is_var(rl) and (ru is rl or is_var(ru)):
+            return "row"
+        if is_var(cl) and (cu is cl or is_var(cu)):
+            return "col"
+        return None
+
+    def note(name, kind):
+        if kind is None or acc.get(name, kind) != kind:
+            bad.add(name)
+        else:
+            acc[name] = kind
 
     def visit(blocks):
         from ..compiler.blocks import IfBlock, WhileBlock, ForBlock
@@ -171,54 +249,78 @@ def data_partitions(b):
             if isinstance(x, BasicBlock):
                 tops = list(x.roots) + list(x.env_out.values())
                 for h in H.walk(tops):
-                    for c in h.inputs:
+                    if h.op == "lix":
+                        base = h
+                        while base.op == "lix":
+                            base = base.inputs[0]
+                        if base.op == "tread" and base.dt == "M":
+                            wr.add(base.p["name"])
+                            note(base.p["name"], kind_of(*h.inputs[2:6]))
+                    for pos, c in enumerate(h.inputs):
                         if c.op != "tread" or c.dt != "M":
                             continue
                         name = c.p["name"]
-                        kind = None
-                        if h.op == "rix" and h.inputs[0] is c:
-                            _, rl, ru, cl, cu = h.inputs
-                            def is_var(z):
-                                return z.op == "tread" and z.p.get("name") == b.var
-                            def empty(z):
-                                return z.op == "lit" and z.value is None
-                            if is_var(rl) and (ru is rl or is_var(ru)) and empty(cl) and empty(cu):
-                                kind = "row"
-                            elif is_var(cl) and (cu is cl or is_var(cu)) and empty(rl) and empty(ru):
-                                kind = "col"
-                        if kind is None:
-                            bad.add(name)
-                        elif acc.get(name, kind) != kind:
-                            bad.add(name)
+                        if h.op == "lix" and pos == 0:
+                            continue                      # the target: classified above
+                        if h.op == "rix" and pos == 0:
+                            note(name, kind_of(*h.inputs[1:5]))
                         else:
-                            acc[name] = kind
+                            bad.add(name)
+                for v, h in x.env_out.items():
+                    if h.op == "tread" and h.dt == "M" and h.p.get("name") != v:
+                        bad.add(h.p["name"])              # aliased whole (Y = X)
             elif isinstance(x, IfBlock):
+                bad.update(x.pred.reads)
                 visit(x.then_blocks)
                 visit(x.else_blocks)
-            elif isinstance(x, (WhileBlock, ForBlock)):
+            elif isinstance(x, WhileBlock):
+                bad.update(x.pred.reads)
+                visit(x.body)
+            elif isinstance(x, ForBlock):
+                for p in (x.start, x.end, x.incr):
+                    if p is not None:
+                        bad.update(p.reads)
                 visit(x.body)
     visit(b.body)
+    wr -= bad
     return {k: v for k, v in acc.items() if k not in bad}
 
 
-def optimize(ctx, b, n_iters):
+def optimize(ctx, b, n_iters, as_int=True):
     """Rule-based parfor optimizer (reference opt/OptimizerRuleBased.java:144-197):
       exec type  REMOTE_SPMD when the run has several ranks and the body reads no
-                 row-partitioned matrix; LOCAL_GPU (worker streams / devices) on a GPU
-                 backend; LOCAL_CPU threads otherwise;
+                 row-partitioned matrix; REMOTE_SPMD_PARTITIONED when every row-partitioned
+                 matrix the body touches is indexed only by the loop variable's row (each
+                 rank runs the iterations of the rows it owns, no collective in the body);
+                 LOCAL_GPU (worker streams / devices) on a GPU backend; LOCAL_CPU threads
+                 otherwise;
       k          the script's par=, else the exec type's parallelism (GPU: hardware queues
-                 = config.parfor_gpu_streams, times the devices used), capped by the iterations;
+                 = config.parfor_gpu_streams, times the devices used), capped by the
+                 iterations and by the memory budget (rewriteSetDegreeOfParallelism,
+                 :1178: free device / host memory over one worker's estimate);
       tasks      the script's taskpartitioner=, else STATIC for bodies of uniform cost (no
                  branches or inner while-loops) and FACTORING otherwise;
-      data       row / column access patterns of the body's matrix reads (data_partitions)."""
+      data       row / column access patterns of the body's matrix reads and left-indexing
+                 writes (data_partitions), applied by the SPMD and multi-device paths;
+      results    in-place result indexing for variables the compiler marked
+                 (compiler/loops.py: one shared private copy, no compare-matrix merge)."""
     from ..compiler.blocks import IfBlock, WhileBlock
     cfg = ctx.config
     pl = ParForPlan()
     mode = str(b.params.get("mode", "")).upper()
     par = b.params.get("par")
     pl.devices = 1
+    pl.part_writes = set()
+    pl.partitions = data_partitions(b, pl.part_writes)
+    pl.dist_parts = None
+    pl.mem_worker = pl.mem_budget = None
     if ctx.dist is not None and ctx.dist.world > 1 and mode != "LOCAL" and _spmd_ok(ctx, b):
         pl.exec_type = "REMOTE_SPMD"
+        k = ctx.dist.world
+    elif ctx.dist is not None and ctx.dist.world > 1 and mode != "LOCAL" and as_int and \
+            (dp := _spmd_partitioned(ctx, b, pl)) is not None:
+        pl.exec_type = "REMOTE_SPMD_PARTITIONED"
+        pl.dist_parts = dp
         k = ctx.dist.world
     elif ctx.dist is not None:
         pl.exec_type = "SEQUENTIAL"          # every rank runs every iteration (row-partitioned body)
@@ -231,19 +333,134 @@ def optimize(ctx, b, n_iters):
     else:
         pl.exec_type = "LOCAL_CPU"
         k = cfg.parallelism
-    if isinstance(par, (int, float)) and par and pl.exec_type not in ("REMOTE_SPMD", "SEQUENTIAL"):
+    if isinstance(par, (int, float)) and par and pl.exec_type not in ("REMOTE_SPMD", "REMOTE_SPMD_PARTITIONED", "SEQUENTIAL"):
         k = int(par)
     pl.k = max(1, min(k, n_iters))
+    pl.inplace = [v for v in getattr(b, "parfor_inplace", ()) if v in b.result_vars and _inplace_ok(ctx.vars.get(v))]
+    if pl.exec_type in ("LOCAL_GPU", "LOCAL_CPU") and pl.k > 1 and not (isinstance(par, (int, float)) and par):
+        kb = _memory_k(ctx, b, pl)
+        if kb is not None and kb < pl.k:
+            pl.k = kb
     if pl.k == 1 and pl.exec_type in ("LOCAL_GPU", "LOCAL_CPU"):
         pl.exec_type = "SEQUENTIAL"
     pl.devices = min(pl.devices, pl.k)
+    if pl.devices > 1:
+        pl.inplace = []                      # workers on other GPUs update copies: merge them
     tp = b.params.get("taskpartitioner")
     if tp is None:
         tp = "factoring" if _body_has(b.body, (IfBlock, WhileBlock)) else "static"
     pl.partitioner = str(tp).lower()
     pl.task_size = b.params.get("tasksize")
-    pl.partitions = data_partitions(b)
     return pl
+
+
+def _inplace_ok(x):
+    return type(x) is torch.Tensor and x.layout == torch.strided and x.dim() == 2
+
+
+def _body_mem(ctx, b, pl):
+    """Bytes one worker needs: the largest basic block's matrix intermediates (sum of output
+    sizes with the shapes of the current variables; an unknown size counts as the largest
+    matrix the body reads) plus its private copies of result variables merged by compare."""
+    from ..compiler import cost as CO
+    from ..compiler import hops as H
+    from ..compiler.blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
+    env = {}
+    big = 0
+    for v in _body_reads(b.body):
+        x = ctx.vars.get(v)
+        d = CO._shape_of(x)
+        env[v] = d
+        if CO._known(d) and d != CO.SCALAR:
+            big = max(big, d[0] * d[1])
+    env[b.var] = CO.SCALAR
+    cell = 4 if (pl.exec_type == "LOCAL_GPU") else 8
+    worst = 0
+
+    def visit(blocks):
+        nonlocal worst
+        for x in blocks:
+            if isinstance(x, BasicBlock):
+                dims = {}
+                tot = 0
+                for h in H.walk(list(x.roots) + list(x.env_out.values())):
+                    try:
+                        d = CO.infer(h, dims, env)
+                    except Exception:  # noqa: BLE001 -- an estimate only
+                        d = CO.UNK
+                    dims[h.id] = d
+                    if h.dt != "M" or h.op in ("tread", "lit"):
+                        continue
+                    m = CO.mem_estimate(d, cell)
+                    tot += big * cell if m is None else m
+                for k, h in x.env_out.items():
+                    env[k] = dims.get(h.id, CO.UNK)
+                worst = max(worst, tot)
+            elif isinstance(x, IfBlock):
+                visit(x.then_blocks)
+                visit(x.else_blocks)
+            elif isinstance(x, (WhileBlock, ForBlock)):
+                visit(x.body)
+    visit(b.body)
+    for v in b.result_vars:
+        if v in pl.inplace:
+            continue
+        x = ctx.vars.get(v)
+        if isinstance(x, torch.Tensor):
+            worst += x.numel() * x.element_size()
+    return worst
+
+
+def _memory_k(ctx, b, pl):
+    """Largest k whose workers fit the memory budget (reference computeMaxK): 70% of the free
+    device memory (LOCAL_GPU) or of the available host memory (LOCAL_CPU), shared read-only
+    inputs counted once (they are not copied per worker)."""
+    try:
+        need = _body_mem(ctx, b, pl)
+    except Exception:  # noqa: BLE001
+        return None
+    if not need:
+        return None
+    try:
+        if pl.exec_type == "LOCAL_GPU":
+            free = torch.cuda.mem_get_info()[0] * pl.devices
+        else:
+            import psutil
+            free = psutil.virtual_memory().available
+    except Exception:  # noqa: BLE001
+        return None
+    budget = 0.7 * free * MEM_FRACTION
+    pl.mem_worker, pl.mem_budget = need, budget
+    return max(1, int(budget // need))
+
+
+MEM_FRACTION = 1.0        # tests shrink the budget
+
+
+def _spmd_partitioned(ctx, b, pl):
+    """The row-partitioned matrices of an SPMD run the body touches, when every one of them is
+    read and written only at row i (the loop variable) and all share one row partitioning:
+    each rank then runs exactly the iterations whose rows it owns against its own block
+    (reference DataPartitionerRemoteSpark + RemoteParForSpark over the partitioned input,
+    here with the partition already in place).  None otherwise."""
+    from ..ops import core as C
+    dist = ctx.dist
+    dv = [v for v in sorted(_body_reads(b.body)) if C.is_dist(ctx.vars.get(v))]
+    if not dv:
+        return None
+    n = None
+    for v in dv:
+        x = ctx.vars[v]
+        if pl.partitions.get(v) != "row" or x.local.layout != torch.strided:
+            return None
+        if n is None:
+            n = x.nrows
+        if x.nrows != n or x.start != dist.partition(n)[0] or x.local.shape[0] != dist.partition(n)[1] - x.start:
+            return None
+    for v in b.result_vars:
+        if C.is_dist(ctx.vars.get(v)) and v not in pl.part_writes:
+            return None
+    return dv
 
 
 def exec_parfor(ctx, b, start, end, incr, as_int):
@@ -251,7 +468,7 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
     if not iters:
         return
     fork = ctx.seeds.fork()
-    pl = optimize(ctx, b, len(iters))
+    pl = optimize(ctx, b, len(iters), as_int)
     b.last_plan = pl                       # -explain / tests
     if ctx.stats is not None:
         ctx.stats.count(f"parfor {pl.exec_type.lower()} k={pl.k}")
@@ -259,6 +476,9 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
     base = {v: ctx.vars.get(v) for v in result_vars}
     if pl.exec_type == "REMOTE_SPMD":
         exec_parfor_spmd(ctx, b, iters, fork, result_vars, base)
+        return
+    if pl.exec_type == "REMOTE_SPMD_PARTITIONED":
+        exec_parfor_spmd_partitioned(ctx, b, iters, fork, result_vars, base, pl.dist_parts)
         return
     if pl.exec_type == "SEQUENTIAL":
         saved = ctx.seeds
@@ -274,14 +494,31 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
     gpu = pl.exec_type == "LOCAL_GPU"
     main = torch.cuda.current_stream() if gpu else None
     main_dev = torch.cuda.current_device() if gpu else None
+    # in-place result indexing: every worker updates one private copy of the pre-loop value
+    from ..ops import core as C
+    shared = {v: C.cvt(base[v]).clone(memory_format=torch.contiguous_format) for v in pl.inplace}
+    # data partitions on other GPUs: each worker owns a fixed set of tasks and receives only
+    # the rows / columns of the read-only partitioned matrices those iterations index
+    parts = {v: a for v, a in pl.partitions.items() if v not in pl.part_writes and v not in result_vars
+             and type(ctx.vars.get(v)) is torch.Tensor and ctx.vars[v].layout == torch.strided} \
+        if gpu and pl.devices > 1 else {}
+    own = [tasks[w::k] for w in range(k)] if parts else None
 
     def worker(w):
         from .program import ExecutionContext
         wctx = ExecutionContext(ctx.program, ctx.config, stats=ctx.stats, out=ctx._out, dist=None)
         wctx.vars = dict(ctx.vars)
         wctx.parfor_worker = True        # program.exec_block: serialise recompiling blocks
+        for v, t in shared.items():
+            wctx.vars[v] = t
+            wctx.owned.add(t)
+        wctx.shared_results = frozenset(id(t) for t in shared.values())
 
         def run():
+            if own is not None:
+                for task in own[w]:
+                    _run_iters(wctx, b, [it for _, it in task], [i for i, _ in task], fork)
+                return
             while True:
                 with lock:
                     if not queue:
@@ -301,7 +538,8 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
             try:
                 with torch.cuda.stream(s):
                     if dev != main_dev:
-                        wctx.vars = _to_device(wctx.vars, torch.device("cuda", dev), pl.partitions)
+                        wctx.vars = _to_device(wctx.vars, torch.device("cuda", dev), parts,
+                                               [it for t in own[w] for _, it in t] if own is not None else None)
                     run()
             finally:
                 backend.set_thread_device(None)
@@ -323,6 +561,9 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
             main.wait_stream(s)
     acc = set(getattr(b, "accumulators", ()))
     for v in result_vars:
+        if v in shared:
+            ctx.vars[v] = shared[v]          # updated in place by every worker
+            continue
         rs = [r[v] for r in results]
         ctx.vars[v] = _accumulate(base[v], rs) if v in acc else _merge(base[v], rs)
     ctx.vars[b.var] = iters[-1]
@@ -341,14 +582,27 @@ def _worker_stream(dev, w):
     return s
 
 
-def _to_device(vars_, dev, partitions):
-    """Copies of a worker's device-resident values on its own GPU (matrices only)."""
+def _to_device(vars_, dev, partitions, its=None):
+    """Copies of a worker's device-resident values on its own GPU (matrices only).  A
+    partitioned matrix (partitions: {var: 'row' | 'col'}) read by iterations `its` is copied
+    as the block of rows / columns min(its)..max(its) only, wrapped as a PartView."""
     out = {}
+    if its:
+        lo, hi = int(min(its)) - 1, int(max(its))
     for k, v in vars_.items():
         if isinstance(v, torch.Tensor) and v.is_cuda and v.device != dev:
-            v = v.to(dev, non_blocking=True)
+            ax = {"row": 0, "col": 1}.get(partitions.get(k)) if partitions and its else None
+            if ax is not None and 0 <= lo < hi <= v.shape[ax]:
+                v = _part_view(v, ax, lo, hi, dev)
+                part_stats["blocks"] += 1
+                part_stats["bytes_saved"] += (v.shape[0] * v.shape[1] - v.local.numel()) * v.local.element_size()
+            else:
+                v = v.to(dev, non_blocking=True)
         out[k] = v
     return out
+
+
+part_stats = {"blocks": 0, "bytes_saved": 0, "spmd_loops": 0}
 
 
 def _accumulate(base, results):
@@ -406,6 +660,47 @@ def exec_parfor_spmd(ctx, b, iters, fork, result_vars, base):
             ctx.vars[v] = _accumulate_spmd(dist, base[v], wctx.vars.get(v), lo < hi)
         else:
             ctx.vars[v] = _merge_spmd(dist, base[v], wctx.vars.get(v), lo < hi, hi)
+    ctx.vars[b.var] = iters[-1]
+
+
+def exec_parfor_spmd_partitioned(ctx, b, iters, fork, result_vars, base, dvars):
+    """Each rank runs the iterations i whose row i it owns in the common row partitioning of
+    the body's row-partitioned matrices, against its local blocks (PartView: indexing moved
+    into the block, no collective).  Row-partitioned results are updated in the rank's own
+    block and need no merge; replicated results merge as in exec_parfor_spmd.  An iteration
+    outside 1..nrow runs on rank 0, where indexing raises as the sequential loop would."""
+    from .program import ExecutionContext
+    from ..ops import core as C
+    dist = ctx.dist
+    n = ctx.vars[dvars[0]].nrows
+    lo, hi = dist.partition(n)
+    mine = [(k, it) for k, it in enumerate(iters)
+            if lo <= int(it) - 1 < hi or (dist.rank == 0 and not 0 <= int(it) - 1 < n)]
+    wctx = ExecutionContext(ctx.program, ctx.config, stats=ctx.stats,
+                            out=ctx._out if dist.rank == 0 else (lambda s: None), dist=None)
+    wctx.vars = dict(ctx.vars)
+    for v in dvars:
+        x = ctx.vars[v]
+        loc = x.local
+        if v in result_vars:
+            loc = C.cvt(loc).clone(memory_format=torch.contiguous_format)
+            wctx.owned.add(loc)
+        wctx.vars[v] = PartView(loc, x.start, 0, x.shape)
+    _run_iters(wctx, b, [it for _, it in mine], [k for k, _ in mine], fork)
+    from ..parallel import dist as D
+    D.stats["parfor_remote_partitioned"] = D.stats.get("parfor_remote_partitioned", 0) + 1
+    part_stats["spmd_loops"] += 1
+    acc = set(getattr(b, "accumulators", ()))
+    last = (mine[-1][0] + 1) if mine else 0
+    for v in result_vars:
+        x = base[v]
+        if C.is_dist(x):
+            pv = wctx.vars.get(v)
+            ctx.vars[v] = x.like(pv.local) if getattr(pv, "is_part_view", False) else x
+        elif v in acc:
+            ctx.vars[v] = _accumulate_spmd(dist, x, wctx.vars.get(v), bool(mine))
+        else:
+            ctx.vars[v] = _merge_spmd(dist, x, wctx.vars.get(v), bool(mine), last)
     ctx.vars[b.var] = iters[-1]
 
 

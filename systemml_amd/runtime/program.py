@@ -37,6 +37,7 @@ class ExecutionContext:
         self.pool = None
         self.seeds = SeedSource(config, dist)
         self.owned = OwnedBuffers()      # buffers owned by update-in-place loops (compiler/loops.py)
+        self.shared_results = frozenset()   # ids of parfor in-place result buffers (runtime/parfor.py)
         if dist is not None and config is not None:
             dist.min_rows = config.dist_min_rows
         if config is not None and getattr(config, "bufferpool", False) and torch.cuda.is_available():
@@ -371,7 +372,9 @@ def _exec_control(ctx, b):
         # after a previous run of this loop), so the first left-indexing copies again
         for v in uip:
             x = ctx.vars.get(v)
-            if isinstance(x, torch.Tensor):
+            # a parfor worker's shared in-place result stays shared: its workers write
+            # disjoint cells of that one buffer (runtime/parfor.py)
+            if isinstance(x, torch.Tensor) and id(x) not in ctx.shared_results:
                 ctx.owned.discard(x)
     if isinstance(b, WhileBlock):
         if RUNAHEAD and _runahead_ok(ctx, b):

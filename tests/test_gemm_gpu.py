@@ -137,3 +137,24 @@ def test_gemm_img_matches_fp32(M, K, nimg, hw, bias, relu):
     assert Kn.counters.get("gemm_dnn", 0) == before + 1
     err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-30)
     assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,trans,pad8", [(64, 27, False, True), (256, 2304, True, False), (147, 60, True, True),
+                                           (8, 8, False, False)])
+def test_weight_cast_one_pass(M, K, trans, pad8):
+    """gemm.hip cast_weight: fp32 filter -> bf16 (RNE), optionally transposed and zero-padded to
+    a multiple of 8 columns, in one pass; equals torch's cast of the same view."""
+    from systemml_amd.ops import kernels as KK
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    KK.load(required=True)
+    W = torch.randn(M, K, device="cuda")
+    c0 = KK.counters.get("cast_weight", 0)
+    out = KK._WeightCasts().get(W, W.device, torch.bfloat16, trans=trans, pad8=pad8)
+    assert KK.counters.get("cast_weight", 0) == c0 + 1
+    ref = (W.t() if trans else W).to(torch.bfloat16)
+    C = ref.shape[1]
+    assert out.shape[0] == ref.shape[0] and out.shape[1] == ((C + 7) // 8 * 8 if pad8 else C)
+    assert torch.equal(out[:, :C], ref)
+    assert not out[:, C:].any()

@@ -87,3 +87,17 @@ def test_append_and_left_indexing_through_dml():
         assert kernels.counters.get(k, 0) > before[k], (k, kernels.counters)
     for k in ("A", "B", "C"):
         np.testing.assert_array_equal(res[True][k], res[False][k])
+
+
+def test_append_of_host_and_device_operands():
+    """GLM's rbind(t(X) %*% w, matrix(sw, 1, 1)): a small host operand joins the device one."""
+    _need()
+    from systemml_amd.runtime.builtins import b_rbind, b_cbind
+    d = torch.arange(12, dtype=torch.float32, device="cuda").reshape(4, 3)
+    h = torch.full((1, 3), 5.0)
+    r = b_rbind(None, d, h)
+    assert r.is_cuda and torch.equal(r.cpu(), torch.cat([d.cpu(), h]))
+    r2 = b_rbind(None, h, d)
+    assert r2.is_cuda and torch.equal(r2.cpu(), torch.cat([h, d.cpu()]))
+    c = b_cbind(None, torch.ones(4, 1), d)
+    assert c.is_cuda and torch.equal(c.cpu(), torch.cat([torch.ones(4, 1), d.cpu()], 1))

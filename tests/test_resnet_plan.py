@@ -59,3 +59,59 @@ def test_resnet_step_on_gemm_paths_with_bf16_activations():
     assert cell.stats["sequential"] == seq0                 # every fused program on a generated kernel
     losses = [float(s.split(" loss ")[1].split(" ")[0]) for s in out if s.startswith("STEP")]
     assert len(losses) == 2 and all(np.isfinite(losses)), out
+
+
+_LIB_GEMM = ("Cijk_", "rocblas", "hipblaslt", "miopen", "MIOpen", "igemm", "naive_conv")
+
+
+@pytest.mark.gpu
+def test_resnet_step_runs_no_library_gemm_or_library_conv():
+    """A training step calls no torch GEMM / convolution entry point on a device tensor and, in
+    a torch.profiler kernel trace of the step, no hipBLASLt / rocBLAS / MIOpen kernel runs and
+    ATen kernels (casts, fills) stay below 5% of the device time."""
+    import torch
+    import torch.nn.functional as F
+    from systemml_amd.api import executor as EX
+    from systemml_amd.conf import DMLConfig
+    from systemml_amd.runtime.udf import register_udf
+    register_udf("sysml.bench.Sync", lambda ctx, A: (0.0,))
+    cfg = DMLConfig(precision="single", gpu_min_cells=0, act_bf16_min_cells=1 << 16)
+    cs, X, Y = _compile(image=64, batch=16, config=cfg)
+    EX.execute(cs, {"X": X, "Y": Y}, out=lambda s: None)      # warm: kernels compiled, caches filled
+    torch.cuda.synchronize()
+    calls = []
+
+    def guard(name, fn):
+        def g(*a, **k):
+            if any(isinstance(t, torch.Tensor) and t.is_cuda for t in a):
+                calls.append(name)
+            return fn(*a, **k)
+        return g
+    fns = [(torch, n) for n in ("matmul", "mm", "bmm", "addmm", "baddbmm", "einsum", "conv2d")] + \
+          [(F, n) for n in ("conv2d", "conv_transpose2d", "linear")] + \
+          [(torch.Tensor, n) for n in ("__matmul__", "matmul", "mm", "bmm")]
+    saved = [(m, n, getattr(m, n)) for m, n in fns]
+    try:
+        for m, n, f in saved:
+            setattr(m, n, guard(n, f))
+        from torch.profiler import profile, ProfilerActivity
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            out = []
+            EX.execute(cs, {"X": X, "Y": Y}, out=out.append)
+            torch.cuda.synchronize()
+    finally:
+        for m, n, f in saved:
+            setattr(m, n, f)
+    assert not calls, sorted(set(calls))
+    kern = {}
+    for e in prof.events():
+        if getattr(e, "device_type", None) == torch.autograd.DeviceType.CUDA:
+            kern[e.name] = kern.get(e.name, 0.0) + e.device_time_total if hasattr(e, "device_time_total") \
+                else kern.get(e.name, 0.0) + e.cuda_time_total
+    if not kern:
+        pytest.skip("torch.profiler recorded no device kernels on this build")
+    lib = [n for n in kern if any(s in n for s in _LIB_GEMM)]
+    assert not lib, lib[:10]
+    tot = sum(kern.values())
+    aten = sum(v for n, v in kern.items() if "at::native" in n)
+    assert aten < 0.05 * tot, sorted(((v, n) for n, v in kern.items() if "at::native" in n), reverse=True)[:10]

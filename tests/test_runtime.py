@@ -489,7 +489,7 @@ def test_parfor_optimizer_rules():
     loops = [b for b in cs.cp.blocks if isinstance(b, ForBlock)]
     p1, p2 = loops[0].last_plan, loops[1].last_plan
     assert p1.exec_type == "LOCAL_CPU" and p1.k == 6 and p1.partitioner == "static"
-    assert p1.partitions == {"X": "row", "Y": "col"}
+    assert p1.partitions == {"X": "row", "Y": "col", "R": "row"}
     assert p2.k == 2 and p2.partitioner == "factoring" and "X" not in p2.partitions
     X = M(res, "R")
     assert X.shape == (6, 1)
