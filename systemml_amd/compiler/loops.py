@@ -245,9 +245,18 @@ def _bb_update_in_place_ok(bb, v):
             if c.id in inner:
                 continue
             return False
-    # everything computed inside the chain's inputs must be consumed only there (no escaping views)
+    # everything computed inside the chain's inputs FROM v must be consumed only there (no
+    # escaping views); values that do not depend on v cannot alias its buffer
+    src_ids = {s.id for s in sources}
+    dep = {}
+
+    def from_v(h):
+        r = dep.get(h.id)
+        if r is None:
+            r = dep[h.id] = h.id in src_ids or any(from_v(c) for c in h.inputs)
+        return r
     for hid, h in inner.items():
-        if h.op in ("tread", "lit") or h.dt == "S":
+        if h.op in ("tread", "lit") or h.dt == "S" or not from_v(h):
             continue                              # scalars hold no view of v's buffer
         for c, i in cons.get(hid, []):
             if isinstance(c, str) or not (c.id in inner or c.id in chain_ids):

@@ -183,6 +183,66 @@ __global__ void __launch_bounds__(NT) col_part(const T* __restrict__ X, St* __re
   }
 }
 
+// ---- columns, 16-B loads (sum / sumsq / mean of bf16 or fp32 with D a multiple of 8 / 4): lane ->
+// a run of VW consecutive columns (one 16-B load per row), the 4 waves interleave rows, so a wave
+// reads 1 KiB of every row it visits; fp64 accumulation as in col_part ----
+template <typename T, int OP>
+__global__ void __launch_bounds__(NT) col_vec(const T* __restrict__ X, St* __restrict__ part, int64_t N, int D,
+                                              int64_t rows) {
+  constexpr int VW = 16 / sizeof(T);
+  __shared__ double red[3][64][VW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = blockIdx.x * 64 + lane;            // column group
+  const int col = g * VW;
+  const int64_t r0 = (int64_t)blockIdx.y * rows, r1 = min(N, r0 + rows);
+  double acc[VW];
+#pragma unroll
+  for (int v = 0; v < VW; ++v) acc[v] = 0.0;
+  if (col < D) {
+    const T* p = X + col;
+    int64_t r = r0 + wave;
+    for (; r + 12 < r1; r += 16) {
+      uint4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = *(const uint4*)(p + (r + 4 * u) * D);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+        for (int v = 0; v < VW; ++v) {
+          double x;
+          if constexpr (sizeof(T) == 2) x = (double)__uint_as_float(v & 1 ? (w[v >> 1] & 0xffff0000u) : (w[v >> 1] << 16));
+          else x = (double)__uint_as_float(w[v]);
+          acc[v] += OP == SUMSQ ? x * x : x;
+        }
+      }
+    }
+    for (; r < r1; r += 4) {
+      const uint4 q = *(const uint4*)(p + r * D);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int v = 0; v < VW; ++v) {
+        double x;
+        if constexpr (sizeof(T) == 2) x = (double)__uint_as_float(v & 1 ? (w[v >> 1] & 0xffff0000u) : (w[v >> 1] << 16));
+        else x = (double)__uint_as_float(w[v]);
+        acc[v] += OP == SUMSQ ? x * x : x;
+      }
+    }
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int v = 0; v < VW; ++v) red[wave - 1][lane][v] = acc[v];
+  }
+  __syncthreads();
+  if (wave == 0 && col < D) {
+#pragma unroll
+    for (int v = 0; v < VW; ++v) {
+      const double t = acc[v] + red[0][lane][v] + red[1][lane][v] + red[2][lane][v];
+      part[(int64_t)blockIdx.y * D + col + v] = St{t, 0, 0};
+    }
+  }
+}
+
 template <typename TO, int OP>
 __global__ void __launch_bounds__(NT) col_final(const St* __restrict__ part, TO* __restrict__ Y, int64_t N, int D,
                                                 int nchunk) {
@@ -235,6 +295,25 @@ inline int grid_for(int64_t work, int per) {
   return (int)(g < 1 ? 1 : g);
 }
 
+template <typename T, int OP>
+inline bool vec_cols(const void* X, int D) {
+  if constexpr ((OP == SUM || OP == SUMSQ || OP == MEAN) && (sizeof(T) == 2 || sizeof(T) == 4)) {
+    constexpr int VW = 16 / sizeof(T);
+    return D >= 64 && D % VW == 0 && ((uintptr_t)X & 15) == 0;
+  }
+  return false;
+}
+
+// row chunks of a column aggregate: enough workgroups for the chip (>= 1024) and >= 256 rows each
+inline void col_chunks(int64_t N, int strips, int64_t& nch, int64_t& rows) {
+  nch = (1024 + strips - 1) / strips;
+  const int64_t maxch = (N + 255) / 256;
+  if (nch > maxch) nch = maxch;
+  if (nch < 1) nch = 1;
+  rows = (N + nch - 1) / nch;
+  nch = (N + rows - 1) / rows;
+}
+
 template <typename T, typename TO, int OP>
 int run(int dir, const void* X, void* Y, void* scratch, int64_t N, int D, hipStream_t st) {
   if (dir == 0) {   // all
@@ -247,6 +326,15 @@ int run(int dir, const void* X, void* Y, void* scratch, int64_t N, int D, hipStr
       hipLaunchKernelGGL((row_thread<T, TO, OP>), dim3(grid_for(N, NT)), dim3(NT), 0, st, (const T*)X, (TO*)Y, N, D);
     else
       hipLaunchKernelGGL((row_wave<T, TO, OP>), dim3(grid_for(N, 4)), dim3(NT), 0, st, (const T*)X, (TO*)Y, N, D);
+  } else if (vec_cols<T, OP>(X, D)) {   // columns, 16-B loads
+    constexpr int VW = 16 / sizeof(T);
+    const int strips = (D / VW + 63) / 64;
+    int64_t nch, rows;
+    col_chunks(N, strips, nch, rows);
+    hipLaunchKernelGGL((col_vec<T, OP>), dim3(strips, (unsigned)nch), dim3(NT), 0, st, (const T*)X, (St*)scratch, N, D,
+                       rows);
+    hipLaunchKernelGGL((col_final<TO, OP>), dim3(grid_for(D, NT)), dim3(NT), 0, st, (const St*)scratch, (TO*)Y, N, D,
+                       (int)nch);
   } else {   // columns
     const int cw = D >= 64 ? 64 : (D > 16 ? 32 : (D > 4 ? 16 : 4));
     const int strips = (D + cw - 1) / cw;
@@ -297,11 +385,11 @@ int64_t sysml_agg_scratch(int dir, int64_t N, int D) {
   if (dir == 0) return 1024 * (int64_t)sizeof(St);
   if (dir == 1) return 0;
   const int cw = D >= 64 ? 64 : (D > 16 ? 32 : (D > 4 ? 16 : 4));
-  const int strips = (D + cw - 1) / cw;
-  int64_t nch = (1024 + strips - 1) / strips;
-  const int64_t maxch = (N + 255) / 256;
-  if (nch > maxch) nch = maxch;
-  if (nch < 1) nch = 1;
+  int strips = (D + cw - 1) / cw;
+  const int vstrips = ((D + 7) / 8 + 63) / 64;    // col_vec with 8-wide bf16 runs: the fewest strips
+  if (vstrips < strips) strips = vstrips;
+  int64_t nch, rows;
+  col_chunks(N, strips, nch, rows);
   return nch * (int64_t)D * (int64_t)sizeof(St);
 }
 

@@ -552,9 +552,21 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
                 v.record_stream(main)        # used on the main stream from now on
         return out, s
 
-    with ThreadPoolExecutor(max_workers=k) as ex:
-        futs = [ex.submit(worker, w) for w in range(k)]
-        done = [f.result() for f in futs]
+    # host workers share the cores: each one's operators get cores / k intra-op threads (the
+    # reference's local workers run single-threaded CP operators), restored afterwards
+    nt = torch.get_num_threads()
+    if not gpu and not getattr(ctx, "parfor_worker", False):
+        torch.set_num_threads(max(1, nt // k))
+    try:
+        if getattr(ctx, "parfor_worker", False):
+            with ThreadPoolExecutor(max_workers=k) as ex:      # nested parfor: a pool of its own
+                done = [f.result() for f in [ex.submit(worker, w) for w in range(k)]]
+        else:
+            ex = _pool(k)
+            done = [f.result() for f in [ex.submit(worker, w) for w in range(k)]]
+    finally:
+        if torch.get_num_threads() != nt:
+            torch.set_num_threads(nt)
     results = [r for r, _ in done]
     for _, s in done:
         if s is not None:
@@ -570,6 +582,19 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
 
 
 _STREAMS = {}
+_POOL = [None, 0]
+
+
+def _pool(k):
+    """Worker threads kept for the process (thread start-up costs ~0.3 ms each here, more
+    than a small parfor body), grown to the largest k seen."""
+    ex, n = _POOL
+    if ex is None or n < k:
+        if ex is not None:
+            ex.shutdown(wait=False)
+        ex = ThreadPoolExecutor(max_workers=k, thread_name_prefix="parfor")
+        _POOL[0], _POOL[1] = ex, k
+    return ex
 
 
 def _worker_stream(dev, w):

@@ -103,3 +103,18 @@ def test_agg_kernel_storage_types_and_nan(dt):
         ref = _ref(o, d, Xr)
         tol = 1e-9 if dt == torch.float64 else 1e-6        # fp32 results for bf16 storage
         torch.testing.assert_close(got.reshape(ref.shape), ref, rtol=tol, atol=tol, equal_nan=True)
+
+
+@pytest.mark.parametrize("o", ["sum", "sumsq", "mean"])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(5000, 64), (3001, 1000), (9, 128), (70000, 512)])
+def test_column_aggregate_16b_loads(o, dt, shape):
+    """agg.hip col_vec (16-B loads of 8 bf16 / 4 fp32 columns, fp64 accumulation) against fp64."""
+    from systemml_amd.ops import kernels
+    kernels.load(required=True)
+    g = torch.Generator().manual_seed(shape[0] + shape[1])
+    X = torch.randn(shape, generator=g, dtype=torch.float64).to("cuda:0", dt)
+    got = kernels.agg(o, "col", X)
+    Xr = X.double().cpu()
+    ref = {"sum": Xr.sum(0), "sumsq": (Xr * Xr).sum(0), "mean": Xr.mean(0)}[o].reshape(1, -1)
+    torch.testing.assert_close(got.double().cpu().reshape(ref.shape), ref, rtol=1e-6, atol=1e-6)   # fp32 result

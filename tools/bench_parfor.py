@@ -20,8 +20,11 @@ import torch  # noqa: E402
 def run(n, iters, par, precision, reps, gpus):
     from systemml_amd.api import executor as EX
     from systemml_amd.conf import DMLConfig
-    rng = np.random.default_rng(5)
-    ins = {"A": rng.uniform(-1, 1, (n, n)), "B": rng.uniform(-1, 1, (n, n))}
+    g = torch.Generator(device="cuda").manual_seed(5)
+    dt = torch.float64 if precision == "double" else torch.float32
+    # device-resident inputs: the timed runs measure the loops, not host -> device copies
+    ins = {"A": torch.rand((n, n), generator=g, device="cuda", dtype=dt) * 2 - 1,
+           "B": torch.rand((n, n), generator=g, device="cuda", dtype=dt) * 2 - 1}
     body = "{\n  C = (A + i) %*% B\n  R[1, i] = sum(C * C)\n}"
     srcs = {"seq": f"R = matrix(0, rows=1, cols={iters})\nfor (i in 1:{iters}) " + body,
             "par": f"R = matrix(0, rows=1, cols={iters})\nparfor (i in 1:{iters}, par={par}) " + body}

@@ -1,8 +1,9 @@
 """Where do large ATen elementwise / conversion kernels come from?  Runs bench_resnet50.main()
-with torch.Tensor arithmetic / conversion methods wrapped: every call on a CUDA tensor of
->= 1M elements records the innermost systemml_amd frames; the histogram goes to stderr.
+(or bench.main() with `--target bench`) with torch.Tensor arithmetic / conversion / indexing
+methods wrapped: every call on a CUDA tensor of >= 1M elements records the innermost
+systemml_amd frames; the histogram goes to stderr.
 
-    python tools/probe/aten_sites.py [bench_resnet50 args]
+    python tools/probe/aten_sites.py [--target bench] [bench / bench_resnet50 args]
 """
 import collections
 import os
@@ -28,15 +29,19 @@ def _wrap(name):
     setattr(torch.Tensor, name, f)
 
 
-for n in ("__mul__", "__rmul__", "__add__", "__radd__", "__sub__", "__truediv__", "to", "float", "sum", "mul",
-          "add", "clone", "contiguous"):
+for n in ("__mul__", "__rmul__", "__add__", "__radd__", "__sub__", "__rsub__", "__truediv__", "__neg__", "to",
+          "float", "double", "sum", "mul", "add", "clone", "contiguous", "__getitem__", "__setitem__", "copy_",
+          "exp", "log", "max", "amax", "masked_fill", "fill_", "zero_", "t", "reshape", "expand"):
     _wrap(n)
 
-import bench_resnet50  # noqa: E402
-
-sys.argv = ["bench_resnet50.py"] + sys.argv[1:]
+args = sys.argv[1:]
+target = "bench_resnet50"
+if args[:1] == ["--target"]:
+    target, args = args[1], args[2:]
+mod = __import__(target)
+sys.argv = [target + ".py"] + args
 try:
-    bench_resnet50.main()
+    mod.main()
 finally:
     for k, v in SITES.most_common(40):
         print(f"{v:6d}  {k}", file=sys.stderr)
