@@ -490,6 +490,30 @@ class Rewriter:
                     return self._hit("colwise-aggregate", Hop("u", [full], {"o": "cast_matrix"}, dt="M", dim1=1,
                                                               dim2=1, pos=h.pos))
             return h
+        if op == "b" and h.p["o"] in ("+", "-") and h.dt == "M" and not self.fuse:
+            # fuseAxpyBinaryOperationChain (Dynamic:2173): X + s * Y -> +*(X, s, Y), X - s * Y ->
+            # -*(X, s, Y) with s a scalar.  With operator fusion on, the Cell template fuses the
+            # chain (and its CP fallback runs it as one axpy, ops/cell.py), so this is for
+            # fusion-off plans.
+            a, b = h.inputs
+
+            def split(m):
+                if m.op != "b" or m.p["o"] != "*" or m.dt != "M" or m.id in self.multi:
+                    return None
+                p, q = m.inputs
+                if p.dt == "S" and q.dt == "M":
+                    return p, q
+                if q.dt == "S" and p.dt == "M":
+                    return q, p
+                return None
+            sgn = 1 if h.p["o"] == "+" else -1
+            for X, m in ((a, b), (b, a)) if sgn > 0 else ((a, b),):
+                sy = split(m) if X.dt == "M" else None
+                if sy is not None:
+                    return self._hit("fuse-axpy", Hop("bi", [X, sy[0], sy[1], H.lit(float(sgn), h.pos)],
+                                                      {"name": "_axpy", "npos": 4}, dt="M", dim1=h.dim1,
+                                                      dim2=h.dim2, pos=h.pos))
+            return h
         if op == "u" and h.p["o"] in ("cumsum", "cumprod", "cummin", "cummax"):
             # removeUnnecessaryCumulativeOp (Dynamic:346): a cumulative aggregate of one row is the row
             x = h.inputs[0]
@@ -633,7 +657,51 @@ class Rewriter:
                 return self._hit("ordered-sort", seq(n, lit(1), -1) if dec else seq(lit(1), n, 1))
             return self._hit("ordered-sort", Hop("bi", [X], {"name": "rev", "npos": 1}, dt="M", pos=h.pos) if dec
                              else X)
+        # fuseOrderOperationChain (Dynamic:2245): order(order(X, by=b1), by=b2) with equal
+        # `decreasing` and data results -> order(X, by=[b2, b1]): the outer stable sort keeps the
+        # inner order among its ties, i.e. one lexicographic sort on (b2, b1)
+        if not ixr and X.op == "bi" and X.p.get("name") == "order" and X.id not in self.multi:
+            inner = self._order_args(X)
+            by2 = args.get("by", lit(1))
+            if inner is not None and not inner[3] and inner[2] == dec and _num_lit(by2):
+                X0, by1 = inner[0], inner[1]
+                keys = [int(by2.value)] + by1
+                data = lit(" ".join(str(k) for k in keys))
+                bym = Hop("bi", [data, lit(len(keys)), lit(1)], {"name": "matrix", "npos": 1},
+                          ["rows", "cols"], dt="M", dim1=len(keys), dim2=1, pos=h.pos)
+                return self._hit("order-chain", Hop("bi", [X0, bym, lit(dec)], {"name": "order", "npos": 1},
+                                                    ["by", "decreasing"], dt="M", dim1=X0.dim1, dim2=X0.dim2,
+                                                    pos=h.pos))
         return h
+
+    def _order_args(self, h):
+        """(target, [by columns], decreasing, index.return) of an order hop with literal
+        arguments (by: an int or a literal column-index matrix), else None."""
+        npos = h.p.get("npos", len(h.inputs) - len(h.named))
+        names = ["target", "by", "decreasing", "index.return"]
+        args = {n: h.inputs[npos + j] for j, n in enumerate(h.named)}
+        for i in range(npos):
+            args[names[i]] = h.inputs[i]
+        if "target" not in args or set(args) - set(names):
+            return None
+        by = args.get("by", lit(1))
+        if _num_lit(by):
+            cols = [int(by.value)]
+        elif by.op == "bi" and by.p.get("name") == "matrix" and by.inputs and by.inputs[0].op == "lit" \
+                and isinstance(by.inputs[0].value, str):
+            try:
+                cols = [int(float(t)) for t in by.inputs[0].value.replace(",", " ").split()]
+            except ValueError:
+                return None
+        else:
+            return None
+        flags = []
+        for k in ("decreasing", "index.return"):
+            v = args.get(k)
+            if v is not None and not (v.op == "lit" and isinstance(v.value, bool)):
+                return None
+            flags.append(bool(v.value) if v is not None else False)
+        return args["target"], cols, flags[0], flags[1]
 
     def _rw_lix_chain(self, h):
         """fuseLeftIndexingChainToAppend (reference RewriteAlgebraicSimplificationDynamic.java:285):

@@ -511,9 +511,21 @@ def b_upper_tri(ctx, target=None, diag=False, values=False):
 def b_order(ctx, target=None, by=1, decreasing=False, **kw):
     m = _mat(target)
     idx_ret = _bool(kw.get("index.return", False))
-    col = m[:, _int(by) - 1]
-    # stable sort (ties keep input order), as the reference
-    perm = torch.sort(col, descending=_bool(decreasing), stable=True).indices
+    dec = _bool(decreasing)
+    if isinstance(by, Tensor) and by.numel() > 1:
+        # several key columns (a column vector of indices): lexicographic, first column major --
+        # stable sorts from the last key to the first
+        keys = [int(v) for v in by.reshape(-1).tolist()]
+        perm = torch.arange(m.shape[0], device=m.device)
+        for k in reversed(keys):
+            if k < 1 or k > m.shape[1]:
+                raise DMLRuntimeError(f"order: by column {k} out of range [1, {m.shape[1]}]")
+            p = torch.sort(m[perm, k - 1], descending=dec, stable=True).indices
+            perm = perm[p]
+    else:
+        col = m[:, _int(by) - 1]
+        # stable sort (ties keep input order), as the reference
+        perm = torch.sort(col, descending=dec, stable=True).indices
     if idx_ret:
         return (perm + 1).to(m.dtype).reshape(-1, 1)
     return m[perm]
@@ -643,6 +655,19 @@ def b_log_nz(ctx, x, base=None):
         return _nz_apply(x, torch.log)
     lb = float(np.log(_float(base)))
     return _nz_apply(x, lambda v: torch.log(v) / lb)
+
+
+@builtin("_axpy")
+def b_axpy(ctx, x, s, y, sign):
+    """X + sign * s * Y (reference TernaryOp PLUS_MULT / MINUS_MULT from
+    fuseAxpyBinaryOperationChain): one pass over equally shaped dense host operands; anything
+    else -- broadcasting, sparse, device or row-partitioned operands -- the two operators."""
+    sg = _float(sign)
+    if type(x) is Tensor and type(y) is Tensor and x.shape == y.shape and not x.is_cuda and not y.is_cuda \
+            and x.layout == torch.strided and y.layout == torch.strided and x.dtype == y.dtype \
+            and not isinstance(s, Tensor):
+        return torch.add(x, y, alpha=sg * _float(s))
+    return C.binary("+" if sg > 0 else "-", x, C.binary("*", s, y))
 
 
 @builtin("_sel")

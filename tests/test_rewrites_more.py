@@ -256,3 +256,38 @@ def test_ipa_function_call_sizes():
     assert "M[50x30]" in body or "M[50x20]" in body, body
     r, _ = EX.execute(cs, {}, out=lambda s: None)
     assert tuple(r["C1"].shape) == (50, 20)
+
+
+def _run_nofuse(src, ins, outs, rewrites=True):
+    cfg = DMLConfig(gpu=False, rewrites=rewrites, fusion=False)
+    cs = EX.compile_script(src, {}, inputs=ins, outputs=outs, config=cfg)
+    r, _ = EX.execute(cs, ins)
+    return cs.cp.rewrite_stats or {}, {k: v.double().numpy() for k, v in r.items()}
+
+
+def test_fuse_axpy_without_operator_fusion():
+    src = "s = 0.5\nZ = A + s * B2\nW = A - B2 * 2\nU = (3 * B2) + A"
+    ins = {"A": A, "B2": RNG.random((6, 4))}
+    st, a = _run_nofuse(src, ins, ["Z", "W", "U"])
+    _, b = _run_nofuse(src, ins, ["Z", "W", "U"], rewrites=False)
+    assert st.get("fuse-axpy", 0) == 3, st
+    for k in ("Z", "W", "U"):
+        np.testing.assert_allclose(a[k], b[k], rtol=1e-14)
+    np.testing.assert_allclose(a["W"], A - 2 * ins["B2"], rtol=1e-14)
+
+
+def test_fuse_axpy_keeps_broadcasting_semantics():
+    src = "Z = A + 2 * r"                        # r: 1 x 4 row vector broadcast over A's rows
+    ins = {"A": A, "r": RNG.random((1, 4))}
+    st, a = _run_nofuse(src, ins, ["Z"])
+    np.testing.assert_allclose(a["Z"], A + 2 * ins["r"], rtol=1e-14)
+
+
+def test_order_chain_to_multi_key_order():
+    M = np.array([[3, 1, 9], [1, 2, 8], [3, 0, 7], [1, 1, 6], [2, 2, 5], [3, 1, 4]], dtype=float)
+    src = "O = order(target=order(target=M, by=2), by=1)\nP = order(target=order(target=M, by=3, decreasing=TRUE), " \
+          "by=1, decreasing=TRUE)"
+    _check(src, {"M": M}, ["O", "P"], "order-chain")
+    st, a, _ = _run(src, {"M": M}, ["O"])
+    # lexicographic on (column 1, column 2), stable
+    np.testing.assert_array_equal(a["O"][:, :2], [[1, 1], [1, 2], [2, 2], [3, 0], [3, 1], [3, 1]])
