@@ -350,8 +350,41 @@ MAGG_MAX = 4
 ROW_AGG_OPS = ("sum", "sumsq", "mean", "min", "max")
 
 
+ROW_MAXW = 16       # widest side matrix of a Row-template product (ops/rowgen.MAXW)
+ROW_MERGE = __import__("os").environ.get("SYSML_ROW_MERGE", "1") != "0"   # multi-output Row programs
+
+
+def _narrow(h):
+    """A side operand of a row product: a D x 1 vector or a D x K matrix with K <= ROW_MAXW
+    (unknown widths are admitted; the kernel re-checks the actual shapes)."""
+    return h.dim2 == -1 or 1 <= h.dim2 <= ROW_MAXW
+
+
+def _const_col(h):
+    """The scalar c of a constant column matrix(c, rows=n, cols=1), else None."""
+    if h.op == "bi" and h.p.get("name") == "matrix" and len(h.inputs) == 3 and h.inputs[0].dt == "S" \
+            and h.inputs[2].op == "lit" and h.inputs[2].value == 1 and h.p.get("npos", 1) == 1:
+        return h.inputs[0]
+    return None
+
+
+def _wcols_k(h):
+    """k of a leading-column slice X[, 1:k] with literal bounds, else None."""
+    if h.op != "rix" or len(h.inputs) != 5:
+        return None
+    _, rl, ru, cl, cu = h.inputs
+    none = lambda z: z.op == "lit" and z.value is None                      # noqa: E731
+    if none(rl) and none(ru) and cl.op == "lit" and cl.value == 1 and cu.op == "lit" \
+            and isinstance(cu.value, (int, float)) and not isinstance(cu.value, bool) and 1 <= cu.value <= ROW_MAXW:
+        return int(cu.value)
+    return None
+
+
 def _row_body_kind(h):
-    """Role of h inside a Row-template region: 'cell' | 'ragg' | 'dot' | None (not fusable)."""
+    """Role of h inside a Row-template region: 'cell' | 'ragg' | 'dot' | 'cbindc' | 'wcols' |
+    None (not fusable).  'cbindc' (a constant column appended) and 'wcols' (leading columns)
+    apply to the narrow per-row vectors of products with side matrices only -- the region
+    admits them when their input is a region product (_form_row_region)."""
     if h.dt != "M" or _is_bias(h):
         return None
     if _cellwise(h):
@@ -359,8 +392,12 @@ def _row_body_kind(h):
     if h.op == "agg" and h.p.get("dir") == "row" and h.p.get("o") in ROW_AGG_OPS and len(h.inputs) == 1:
         return "ragg"
     if h.op == "mm" and not h.p.get("transA") and not h.p.get("mvagg") and len(h.inputs) == 2 \
-            and h.inputs[1].dim2 in (-1, 1) and h.inputs[0].dim2 != 1:
+            and _narrow(h.inputs[1]) and h.inputs[0].dim2 != 1:
         return "dot"
+    if h.op == "bi" and h.p.get("name") == "cbind" and len(h.inputs) == 2 and _const_col(h.inputs[1]) is not None:
+        return "cbindc"
+    if _wcols_k(h) is not None:
+        return "wcols"
     return None
 
 
@@ -373,16 +410,24 @@ def _row_root_kind(h):
             and h.inputs[0].dt == "M":
         return "all"
     if h.dt == "M" and h.op == "mm" and h.p.get("transA") and not h.p.get("mvagg") and len(h.inputs) == 2 \
-            and h.inputs[1].dim2 in (-1, 1):
+            and _narrow(h.inputs[1]):
         return "tmv"
     return None
 
 
 def _body_inputs(h, kind):
     """Inputs of a region hop that may join the region (a dot's side vector never does)."""
-    if kind == "dot":
+    if kind in ("dot", "cbindc", "wcols"):
         return [h.inputs[0]]
     return _operands(h) if kind == "cell" else list(h.inputs)
+
+
+def _narrow_source(x, kinds):
+    """x is (derived from) a region product with a side matrix: a K-wide per-row vector."""
+    k = kinds.get(x.id)
+    if k in ("dot", "cbindc", "wcols"):
+        return True
+    return k == "cell" and any(_narrow_source(c, kinds) for c in _operands(x) if c.id in kinds)
 
 
 def _size_class(h, memo):
@@ -397,7 +442,9 @@ def _size_class(h, memo):
     if h.dt == "S" or h.op == "lit":
         r = 0.0
     elif h.dim1 >= 0 and h.dim2 >= 0:
-        r = 0.0 if h.dim1 * h.dim2 <= 1 else (1.0 if (h.dim1 > 1 and h.dim2 > 1) else 1e-3)
+        # narrow matrices (N x K, K <= ROW_MAXW: per-row vectors of products with side
+        # matrices) are priced by their width like K per-row scalars
+        r = 0.0 if h.dim1 * h.dim2 <= 1 else (1.0 if (h.dim1 > 1 and h.dim2 > ROW_MAXW) else 1e-3 * max(h.dim2, 1))
     else:
         k = _row_body_kind(h)
         if k in ("ragg", "dot"):
@@ -483,6 +530,119 @@ def fuse_rows(bb, costed=True):
             return n
 
 
+def _row_key(h):
+    """The matrix a Row-template hop streams: its first product's row operand, else its first
+    matrix input that is not narrow (rows of the program)."""
+    prog = h.p["prog"]
+    for kind, _, a, _ in prog.ops:
+        if kind == "dot" and a < prog.n_in:
+            return h.inputs[a]
+    for x in h.inputs:
+        if x.dt == "M" and not (0 < x.dim2 <= ROW_MAXW):
+            return x
+    return None
+
+
+def merge_row_programs(bb):
+    """Multi-output Row template (reference: the multi-aggregate / multi-output CPlans of
+    hops/codegen): Row-template hops of a block that stream the same matrix and do not depend
+    on each other become ONE program with several outputs, its operators de-duplicated (a
+    product X %*% B recomputed by several regions is computed once), so the kernel reads the
+    rows once for all of them.  The original hops become fout views of the merged one.
+    Returns the number of hops merged away."""
+    from ..ops.rowgen import RowProgram, MAXIN as RMAXIN, MAXOPS as RMAXOPS, MAXOUT as RMAXOUT
+    allroots = list(bb.roots) + list(bb.env_out.values())
+    order = walk(allroots)
+    rows = [h for h in order if h.op == "row" and not h.p["prog"].more]
+    groups = {}
+    for h in rows:
+        k = _row_key(h)
+        if k is not None:
+            groups.setdefault(k.id, []).append(h)
+    merged = 0
+    if not ROW_MERGE:
+        return 0
+    for grp in groups.values():
+        while len(grp) > 1:
+            taken = [grp[0]]
+            for h in grp[1:]:
+                if len(taken) >= RMAXOUT:
+                    break
+                # independent of every taken hop, both ways
+                if any(_reaches(h, t) or _reaches(t, h) for t in taken):
+                    continue
+                taken.append(h)
+            grp = [h for h in grp if h not in taken]
+            if len(taken) < 2:
+                continue
+            r = _merge(taken, RowProgram, RMAXIN, RMAXOPS)
+            if r is None:
+                continue
+            prog, leaves = r
+            M = Hop("row", leaves, {"o": prog.describe(), "prog": prog,
+                                    "lines": sorted({ln for t in taken for ln in t.p.get("lines", ())})},
+                    dt="U", pos=taken[0].pos)
+            for i, t in enumerate(taken):
+                t.op = "fout"
+                t.inputs = [M]
+                t.named = []
+                t.p = {"i": i}
+            merged += len(taken) - 1
+    return merged
+
+
+def _reaches(a, b):
+    """b is (transitively) an input of a."""
+    seen = set()
+    stack = list(a.inputs)
+    while stack:
+        x = stack.pop()
+        if x is b:
+            return True
+        if x.id in seen:
+            continue
+        seen.add(x.id)
+        stack.extend(x.inputs)
+    return False
+
+
+def _merge(hops, RowProgram, RMAXIN, RMAXOPS):
+    leaves = []
+
+    def leaf(x):
+        for i, y in enumerate(leaves):
+            if y is x:
+                return i
+        leaves.append(x)
+        return len(leaves) - 1
+    maps = []
+    for h in hops:
+        maps.append([leaf(x) for x in h.inputs])
+    nin = len(leaves)
+    if nin > RMAXIN:
+        return None
+    ops, seen, outs = [], {}, []
+    for h, m in zip(hops, maps):
+        prog = h.p["prog"]
+        loc = list(m)
+        for kind, o, a, b in prog.ops:
+            a2 = loc[a]
+            b2 = loc[b] if kind in ("b", "dot", "cbindc") else b
+            key = (kind, o, a2, b2)
+            j = seen.get(key)
+            if j is None:
+                ops.append(key)
+                j = seen[key] = nin + len(ops) - 1
+            loc.append(j)
+        for node, ot, oagg, extra in prog.outputs():
+            outs.append((loc[node], ot, oagg, loc[extra] if extra is not None else None))
+    if len(ops) > RMAXOPS:
+        return None
+    p0 = outs[0]
+    parts = tuple((h.p["prog"], tuple(m)) for h, m in zip(hops, maps))
+    return RowProgram(nin, ops, p0[0], p0[1], p0[2], p0[3], more=outs[1:], parts=parts), leaves
+
+
 def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXIN, RMAXOPS):
     rk = _row_root_kind(root)
     bk = _row_body_kind(root)
@@ -508,6 +668,9 @@ def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXI
             ck = _row_body_kind(c)
             if ck is None:
                 continue
+            if ck in ("cbindc", "wcols") and c.inputs[0].id not in region and \
+                    _row_body_kind(c.inputs[0]) not in ("dot", "cell", "cbindc", "wcols"):
+                continue             # a plain matrix's column slice / append stays outside
             # closure: every consumer is in the region and none of them is a recomputed copy
             # (a copied operator stays alive outside the region and still reads c)
             closed = c.id not in outs and all(p.id in region and p.id not in dup for p in consumers.get(c.id, ()))
@@ -548,6 +711,13 @@ def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXI
         return len(leaves) - 1
     for h in body:
         k = kinds[h.id]
+        if k in ("cbindc", "wcols") and h.inputs[0].id not in kinds:
+            return 0                 # applies to region products only
+        if k == "cbindc":
+            leaf(_const_col(h.inputs[1]))
+            continue
+        if k == "wcols":
+            continue
         for c in h.inputs:
             if c.id not in kinds and not (k == "cell" and h.op == "b" and _is_sq(h) and c is h.inputs[1]):
                 leaf(c)
@@ -579,6 +749,10 @@ def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXI
                 ops.append(("u", h.p["o"], ref(h.inputs[0]), 0))
         elif k == "ragg":
             ops.append(("ragg", h.p["o"], ref(h.inputs[0]), 0))
+        elif k == "cbindc":
+            ops.append(("cbindc", None, ref(h.inputs[0]), ref(_const_col(h.inputs[1]))))
+        elif k == "wcols":
+            ops.append(("wcols", None, ref(h.inputs[0]), _wcols_k(h)))
         else:
             ops.append(("dot", None, ref(h.inputs[0]), ref(h.inputs[1])))
         idx[h.id] = nin + len(ops) - 1

@@ -125,6 +125,8 @@ def infer(h, dims, env):
         return (m, kb) if ot == "left" else (nn, kb)
     if op == "row":
         from ..ops.rowgen import out_shape
+        if h.p["prog"].more:
+            return UNK                   # a tuple of outputs, read through fout hops
         if h.p["prog"].otype == "all":
             return SCALAR
         if not all(x == SCALAR or _known(x) for x in ins):

@@ -1280,6 +1280,9 @@ def cse(roots):
 
 _ROWGEN = __import__('os').environ.get('SYSML_ROWGEN', '1') != '0'   # Row / Outer templates on
 _VECGEN = __import__('os').environ.get('SYSML_VECGEN', '1') != '0'   # Vector template on
+# the hand-matched softmax gradient / objective operators (smgrad / smobj, chain4m kernels); off:
+# the Row template plans the same passes as generated multi-output programs
+SOFTMAX_MATCHER = __import__('os').environ.get('SYSML_SOFTMAX_MATCHER', '1') != '0'
 
 
 def _conv_gemm_path(c, config):
@@ -1391,7 +1394,7 @@ def rewrite_block(bb, config=None):
         n = fuse_conv_bias(bb, config)
         if n:
             rw.stats["conv2d-bias-add"] = n
-        n = fuse_softmax_grad(bb)
+        n = fuse_softmax_grad(bb) if SOFTMAX_MATCHER else 0
         if n:
             rw.stats["softmax-grad"] = n
             nobj = sum(1 for h in H.walk(list(bb.roots) + list(bb.env_out.values())) if h.op == "smobj")
@@ -1405,6 +1408,10 @@ def rewrite_block(bb, config=None):
             n = fuse_rows(bb)
             if n:
                 rw.stats["row-fused-ops"] = n
+                from .codegen import merge_row_programs
+                m = merge_row_programs(bb)
+                if m:
+                    rw.stats["row-multi-output"] = m
         if _VECGEN and (config is None or getattr(config, "gpu", True)):
             # Vector template: only a GPU backend has launches and round trips to save
             from .vecgen import fuse_vectors

@@ -304,10 +304,10 @@ inline bool vec_cols(const void* X, int D) {
   return false;
 }
 
-// row chunks of a column aggregate: enough workgroups for the chip (>= 1024) and >= 256 rows each
+// row chunks of a column aggregate: enough workgroups for the chip (>= 1024) and >= 64 rows each
 inline void col_chunks(int64_t N, int strips, int64_t& nch, int64_t& rows) {
   nch = (1024 + strips - 1) / strips;
-  const int64_t maxch = (N + 255) / 256;
+  const int64_t maxch = (N + 63) / 64;
   if (nch > maxch) nch = maxch;
   if (nch < 1) nch = 1;
   rows = (N + nch - 1) / nch;

@@ -31,7 +31,18 @@ def _inputs(n=500, d=37, seed=0):
 
 
 def _row_hops(cs):
-    return [ln for ln in EX.explain(cs.cp, "hops").splitlines() if "row[" in ln]
+    """Descriptions of the Row-template programs of the plan; a merged multi-output program
+    (codegen.merge_row_programs) contributes its own and its source programs'."""
+    from systemml_amd.compiler import hops as H
+    from systemml_amd.compiler.blocks import BasicBlock
+    out = []
+    for b in cs.cp.blocks:
+        if isinstance(b, BasicBlock):
+            for h in H.walk(list(b.roots) + list(b.env_out.values())):
+                if h.op == "row":
+                    out.append(h.p["prog"].describe())
+                    out.extend(p.describe() for p, _ in h.p["prog"].parts)
+    return out
 
 
 def test_row_plans_and_parity_with_unfused():
@@ -47,6 +58,8 @@ def test_row_plans_and_parity_with_unfused():
     # in each of them and never materialised (no plain matrix product left in the plan)
     plan = EX.explain(cs.cp, "hops")
     assert " mm " not in plan.replace("(", " ").replace(")", " "), plan
+    # all regions stream X: they are merged into multi-output programs (one pass over X)
+    assert cs.cp.rewrite_stats.get("row-multi-output", 0) >= 1, cs.cp.rewrite_stats
     res, _ = EX.execute(cs, ins)
     cs0 = EX.compile_script(SCRIPT, {}, inputs=ins, outputs=OUTS, config=DMLConfig(gpu=False, fusion=False))
     assert not _row_hops(cs0)
@@ -223,3 +236,150 @@ def test_row_script_on_gpu_matches_cp():
         a = a.double().cpu() if isinstance(a, torch.Tensor) else torch.tensor(float(a.value() if hasattr(a, "value") else a))
         b = b.double().cpu() if isinstance(b, torch.Tensor) else torch.tensor(float(b))
         assert torch.allclose(a, b, rtol=1e-9, atol=1e-9), k
+
+
+# ----------------------------------------------------------------------------- K-wide row vectors
+def _ref_w(prog, args):
+    """fp64 torch evaluation of a RowProgram with K-wide vectors and several outputs."""
+    B = {"+": torch.add, "-": torch.sub, "*": torch.mul, "/": torch.div}
+    U = {"exp": torch.exp, "log": torch.log, "sq": lambda x: x * x}
+    RA = {"sum": lambda t: t.sum(1, keepdim=True), "max": lambda t: t.amax(1, keepdim=True),
+          "mean": lambda t: t.mean(1, keepdim=True)}
+    vals = [a.double().cpu() if isinstance(a, torch.Tensor) else torch.tensor(float(a), dtype=torch.float64)
+            for a in args]
+    for kind, o, a, b in prog.ops:
+        if kind == "b":
+            vals.append(B[o](vals[a], vals[b]))
+        elif kind == "u":
+            vals.append(U[o](vals[a]))
+        elif kind == "ragg":
+            vals.append(RA[o](vals[a]))
+        elif kind == "cbindc":
+            vals.append(torch.cat([vals[a], vals[b].reshape(1, 1).expand(vals[a].shape[0], 1)], 1))
+        elif kind == "wcols":
+            vals.append(vals[a][:, :b])
+        else:
+            vals.append(vals[a] @ vals[b])
+    res = []
+    for node, ot, oagg, extra in prog.outputs():
+        r = vals[node]
+        if ot == "tmv":
+            r = r.t() @ vals[extra]
+        elif ot == "col":
+            r = r.sum(0, keepdim=True)
+        elif ot == "all":
+            r = r.sum() if oagg == "sum" else r.max()
+        res.append(r)
+    return res
+
+
+def _softmax_objective_program():
+    from systemml_amd.ops.rowgen import RowProgram
+    # inputs: 0 X (N x D), 1 B (D x K side), 2 Y (N x K+1), 3 c (scalar 0), 4 Yk (N x K)
+    ops = [("dot", None, 0, 1),          # 5  W = X %*% B
+           ("cbindc", None, 5, 3),       # 6  LT = cbind(W, 0)
+           ("ragg", "max", 6, 0),        # 7  rowMaxs(LT)
+           ("b", "-", 6, 7),             # 8  LT - rowMaxs
+           ("u", "exp", 8, 0),           # 9  E
+           ("ragg", "sum", 9, 0),        # 10 rowSums(E)
+           ("b", "/", 9, 10),            # 11 P
+           ("b", "*", 2, 8),             # 12 Y * LT
+           ("u", "log", 10, 0),          # 13 log(rowSums(E))
+           ("wcols", None, 11, None),    # 14 P[, 1:K]  (k filled below)
+           ("b", "-", 14, 4)]            # 15 P[, 1:K] - Yk
+    return ops
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d,k", [(2049, 1000, 5), (3001, 37, 3), (257, 130, 10), (40000, 256, 2)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_row_kernel_side_matrix_multi_output(n, d, k, dt):
+    """The MultiLogReg candidate pass as ONE generated program: X %*% B (D x K side matrix),
+    cbind of the baseline column, row max / exp / row sum softmax, the objective's data terms
+    and t(X) %*% (P[, 1:K] - Y[, 1:K]) -- five outputs from one pass over X."""
+    from systemml_amd.ops import rowgen, kernels
+    from systemml_amd.ops.rowgen import RowProgram
+    from systemml_amd.ops.backend import backend
+    ops = _softmax_objective_program()
+    ops[9] = ("wcols", None, 11, k)
+    prog = RowProgram(5, ops, 11, "vec", more=[(12, "all", "sum", None), (13, "all", "sum", None),
+                                              (0, "tmv", None, 15), (10, "row", None, None)])
+    X = _mk((n, d), dt, 1)
+    Bm = _mk((d, k), torch.float32, 2, -2.0 / d ** 0.5, 2.0 / d ** 0.5)
+    Y = torch.zeros(n, k + 1)
+    Y[torch.arange(n), torch.randint(0, k + 1, (n,), generator=torch.Generator().manual_seed(3))] = 1.0
+    args = [X, Bm, Y, 0.0, Y[:, :k].contiguous()]
+    backend.configure(DMLConfig(gpu=True, precision="single"))
+    dev = torch.device("cuda:0")
+    dargs = [a.to(dev) if isinstance(a, torch.Tensor) else a for a in args]
+    c0 = kernels.counters.get("row", 0)
+    got = rowgen._kernel(prog, dargs)
+    assert got is not None, "operands outside the kernel's scope"
+    torch.cuda.synchronize()
+    assert kernels.counters.get("row", 0) == c0 + 1 and len(got) == 5
+    refs = _ref_w(prog, [X.double(), Bm, Y, 0.0, Y[:, :k]])
+    for q, (g, r) in enumerate(zip(got, refs)):
+        g = torch.as_tensor(g.value() if hasattr(g, "value") else g, dtype=torch.float64).cpu().reshape(r.shape)
+        err = (g - r).abs().max().item() / (r.abs().max().item() + 1e-30)
+        assert err < 2e-5, (q, err)
+
+
+@pytest.mark.gpu
+def test_multilogreg_pass_planned_by_row_template_on_gpu():
+    """With the hand matcher off, the candidate pass of MultiLogReg is planned by the Row
+    template (merged multi-output program) and runs as generated kernels on the GPU, matching
+    the CPU plan."""
+    import systemml_amd.compiler.rewrites as RW
+    from systemml_amd.ops import rowgen
+    src = """
+    LT = cbind(X %*% B, matrix(0, rows=nrow(X), cols=1))
+    LT = LT - rowMaxs(LT)
+    E = exp(LT)
+    P = E / rowSums(E)
+    o1 = sum(Y * LT)
+    o2 = sum(log(rowSums(E)))
+    G = t(X) %*% (P[, 1:4] - Y[, 1:4])
+    """
+    rng = np.random.default_rng(0)
+    ins = {"X": rng.standard_normal((20000, 300)) * 0.05, "B": rng.standard_normal((300, 4)),
+           "Y": np.eye(5)[rng.integers(0, 5, 20000)]}
+    outs = ["P", "o1", "o2", "G"]
+    old = RW.SOFTMAX_MATCHER
+    RW.SOFTMAX_MATCHER = False
+    try:
+        res = {}
+        for gpu in (True, False):
+            cfg = DMLConfig(gpu=gpu, precision="double", gpu_min_cells=0)
+            cs = EX.compile_script(src, {}, inputs=ins, outputs=outs, config=cfg)
+            assert cs.cp.rewrite_stats.get("row-multi-output", 0) >= 1, cs.cp.rewrite_stats
+            k0 = rowgen.stats["kernel"]
+            r, _ = EX.execute(cs, ins)
+            if gpu:
+                assert rowgen.stats["kernel"] > k0
+            res[gpu] = {k: (v.double().cpu().numpy() if hasattr(v, "numpy") else np.array(float(v))) for k, v in r.items()}
+    finally:
+        RW.SOFTMAX_MATCHER = old
+    for k in outs:
+        np.testing.assert_allclose(res[True][k], res[False][k], rtol=1e-9, atol=1e-9, err_msg=k)
+
+
+
+
+def test_softmax_layer_forward_backward_row_fused():
+    """nn/layers/softmax.dml forward and backward each become ONE Row-template operator."""
+    import os
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    src = 'source("nn/layers/softmax.dml") as softmax\nP = softmax::forward(S)\ndS = softmax::backward(dP, S)'
+    rng = np.random.default_rng(4)
+    ins = {"S": rng.standard_normal((300, 10)), "dP": rng.standard_normal((300, 10))}
+    cs = EX.compile_script(src, {}, inputs=ins, outputs=["P", "dS"], config=DMLConfig(gpu=False),
+                           filename=os.path.join(SCRIPTS_DIR, "sm.dml"))
+    main = EX.explain(cs.cp, "runtime").split("MAIN PROGRAM")[1]
+    ops = [ln.split()[0] for ln in main.splitlines()[1:] if ln.strip()]
+    assert ops.count("spoofRA") + ops.count("fout") >= 2 and "rowSums" not in main, main
+    res, _ = EX.execute(cs, ins)
+    S, dP = ins["S"], ins["dP"]
+    e = np.exp(S - S.max(1, keepdims=True))
+    P = e / e.sum(1, keepdims=True)
+    np.testing.assert_allclose(res["P"].numpy(), P, rtol=1e-12)
+    np.testing.assert_allclose(res["dS"].numpy(), P * (dP - (dP * P).sum(1, keepdims=True)), rtol=1e-12)
