@@ -513,9 +513,13 @@ def generate(prog: RowProgram, T, modes, dts, kinds, L, dcap, vec=1, slices=None
         if modes[k] == SIDEM:
             K = widths[k]
             if dcap and dcap * K * (4 if T == torch.float32 else 8) <= 32768:
+                # column-major in LDS ([K][dcap]): a lane's VEC consecutive d of one column are
+                # adjacent words (vector LDS reads; the row-major [d][K] layout put the lanes'
+                # d, VEC apart, on one bank)
                 w(f"  __shared__ T sm{k}[{dcap * K}];")
-                w(f"  for (int q = tid; q < D * {K}; q += 256) sm{k}[q] = sysml_ld<T>(A.in[{k}], {dts[k]}, q);")
-                smat[k] = lambda d, kk, k=k, K=K: f"sm{k}[({d}) * {K} + {kk}]"
+                w(f"  for (int q = tid; q < D * {K}; q += 256) sm{k}[(q % {K}) * {dcap} + q / {K}] = "
+                  f"sysml_ld<T>(A.in[{k}], {dts[k]}, q);")
+                smat[k] = lambda d, kk, k=k, dc=dcap: f"sm{k}[({kk}) * {dc} + ({d})]"
             else:
                 smat[k] = lambda d, kk, k=k, K=K: f"sysml_ld<T>(A.in[{k}], {dts[k]}, ({d}) * {K} + {kk})"
     colacc = ca is not None
