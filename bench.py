@@ -295,6 +295,9 @@ def main():
         ps = pstats.Stats(prof, stream=buf)
         ps.sort_stats("tottime").print_stats(45)
         ps.sort_stats("cumulative").print_stats(60)
+        # who waits for the device: the callers of the blocking reads
+        for fn in ("tolist", "synchronize", "'cpu'", "'item'", "'to'"):
+            ps.print_callers(fn)
         with open(a.host_profile, "w") as f:
             f.write(buf.getvalue())
     if rank == 0:

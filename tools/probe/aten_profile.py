@@ -28,23 +28,22 @@ def main():
     sys.argv = [target + ".py"] + args
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
         mod.main()
-    agg = collections.defaultdict(lambda: [0, 0.0])
-    for e in prof.events():
-        if not e.name.startswith("aten::"):
+    rows = []
+    for e in prof.key_averages(group_by_stack_n=12):
+        if not e.key.startswith("aten::"):
             continue
-        dev = getattr(e, "self_device_time_total", None)      # self: nested aten ops counted once
+        dev = getattr(e, "self_device_time_total", None)
         if dev is None:
             dev = getattr(e, "self_cuda_time_total", 0.0)
         if not dev:
             continue
-        st = [f for f in (e.stack or []) if "systemml_amd" in f]
-        key = (e.name,) + tuple(os.path.basename(f.split("(")[0]) + f[f.find("("):f.find(")") + 1] for f in st[:3])
-        agg[key][0] += 1
-        agg[key][1] += dev
-    tot = sum(v[1] for v in agg.values())
-    print(f"ATen device time {tot / 1e3:.1f} ms over {sum(v[0] for v in agg.values())} calls", file=sys.stderr)
-    for k, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
-        print(f"{t / 1e3:9.2f} ms {n:6d}  {k}", file=sys.stderr)
+        st = [f for f in (e.stack or []) if "systemml_amd" in f or "bench" in f]
+        rows.append((dev, e.count, e.key, [f.split("/")[-1] for f in st[:4]]))
+    rows.sort(key=lambda r: -r[0])
+    tot = sum(r[0] for r in rows)
+    print(f"ATen self device time {tot / 1e3:.1f} ms", file=sys.stderr)
+    for dev, n, k, st in rows[:top]:
+        print(f"{dev / 1e3:9.2f} ms {n:6d}  {k}  {' < '.join(st)}", file=sys.stderr)
 
 
 if __name__ == "__main__":
