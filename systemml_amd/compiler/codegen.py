@@ -369,15 +369,19 @@ def _const_col(h):
 
 
 def _wcols_k(h):
-    """k of a leading-column slice X[, 1:k] with literal bounds, else None."""
+    """k of a leading-column slice X[, 1:k]: an int for a literal bound, the bound's hop for a
+    scalar expression (the kernel is specialised on its value at run time), else None."""
     if h.op != "rix" or len(h.inputs) != 5:
         return None
     _, rl, ru, cl, cu = h.inputs
     none = lambda z: z.op == "lit" and z.value is None                      # noqa: E731
-    if none(rl) and none(ru) and cl.op == "lit" and cl.value == 1 and cu.op == "lit" \
-            and isinstance(cu.value, (int, float)) and not isinstance(cu.value, bool) and 1 <= cu.value <= ROW_MAXW:
-        return int(cu.value)
-    return None
+    if not (none(rl) and none(ru) and cl.op == "lit" and cl.value == 1):
+        return None
+    if cu.op == "lit":
+        if isinstance(cu.value, (int, float)) and not isinstance(cu.value, bool) and 1 <= cu.value <= ROW_MAXW:
+            return int(cu.value)
+        return None
+    return cu if cu.dt == "S" else None
 
 
 def _row_body_kind(h):
@@ -627,7 +631,7 @@ def _merge(hops, RowProgram, RMAXIN, RMAXOPS):
         loc = list(m)
         for kind, o, a, b in prog.ops:
             a2 = loc[a]
-            b2 = loc[b] if kind in ("b", "dot", "cbindc") else b
+            b2 = loc[b] if kind in ("b", "dot", "cbindc", "wcolsv") else b
             key = (kind, o, a2, b2)
             j = seen.get(key)
             if j is None:
@@ -717,6 +721,9 @@ def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXI
             leaf(_const_col(h.inputs[1]))
             continue
         if k == "wcols":
+            kb = _wcols_k(h)
+            if not isinstance(kb, int):
+                leaf(kb)
             continue
         for c in h.inputs:
             if c.id not in kinds and not (k == "cell" and h.op == "b" and _is_sq(h) and c is h.inputs[1]):
@@ -752,7 +759,9 @@ def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXI
         elif k == "cbindc":
             ops.append(("cbindc", None, ref(h.inputs[0]), ref(_const_col(h.inputs[1]))))
         elif k == "wcols":
-            ops.append(("wcols", None, ref(h.inputs[0]), _wcols_k(h)))
+            kb = _wcols_k(h)
+            ops.append(("wcols", None, ref(h.inputs[0]), kb) if isinstance(kb, int)
+                       else ("wcolsv", None, ref(h.inputs[0]), ref(kb)))
         else:
             ops.append(("dot", None, ref(h.inputs[0]), ref(h.inputs[1])))
         idx[h.id] = nin + len(ops) - 1

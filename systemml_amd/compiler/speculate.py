@@ -108,13 +108,16 @@ def _clone_into(root, bb1, src_var):
 
 def _fuses(bb1, var, config):
     """Trial rewrite of a copy of bb1: does the speculative product end up as an output of
-    a fused softmax pass (smobj / smgrad)?"""
+    a fused pass over X (smobj / smgrad, or a multi-output Row-template program)?"""
     from . import rewrites as RW
     trial = copy.deepcopy(bb1)
     trial.live_out = None
     RW.rewrite_block(trial, config)
     h = trial.env_out.get(var)
-    return h is not None and h.op == "fout" and h.inputs[0].op in ("smobj", "smgrad")
+    # absorbed by the hand-matched softmax pass, or an output of a merged multi-output Row
+    # program that streams X anyway (codegen.merge_row_programs)
+    return h is not None and h.op == "fout" and (h.inputs[0].op in ("smobj", "smgrad") or
+                                                  (h.inputs[0].op == "row" and h.inputs[0].p["prog"].more))
 
 
 def _try_pair(bb1, mid_writes, bb2, config, stats):

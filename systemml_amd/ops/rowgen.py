@@ -92,7 +92,7 @@ class RowProgram:
         return {b for kind, _, _, b in self.ops if kind == "dot"}
 
     def describe(self):
-        body = ",".join(("dot" if k == "dot" else (f"r{o}" if k == "ragg" else (k if k in ("cbindc", "wcols") else o)))
+        body = ",".join(("dot" if k == "dot" else (f"r{o}" if k == "ragg" else (k if k in ("cbindc", "wcols", "wcolsv") else o)))
                         for k, o, _, _ in self.ops)
         tails = []
         for _, ot, oagg, _ in self.outputs():
@@ -114,7 +114,7 @@ def _seq_value(kind, o, va, vb):
         col = vb if isinstance(vb, torch.Tensor) and vb.dim() == 2 else \
             torch.full((va.shape[0], 1), float(C._num(vb)), dtype=va.dtype, device=va.device)
         return torch.cat([va, col.to(va.dtype).to(va.device).expand(va.shape[0], 1)], 1)
-    if kind == "wcols":
+    if kind in ("wcols", "wcolsv"):
         return C.rix(va, None, None, 1, vb)
     return C.mm(va, vb, False)
 
@@ -134,7 +134,7 @@ def sequential(prog: RowProgram, args):
     """The fused DAG's original operators, one after the other."""
     vals = list(args)
     for kind, o, a, b in prog.ops:
-        vals.append(_seq_value(kind, o, vals[a], vals[b] if kind in ("b", "dot", "cbindc") else b))
+        vals.append(_seq_value(kind, o, vals[a], vals[b] if kind in ("b", "dot", "cbindc", "wcolsv") else b))
     outs = tuple(_seq_output(vals, *o) for o in prog.outputs())
     return outs if prog.more else outs[0]
 
@@ -315,6 +315,8 @@ def out_shape(prog: RowProgram, shapes, which=0):
             if sa is None or b > sa[1]:
                 return None
             v.append((sa[0], b))
+        elif kind == "wcolsv":
+            return None                      # width known at run time only
         else:
             sb = v[b]
             if sa is None or sb is None or sa[1] != sb[0]:
@@ -1139,13 +1141,40 @@ def _make_plan(prog: RowProgram, args):
 _plans = {}
 
 
+_spec = {}
+
+
+def _specialise(prog, args):
+    """prog with every run-time column bound (wcolsv: X[, 1:k], k a scalar operand) replaced by
+    its value, or None when a bound is not a host integer in range."""
+    if not any(k == "wcolsv" for k, _, _, _ in prog.ops):
+        return prog, ()
+    bounds = []
+    for kind, _, _, b in prog.ops:
+        if kind == "wcolsv":
+            v = args[b] if b < prog.n_in else None
+            if type(v) not in (int, float) or v != int(v) or not 1 <= int(v) <= MAXW:
+                return None, None
+            bounds.append(int(v))
+    key = (id(prog), tuple(bounds))
+    sp = _spec.get(key)
+    if sp is None or sp[0] is not prog:
+        it = iter(bounds)
+        ops = [("wcols", None, a, next(it)) if k == "wcolsv" else (k, o, a, b) for k, o, a, b in prog.ops]
+        sp = _spec[key] = (prog, RowProgram(prog.n_in, ops, prog.out, prog.otype, prog.oagg, prog.extra, prog.more))
+    return sp[1], tuple(bounds)
+
+
 def _kernel(prog: RowProgram, args):
     """One launch of the generated row kernel, or None when the operands are outside its scope
     (launch plans cached per program and operand signature)."""
     sig = _signature(args)
     if sig is None:
         return None
-    key = (id(prog), sig)
+    prog, bounds = _specialise(prog, args)
+    if prog is None:
+        return None
+    key = (id(prog), sig, bounds)
     pl = _plans.get(key, False)
     if pl is False or (pl is not None and pl.prog is not prog):
         pl = _make_plan(prog, args)

@@ -14,4 +14,9 @@ rc=$?; echo "aten rc=$rc $(date)" >> $P; [ $rc -gt 1 ] && exit $rc
 timeout -k 10 300 python -u bench.py --rows 1250000 --steps 4 --warmup 3 --host-profile gpurun_out/rl_hprof.txt \
     > gpurun_out/rl_hprof.log 2>&1
 rc=$?; echo "hprof rc=$rc $(date)" >> $P
+
+SYSML_SOFTMAX_MATCHER=0 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 > gpurun_out/rl_10m_nomatch.log 2>&1
+rc=$?; echo "10m nomatcher rc=$rc $(date)" >> $P
+SYSML_SOFTMAX_MATCHER=0 timeout -k 10 300 python -u bench.py --rows 1250000 --steps 10 --warmup 3 > gpurun_out/rl_1250k_nomatch.log 2>&1
+rc=$?; echo "1250k nomatcher rc=$rc $(date)" >> $P
 echo "done $(date)" >> $P
