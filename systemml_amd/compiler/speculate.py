@@ -39,6 +39,7 @@ from .blocks import BasicBlock, IfBlock, WhileBlock, ForBlock
 from .loops import assigned_in, _pure
 
 _names = itertools.count(1)
+SPEC_ROW = __import__("os").environ.get("SYSML_SPEC_ROW", "0") == "1"
 
 
 def _treads(root):
@@ -114,10 +115,13 @@ def _fuses(bb1, var, config):
     trial.live_out = None
     RW.rewrite_block(trial, config)
     h = trial.env_out.get(var)
-    # absorbed by the hand-matched softmax pass, or an output of a merged multi-output Row
-    # program that streams X anyway (codegen.merge_row_programs)
+    # absorbed by the hand-matched softmax pass, or (SYSML_SPEC_ROW=1) an output of a merged
+    # multi-output Row program that streams X anyway (codegen.merge_row_programs).  The latter
+    # is off by default: measured on the MI355X, the generated kernel that adds t(X) %*% W to
+    # the candidate pass (VALU register accumulators) is slower than the separate MFMA product
+    # on acceptance (MultiLogReg 10M x 1K: 520 vs 461 ms/step with the softmax matcher off)
     return h is not None and h.op == "fout" and (h.inputs[0].op in ("smobj", "smgrad") or
-                                                  (h.inputs[0].op == "row" and h.inputs[0].p["prog"].more))
+                                                  (SPEC_ROW and h.inputs[0].op == "row" and h.inputs[0].p["prog"].more))
 
 
 def _try_pair(bb1, mid_writes, bb2, config, stats):

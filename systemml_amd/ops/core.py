@@ -751,7 +751,7 @@ def smgrad(X, V, Y, cu=None):
     return smgrad_ref(X, V, Y, kc)
 
 
-def smobj(X, V, Y, cu=None):
+def smobj(X, V, Y, cu=None, defer=False):
     """Fused multinomial-logreg candidate evaluation with the objective (compiler op `smobj`,
     rewrites.fuse_softmax_grad): with L = cbind(X %*% V, 0), LT = L - rowMaxs(L), E = exp(LT),
     returns (P, G, s1, s2): P = E / rowSums(E), G = t(X) %*% (P[, 1:cu] - Y[, 1:cu]),
@@ -769,7 +769,7 @@ def smobj(X, V, Y, cu=None):
             and not SP.is_sparse(X) and kc == K and isinstance(V, Tensor) and isinstance(Y, Tensor) \
             and not SP.is_sparse(Y):
         from . import kernels
-        r = kernels.smobj(X, V, Y)
+        r = kernels.smobj(X, V, Y, defer=defer)
         if r is not None:
             return r
     return smobj_ref(X, V, Y, kc)

@@ -582,7 +582,7 @@ def mmchain(ctype, X, V, W=None):
     return _result(R if kp == K else R[:, :K].contiguous())
 
 
-def smobj(X, V, Y):
+def smobj(X, V, Y, defer=False):
     """Multinomial-logreg candidate evaluation in one pass over X (chain4m mode XTSMGO):
     with L = cbind(X %*% V, 0) and E = exp(L - rowMaxs(L)), returns (P, G, s1, s2):
     P = E / rowSums(E) (N x (K+1)), G = t(X) %*% (P[, 1:K] - Y[, 1:K]),
@@ -603,6 +603,9 @@ def smobj(X, V, Y):
         if G is None:
             return None
         _count("mfma.smobj_wide")
+        if defer:
+            s = ob[0].sum(0)
+            return _result(P), _result(G), s[0], s[1]
         s = ob[0].sum(0).tolist()
         return _result(P), _result(G), s[0], s[1]
     kp = 4                  # the matrix-core kernel's class layout; classes past K are masked
@@ -617,6 +620,9 @@ def smobj(X, V, Y):
     if G is None:
         return None
     _count("chain4m.smobj")
+    if defer:                           # the caller reduces the sums further (one all-reduce)
+        s = ob[0].sum(0)
+        return _result(Ppad[:N]), _result(G if kp == K else G[:, :K].contiguous()), s[0], s[1]
     s = ob[0].sum(0).tolist()            # one device sync for both objective terms
     return _result(Ppad[:N]), _result(G if kp == K else G[:, :K].contiguous()), s[0], s[1]
 

@@ -82,6 +82,29 @@ class DistContext:
         self.allreduce_(t, op)
         return float(t.item())
 
+    def allreduce_dev(self, v, op="sum"):
+        """All-reduce of a scalar partial that stays on the device when the collective does
+        (RCCL): the result is a device scalar (runtime.scalars.DevScalar), so the host reads
+        it only where it must branch or print -- no host round trip per reduction.  With a
+        host collective (gloo) a float."""
+        dev = self._coll_device()
+        if dev.type != "cuda":
+            return self.allreduce_scalar(float(v.reshape(-1)[0].item()) if isinstance(v, torch.Tensor) else
+                                         float(v), op)
+        if isinstance(v, torch.Tensor):
+            t = v.reshape(1).to(device=dev, dtype=torch.float64)
+            if t.data_ptr() == v.data_ptr():
+                t = t.clone()
+        else:
+            from ..runtime.scalars import DevScalar
+            if isinstance(v, DevScalar):
+                t = v.t.reshape(1).to(device=dev, dtype=torch.float64).clone()
+            else:
+                t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+        self.allreduce_(t, op)
+        from ..runtime.scalars import DevScalar
+        return DevScalar(t.reshape(()))
+
     def _coll_device(self):
         return self.device if tdist.get_backend(self.group) != "gloo" else torch.device("cpu")
 
@@ -445,7 +468,7 @@ def agg(o, d, x):
             part = C.agg(o, d, loc)
         rop = {"sum": "sum", "sumsq": "sum", "min": "min", "max": "max", "prod": "prod"}[o]
         if d == "all":
-            return ctx.allreduce_scalar(part, rop, device=loc.device if loc.is_cuda else None)
+            return ctx.allreduce_dev(part, rop)
         t = part.contiguous().clone()
         ctx.allreduce_(t, rop)
         return t
@@ -601,15 +624,24 @@ def smgrad(X, V, Y, cu=None):
 
 def smobj(X, V, Y, kc):
     """Row-partitioned fused softmax objective / gradient: each rank streams its rows once,
-    P stays row-distributed, the gradient and the two objective sums are all-reduced."""
+    P stays row-distributed; the D x K gradient and the two objective sums travel in ONE
+    all-reduce (packed), and the sums are read by the host once, after it."""
     C = _C()
     if not _is_d(X):
         return C.smobj(X, _bcast(V, "smobj"), _fallback(Y, "smobj:Y"), kc)
     V = _bcast(V, "smobj")
-    p, g, s1, s2 = C.smobj(X.local, V, _align(Y, X), kc)
-    g = g.contiguous()
-    X.ctx.allreduce_(g, "sum")
-    s = X.ctx.allreduce_scalar(s1, "sum"), X.ctx.allreduce_scalar(s2, "sum")
+    p, g, s1, s2 = C.smobj(X.local, V, _align(Y, X), kc, defer=True)
+    ctx = X.ctx
+    dev = ctx._coll_device()
+    parts = [g.reshape(-1).to(device=dev, dtype=torch.float64)]
+    for s in (s1, s2):
+        parts.append(s.reshape(1).to(device=dev, dtype=torch.float64) if isinstance(s, torch.Tensor)
+                     else torch.tensor([float(s)], dtype=torch.float64, device=dev))
+    buf = torch.cat(parts)
+    ctx.allreduce_(buf, "sum")
+    n = g.numel()
+    g = buf[:n].reshape(g.shape).to(device=g.device, dtype=g.dtype)
+    s = buf[n:].tolist()
     return DistMatrix(p, X.nrows, p.shape[1], X.start, X.ctx), g, s[0], s[1]
 
 

@@ -574,7 +574,11 @@ def exec_parfor(ctx, b, start, end, incr, as_int):
     acc = set(getattr(b, "accumulators", ()))
     for v in result_vars:
         if v in shared:
-            ctx.vars[v] = shared[v]          # updated in place by every worker
+            # updated in place by every worker -- unless a worker's writes went to a copy (an
+            # operand moved between host and device for the operator's exec type, a dtype
+            # cast): those copies merge by comparison against the pre-loop value
+            rs = [r[v] for r in results if r[v] is not shared[v]]
+            ctx.vars[v] = shared[v] if not rs else _merge(base[v], [shared[v]] + rs)
             continue
         rs = [r[v] for r in results]
         ctx.vars[v] = _accumulate(base[v], rs) if v in acc else _merge(base[v], rs)
