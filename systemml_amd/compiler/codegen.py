@@ -198,10 +198,15 @@ def _plan_cost(order, groups, absorbed, aggs, ncons, memo):
         n = _cells(h, memo)
         cost += n + sum(_cells(c, memo) for c in leaves)
         cost += sum((0.25 if o.p.get("o") in _HEAVY_OPS else 0.05) * n for o in ops)
+    fused = set()
     for h, (ops, leaves) in aggs:                     # fused aggregates: read the leaves once
         n = _cells(h.inputs[0], memo)
         cost += sum(_cells(c, memo) for c in leaves)
         cost += sum((0.25 if o.p.get("o") in _HEAVY_OPS else 0.05) * n for o in ops)
+        fused.add(h.id)
+    for h in order:                                   # plain aggregates read their materialised input
+        if h.id not in fused and _is_cell_agg(h) and h.inputs[0].id in groups:
+            cost += _cells(h.inputs[0], memo)
     return cost
 
 
@@ -929,8 +934,18 @@ def _multi_agg(built):
     into one `magg` hop evaluated in a single pass (ops/cell.evaluate_multi); each original
     aggregate hop becomes output i of it.  Aggregates that depend on each other are never
     grouped.  Returns the ids of the replaced roots."""
-    cands = [b for b in built if b[3].agg and b[3].agg[1] == "all" and
-             not any(o in ("bias+", "bias*") for _, o, _, _, _ in b[3].ops)]
+    done = set()
+    # full aggregates (no per-channel operands), and column sums (per-channel operands
+    # allowed: the batch-norm statistics of a convolution output) -- never mixed in one group
+    alls = [b for b in built if b[3].agg and b[3].agg[1] == "all" and
+            not any(o in ("bias+", "bias*") for _, o, _, _, _ in b[3].ops)]
+    cols = [b for b in built if b[3].agg and b[3].agg[1] == "col" and b[3].agg[0] in ("sum", "sumsq", "mean")]
+    for cands in (alls, cols):
+        done |= _multi_agg_group(cands)
+    return done
+
+
+def _multi_agg_group(cands):
     if len(cands) < 2:
         return set()
     reach = {}

@@ -711,6 +711,9 @@ def _kernel(prog: CellProgram, args):
 
 
 # ----------------------------------------------------------------------------- multi-aggregate
+MAGG_COL_CW = 64           # column groups (of 4 columns) per workgroup of the column MAgg kernel
+
+
 class MultiAggProgram:
     """MAgg template (reference: hops/codegen/template/TemplateMultiAgg.java, runtime
     SpoofMultiAggregate): several full aggregates of cellwise programs over the same output
@@ -743,7 +746,7 @@ def evaluate_multi(m: MultiAggProgram, args):
     return tuple(evaluate(p, [args[i] for i in mp]) for p, mp in zip(m.progs, m.maps))
 
 
-def generate_multi(m: MultiAggProgram, T, modes, dts, vecs):
+def generate_multi(m: MultiAggProgram, T, modes, dts, vecs, col=False, ch4=False):
     ct = "float" if T == torch.float32 else "double"
     body, outs = [], []
     q = 0
@@ -756,7 +759,8 @@ def generate_multi(m: MultiAggProgram, T, modes, dts, vecs):
             q += 1
         outs.append(f"    o[{k}] = {var[prog.out]};")
     aggs = [AGG_CODES[p.agg[0]] for p in m.progs]
-    need_ij = int(any(x in (ROWV, COLV) for x in modes))
+    need_ij = int(any(x in (ROWV, COLV, CHAN) for x in modes))
+    call = f"sysml_cell_magg_col4<Spec, {MAGG_COL_CW}>(A);" if col else "sysml_cell_magg<Spec>(A);"
     return (_prelude() + f"""
 // generated: {m.describe()}
 struct Spec {{
@@ -765,7 +769,7 @@ struct Spec {{
   static constexpr int NOUT = {len(m.progs)};
   static constexpr int NEED_IJ = {need_ij};
   static constexpr int IDX32 = 0;
-  static constexpr int CH4 = 0;
+  static constexpr int CH4 = {int(ch4)};
   static constexpr int mode(int k) {{ return {_cases(modes)}; }}
   static constexpr int dt(int k) {{ return {_cases(dts)}; }}
   static constexpr int vec(int k) {{ return {_cases(vecs)}; }}
@@ -776,7 +780,7 @@ struct Spec {{
   }}
 }};
 
-extern "C" __global__ void __launch_bounds__(256) sysml_cell_k(const SysmlCellArgs A) {{ sysml_cell_magg<Spec>(A); }}
+extern "C" __global__ void __launch_bounds__(256) sysml_cell_k(const SysmlCellArgs A) {{ {call} }}
 """)
 
 
@@ -814,12 +818,39 @@ def _kernel_multi(m: MultiAggProgram, args):
     if shp is None or shp[0] <= 0 or shp[1] <= 0:
         return None
     R, Cc = shp
+    dirs = {p.agg[1] for p in m.progs}
+    if len(dirs) != 1:
+        return None
+    col = dirs.pop() == "col"
+    if col and (Cc % 4 or any(p.agg[0] not in ("sum", "sumsq", "mean") for p in m.progs)):
+        return None
+    # per-channel operands (bias_add / bias_multiply inside the programs): union positions
+    chan = set()
+    for p, mp in zip(m.progs, m.maps):
+        ci = chan_inputs(p)
+        if ci is None:
+            return None
+        chan |= {mp[i] for i in ci}
     T = torch.float64 if (f64 or (bf16 and backend.dtype == torch.float64)) else torch.float32
     A = _RtcArgs()
     keep, modes, dts, vecs = [], [], [], []
+    hws = []
     for k, x in enumerate(args):
         tx = type(x)
         mode, dt, vec = HSCALAR, 0, 0
+        if k in chan:
+            if tx is not _Tensor or x.dim() != 2 or x.shape[1] != 1 or Cc % x.shape[0]:
+                return None
+            if not x.is_contiguous():
+                x = x.contiguous()
+            keep.append(x)
+            A.inp[k] = x.data_ptr()
+            A.s[k] = Cc // x.shape[0]
+            hws.append(Cc // x.shape[0])
+            modes.append(CHAN)
+            dts.append(_DT[x.dtype])
+            vecs.append(0)
+            continue
         if tx is _Tensor:
             if not x.is_contiguous():
                 x = x.contiguous()
@@ -847,11 +878,15 @@ def _kernel_multi(m: MultiAggProgram, args):
         modes.append(mode)
         dts.append(dt)
         vecs.append(vec)
-    key = ("magg", m.key(), T, tuple(modes), tuple(dts), tuple(vecs), str(dev))
+    ch4 = bool(hws) and Cc % 4 == 0 and all(h % 4 == 0 for h in hws)
+    if hws and not col:
+        return None                      # per-channel operands: column form only
+    key = ("magg", m.key(), T, tuple(modes), tuple(dts), tuple(vecs), str(dev), col, ch4)
     f = _rtc_funcs.get(key, False)
     if f is False:
         try:
-            code = compile_source(generate_multi(m, T, tuple(modes), tuple(dts), tuple(vecs)), gpu_arch(dev))
+            code = compile_source(generate_multi(m, T, tuple(modes), tuple(dts), tuple(vecs), col, ch4),
+                                  gpu_arch(dev))
             fn = ctypes.c_void_p()
             cbuf = ctypes.create_string_buffer(code, len(code))
             rc = _rtc_lib().sysml_rtc_load(cbuf, b"sysml_cell_k", ctypes.byref(fn))
@@ -866,20 +901,32 @@ def _kernel_multi(m: MultiAggProgram, args):
     if f is None:
         return None
     nout = len(m.progs)
-    nblk = _lib().sysml_cell_blocks(1, R, Cc)
-    part = torch.empty(nblk * nout, dtype=torch.float64, device=dev)
+    if col:
+        nblk = _lib().sysml_cell_blocks(3, R, Cc)
+        part = torch.empty((nblk, nout, Cc), dtype=torch.float64, device=dev)
+        gx, gy = (Cc + 4 * MAGG_COL_CW - 1) // (4 * MAGG_COL_CW), nblk
+    else:
+        nblk = _lib().sysml_cell_blocks(1, R, Cc)
+        part = torch.empty(nblk * nout, dtype=torch.float64, device=dev)
+        gx, gy = nblk, 1
     A.rows, A.cols, A.total = R, Cc, R * Cc
     A.chunk = (R + nblk - 1) // nblk
     A.out = 0
     A.part = part.data_ptr()
     st = torch.cuda.current_stream(dev).cuda_stream
-    rc = _rtc_lib().sysml_rtc_launch(f[0], nblk, 1, 256, ctypes.byref(A), ctypes.sizeof(A), st)
+    rc = _rtc_lib().sysml_rtc_launch(f[0], gx, gy, 256, ctypes.byref(A), ctypes.sizeof(A), st)
     if rc != 0:
         raise RuntimeError(f"multi-aggregate kernel launch failed: {rc}")
     stats["rtc_launches"] += 1
     from . import kernels
     kernels._count("magg")
     del keep
+    if col:
+        res = []
+        for k, prog in enumerate(m.progs):
+            r = part[:, k, :].sum(0, keepdim=True).to(T)
+            res.append(r / R if prog.agg[0] == "mean" else r)
+        return tuple(res)
     P = part.view(nblk, nout)
     res = []
     for k, prog in enumerate(m.progs):

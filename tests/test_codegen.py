@@ -412,3 +412,43 @@ s = sum(o)
     cs0 = EX.compile_script(src, {}, inputs=ins, outputs=["o", "s"], config=DMLConfig(gpu=False, rewrites=False))
     ref, _ = EX.execute(cs0, ins)
     assert torch.allclose(res["o"], ref["o"], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_column_multi_aggregate_with_channel_operands_on_gpu(dt):
+    """Batch-norm statistics and parameter gradients: column sums over the same activations
+    with per-channel (bias_add / bias_multiply) operands fuse into ONE column MAgg kernel
+    (cell_rtc.inc sysml_cell_magg_col4) and match fp64 torch."""
+    from systemml_amd.ops import cell as CELL, kernels
+    from systemml_amd.ops.backend import backend
+    src = """
+    Xs = bias_add(X, -em)
+    s1 = colSums(Xs)
+    s2 = colSums(Xs ^ 2)
+    db = colSums(dout)
+    dg = colSums(dout * bias_multiply(bias_add(X, -m), istd))
+    """
+    C, HW, N = 16, 49, 64
+    rng = np.random.default_rng(3)
+    ins = {"X": rng.standard_normal((N, C * HW)), "dout": rng.standard_normal((N, C * HW)),
+           "em": rng.standard_normal((C, 1)), "m": rng.standard_normal((C, 1)), "istd": rng.random((C, 1)) + 0.5}
+    cfg = DMLConfig(gpu=True, precision="single", gpu_min_cells=0)
+    cs = EX.compile_script(src, {}, inputs=ins, outputs=["s1", "s2", "db", "dg"], config=cfg)
+    text = EX.explain(cs.cp, "hops")
+    assert text.count("magg(") >= 1, text
+    backend.configure(cfg)
+    dins = {k: torch.tensor(v, dtype=torch.float32).to("cuda").to(dt if k in ("X", "dout") else torch.float32)
+            for k, v in ins.items()}
+    b0 = CELL.stats.get("magg_kernel", 0)
+    res, _ = EX.execute(cs, dins)
+    assert CELL.stats.get("magg_kernel", 0) > b0
+    X = dins["X"].double().cpu().numpy()
+    D = dins["dout"].double().cpu().numpy()
+    ch = np.repeat(np.arange(C), HW)
+    Xs = X - ins["em"][ch, 0].astype(np.float32)
+    ref = {"s1": Xs.sum(0), "s2": (Xs ** 2).sum(0), "db": D.sum(0),
+           "dg": (D * (X - ins["m"][ch, 0].astype(np.float32)) * ins["istd"][ch, 0].astype(np.float32)).sum(0)}
+    for k, r in ref.items():
+        g = res[k].double().cpu().numpy().ravel()
+        np.testing.assert_allclose(g, r, rtol=2e-4, atol=2e-3, err_msg=k)
