@@ -119,7 +119,141 @@ int launch(const int64_t* crow, const I* col, const T* U, const T* V, int64_t m,
 
 }  // namespace sysml_sd
 
+namespace sysml_sd {
+
+// ---- fused weighted divide / multiply matrix multiplication (wdivmm right form) ----------------
+// out[i, :] = sum over the non-zeros p = (i, j) of q_p * V[j, :] with q_p = f(w_p, <U[i, :], V[j, :]>,
+// x_p):  mode 0: w * uv,  1: w * (uv - x),  2: w / (uv + eps).  One pass over the pattern: the V[j]
+// row gathered for the dot product is the row that is accumulated (the separate sampled product
+// + SpMM read it twice and wrote / read the sampled values).  Non-zeros are split into equal
+// chunks over the waves (rows spanning chunks finish with atomics, as spmm_bal); a group of G
+// lanes owns one non-zero, lane k its factor column k (K <= 64); the group reduces the dot
+// product with xor-shuffles, every lane then accumulates q * V[j, k].  w == nullptr: w = 1.
+template <typename I>
+__device__ __forceinline__ int64_t wd_first_row(const int64_t* __restrict__ crow, int64_t m, int64_t p) {
+  int64_t lo = 0, hi = m;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (crow[mid] <= p) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+template <typename T, typename I, int G>
+__global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __restrict__ crow,
+                                                            const I* __restrict__ col, const T* __restrict__ wv,
+                                                            const T* __restrict__ xv, const T* __restrict__ U,
+                                                            const T* __restrict__ V, T* __restrict__ out, int64_t m,
+                                                            int K, int mode, T eps, int64_t chunk, int64_t nchunks) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int NG = 64 / G;
+  const int g = lane / G, gl = lane & (G - 1);
+  const int64_t nnz = crow[m];
+  const bool kin = gl < K;
+  for (int64_t c = (int64_t)blockIdx.x * WAVES + w; c < nchunks; c += (int64_t)gridDim.x * WAVES) {
+    const int64_t s = c * chunk;
+    const int64_t e = s + chunk < nnz ? s + chunk : nnz;
+    if (s >= e) continue;
+    int64_t r = wd_first_row<I>(crow, m, s);
+    while (r < m) {
+      const int64_t rb = crow[r], re = crow[r + 1];
+      if (rb >= e) break;
+      const int64_t b = rb > s ? rb : s;
+      const int64_t q = re < e ? re : e;
+      if (b < q) {
+        const bool whole = (rb >= s) && (re <= e);
+        const T u = kin ? U[r * K + gl] : T(0);
+        T acc = T(0);
+        // 4 non-zeros per group in flight: indices, weights and the 4 V-row gathers first
+        for (int64_t p0 = b + g; p0 < q; p0 += 4 * NG) {
+          int64_t cj[4];
+          T wt[4], xt[4], bv[4], dt[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int64_t p = p0 + t * NG;
+            const bool in = p < q;
+            cj[t] = in ? (int64_t)col[p] : 0;
+            wt[t] = in ? (wv != nullptr ? wv[p] : T(1)) : T(0);
+            xt[t] = (in && mode == 1) ? xv[p] : T(0);
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) bv[t] = kin ? V[cj[t] * K + gl] : T(0);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) dt[t] = u * bv[t];
+#pragma unroll
+          for (int off = G / 2; off >= 1; off >>= 1)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) dt[t] += __shfl_xor(dt[t], off, G);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            T qv;
+            if (mode == 0) qv = wt[t] * dt[t];
+            else if (mode == 1) qv = wt[t] * (dt[t] - xt[t]);
+            else qv = wt[t] / (dt[t] + eps);
+            if (wt[t] == T(0)) qv = T(0);          // outside the pattern / padding slots
+            acc += qv * bv[t];
+          }
+        }
+#pragma unroll
+        for (int o = G; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);
+        if (g == 0 && kin) {
+          if (whole) out[r * K + gl] = acc;
+          else atomicAdd(out + r * K + gl, acc);
+        }
+      }
+      ++r;
+    }
+  }
+}
+
+template <typename T, typename I>
+int launch_wd(const int64_t* crow, const I* col, const T* wv, const T* xv, const T* U, const T* V, T* out, int64_t m,
+              int K, int mode, double eps, int64_t nnz, hipStream_t st) {
+  int64_t chunk = (nnz + 256 * 16 - 1) / (256 * 16);
+  if (chunk < 32) chunk = 32;
+  const int64_t nchunks = (nnz + chunk - 1) / chunk;
+  int64_t blocks = (nchunks + WAVES - 1) / WAVES;
+  if (blocks > 256 * 32) blocks = 256 * 32;
+  if (blocks < 1) blocks = 1;
+  const dim3 gr((unsigned)blocks), t(WAVES * 64);
+#define WD_CASE(G_) hipLaunchKernelGGL((wdivmm_kernel<T, I, G_>), gr, t, 0, st, crow, col, wv, xv, U, V, out, m, K, mode, \
+                                       (T)eps, chunk, nchunks)
+  if (K <= 4) WD_CASE(4);
+  else if (K <= 8) WD_CASE(8);
+  else if (K <= 16) WD_CASE(16);
+  else if (K <= 32) WD_CASE(32);
+  else if (K <= 64) WD_CASE(64);
+  else return -1;
+#undef WD_CASE
+  return (int)hipGetLastError();
+}
+
+}  // namespace sysml_sd
+
 extern "C" {
+
+// Fused wdivmm (right form, see wdivmm_kernel): out (m x K, zeroed by the caller) for a CSR pattern
+// (crow int64, col int32 if idx32 else int64), weights wv (nullptr: 1), x values xv (mode 1, the
+// pattern's order), factors U (m x K), V (n x K).  dtype 0 fp32, 1 fp64.  -1: unsupported.
+int sysml_wdivmm(int dtype, int idx32, const void* crow, const void* col, const void* wv, const void* xv,
+                 const void* U, const void* V, void* out, int64_t m, int K, int mode, double eps, int64_t nnz,
+                 void* stream) {
+  if (K < 1 || K > 64 || nnz <= 0 || (mode == 1 && xv == nullptr)) return -1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const auto* cr = static_cast<const int64_t*>(crow);
+#define WD_T(T_)                                                                                             \
+  (idx32 ? sysml_sd::launch_wd<T_, int32_t>(cr, static_cast<const int32_t*>(col), static_cast<const T_*>(wv),           \
+                                  static_cast<const T_*>(xv), static_cast<const T_*>(U), static_cast<const T_*>(V), \
+                                  static_cast<T_*>(out), m, K, mode, eps, nnz, st)                           \
+         : sysml_sd::launch_wd<T_, int64_t>(cr, static_cast<const int64_t*>(col), static_cast<const T_*>(wv),           \
+                                  static_cast<const T_*>(xv), static_cast<const T_*>(U), static_cast<const T_*>(V), \
+                                  static_cast<T_*>(out), m, K, mode, eps, nnz, st))
+  if (dtype == 0) return WD_T(float);
+  if (dtype == 1) return WD_T(double);
+#undef WD_T
+  return -1;
+}
 
 // dtype 0 = fp32, 1 = fp64.  Returns 0 on success, -1 on unsupported shape, else a hipError_t.
 // idx32: the column indices are int32 (half the index bytes of the pass).

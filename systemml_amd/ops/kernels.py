@@ -129,6 +129,9 @@ def load(required=False):
     L.sysml_cast_weight.restype = ctypes.c_int
     L.sysml_cast_weight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_void_p]
+    L.sysml_wdivmm.restype = ctypes.c_int
+    L.sysml_wdivmm.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 7 + \
+        [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int64, ctypes.c_void_p]
     L.sysml_pad_pixels.restype = ctypes.c_int
     L.sysml_pad_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
@@ -747,6 +750,38 @@ def sumsq(x, d):
         return tot
     xx = cvt(x)
     return torch.sum(xx * xx, dim=1 if d == "row" else 0, keepdim=True)
+
+
+def wdivmm(crow, col, wv, xv, U, V, mode, eps=0.0, dtype=None):
+    """Fused weighted divide / multiply product (ops/hip/sddmm.hip wdivmm_kernel):
+    out[i, :] = sum_p q_p V[col_p, :] over row i's non-zeros with q = w * <U[i], V[j]> (mode 0),
+    w * (<U[i], V[j]> - x) (1) or w / (<U[i], V[j]> + eps) (2); wv None: w = 1.  Returns m x K,
+    or None when unsupported (K > 64)."""
+    import torch
+    L = load(required=True)
+    m, K = U.shape
+    if K < 1 or K > 64 or V.shape[1] != K or col.numel() == 0:
+        return None
+    if dtype is None:
+        dtype = torch.float64 if torch.float64 in (U.dtype, V.dtype) else torch.float32
+    U = U.to(dtype).contiguous()
+    V = V.to(dtype).contiguous()
+    crow = crow.to(torch.int64).contiguous()
+    idx32 = col.dtype == torch.int32
+    col = col.contiguous() if idx32 else col.to(torch.int64).contiguous()
+    wv = wv.to(dtype).contiguous() if wv is not None else None
+    xv = xv.to(dtype).contiguous() if xv is not None else None
+    out = torch.zeros((m, K), dtype=dtype, device=U.device)
+    rc = L.sysml_wdivmm(0 if dtype == torch.float32 else 1, int(idx32), crow.data_ptr(), col.data_ptr(),
+                        wv.data_ptr() if wv is not None else None, xv.data_ptr() if xv is not None else None,
+                        U.data_ptr(), V.data_ptr(), out.data_ptr(), m, K, int(mode), float(eps), int(col.numel()),
+                        _stream())
+    if rc == -1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"sysml_wdivmm failed: {rc}")
+    _count("wdivmm")
+    return out
 
 
 def sddmm(crow, col, U, V, dtype=None):

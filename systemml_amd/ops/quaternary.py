@@ -233,6 +233,9 @@ def wdivmm(W, U, V, left, mult=False, eps=None, X=None):
     if SP.is_sparse(W) and _plain(U) and _plain(V) and (X is None or _plain(X) or SP.is_sparse(X)):
         _check(U, V, W.shape[0], W.shape[1])
         dt = _cdt(W, U, V)
+        r = _wdivmm_fused(W, U, V, left, mult, eps, X, dt)
+        if r is not None:
+            return r
         r, c, wv, uv = _sd(W, U, V, dt)
         if X is not None:
             if tuple(X.shape) != tuple(W.shape):
@@ -256,6 +259,54 @@ def wdivmm(W, U, V, left, mult=False, eps=None, X=None):
         uv = C.binary("-", uv, SP.densify(X))
     q = C.binary("*", SP.densify(W), uv) if mult else _sparse_safe(W, C.binary("/", 1.0, uv))
     return C.mm(U, q, True) if left else C.mm(q, V)
+
+
+_PATEQ = {}
+
+
+def _same_pattern(A, B):
+    """A and B are CSR with the same pattern (shared index tensors, or equal ones -- compared
+    once per pair of index storages)."""
+    if A.layout != torch.sparse_csr or B.layout != torch.sparse_csr or A.shape != B.shape:
+        return False
+    ca, cb = A.crow_indices(), B.crow_indices()
+    ia, ib = A.col_indices(), B.col_indices()
+    if ca.data_ptr() == cb.data_ptr() and ia.data_ptr() == ib.data_ptr():
+        return True
+    if ia.numel() != ib.numel():
+        return False
+    key = (ca.data_ptr(), cb.data_ptr(), ia.data_ptr(), ib.data_ptr(), ia.numel(), ca._version, ia._version)
+    r = _PATEQ.get(key)
+    if r is None:
+        if len(_PATEQ) >= 8:
+            _PATEQ.pop(next(iter(_PATEQ), None), None)
+        r = _PATEQ[key] = (bool(torch.equal(ca, cb)) and bool(torch.equal(ia, ib)), (ca, cb, ia, ib))
+    return r[0]
+
+
+def _wdivmm_fused(W, U, V, left, mult, eps, X, dt):
+    """The fused kernel (ops/hip/sddmm.hip wdivmm_kernel) for a CSR W on the MI355X: one pass
+    over W's pattern gathering each V (U for the left form) row once; the left form runs on
+    the transposed pattern of W, which -- with W's values and X's values in its order -- is
+    cached per pattern (ALS: W and X are fixed across all iterations).  None: not applicable
+    (X of another pattern, rank > 64, host operands)."""
+    from .backend import backend
+    if not (backend.use_kernels and W.is_cuda and W.layout == torch.sparse_csr and U.is_cuda and V.is_cuda):
+        return None
+    if X is not None and not (mult and SP.is_sparse(X) and X.is_cuda and _same_pattern(W, X)):
+        return None
+    from . import kernels
+    mode = 1 if X is not None else (0 if mult else 2)
+    e = float(eps) if (eps is not None and not mult) else 0.0
+    if not left:
+        xv = X.values() if X is not None else None
+        col = kernels.idx32_of(W.col_indices()) if W.shape[1] < 2 ** 31 else W.col_indices()
+        return kernels.wdivmm(W.crow_indices(), col, W.values(), xv, U, V, mode, e, dt)
+    Wt = SP._transposed(W)
+    xt = SP._transposed(X).values() if X is not None else None
+    col = kernels.idx32_of(Wt.col_indices()) if Wt.shape[1] < 2 ** 31 else Wt.col_indices()
+    r = kernels.wdivmm(Wt.crow_indices(), col, Wt.values(), xt, V, U, mode, e, dt)
+    return r.t().contiguous() if r is not None else None
 
 
 # ------------------------------------------------------------------------------- wcemm

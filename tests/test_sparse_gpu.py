@@ -139,3 +139,36 @@ def test_sparse_sparse_product_elementwise(prec):
     else:
         assert kernels.counters.get("spgemm", 0) == before
         np.testing.assert_allclose(C, ref, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 10, 33, 64])
+@pytest.mark.parametrize("form", ["mult", "multx", "div"])
+@pytest.mark.parametrize("left", [False, True])
+def test_fused_wdivmm_matches_dense(K, form, left):
+    """sddmm.hip wdivmm_kernel (one pass over W's pattern, the gathered factor row reused for
+    the accumulation) against fp64 torch on the dense equivalent, right and left forms."""
+    from systemml_amd.ops import quaternary as Q, kernels
+    from systemml_amd.ops.backend import backend
+    from systemml_amd.conf import DMLConfig
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    backend.configure(DMLConfig(gpu=True, precision="double"))
+    g = torch.Generator().manual_seed(K)
+    m, n = 3001, 2003
+    mask = torch.rand(m, n, generator=g) < 0.01
+    mask[7] = True                                   # a dense row: chunks split it
+    Xd = torch.where(mask, torch.rand(m, n, generator=g, dtype=torch.float64) + 0.5, torch.zeros((), dtype=torch.float64))
+    Wd = (Xd != 0).double() * (1.0 + torch.rand(m, n, generator=g, dtype=torch.float64))
+    U = torch.rand(m, K, generator=g, dtype=torch.float64)
+    V = torch.rand(n, K, generator=g, dtype=torch.float64)
+    X = Xd.to_sparse_csr().cuda()
+    W = torch.sparse_csr_tensor(X.crow_indices(), X.col_indices(), Wd[mask.nonzero(as_tuple=True)].cuda(), (m, n))
+    uv = U @ V.t()
+    q = {"mult": Wd * uv, "multx": Wd * (uv - Xd), "div": torch.where(mask, Wd / (uv + 0.5), torch.zeros((), dtype=torch.float64))}[form]
+    ref = U.t() @ q if left else q @ V
+    c0 = kernels.counters.get("wdivmm", 0)
+    got = Q.wdivmm(W, U.cuda(), V.cuda(), left, mult=form != "div", eps=0.5 if form == "div" else None,
+                   X=X if form == "multx" else None)
+    assert kernels.counters.get("wdivmm", 0) == c0 + 1
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-9, atol=1e-9)
