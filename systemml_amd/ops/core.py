@@ -885,8 +885,12 @@ def _check_range(r0, r1, c0, c1, nr, nc):
 def lix(x, y, rl, ru, cl, cu, list_mode=False, owned=None):
     """X[rl:ru, cl:cu] = y.  `owned` (update-in-place loops, compiler/loops.py): a WeakSet of
     buffers this loop execution already copied; those are modified in place, anything else is
-    copied once and registered."""
+    copied once and registered.  y may be a device-resident scalar (DevScalar): written into
+    a device matrix without a host round trip."""
     from ..runtime.data import ListObject
+    from ..runtime.scalars import DevScalar
+    if type(y) is DevScalar and not (type(x) is Tensor and x.is_cuda and y.t.is_cuda):
+        y = y.value()
     if isinstance(x, ListObject):
         i = _bound(rl, 1)
         data = list(x.data)
@@ -927,6 +931,14 @@ def lix(x, y, rl, ru, cl, cu, list_mode=False, owned=None):
         # one pass on reorg.hip: every output cell written once (or only the window, in place)
         xc = cvt(x).contiguous()
         yv = y
+        if type(y) is DevScalar:
+            out = xc if (inplace and xc is x) else torch.empty_like(xc)
+            from . import kernels
+            if kernels.lix(xc, None, out, r0 - 1, r1, c0 - 1, c1, sdev=y.t):
+                if owned is not None and out is not x:
+                    owned.add(out)
+                return out
+            y = yv = y.value()
         if isinstance(y, Tensor):
             yv = cvt(y)
             if tuple(yv.shape) != (r1 - r0 + 1, c1 - c0 + 1):

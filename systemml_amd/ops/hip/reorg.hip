@@ -49,10 +49,23 @@ __global__ void __launch_bounds__(NT) cat_kernel(const Cat c, T* __restrict__ ou
   }
 }
 
+// the bit pattern of a device-resident fp64 scalar in the cell type of T (bf16: round to
+// nearest even of its fp32 value)
+template <typename T> __device__ __forceinline__ T dev_bits(double d);
+template <> __device__ __forceinline__ uint64_t dev_bits<uint64_t>(double d) { return (uint64_t)__double_as_longlong(d); }
+template <> __device__ __forceinline__ uint32_t dev_bits<uint32_t>(double d) { return __float_as_uint((float)d); }
+template <> __device__ __forceinline__ uint16_t dev_bits<uint16_t>(double d) {
+  uint32_t u = __float_as_uint((float)d);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(NT) lix_kernel(const T* X, const T* __restrict__ Y, T* out,   // out may be X
                                                  int64_t N, int64_t D, int64_t r0, int64_t r1, int64_t c0,
-                                                 int64_t c1, int scalar, T sval, int window_only) {
+                                                 int64_t c1, int scalar, T sval, int window_only,
+                                                 const double* __restrict__ sdev) {
+  if (sdev != nullptr) sval = dev_bits<T>(*sdev);     // a device scalar: no host round trip
   const int64_t wr = r1 - r0, wc = c1 - c0;
   const int64_t total = window_only ? wr * wc : N * D;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
@@ -113,8 +126,17 @@ int sysml_cat(int rows, int esize, int n, const void* const* srcs, const int64_t
 
 // out = X with out[r0:r1, c0:c1] (0-based, half-open) = Y (wr x wc row-major) or the scalar bit
 // pattern `sbits`; out == X: only the window is written.
+int sysml_lix2(int esize, const void* X, const void* Y, void* out, int64_t N, int64_t D, int64_t r0, int64_t r1,
+               int64_t c0, int64_t c1, int scalar, uint64_t sbits, const double* sdev, void* stream);
+
 int sysml_lix(int esize, const void* X, const void* Y, void* out, int64_t N, int64_t D, int64_t r0, int64_t r1,
               int64_t c0, int64_t c1, int scalar, uint64_t sbits, void* stream) {
+  return sysml_lix2(esize, X, Y, out, N, D, r0, r1, c0, c1, scalar, sbits, nullptr, stream);
+}
+
+// as sysml_lix; sdev (scalar mode): the value is read on the device from this fp64 cell
+int sysml_lix2(int esize, const void* X, const void* Y, void* out, int64_t N, int64_t D, int64_t r0, int64_t r1,
+               int64_t c0, int64_t c1, int scalar, uint64_t sbits, const double* sdev, void* stream) {
   using namespace sysml_rg;
   if (N <= 0 || D <= 0 || r0 < 0 || r1 > N || c0 < 0 || c1 > D || r0 >= r1 || c0 >= c1) return -1;
   if (!scalar && Y == nullptr) return -1;
@@ -123,13 +145,13 @@ int sysml_lix(int esize, const void* X, const void* Y, void* out, int64_t N, int
   const dim3 g(grid_for(wo ? (r1 - r0) * (c1 - c0) : N * D));
   if (esize == 2)
     hipLaunchKernelGGL(lix_kernel<uint16_t>, g, dim3(NT), 0, st, (const uint16_t*)X, (const uint16_t*)Y,
-                       (uint16_t*)out, N, D, r0, r1, c0, c1, scalar, (uint16_t)sbits, wo);
+                       (uint16_t*)out, N, D, r0, r1, c0, c1, scalar, (uint16_t)sbits, wo, sdev);
   else if (esize == 4)
     hipLaunchKernelGGL(lix_kernel<uint32_t>, g, dim3(NT), 0, st, (const uint32_t*)X, (const uint32_t*)Y,
-                       (uint32_t*)out, N, D, r0, r1, c0, c1, scalar, (uint32_t)sbits, wo);
+                       (uint32_t*)out, N, D, r0, r1, c0, c1, scalar, (uint32_t)sbits, wo, sdev);
   else if (esize == 8)
     hipLaunchKernelGGL(lix_kernel<uint64_t>, g, dim3(NT), 0, st, (const uint64_t*)X, (const uint64_t*)Y,
-                       (uint64_t*)out, N, D, r0, r1, c0, c1, scalar, sbits, wo);
+                       (uint64_t*)out, N, D, r0, r1, c0, c1, scalar, sbits, wo, sdev);
   else
     return -1;
   return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -129,6 +129,9 @@ def load(required=False):
     L.sysml_cast_weight.restype = ctypes.c_int
     L.sysml_cast_weight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_void_p]
+    L.sysml_lix2.restype = ctypes.c_int
+    L.sysml_lix2.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int64] * 6 + \
+        [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
     L.sysml_wdivmm.restype = ctypes.c_int
     L.sysml_wdivmm.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 7 + \
         [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int64, ctypes.c_void_p]
@@ -1196,10 +1199,10 @@ def cat(rows, mats):
     return out
 
 
-def lix(X, Y, out, r0, r1, c0, c1):
+def lix(X, Y, out, r0, r1, c0, c1, sdev=None):
     """out = X with out[r0:r1, c0:c1] = Y (0-based, half-open; Y a wr x wc tensor or a Python
-    number) in one pass; out may be X itself (only the window is written).  False when not
-    covered."""
+    number; sdev instead: a device fp64 scalar read by the kernel) in one pass; out may be X
+    itself (only the window is written).  False when not covered."""
     if X.dtype not in _ESIZE or not X.is_cuda or X.dim() != 2 or not X.is_contiguous() or out.dtype != X.dtype \
             or not out.is_contiguous():
         return False
@@ -1208,7 +1211,15 @@ def lix(X, Y, out, r0, r1, c0, c1):
     scalar = not isinstance(Y, torch.Tensor)
     sbits = 0
     yp = None
-    if scalar:
+    sp = None
+    if sdev is not None:
+        if not sdev.is_cuda or sdev.device != X.device:
+            return False
+        sd = sdev.reshape(1)
+        if sd.dtype != torch.float64:
+            sd = sd.double()
+        sp = sd.data_ptr()
+    elif scalar:
         v = float(Y)
         if X.dtype == torch.float64:
             sbits = struct.unpack("<Q", struct.pack("<d", v))[0]
@@ -1219,8 +1230,8 @@ def lix(X, Y, out, r0, r1, c0, c1):
     else:
         Y = Y.to(device=X.device, dtype=X.dtype).contiguous()
         yp = Y.data_ptr()
-    rc = L.sysml_lix(_ESIZE[X.dtype], X.data_ptr(), yp, out.data_ptr(), X.shape[0], X.shape[1], r0, r1, c0, c1,
-                     int(scalar), sbits, _stream())
+    rc = L.sysml_lix2(_ESIZE[X.dtype], X.data_ptr(), yp, out.data_ptr(), X.shape[0], X.shape[1], r0, r1, c0, c1,
+                      int(scalar), sbits, sp, _stream())
     if rc != 0:
         raise RuntimeError(f"sysml_lix failed: {rc}")
     _count("lix")

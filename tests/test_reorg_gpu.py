@@ -101,3 +101,19 @@ def test_append_of_host_and_device_operands():
     assert r2.is_cuda and torch.equal(r2.cpu(), torch.cat([h, d.cpu()]))
     c = b_cbind(None, torch.ones(4, 1), d)
     assert c.is_cuda and torch.equal(c.cpu(), torch.cat([torch.ones(4, 1), d.cpu()], 1))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64, torch.bfloat16])
+def test_left_index_device_scalar_without_host_read(dt):
+    """R[i, j] = s with s a device-resident scalar: the kernel reads s on the device; the
+    DevScalar is never materialised on the host."""
+    _need()
+    from systemml_amd.ops import core as C
+    from systemml_amd.runtime.scalars import DevScalar
+    X = torch.zeros(50, 7, dtype=dt, device="cuda")
+    s = DevScalar(torch.tensor(3.25, dtype=torch.float64, device="cuda"))
+    out = C.lix(X, s, 5, 5, 2, 3)
+    assert s._v is None                                 # not read on the host
+    ref = torch.zeros(50, 7, dtype=torch.float64)
+    ref[4, 1:3] = 3.25
+    assert torch.equal(out.double().cpu(), ref)
