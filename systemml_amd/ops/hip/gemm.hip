@@ -228,14 +228,15 @@ __device__ __forceinline__ void bar_keep_dma() {
 // BKT = 64: two LDS stages (DMA of tile t+1 overlaps tile t; drain + barrier per tile).
 // BKT = 32: four LDS stages of 32 KiB, three K-tiles in flight; per tile a COUNTED vmcnt
 //           (own DMAs of tile t retired, later tiles keep streaming) + a raw s_barrier.
-// BMT = rows of A per block: 256 (waves 2 x 4 of 128 x 64) or 64 (waves 2 x 4 of 32 x 64, for
-// GEMMs with few rows -- convolutions with 64 filters / channels; K-major A, BKT 64 only)
+// BMT = rows of A per block: 256 (waves 2 x 4 of 128 x 64), 128 (2 x 4 of 64 x 64: twice the
+// workgroups for GEMMs whose 256-row tiles leave CUs idle) or 64 (waves 2 x 4 of 32 x 64, for GEMMs
+// with few rows -- convolutions with 64 filters / channels); the smaller tiles K-major A, BKT 64
 template <bool TA, bool TB, int BKT, int BMT = 256>
 __global__ void __launch_bounds__(NTHR, 2)
 gemm_bf16_kernel(Args a) {
   constexpr bool AK = !TA;   // A K-major
   constexpr bool BKM = TB;   // B K-major
-  static_assert(BMT == 256 || (BMT == 64 && !TA && BKT == 64), "row-tile variants");
+  static_assert(BMT == 256 || ((BMT == 64 || BMT == 128) && !TA && BKT == 64), "row-tile variants");
   constexpr int WM = BMT / 2;                    // rows per wave
   constexpr int MI = WM / 16;                    // 16-row MFMA tiles per wave
   constexpr int NST = BKT == 64 ? 2 : 4;         // LDS stages
@@ -867,8 +868,8 @@ int sysml_gemm_dnn(const void* A, int64_t lda, const void* B, int64_t ldb, int64
   // 32-bit lane offsets: a 256-column tile spans at most 256 / hwb + 2 images
   if (((int64_t)(256 / hwb + 2) * simgB + (int64_t)BK * ldb) * 2 >= ((int64_t)1 << 31)) return -4;
   if (lda * 256 >= (int64_t)1 << 31) return -4;
-  const bool small = rowtile == 64;       // the host picks the row tile (ops/kernels.py _gemm_img)
-  const int tile = small ? 64 : BM;
+  const bool small = rowtile == 64 || rowtile == 128;   // the host picks the row tile (ops/kernels.py _gemm_img)
+  const int tile = small ? rowtile : BM;
   const int bk = small ? 64 : (g_bk ? g_bk : (ksplit > 1 ? 32 : 64));
   Args a;
   a.veca = a.vecb = 0;
@@ -895,7 +896,7 @@ int sysml_gemm_dnn(const void* A, int64_t lda, const void* B, int64_t ldb, int64
   a.vec = use_slab ? ((N % 4 == 0) && (((uintptr_t)slab & 15) == 0) && (a.slab % 4 == 0))
                    : ((ldc % 4 == 0) && (simgC % 4 == 0) && (((uintptr_t)C & (obf16 ? 7 : 15)) == 0));
   int rc;
-  if (small) rc = launch_bf16_t<false, false, 64, 64>(a, st);
+  if (small) rc = rowtile == 64 ? launch_bf16_t<false, false, 64, 64>(a, st) : launch_bf16_t<false, false, 64, 128>(a, st);
   else rc = bk == 64 ? launch_bf16_t<false, false, 64>(a, st) : launch_bf16_t<false, false, 32>(a, st);
   if (rc || !use_slab) return rc;
   const int64_t total = (int64_t)M * N;

@@ -884,6 +884,7 @@ def _conv_code(dt):
 
 
 GEMM_DNN_FILL = int(os.environ.get("SYSML_GEMM_DNN_FILL", "240"))   # workgroups that count as a full chip
+GEMM_DNN_T128 = int(os.environ.get("SYSML_GEMM_DNN_T128", "0"))      # 128-row tiles below this many 256-row tiles
 
 
 def _gemm_img(A, B, out, M, K, nimg, hw, hwb=None, bias=None, relu=False):
@@ -910,6 +911,8 @@ def _gemm_img(A, B, out, M, K, nimg, hw, hwb=None, bias=None, relu=False):
     # on 800 for deep K -- the 64-row tile is LDS-bound)
     nt = (Ncol + 255) // 256
     te = 64 if M <= 128 else 256
+    if te == 256 and GEMM_DNN_T128 and ((M + 255) // 256) * nt < GEMM_DNN_T128:
+        te = 128                      # 256-row tiles would leave CUs idle: twice the workgroups
     tiles = ((M + te - 1) // te) * nt
     ksplit = 1
     if tiles < GEMM_DNN_FILL // 2 and K >= 1024:

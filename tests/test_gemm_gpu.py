@@ -158,3 +158,24 @@ def test_weight_cast_one_pass(M, K, trans, pad8):
     assert out.shape[0] == ref.shape[0] and out.shape[1] == ((C + 7) // 8 * 8 if pad8 else C)
     assert torch.equal(out[:, :C], ref)
     assert not out[:, C:].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,nimg,hw", [(256, 2304, 16, 196), (512, 2048, 8, 49), (200, 576, 4, 784)])
+def test_gemm_img_128_row_tiles(M, K, nimg, hw, monkeypatch):
+    """The 128-row tile variant of the image-blocked GEMM (gemm_bf16_kernel<.., 64, 128>)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from systemml_amd.ops import kernels as Kn
+    Kn.load(required=True)
+    monkeypatch.setattr(Kn, "GEMM_DNN_T128", 1 << 20)
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    A = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    B = torch.randn(nimg, K, hw, device="cuda", generator=g).to(torch.bfloat16)
+    b = torch.randn(M, device="cuda", generator=g)
+    out = torch.empty(nimg, M, hw, dtype=torch.bfloat16, device="cuda")
+    Kn._gemm_img(A, B, out, M, K, nimg, hw, bias=b, relu=True)
+    ref = torch.relu(torch.matmul(A.float(), B.float()) + b.reshape(1, -1, 1))
+    torch.cuda.synchronize()
+    err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-30)
+    assert err < 1e-2, err
