@@ -1285,31 +1285,11 @@ _VECGEN = __import__('os').environ.get('SYSML_VECGEN', '1') != '0'   # Vector te
 SOFTMAX_MATCHER = __import__('os').environ.get('SYSML_SOFTMAX_MATCHER', '1') != '0'
 
 
-def _conv_gemm_path(c, config):
-    """A 1x1 / stride-1 / unpadded conv2d of bf16 activations runs as a batched library GEMM
-    (ops/kernels.conv2d): its bias would be one more pass, so it stays a cellwise bias_add that
-    the Cell template fuses into the consumers instead."""
-    if config is None or not getattr(config, "gpu", False) or getattr(config, "act_bf16_min_cells", 0) <= 0:
-        return False
-    named = list(c.named)
-    base = len(c.inputs) - len(named)
-
-    def vals(name):
-        """literal entries of a shape-list argument (None where not a literal)"""
-        if name not in named:
-            return None
-        h = c.inputs[base + named.index(name)]
-        if h.op == "bi" and h.p.get("name") == "list":
-            return [x.value if x.op == "lit" else None for x in h.inputs]
-        return None
-    f, st, pd = vals("filter_shape"), vals("stride"), vals("padding")
-    return f is not None and len(f) == 4 and f[2] == 1 and f[3] == 1 and st == [1, 1] and pd == [0, 0]
-
-
 def fuse_conv_bias(bb, config=None):
     """bias_add(conv2d(X, W, ...), b) -> conv2d(X, W, ..., bias = b) when the convolution has no
     other consumer (reference: hops/DnnOp CONV2D_BIAS_ADD): the bias is added in the
-    convolution kernel's epilogue instead of a second pass over the output.  Returns the
+    convolution kernel's epilogue instead of a second pass over the output -- on every path,
+    the 1x1 convolutions' image-blocked GEMM (gemm.hip sysml_gemm_dnn) included.  Returns the
     number of fused pairs."""
     live = getattr(bb, "live_out", None)
     tops = list(bb.roots) + list(bb.env_out.values())
@@ -1321,7 +1301,7 @@ def fuse_conv_bias(bb, config=None):
             continue
         c, b = h.inputs
         if not (c.op == "bi" and c.p.get("name") == "conv2d" and "bias" not in c.named) or c.id in outs \
-                or c.id in shared or _conv_gemm_path(c, config):
+                or c.id in shared:
             continue
         h.p = dict(c.p)
         h.inputs = list(c.inputs) + [b]

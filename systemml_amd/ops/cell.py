@@ -39,7 +39,7 @@ UN_CODES = {"sq": 20,               # x ^ 2 (binary '^' with the literal 2, lowe
             "sinh": 48, "cosh": 49, "tanh": 50, "sigmoid": 51}
 AGG_CODES = {"sum": 0, "sumsq": 1, "mean": 0, "min": 2, "max": 3}
 AGG_DIRS = {"all": 1, "row": 2, "col": 3}
-MAXIN, MAXOPS, NR = 8, 40, 16
+MAXIN, MAXOPS, NR = 12, 40, 16
 COL4 = 1000           # column-aggregate variant offset: 4 adjacent columns per lane (sysml_cell_col4)
 FULL, ROWV, COLV, HSCALAR, DSCALAR, CHAN = range(6)
 # per-channel broadcast operators (bias_add / bias_multiply: a C x 1 vector over the H*W columns
@@ -922,9 +922,15 @@ def _kernel_multi(m: MultiAggProgram, args):
     kernels._count("magg")
     del keep
     if col:
+        # the workgroup partials of all outputs in one column reduction (agg.hip; torch's
+        # per-output sum + cast was two ATen launches per output)
+        tot = kernels.agg("sum", "col", part.view(nblk, nout * Cc), ydt=T) if nblk > 1 else part.to(T)
+        if tot is None:
+            tot = part.sum(0).to(T)
+        tot = tot.view(nout, Cc)
         res = []
         for k, prog in enumerate(m.progs):
-            r = part[:, k, :].sum(0, keepdim=True).to(T)
+            r = tot[k:k + 1]
             res.append(r / R if prog.agg[0] == "mean" else r)
         return tuple(res)
     P = part.view(nblk, nout)

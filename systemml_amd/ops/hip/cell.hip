@@ -27,7 +27,7 @@
 
 namespace sysml_cl {
 
-constexpr int MAXIN = 8;
+constexpr int MAXIN = 12;
 constexpr int MAXOPS = 40;
 constexpr int NR = 16;
 constexpr int THREADS = 256;
@@ -57,7 +57,7 @@ struct Prog {
 };
 
 static_assert(sizeof(In) == 32, "In layout");
-static_assert(sizeof(Prog) == 8 * 32 + 24 + 24, "Prog layout");
+static_assert(sizeof(Prog) == MAXIN * 32 + 24 + 24, "Prog layout");
 
 __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
 

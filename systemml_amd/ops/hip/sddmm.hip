@@ -14,6 +14,7 @@
 // read once per row.  Rows that need more than 64 lanes (r*sizeof(T) > 1 KiB) loop over chunks.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 namespace sysml_sd {
 
@@ -140,7 +141,7 @@ __device__ __forceinline__ int64_t wd_first_row(const int64_t* __restrict__ crow
   return lo;
 }
 
-template <typename T, typename I, int G>
+template <typename T, typename I, int G, int UN>
 __global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __restrict__ crow,
                                                             const I* __restrict__ col, const T* __restrict__ wv,
                                                             const T* __restrict__ xv, const T* __restrict__ U,
@@ -165,12 +166,12 @@ __global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __res
         const bool whole = (rb >= s) && (re <= e);
         const T u = kin ? U[r * K + gl] : T(0);
         T acc = T(0);
-        // 4 non-zeros per group in flight: indices, weights and the 4 V-row gathers first
-        for (int64_t p0 = b + g; p0 < q; p0 += 4 * NG) {
-          int64_t cj[4];
-          T wt[4], xt[4], bv[4], dt[4];
+        // UN non-zeros per group in flight: indices, weights and the 4 V-row gathers first
+        for (int64_t p0 = b + g; p0 < q; p0 += UN * NG) {
+          int64_t cj[UN];
+          T wt[UN], xt[UN], bv[UN], dt[UN];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
+          for (int t = 0; t < UN; ++t) {
             const int64_t p = p0 + t * NG;
             const bool in = p < q;
             cj[t] = in ? (int64_t)col[p] : 0;
@@ -178,15 +179,15 @@ __global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __res
             xt[t] = (in && mode == 1) ? xv[p] : T(0);
           }
 #pragma unroll
-          for (int t = 0; t < 4; ++t) bv[t] = kin ? V[cj[t] * K + gl] : T(0);
+          for (int t = 0; t < UN; ++t) bv[t] = kin ? V[cj[t] * K + gl] : T(0);
 #pragma unroll
-          for (int t = 0; t < 4; ++t) dt[t] = u * bv[t];
+          for (int t = 0; t < UN; ++t) dt[t] = u * bv[t];
 #pragma unroll
           for (int off = G / 2; off >= 1; off >>= 1)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) dt[t] += __shfl_xor(dt[t], off, G);
+            for (int t = 0; t < UN; ++t) dt[t] += __shfl_xor(dt[t], off, G);
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
+          for (int t = 0; t < UN; ++t) {
             T qv;
             if (mode == 0) qv = wt[t] * dt[t];
             else if (mode == 1) qv = wt[t] * (dt[t] - xt[t]);
@@ -210,21 +211,30 @@ __global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __res
 template <typename T, typename I>
 int launch_wd(const int64_t* crow, const I* col, const T* wv, const T* xv, const T* U, const T* V, T* out, int64_t m,
               int K, int mode, double eps, int64_t nnz, hipStream_t st) {
-  int64_t chunk = (nnz + 256 * 16 - 1) / (256 * 16);
+  // the kernel is bound by the latency of its random V-row gathers: one chunk per wave and
+  // enough waves for a full CU (8 per SIMD at <= 64 VGPRs), each with UN gathers per group in
+  // flight.  SYSML_WD_WAVES / SYSML_WD_UNROLL override (tuning).
+  static const int wps = [] { const char* e = getenv("SYSML_WD_WAVES"); return e ? atoi(e) : 32; }();
+  static const int un = [] { const char* e = getenv("SYSML_WD_UNROLL"); return e ? atoi(e) : 4; }();
+  int64_t chunk = (nnz + 256LL * wps - 1) / (256LL * wps);
   if (chunk < 32) chunk = 32;
   const int64_t nchunks = (nnz + chunk - 1) / chunk;
   int64_t blocks = (nchunks + WAVES - 1) / WAVES;
   if (blocks > 256 * 32) blocks = 256 * 32;
   if (blocks < 1) blocks = 1;
   const dim3 gr((unsigned)blocks), t(WAVES * 64);
-#define WD_CASE(G_) hipLaunchKernelGGL((wdivmm_kernel<T, I, G_>), gr, t, 0, st, crow, col, wv, xv, U, V, out, m, K, mode, \
-                                       (T)eps, chunk, nchunks)
-  if (K <= 4) WD_CASE(4);
-  else if (K <= 8) WD_CASE(8);
-  else if (K <= 16) WD_CASE(16);
-  else if (K <= 32) WD_CASE(32);
-  else if (K <= 64) WD_CASE(64);
+#define WD_LAUNCH(G_, U_) hipLaunchKernelGGL((wdivmm_kernel<T, I, G_, U_>), gr, t, 0, st, crow, col, wv, xv, U, V, out, m, K, \
+                                            mode, (T)eps, chunk, nchunks)
+#define WD_CASE(G_) \
+  if (un >= 8) WD_LAUNCH(G_, 8); \
+  else WD_LAUNCH(G_, 4)
+  if (K <= 4) { WD_CASE(4); }
+  else if (K <= 8) { WD_CASE(8); }
+  else if (K <= 16) { WD_CASE(16); }
+  else if (K <= 32) { WD_CASE(32); }
+  else if (K <= 64) { WD_CASE(64); }
   else return -1;
+#undef WD_LAUNCH
 #undef WD_CASE
   return (int)hipGetLastError();
 }

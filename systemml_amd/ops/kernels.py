@@ -126,6 +126,11 @@ def load(required=False):
                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    L.sysml_conv3s1.restype = ctypes.c_int
+    L.sysml_conv3s1.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 7 + [ctypes.c_void_p]
+    L.sysml_conv3_weight.restype = ctypes.c_int
+    L.sysml_conv3_weight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p]
     L.sysml_cast_weight.restype = ctypes.c_int
     L.sysml_cast_weight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_void_p]
@@ -822,6 +827,7 @@ CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) in
 # 1x1 stride-1 convolutions of bf16 activations as image-blocked gemm.hip GEMMs (_gemm_img;
 # SYSML_CONV1X1_GEMM=0: the implicit-GEMM kernel of dnn.hip)
 CONV1X1_GEMM = os.environ.get("SYSML_CONV1X1_GEMM", "1") != "0"
+CONV3_DIRECT = os.environ.get("SYSML_CONV3_DIRECT", "1") != "0"   # 3x3 stride-1 layers on conv3.hip
 IM2COL_MAX_HW = int(os.environ.get("SYSML_IM2COL_MAX_HW", "196"))   # forward k x k convolutions via im2col + GEMM up to this Ho*Wo
 COL2IM_MAX_HW = int(os.environ.get("SYSML_COL2IM_MAX_HW", "196"))   # stride-1 backward data via GEMM + col2im up to this H*W (measured: faster at 14 x 14 and 7 x 7, slower at 28 x 28 and 56 x 56)
 CONV_SPLIT_BLOCKS = int(os.environ.get("SYSML_CONV_SPLIT_BLOCKS", "2048"))   # split K until ~this many blocks
@@ -835,17 +841,30 @@ class _WeightCasts:
     def __init__(self):
         self._d = {}
 
-    def get(self, t, dev, dt, trans=False, pad8=False):
+    def get(self, t, dev, dt, trans=False, pad8=False, taps=0):
         """t (2-D) cast to dt on dev; trans: its transpose, contiguous (the K-major filter
         operand of a backward-data GEMM); pad8: rows zero-padded to a multiple of 8 columns (a
-        16-B aligned row pitch for the GEMM's LDS-DMA staging; the padding is never read as data)."""
+        16-B aligned row pitch for the GEMM's LDS-DMA staging; the padding is never read as data).
+        taps: the tap-major operand of the direct 3x3 convolution (conv3.hip) of an F x C*9
+        filter -- 1: forward, F x 9 x C; 2: backward data, flipped and transposed, C x 9 x F."""
         import weakref
-        k = (id(t), trans, pad8)
+        k = (id(t), trans, pad8, taps)
         e = self._d.get(k)
         if e is not None and e[0]() is t and e[1] == t._version and e[2].device == dev and e[2].dtype == dt:
             return e[2]
         L = _lib
-        if dt == torch.bfloat16 and t.dtype == torch.float32 and t.is_cuda and t.device == dev and t.dim() == 2 \
+        if taps:
+            F, CK = t.shape
+            C = CK // 9
+            src = t if (t.dtype == torch.float32 and t.is_contiguous() and t.device == dev) else \
+                t.to(device=dev, dtype=torch.float32).contiguous()
+            c = torch.empty(((F, 9 * C) if taps == 1 else (C, 9 * F)), dtype=torch.bfloat16, device=dev)
+            rc = L.sysml_conv3_weight(src.data_ptr(), c.data_ptr(), F, C, int(taps == 2), _stream())
+            if rc != 0:
+                raise RuntimeError(f"sysml_conv3_weight failed: {rc}")
+            counters["cast_weight"] = counters.get("cast_weight", 0) + 1
+            pad8 = False
+        elif dt == torch.bfloat16 and t.dtype == torch.float32 and t.is_cuda and t.device == dev and t.dim() == 2 \
                 and t.is_contiguous() and L is not None:
             # one pass: cast, transpose and pad (gemm.hip cast_weight)
             M, K = t.shape
@@ -968,6 +987,26 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
     else:
         shape = (F, C * KH * KW)
     Wsrc = W0 if W0 is not None else W         # the filter as given (cache key of its transposed bf16 copy)
+    if CONV3_DIRECT and mode != 2 and KH == 3 and KW == 3 and sh == 1 and sw == 1 and ph == 1 and pw == 1 \
+            and dt == torch.bfloat16 and (C if mode == 0 else F) % 32 == 0 \
+            and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+        # 3x3 stride-1 layers: the direct convolution of conv3.hip (input patch staged in LDS once
+        # per 32 channels, the nine taps as LDS offsets); backward data is the forward convolution
+        # of dout with the flipped, transposed filter
+        y = torch.empty(shape, dtype=torch.bfloat16, device=dev)
+        inp, Cin, M = (X, C, F) if mode == 0 else (D, F, C)
+        A = _wcast.get(Wsrc, dev, dt, taps=1 + mode)
+        bb = None
+        if mode == 0 and bias is not None:
+            bb = bias.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+        rc = L.sysml_conv3s1(inp.data_ptr(), A.data_ptr(), _ptr(bb), y.data_ptr(), 0, N, Cin, H, Wd, M,
+                             int(bool(relu and mode == 0)), _stream())
+        if rc == 0:
+            _count(("conv2d", "conv2d_bwd_data")[mode])
+            _count("conv3_direct")
+            return y
+        if rc != -1:
+            raise RuntimeError(f"sysml_conv3s1 failed: {rc}")
     if CONV1X1_GEMM and mode != 2 and KH == 1 and KW == 1 and sh == 1 and sw == 1 and ph == 0 and pw == 0 \
             and dt == torch.bfloat16 and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
         # a 1x1 stride-1 convolution of bf16 activations is ONE GEMM over all images (gemm.hip
@@ -1131,10 +1170,10 @@ _AGG_DIR = {"all": 0, "row": 1, "col": 2}
 _AGG_XDT = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2}
 
 
-def agg(o, d, X):
+def agg(o, d, X, ydt=None):
     """Unary aggregate of a dense device matrix on ops/hip/agg.hip (fp64 accumulation, bf16 /
-    fp32 / fp64 read as stored).  d = 'all' -> 0-d fp64 tensor; 'row' -> N x 1; 'col' -> 1 x D.
-    None when the operator / layout is not covered."""
+    fp32 / fp64 read as stored).  d = 'all' -> 0-d fp64 tensor; 'row' -> N x 1; 'col' -> 1 x D
+    (stored as `ydt` when given, fp32 or fp64).  None when the operator / layout is not covered."""
     op, dr, xdt = _AGG_OPS.get(o), _AGG_DIR.get(d), _AGG_XDT.get(X.dtype)
     if op is None or dr is None or xdt is None or X.dim() != 2 or (op >= 8 and dr != 1):
         return None
@@ -1143,8 +1182,9 @@ def agg(o, d, X):
     if N == 0 or D == 0:
         return None
     X = X.contiguous()
-    ydt = torch.float64 if (X.dtype == torch.float64 or (X.dtype == torch.bfloat16 and backend.dtype == torch.float64)) \
-        else torch.float32
+    if ydt is None:
+        ydt = torch.float64 if (X.dtype == torch.float64 or (X.dtype == torch.bfloat16
+                                                             and backend.dtype == torch.float64)) else torch.float32
     if dr == 0:
         Y = torch.empty((), dtype=torch.float64, device=X.device)
     elif dr == 1:

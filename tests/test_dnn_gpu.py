@@ -198,3 +198,37 @@ def test_compare_backends_harness_quick():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.main(["--quick"]) == 0
+
+
+@pytest.mark.parametrize("shape", [(3, 64, 7, 7, 64), (2, 32, 14, 14, 160), (2, 64, 56, 56, 64), (3, 128, 28, 28, 128),
+                                   (5, 96, 5, 9, 40), (1, 32, 3, 100, 256)])
+def test_conv3_direct_forward_and_backward_data(shape, monkeypatch):
+    """3x3 stride-1 pad-1 layers on the direct convolution of conv3.hip (input patch staged once
+    per 32 channels; pixel tiles spanning images at 7x7 / 5x9; 64-row filter tiles for <= 64
+    outputs; ragged filter tiles): forward with bias + relu epilogue and backward data against
+    fp64 torch on the bf16-rounded operands."""
+    from systemml_amd.ops import kernels as Kn
+    from systemml_amd.ops.backend import backend
+    monkeypatch.setattr(backend, "act_bf16_min_cells", 1)
+    N, C, H, Wd, F_ = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    X = torch.randn(N, C * H * Wd, generator=g, dtype=torch.float64).to(torch.bfloat16).double()
+    W = (torch.randn(F_, C * 9, generator=g, dtype=torch.float64) / (3 * C ** 0.5)).to(torch.bfloat16).double()
+    b = torch.randn(F_, 1, generator=g, dtype=torch.float64)
+    out, G, dX, _ = _ref_conv(X, W, N, C, H, Wd, F_, 3, 1, 1)
+    G = G.to(torch.bfloat16).double()
+    x = X.reshape(N, C, H, Wd)
+    dX = torch.nn.grad.conv2d_input(x.shape, W.reshape(F_, C, 3, 3), G.reshape(N, F_, H, Wd), padding=1).reshape(N, -1)
+    ref = torch.relu(out.reshape(N, F_, H * Wd) + b.reshape(1, F_, 1)).reshape(N, -1)
+    dev = torch.device("cuda:0")
+    c0 = Kn.counters.get("conv3_direct", 0)
+    got = Kn.conv2d(0, X.to(dev, torch.bfloat16), W.float().to(dev), None, N, C, H, Wd, F_, 3, 3, 1, 1, 1, 1,
+                    bias=b.float().to(dev), relu=True)
+    gx = Kn.conv2d(1, None, W.float().to(dev), G.to(dev, torch.bfloat16), N, C, H, Wd, F_, 3, 3, 1, 1, 1, 1)
+    torch.cuda.synchronize()
+    assert Kn.counters.get("conv3_direct", 0) == c0 + 2
+    assert got.dtype == torch.bfloat16 and gx.dtype == torch.bfloat16
+    for name, a, r in (("fwd", got, ref), ("bwd_data", gx, dX)):
+        a = a.double().cpu()
+        err = (a - r).abs().max().item() / (r.abs().max().item() + 1e-30)
+        assert err < 1e-2, (name, err)

@@ -104,11 +104,13 @@ def test_append_of_host_and_device_operands():
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64, torch.bfloat16])
-def test_left_index_device_scalar_without_host_read(dt):
+def test_left_index_device_scalar_without_host_read(dt, monkeypatch):
     """R[i, j] = s with s a device-resident scalar: the kernel reads s on the device; the
     DevScalar is never materialised on the host."""
     _need()
     from systemml_amd.ops import core as C
+    from systemml_amd.ops.backend import backend
+    monkeypatch.setattr(backend, "use_kernels", True)
     from systemml_amd.runtime.scalars import DevScalar
     X = torch.zeros(50, 7, dtype=dt, device="cuda")
     s = DevScalar(torch.tensor(3.25, dtype=torch.float64, device="cuda"))

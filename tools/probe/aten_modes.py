@@ -18,6 +18,7 @@ import torch  # noqa: E402
 from torch.overrides import TorchFunctionMode  # noqa: E402
 
 SITES = collections.defaultdict(lambda: [0, 0])
+MIN = 1 << 20          # smallest tensor (elements) recorded
 _SKIP = {"__get__", "__repr__", "size", "dim", "numel", "is_contiguous", "data_ptr", "stride", "element_size",
          "__len__", "shape", "dtype", "device", "is_cuda", "layout", "storage_offset", "__hash__", "__eq__"}
 
@@ -28,7 +29,7 @@ class Rec(TorchFunctionMode):
         name = getattr(func, "__name__", str(func))
         if name not in _SKIP:
             big = [a for a in list(args) + list(kwargs.values())
-                   if isinstance(a, torch.Tensor) and a.is_cuda and a.numel() >= (1 << 20)]
+                   if isinstance(a, torch.Tensor) and a.is_cuda and a.numel() >= MIN]
             if big:
                 fr = [x for x in traceback.extract_stack(limit=16)[:-1] if "systemml_amd" in x.filename]
                 key = (name,) + tuple(f"{os.path.basename(x.filename)}:{x.lineno}" for x in fr[-3:])
