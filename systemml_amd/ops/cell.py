@@ -924,7 +924,7 @@ def _kernel_multi(m: MultiAggProgram, args):
     if col:
         # the workgroup partials of all outputs in one column reduction (agg.hip; torch's
         # per-output sum + cast was two ATen launches per output)
-        tot = kernels.agg("sum", "col", part.view(nblk, nout * Cc), ydt=T) if nblk > 1 else part.to(T)
+        tot = kernels.agg("sum", "col", part.view(nblk, nout * Cc), ydt=T)
         if tot is None:
             tot = part.sum(0).to(T)
         tot = tot.view(nout, Cc)

@@ -173,6 +173,20 @@ def matmul(P, Q, out_dtype=None):
         dt = out_dtype or (torch.float32 if pb or qb else torch.promote_types(P.dtype, Q.dtype))
         return torch.zeros((M, N), dtype=dt, device=dev)
     if pb or qb:
+        from .backend import backend
+        if backend.act_bf16_min_cells > 0 and pb != qb:
+            # bf16-activation training (DNN layers): the fp32 operand (a weight) is used as ONE
+            # bf16 plane, cached per tensor version (kernels._wcast), like the convolutions' filters
+            # -- not the hi / lo two-plane split that keeps fp32 accuracy for the solvers
+            from . import kernels
+            def one_plane(t):
+                if t.is_contiguous():
+                    return kernels._wcast.get(t, dev, torch.bfloat16)
+                if t.t().is_contiguous():              # t(W) of a stored weight: its cached transposed copy
+                    return kernels._wcast.get(t.t(), dev, torch.bfloat16, trans=True)
+                return t.to(torch.bfloat16)
+            C = _bf16(P, one_plane(Q)) if pb else _bf16(one_plane(P), Q)
+            return C if out_dtype is None else C.to(out_dtype)
         if pb and not qb:
             # one pass over the bf16 operand: stack Q's hi / lo planes along N
             hi, lo = _planes(Q)

@@ -60,7 +60,7 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 }
 
 template <int TM, typename TO>
-__global__ void __launch_bounds__(NT) conv3_kernel(C3 c) {
+__global__ void __launch_bounds__(NT, 2) conv3_kernel(C3 c) {
   constexpr int FI = TM / 32;                          // 16-row fragments per wave (TM / 2 rows)
   constexpr int FJ = 4;                                // 16-column fragments per wave (64 pixels)
   constexpr int AV = TM * (CB / 8) / NT;               // 16-B filter vectors per thread per tap

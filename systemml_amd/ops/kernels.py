@@ -131,6 +131,14 @@ def load(required=False):
     L.sysml_conv3_weight.restype = ctypes.c_int
     L.sysml_conv3_weight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_void_p]
+    L.sysml_wgrad_splits.restype = ctypes.c_int
+    L.sysml_wgrad_splits.argtypes = [ctypes.c_int] * 4
+    L.sysml_wgrad3_splits.restype = ctypes.c_int
+    L.sysml_wgrad3_splits.argtypes = [ctypes.c_int] * 5
+    L.sysml_wgrad3.restype = ctypes.c_int
+    L.sysml_wgrad3.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 5 + [ctypes.c_void_p]
+    L.sysml_wgrad_nt.restype = ctypes.c_int
+    L.sysml_wgrad_nt.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_int64] * 2 + [ctypes.c_void_p]
     L.sysml_cast_weight.restype = ctypes.c_int
     L.sysml_cast_weight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_void_p]
@@ -828,6 +836,10 @@ CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) in
 # SYSML_CONV1X1_GEMM=0: the implicit-GEMM kernel of dnn.hip)
 CONV1X1_GEMM = os.environ.get("SYSML_CONV1X1_GEMM", "1") != "0"
 CONV3_DIRECT = os.environ.get("SYSML_CONV3_DIRECT", "1") != "0"   # 3x3 stride-1 layers on conv3.hip
+# 3x3 stride-1 filter gradient on wgrad.hip's patch kernel: off by default -- measured slower than
+# the implicit GEMM (tools/bench_conv_rn50.py, profiles/conv_rn50_b256_r5.txt: 120-212 vs 180-215 TF;
+# its staging is not overlapped with the MFMAs)
+WGRAD3 = os.environ.get("SYSML_WGRAD3", "0") == "1"
 IM2COL_MAX_HW = int(os.environ.get("SYSML_IM2COL_MAX_HW", "196"))   # forward k x k convolutions via im2col + GEMM up to this Ho*Wo
 COL2IM_MAX_HW = int(os.environ.get("SYSML_COL2IM_MAX_HW", "196"))   # stride-1 backward data via GEMM + col2im up to this H*W (measured: faster at 14 x 14 and 7 x 7, slower at 28 x 28 and 56 x 56)
 CONV_SPLIT_BLOCKS = int(os.environ.get("SYSML_CONV_SPLIT_BLOCKS", "2048"))   # split K until ~this many blocks
@@ -987,6 +999,36 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
     else:
         shape = (F, C * KH * KW)
     Wsrc = W0 if W0 is not None else W         # the filter as given (cache key of its transposed bf16 copy)
+    if CONV1X1_GEMM and mode == 2 and KH == 1 and KW == 1 and sh == 1 and sw == 1 and ph == 0 and pw == 0 \
+            and dt == torch.bfloat16:
+        # 1x1 stride-1 filter gradient: dW = sum_img dout[img] . t(X[img]) as one batched NT GEMM
+        # (wgrad.hip: 16-B pixel-vector loads, images as the split-K axis, slab reduction)
+        HW = H * Wd
+        S = L.sysml_wgrad_splits(F, C, HW, N)
+        slab = torch.empty((S * F * C,), dtype=torch.float32, device=dev) if S > 1 else None
+        y = torch.empty((F, C), dtype=torch.float32, device=dev)
+        rc = L.sysml_wgrad_nt(D.data_ptr(), X.data_ptr(), y.data_ptr(), _ptr(slab), F, C, HW, N, F * HW, C * HW,
+                              _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_wgrad_nt failed: {rc}")
+        _count("conv2d_bwd_filter")
+        _count("wgrad_1x1")
+        return y
+    if WGRAD3 and mode == 2 and KH == 3 and KW == 3 and sh == 1 and sw == 1 and ph == 1 and pw == 1 \
+            and dt == torch.bfloat16 and Wd <= 64:
+        # 3x3 stride-1 filter gradient (wgrad.hip: 8-pixel runs of padded rows, the input patch as
+        # three column-shifted LDS copies, chunks split over blocks with a slab reduction)
+        S = L.sysml_wgrad3_splits(N, C, H, Wd, F)
+        if S >= 1:
+            slab = torch.empty((S * F * C * 9,), dtype=torch.float32, device=dev) if S > 1 else None
+            y = torch.empty((F, C * 9), dtype=torch.float32, device=dev)
+            rc = L.sysml_wgrad3(X.data_ptr(), D.data_ptr(), y.data_ptr(), _ptr(slab), N, C, H, Wd, F, _stream())
+            if rc == 0:
+                _count("conv2d_bwd_filter")
+                _count("wgrad_3x3")
+                return y
+            if rc != -1:
+                raise RuntimeError(f"sysml_wgrad3 failed: {rc}")
     if CONV3_DIRECT and mode != 2 and KH == 3 and KW == 3 and sh == 1 and sw == 1 and ph == 1 and pw == 1 \
             and dt == torch.bfloat16 and (C if mode == 0 else F) % 32 == 0 \
             and 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:

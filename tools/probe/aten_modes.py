@@ -27,15 +27,18 @@ class Rec(TorchFunctionMode):
     def __torch_function__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
         name = getattr(func, "__name__", str(func))
-        if name not in _SKIP:
-            big = [a for a in list(args) + list(kwargs.values())
-                   if isinstance(a, torch.Tensor) and a.is_cuda and a.numel() >= MIN]
-            if big:
-                fr = [x for x in traceback.extract_stack(limit=16)[:-1] if "systemml_amd" in x.filename]
-                key = (name,) + tuple(f"{os.path.basename(x.filename)}:{x.lineno}" for x in fr[-3:])
-                SITES[key][0] += 1
-                SITES[key][1] += sum(a.numel() * a.element_size() for a in big)
-        return func(*args, **kwargs)
+        r = func(*args, **kwargs)
+        if name in _SKIP or not isinstance(r, torch.Tensor) or not r.is_cuda:
+            return r
+        big = [a for a in list(args) + list(kwargs.values())
+               if isinstance(a, torch.Tensor) and a.is_cuda and a.numel() >= MIN]
+        # only calls that produce new device memory (views and no-op casts launch nothing)
+        if big and not any(r.untyped_storage().data_ptr() == a.untyped_storage().data_ptr() for a in big):
+            fr = [x for x in traceback.extract_stack(limit=16)[:-1] if "systemml_amd" in x.filename]
+            key = (name,) + tuple(f"{os.path.basename(x.filename)}:{x.lineno}" for x in fr[-3:])
+            SITES[key][0] += 1
+            SITES[key][1] += sum(a.numel() * a.element_size() for a in big)
+        return r
 
 
 def main():
