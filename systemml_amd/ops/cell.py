@@ -704,9 +704,14 @@ def _kernel(prog: CellProgram, args):
     if part is None:
         r = out
     else:
-        r = part.sum(0, keepdim=True) if AGG_CODES[o] <= 1 else (part.amin(0, keepdim=True) if o == "min"
-                                                                 else part.amax(0, keepdim=True))
-        r = r.to(T)
+        # row-block partials folded on agg.hip (fp64 in, T out): no ATen reduce + cast
+        from . import kernels
+        ko = "sum" if AGG_CODES[o] <= 1 or o == "mean" else o
+        r = kernels.fold_rows(part, ko, T)
+        if r is None:
+            r = part.sum(0, keepdim=True) if AGG_CODES[o] <= 1 else (part.amin(0, keepdim=True) if o == "min"
+                                                                     else part.amax(0, keepdim=True))
+            r = r.to(T)
     return r / R if o == "mean" else r
 
 
@@ -924,7 +929,7 @@ def _kernel_multi(m: MultiAggProgram, args):
     if col:
         # the workgroup partials of all outputs in one column reduction (agg.hip; torch's
         # per-output sum + cast was two ATen launches per output)
-        tot = kernels.agg("sum", "col", part.view(nblk, nout * Cc), ydt=T)
+        tot = kernels.fold_rows(part.view(nblk, nout * Cc), "sum", T)
         if tot is None:
             tot = part.sum(0).to(T)
         tot = tot.view(nout, Cc)

@@ -638,6 +638,11 @@ def tak(a, b):
         b = b.to(a.dtype)
     if a.device != b.device:
         b = b.to(a.device)
+    if backend.use_kernels and a.is_cuda:
+        from . import kernels
+        r = kernels.dot(a, b)                   # agg.hip: one pass, fp64 accumulation
+        if r is not None:
+            return _lazy_out(r)
     return _lazy_out(torch.dot(a.reshape(-1), b.reshape(-1)))
 
 

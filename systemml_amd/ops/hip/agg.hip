@@ -289,6 +289,46 @@ __global__ void __launch_bounds__(64) all_final(const St* __restrict__ part, dou
   if (lane == 0) *y = st_result<OP>(s, n);
 }
 
+// ---- fold of row-block partials: y[j] = op_b part[b, j] (fp64 partials of a column aggregate) --
+template <typename TO, int OP>
+__global__ void __launch_bounds__(NT) fold_rows(const double* __restrict__ part, TO* __restrict__ y, int nb, int64_t n) {
+  for (int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x; j < n; j += (int64_t)gridDim.x * NT) {
+    double a = part[j];
+    for (int b = 1; b < nb; ++b) {
+      const double v = part[(int64_t)b * n + j];
+      a = OP == MIN ? (v < a ? v : a) : (OP == MAX ? (v > a ? v : a) : a + v);
+    }
+    y[j] = (TO)a;
+  }
+}
+
+// ---- dot product sum(a * b) (TernaryAggregate tak+*) -------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(NT) dot_part(const T* __restrict__ A, const T* __restrict__ B, St* __restrict__ part,
+                                               int64_t n) {
+  __shared__ St red[NT / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  St s = st_init<SUM>();
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld(A, i + u * stride) * ld(B, i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s.a += v[u];
+  }
+  for (; i < n; i += stride) s.a += ld(A, i) * ld(B, i);
+  s = wave_reduce<SUM>(s, lane);
+  if (lane == 0) red[wave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    St t = red[0];
+    for (int w = 1; w < NT / 64; ++w) st_merge<SUM>(t, red[w]);
+    part[blockIdx.x] = t;
+  }
+}
+
 inline int grid_for(int64_t work, int per) {
   int64_t g = (work + per - 1) / per;
   if (g > 4096) g = 4096;
@@ -408,6 +448,39 @@ int sysml_agg(int op, int dir, int xdt, int ydt, const void* X, void* Y, void* s
   if (xdt == 2) return ydt == 1 ? by_op<double, float>(op, dir, X, Y, scratch, N, D, st)
                                 : by_op<double, double>(op, dir, X, Y, scratch, N, D, st);
   return -1;
+}
+
+// y (one double, device) = sum(A .* B) over n cells of two same-typed dense arrays (dt: 0 bf16,
+// 1 fp32, 2 fp64), fp64 accumulation; scratch: sysml_agg_scratch(0, n, 1) bytes.
+int sysml_dot(int dt, const void* A, const void* B, double* y, void* scratch, int64_t n, void* stream) {
+  using namespace sysml_ag;
+  if (n <= 0) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  int nb = grid_for(n, NT * 8);
+  if (nb > 1024) nb = 1024;                      // the scratch holds 1024 partials
+  St* part = (St*)scratch;
+  if (dt == 0) hipLaunchKernelGGL(dot_part<uint16_t>, dim3(nb), dim3(NT), 0, st, (const uint16_t*)A, (const uint16_t*)B, part, n);
+  else if (dt == 1) hipLaunchKernelGGL(dot_part<float>, dim3(nb), dim3(NT), 0, st, (const float*)A, (const float*)B, part, n);
+  else if (dt == 2) hipLaunchKernelGGL(dot_part<double>, dim3(nb), dim3(NT), 0, st, (const double*)A, (const double*)B, part, n);
+  else return -1;
+  hipLaunchKernelGGL(all_final<SUM>, dim3(1), dim3(64), 0, st, (const St*)part, y, nb, n);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// y (n values, fp32 when ydt == 1 else fp64) = sum / min / max (op 0 / 3 / 4) over the nb rows of
+// an nb x n fp64 partial block -- one pass, the last step of a blocked column aggregate.
+int sysml_fold_rows(int op, int ydt, const double* part, void* y, int nb, int64_t n, void* stream) {
+  using namespace sysml_ag;
+  if (nb <= 0 || n <= 0) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(grid_for(n, NT * 4)), t(NT);
+#define FOLD(TO_, OP_) hipLaunchKernelGGL((fold_rows<TO_, OP_>), g, t, 0, st, part, (TO_*)y, nb, n)
+  if (op == SUM) { if (ydt == 1) FOLD(float, SUM); else FOLD(double, SUM); }
+  else if (op == MIN) { if (ydt == 1) FOLD(float, MIN); else FOLD(double, MIN); }
+  else if (op == MAX) { if (ydt == 1) FOLD(float, MAX); else FOLD(double, MAX); }
+  else return -1;
+#undef FOLD
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 }  // extern "C"

@@ -405,9 +405,12 @@ int64_t sysml_cell_blocks(int agg, int64_t rows, int64_t cols) {
     int64_t b = (rows + THREADS / G - 1) / (THREADS / G);
     return b < 1 ? 1 : (b > 16384 ? 16384 : b);
   }
+  // >= 16 rows per thread (4 groups of U = 4 loads in flight): a batch-norm column aggregate
+  // (256 image rows x C*H*W columns) then has 4 row blocks per column strip instead of one --
+  // one block per strip left ~3 blocks per CU with one load in flight each
   const int cw = cols <= 8 ? 8 : 64;
   const int64_t rph = THREADS / cw;
-  int64_t b = (rows + rph * 64 - 1) / (rph * 64);     // >= 64 rows per thread
+  int64_t b = (rows + rph * 16 - 1) / (rph * 16);
   return b < 1 ? 1 : (b > 1024 ? 1024 : b);
 }
 

@@ -669,15 +669,40 @@ splitk_reduce_dnn(const float* __restrict__ slab, int64_t stride, int ks, void* 
   }
 }
 
-// B [N][C][hw] -> [N][C][hwp] (zero padding): image-blocked GEMM operands need 8-pixel pieces
+// B [N][C][hw] -> [N][C][hwp] (zero padding): image-blocked GEMM operands need 8-pixel pieces.
+// One thread per 8 output pixels (one 16-B store); the source run is read with the widest loads
+// its alignment allows (VEC = 4: hw % 4 == 0, 8-B loads; 2: 4-B loads; 1: 2-B loads).
+template <int VEC>
 __global__ void __launch_bounds__(256)
 pad_pixels(const uint16_t* __restrict__ X, uint16_t* __restrict__ Y, int64_t planes, int hw, int hwp) {
-  const int64_t total = planes * hwp;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t pl = idx / hwp;
-    const int px = (int)(idx - pl * hwp);
-    Y[idx] = px < hw ? X[pl * hw + px] : (uint16_t)0;
+  const int gpp = hwp >> 3;                       // 8-pixel groups per plane
+  const int64_t total = planes * gpp;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pl = g / gpp;
+    const int px = (int)(g - pl * gpp) * 8;
+    const uint16_t* src = X + pl * hw + px;
+    uint16_t v[8];
+    if (px + 8 <= hw) {
+      if (VEC == 4) {
+        const uint2 a = *(const uint2*)src, b = *(const uint2*)(src + 4);
+        v[0] = (uint16_t)a.x; v[1] = (uint16_t)(a.x >> 16); v[2] = (uint16_t)a.y; v[3] = (uint16_t)(a.y >> 16);
+        v[4] = (uint16_t)b.x; v[5] = (uint16_t)(b.x >> 16); v[6] = (uint16_t)b.y; v[7] = (uint16_t)(b.y >> 16);
+      } else if (VEC == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const uint32_t a = *(const uint32_t*)(src + e);
+          v[e] = (uint16_t)a; v[e + 1] = (uint16_t)(a >> 16);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = src[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = px + e < hw ? src[e] : (uint16_t)0;
+    }
+    *(uint4*)(Y + pl * hwp + px) = uint4{(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+                                         (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16)};
   }
 }
 
@@ -909,12 +934,18 @@ int sysml_gemm_dnn(const void* A, int64_t lda, const void* B, int64_t ldb, int64
 
 // Y[planes][hwp] = X[planes][hw] zero-padded to hwp pixels (bf16)
 int sysml_pad_pixels(const void* X, void* Y, int64_t planes, int hw, int hwp, void* stream) {
-  if (planes <= 0 || hw <= 0 || hwp < hw) return -1;
-  const int64_t total = planes * hwp;
+  if (planes <= 0 || hw <= 0 || hwp < hw || (hwp & 7) || ((uintptr_t)Y & 15)) return -1;
+  const int64_t total = planes * (hwp >> 3);
   int g = (int)((total + 255) / 256);
   g = g < 65536 ? g : 65536;
-  hipLaunchKernelGGL(pad_pixels, dim3(g), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)X, (uint16_t*)Y, planes,
-                     hw, hwp);
+  const bool a8 = ((uintptr_t)X & 7) == 0, a4 = ((uintptr_t)X & 3) == 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (hw % 4 == 0 && a8)
+    hipLaunchKernelGGL(pad_pixels<4>, dim3(g), dim3(256), 0, st, (const uint16_t*)X, (uint16_t*)Y, planes, hw, hwp);
+  else if (hw % 2 == 0 && a4)
+    hipLaunchKernelGGL(pad_pixels<2>, dim3(g), dim3(256), 0, st, (const uint16_t*)X, (uint16_t*)Y, planes, hw, hwp);
+  else
+    hipLaunchKernelGGL(pad_pixels<1>, dim3(g), dim3(256), 0, st, (const uint16_t*)X, (uint16_t*)Y, planes, hw, hwp);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

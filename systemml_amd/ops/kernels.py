@@ -139,6 +139,21 @@ def load(required=False):
     L.sysml_wgrad3.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 5 + [ctypes.c_void_p]
     L.sysml_wgrad_nt.restype = ctypes.c_int
     L.sysml_wgrad_nt.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_int64] * 2 + [ctypes.c_void_p]
+    L.sysml_csrt_count.restype = ctypes.c_int
+    L.sysml_csrt_count.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+    L.sysml_csrt_fill.restype = ctypes.c_int
+    L.sysml_csrt_fill.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.sysml_gather.restype = ctypes.c_int
+    L.sysml_gather.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                               ctypes.c_void_p]
+    L.sysml_fold_rows.restype = ctypes.c_int
+    L.sysml_fold_rows.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                  ctypes.c_int64, ctypes.c_void_p]
+    L.sysml_dot.restype = ctypes.c_int
+    L.sysml_dot.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_int64, ctypes.c_void_p]
     L.sysml_cast_weight.restype = ctypes.c_int
     L.sysml_cast_weight.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_void_p]
@@ -1244,6 +1259,91 @@ def agg(o, d, X, ydt=None):
 
 
 _ESIZE = {torch.bfloat16: 2, torch.float32: 4, torch.float64: 8}
+
+
+def csr_transpose_plan(crow, col, m, n):
+    """Transposed pattern of an m x n CSR pattern by counting sort (csrt.hip): (crowT int64,
+    colT int64, perm int64) with colT sorted inside every row of t(A) -- the arrays a stable key
+    sort gives.  The int32 copy of colT the kernels read is registered with idx32_of.  None when
+    a column is longer than the in-LDS segment sort handles."""
+    L = load(required=True)
+    nnz = col.numel()
+    dev = col.device
+    idx32 = int(col.dtype == torch.int32)
+    colc = col.contiguous() if idx32 else col.to(torch.int64).contiguous()
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    mx = torch.zeros(1, dtype=torch.int32, device=dev)
+    rc = L.sysml_csrt_count(colc.data_ptr(), idx32, nnz, cnt.data_ptr(), mx.data_ptr(), _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_csrt_count failed: {rc}")
+    if int(mx.item()) > 0:
+        return None
+    crowT = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(cnt, 0, dtype=torch.int64, out=crowT[1:])
+    cursor = torch.zeros(n, dtype=torch.int32, device=dev)
+    rows32 = torch.empty(nnz, dtype=torch.int32, device=dev)
+    perm = torch.empty(nnz, dtype=torch.int64, device=dev)
+    rc = L.sysml_csrt_fill(crow.to(torch.int64).contiguous().data_ptr(), colc.data_ptr(), idx32, m, n,
+                           crowT.data_ptr(), cursor.data_ptr(), rows32.data_ptr(), perm.data_ptr(), _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_csrt_fill failed: {rc}")
+    colT = rows32.to(torch.int64)
+    if len(_IDX32) >= 8:
+        _IDX32.pop(next(iter(_IDX32), None), None)
+    _IDX32[(colT.data_ptr(), colT.numel(), colT._version)] = (colT, rows32)
+    _count("csr_transpose")
+    return crowT, colT, perm
+
+
+def gather(v, perm):
+    """v[perm] for a 1-D device tensor and an int64 index vector (csrt.hip gather)."""
+    es = v.element_size()
+    if es not in (2, 4, 8) or not v.is_cuda or perm.dtype != torch.int64:
+        return v[perm]
+    L = load(required=True)
+    v = v.contiguous()
+    out = torch.empty(perm.numel(), dtype=v.dtype, device=v.device)
+    rc = L.sysml_gather(es, v.data_ptr(), perm.contiguous().data_ptr(), out.data_ptr(), perm.numel(), _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_gather failed: {rc}")
+    return out
+
+
+def fold_rows(part, op="sum", ydt=torch.float32):
+    """1 x n column result of an nb x n fp64 block of row-block partials (sum / min / max),
+    stored as ydt (fp32 / fp64): one agg.hip pass (fold_rows)."""
+    code = {"sum": 0, "min": 3, "max": 4}.get(op)
+    if code is None or part.dtype != torch.float64 or not part.is_cuda or ydt not in (torch.float32, torch.float64):
+        return None
+    L = load(required=True)
+    part = part.contiguous()
+    nb, n = part.shape[0], part[0].numel()
+    y = torch.empty((1, n), dtype=ydt, device=part.device)
+    rc = L.sysml_fold_rows(code, 1 if ydt == torch.float32 else 2, part.data_ptr(), y.data_ptr(), nb, n, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_fold_rows failed: {rc}")
+    return y
+
+
+def dot(A, B):
+    """sum(A * B) of two same-shaped dense device matrices as a 0-d fp64 device tensor
+    (agg.hip dot_part, fp64 accumulation; one pass, no product materialised); None when the
+    dtypes differ or are not covered."""
+    code = _AGG_XDT.get(A.dtype)
+    if code is None or B.dtype != A.dtype or A.shape != B.shape or not A.is_cuda or A.device != B.device:
+        return None
+    L = load(required=True)
+    n = A.numel()
+    if n == 0:
+        return None
+    A, B = A.contiguous(), B.contiguous()
+    y = torch.empty((), dtype=torch.float64, device=A.device)
+    scr = torch.empty((L.sysml_agg_scratch(0, n, 1),), dtype=torch.uint8, device=A.device)
+    rc = L.sysml_dot(code, A.data_ptr(), B.data_ptr(), y.data_ptr(), scr.data_ptr(), n, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_dot failed: {rc}")
+    _count("dot")
+    return y
 
 
 def cat(rows, mats):

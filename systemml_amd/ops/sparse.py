@@ -159,6 +159,17 @@ def _transpose_plan(a):
     crow, col = a.crow_indices(), a.col_indices()
     key = (crow.data_ptr(), col.data_ptr(), tuple(a.shape), col.numel())
     p = _TPLANS.get(key)
+    if p is None and a.is_cuda:
+        from .backend import backend
+        if backend.use_kernels:
+            # counting sort on the device (ops/hip/csrt.hip), no key sort
+            from . import kernels
+            t = kernels.csr_transpose_plan(crow, col, a.shape[0], a.shape[1])
+            if t is not None:
+                p = (t[0], t[1], t[2], crow, col)
+                if len(_TPLANS) >= 4:
+                    _TPLANS.pop(next(iter(_TPLANS), None), None)
+                _TPLANS[key] = p
     if p is None:
         r, c = a.shape
         rows = torch.repeat_interleave(torch.arange(r, device=crow.device), crow[1:] - crow[:-1])
@@ -229,7 +240,13 @@ def _transposed(a):
     if e is None:
         if len(_TVALS) >= 2:
             _TVALS.pop(next(iter(_TVALS), None), None)   # tolerant of a concurrent parfor worker's eviction
-        e = _TVALS[key] = (v, torch.sparse_csr_tensor(crowT, colT, v[perm], (a.shape[1], a.shape[0]),
+        from .backend import backend
+        if a.is_cuda and backend.use_kernels:
+            from . import kernels
+            vt = kernels.gather(v, perm)
+        else:
+            vt = v[perm]
+        e = _TVALS[key] = (v, torch.sparse_csr_tensor(crowT, colT, vt, (a.shape[1], a.shape[0]),
                                                       device=a.device))
     return e[1]
 

@@ -179,3 +179,21 @@ def test_gemm_img_128_row_tiles(M, K, nimg, hw, monkeypatch):
     torch.cuda.synchronize()
     err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-30)
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("hw", [196, 49, 30, 8])
+def test_pad_pixels_vector_paths(hw):
+    """The image-blocked GEMM's pixel padding (gemm.hip pad_pixels: 8-B / 4-B / 2-B source runs,
+    one 16-B store per 8 output pixels) against torch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from systemml_amd.ops import kernels as K
+    L = K.load(required=True)
+    planes = 333
+    hwp = (hw + 7) & ~7
+    x = torch.randn(planes, hw, device="cuda").to(torch.bfloat16)
+    y = torch.full((planes, hwp), 7.0, device="cuda", dtype=torch.bfloat16)
+    assert L.sysml_pad_pixels(x.data_ptr(), y.data_ptr(), planes, hw, hwp, K._stream()) == 0
+    ref = torch.zeros(planes, hwp, dtype=torch.bfloat16)
+    ref[:, :hw] = x.cpu()
+    assert torch.equal(y.cpu(), ref)

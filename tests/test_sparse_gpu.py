@@ -172,3 +172,46 @@ def test_fused_wdivmm_matches_dense(K, form, left):
                    X=X if form == "multx" else None)
     assert kernels.counters.get("wdivmm", 0) == c0 + 1
     torch.testing.assert_close(got.cpu(), ref, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("m,n,per", [(1000, 700, 9), (50, 100000, 40), (3000, 5, 3)])
+def test_csr_transpose_counting_sort(m, n, per):
+    """Transposed CSR pattern by counting sort (csrt.hip: column counts, atomic slot claims,
+    per-segment bitonic sort by row) equals the key-sort plan: canonical t(A), and the value
+    permutation gathers A's values into t(A)'s order."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from systemml_amd.ops import kernels
+    kernels.load(required=True)
+    g = torch.Generator().manual_seed(m + n)
+    dense = (torch.rand(m, n, generator=g) < per / n).double() * torch.randn(m, n, generator=g, dtype=torch.float64)
+    A = dense.to_sparse_csr().to("cuda")
+    crow, col = A.crow_indices(), A.col_indices()
+    t = kernels.csr_transpose_plan(crow, col, m, n)
+    if (dense != 0).sum(0).max().item() > 1024:
+        assert t is None                    # segments longer than the in-LDS sort: key-sort fallback
+        return
+    assert t is not None
+    crowT, colT, perm = t
+    ref = dense.t().contiguous().to_sparse_csr()
+    assert torch.equal(crowT.cpu(), ref.crow_indices())
+    assert torch.equal(colT.cpu(), ref.col_indices())
+    vt = kernels.gather(A.values(), perm)
+    assert torch.equal(vt.cpu(), ref.values())
+    assert torch.equal(kernels.idx32_of(colT).cpu(), ref.col_indices().int())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64, torch.bfloat16])
+def test_dot_kernel(dt):
+    """sum(a * b) (tak+*) on agg.hip: fp64 accumulation against fp64 torch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from systemml_amd.ops import kernels
+    kernels.load(required=True)
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(1234, 567, generator=g, dtype=torch.float64).to(dt)
+    b = torch.randn(1234, 567, generator=g, dtype=torch.float64).to(dt)
+    r = kernels.dot(a.cuda(), b.cuda())
+    ref = (a.double() * b.double()).sum().item()
+    assert r.dtype == torch.float64 and r.dim() == 0
+    assert r.item() == pytest.approx(ref, rel=1e-10, abs=1e-8)

@@ -19,8 +19,14 @@ from torch.overrides import TorchFunctionMode  # noqa: E402
 
 SITES = collections.defaultdict(lambda: [0, 0])
 MIN = 1 << 20          # smallest tensor (elements) recorded
-_SKIP = {"__get__", "__repr__", "size", "dim", "numel", "is_contiguous", "data_ptr", "stride", "element_size",
+_SKIP = {"crow_indices", "col_indices", "values", "__get__", "__repr__", "size", "dim", "numel", "is_contiguous", "data_ptr", "stride", "element_size",
          "__len__", "shape", "dtype", "device", "is_cuda", "layout", "storage_offset", "__hash__", "__eq__"}
+
+
+def _same_storage(r, a):
+    if r.layout != torch.strided or a.layout != torch.strided:
+        return False                       # sparse results: count them
+    return r.untyped_storage().data_ptr() == a.untyped_storage().data_ptr()
 
 
 class Rec(TorchFunctionMode):
@@ -32,8 +38,8 @@ class Rec(TorchFunctionMode):
             return r
         big = [a for a in list(args) + list(kwargs.values())
                if isinstance(a, torch.Tensor) and a.is_cuda and a.numel() >= MIN]
-        # only calls that produce new device memory (views and no-op casts launch nothing)
-        if big and not any(r.untyped_storage().data_ptr() == a.untyped_storage().data_ptr() for a in big):
+        # calls that produce new device memory or write in place (views and no-op casts launch nothing)
+        if big and (name.endswith("_") or not any(_same_storage(r, a) for a in big)):
             fr = [x for x in traceback.extract_stack(limit=16)[:-1] if "systemml_amd" in x.filename]
             key = (name,) + tuple(f"{os.path.basename(x.filename)}:{x.lineno}" for x in fr[-3:])
             SITES[key][0] += 1
