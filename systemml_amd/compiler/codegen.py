@@ -992,3 +992,102 @@ def _multi_agg_group(cands):
             root.p = {"i": i, "lines": lines}
             done.add(root.id)
     return done
+
+
+# ------------------------------------------------------------------ horizontal Cell batches
+BATCH_MIN = 3      # smallest group of same-program Cell hops made one launch
+BATCH_MAX_CELLS = 1 << 22   # largest member output batched
+
+
+def batch_cells(bb):
+    """Horizontal fusion of the Cell template: unaggregated Cell hops of a block that run the
+    SAME program on different, independent operands -- the per-parameter optimizer updates of a
+    network (`v = mu * v - lr * dW`, `W = W + v` once per weight) -- become one `hcell` hop whose
+    kernel covers all of their cells in one launch (ops/cell.evaluate_batch: a per-operand table
+    and a block -> operand map), instead of one launch per parameter.  Members must be
+    independent (no member an ancestor of another), their matrix inputs of the output's shape
+    and the rest scalars.  The original hops become fout views.  Returns the number of hops
+    batched.  (Reference analogue: the multi-threaded per-parameter updates of the CP backend;
+    on a GPU every tiny launch costs a few microseconds of device time.)"""
+    allroots = list(bb.roots) + list(bb.env_out.values())
+    order = walk(allroots)
+    cand = []
+    for h in order:
+        if h.op != "cell":
+            continue
+        prog = h.p.get("prog")
+        # small operands only (weights, per-channel vectors): batching delays every member to
+        # the last one's inputs, which for activations would stretch their lifetimes
+        if prog is None or prog.agg or h.dim1 <= 0 or h.dim2 <= 0 or h.dim1 * h.dim2 > BATCH_MAX_CELLS:
+            continue
+        kinds = []
+        for x in h.inputs:
+            if x.dt == "S":
+                kinds.append("s")
+            elif x.dt == "M" and ((x.dim1 == h.dim1 and x.dim2 == h.dim2) or x.dim1 < 0 or x.dim2 < 0):
+                kinds.append("m")               # unknown dims: checked per operand set at run time
+            else:
+                kinds = None
+                break
+        if kinds is None or "m" not in kinds:
+            continue
+        cand.append((h, (prog.key(), tuple(kinds))))
+    if len(cand) < BATCH_MIN:
+        return 0
+    groups = {}
+    for h, k in cand:
+        groups.setdefault(k, []).append(h)
+    groups = {k: v for k, v in groups.items() if len(v) >= BATCH_MIN}
+    if not groups:
+        return 0
+    n = 0
+    for key in list(groups):
+        # ancestor sets over this group's hops, as bitsets, in topological order -- recomputed
+        # per group, since a batch made for an earlier group adds dependences (its hop reads
+        # all of its members' inputs)
+        order = walk(list(bb.roots) + list(bb.env_out.values()))
+        members = [h for h in order if h.op == "cell" and h.id in {m.id for m in groups[key]}]
+        bit = {h.id: 1 << i for i, h in enumerate(members)}
+        anc = {}
+        for h in order:
+            a = 0
+            for x in h.inputs:
+                a |= anc.get(x.id, 0) | bit.get(x.id, 0)
+            anc[h.id] = a
+        rest = members
+        while len(rest) >= BATCH_MIN:
+            # greedy antichains in both topological directions, the larger one is taken (a member
+            # that feeds all the others -- an early `a + b` ahead of the update sweep -- blocks the
+            # forward sweep, the backward one skips it)
+            fwd, mask = [], 0
+            for h in rest:                      # forward: only earlier members can be ancestors
+                if not anc[h.id] & mask:
+                    fwd.append(h)
+                    mask |= bit[h.id]
+            bwd, under = [], 0
+            for h in reversed(rest):            # backward: skip ancestors of the members taken
+                if not bit[h.id] & under:
+                    bwd.append(h)
+                    under |= anc[h.id]
+            taken = fwd if len(fwd) >= len(bwd) else bwd[::-1]
+            ids = {t.id for t in taken}
+            rest = [h for h in rest if h.id not in ids]
+            if len(taken) < BATCH_MIN:
+                break
+            prog = taken[0].p["prog"]
+            leaves = [x for t in taken for x in t.inputs]
+            M = Hop("hcell", leaves, {"o": "batch[" + prog.describe() + f"]x{len(taken)}", "prog": prog,
+                                      "n": len(taken), "lines": sorted({ln for t in taken
+                                                                       for ln in t.p.get("lines", ())})},
+                    dt="U", pos=taken[0].pos)
+            for i, t in enumerate(taken):
+                t.op = "fout"
+                t.inputs = [M]
+                t.named = []
+                t.p = {"i": i}
+            n += len(taken)
+            # the taken hops are fouts of M now: later batches of this group must not read them
+            # through M's inputs (rest are independent of taken by construction, but M reads all
+            # taken inputs, so recompute reachability before the next batch)
+            break
+    return n

@@ -123,6 +123,8 @@ def infer(h, dims, env):
             return (m, nn)
         kb = ins[-1][1]
         return (m, kb) if ot == "left" else (nn, kb)
+    if op == "hcell":
+        return UNK                       # a tuple of outputs, read through fout hops
     if op == "row":
         from ..ops.rowgen import out_shape
         if h.p["prog"].more:

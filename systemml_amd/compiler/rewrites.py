@@ -1283,6 +1283,9 @@ _VECGEN = __import__('os').environ.get('SYSML_VECGEN', '1') != '0'   # Vector te
 # the hand-matched softmax gradient / objective operators (smgrad / smobj, chain4m kernels); off:
 # the Row template plans the same passes as generated multi-output programs
 SOFTMAX_MATCHER = __import__('os').environ.get('SYSML_SOFTMAX_MATCHER', '1') != '0'
+# horizontal Cell batches (codegen.batch_cells): same-program updates of many small operands in
+# one launch
+CELL_BATCH = __import__('os').environ.get('SYSML_CELL_BATCH', '1') != '0'
 
 
 def fuse_conv_bias(bb, config=None):
@@ -1401,6 +1404,11 @@ def rewrite_block(bb, config=None):
         n = fuse_cells(bb, single=_VECGEN and (config is None or getattr(config, "gpu", True)), stats=rw.stats)
         if n:
             rw.stats["cell-fused-ops"] = n
+        if CELL_BATCH and (config is None or getattr(config, "gpu", True)):
+            from .codegen import batch_cells
+            n = batch_cells(bb)
+            if n:
+                rw.stats["cell-batched"] = n
     return rw.stats
 
 

@@ -715,6 +715,199 @@ def _kernel(prog: CellProgram, args):
     return r / R if o == "mean" else r
 
 
+# ----------------------------------------------------------------------------- horizontal batches
+class _HTab(ctypes.Structure):
+    """One operand set of a batched Cell launch (mirrors SysmlHT of generate_batch)."""
+    _fields_ = [("inp", ctypes.c_void_p * MAXIN), ("s", ctypes.c_double * MAXIN), ("out", ctypes.c_void_p),
+                ("total", ctypes.c_int64), ("b0", ctypes.c_int64)]
+
+
+class _HArgs(ctypes.Structure):
+    _fields_ = [("tab", ctypes.c_void_p), ("nt", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+BATCH_CELLS = 4 * 256                  # cells per workgroup of the batched kernel
+_hpinned = []                          # pinned host tables in flight (kept until reused)
+
+
+def generate_batch(prog: CellProgram, T, modes, dts):
+    """HIP source of the batched kernel: workgroup b finds its operand set t (the last table entry
+    with b0 <= b) and computes 4 cells per lane of that set's output."""
+    ct = "float" if T == torch.float32 else "double"
+    var = [f"x[{k}]" for k in range(prog.n_in)] + [None] * (NR - prog.n_in)
+    body = []
+    for q, (kind, o, d, a, b) in enumerate(prog.ops):
+        e = (_C_BIN[o] if kind == "b" else _C_UN[o]).format(a=var[a], b=var[b] if kind == "b" else "")
+        body.append(f"    const T v{q} = {e};")
+        var[d] = f"v{q}"
+    loads = []
+    for k in range(prog.n_in):
+        if modes[k] == FULL:
+            loads.append(f"        x[{k}] = sysml_ld<T>(A.in[{k}], {dts[k]}, e);")
+        elif modes[k] == DSCALAR:
+            loads.append(f"        x[{k}] = sysml_ld<T>(A.in[{k}], {dts[k]}, 0);")
+        else:
+            loads.append(f"        x[{k}] = (T)A.s[{k}];")
+    name = "sysml_hcell_" + kernel_name(prog, 0)[len("sysml_cell_"):]
+    return (_prelude() + f"""
+// generated (batched): {prog.describe()}
+struct SysmlHT {{ const void* in[{MAXIN}]; double s[{MAXIN}]; void* out; long long total; long long b0; }};
+struct Spec {{
+  typedef {ct} T;
+  static constexpr int NIN = {prog.n_in};
+  static __device__ __forceinline__ T f(const T (&x)[NIN]) {{
+{chr(10).join(body)}
+    return {var[prog.out]};
+  }}
+}};
+
+extern "C" __global__ void __launch_bounds__(256) {name}(const SysmlHT* __restrict__ tab, const int nt) {{
+  typedef Spec::T T;
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {{
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].b0 <= (long long)blockIdx.x) lo = mid; else hi = mid - 1;
+  }}
+  const SysmlHT& A = tab[lo];
+  const long long e0 = ((long long)blockIdx.x - A.b0) * {BATCH_CELLS} + threadIdx.x;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {{
+    const long long e = e0 + v * 256;
+    if (e < A.total) {{
+      T x[Spec::NIN];
+{chr(10).join(loads)}
+      static_cast<T*>(A.out)[e] = Spec::f(x);
+    }}
+  }}
+}}
+"""), name
+
+
+def evaluate_batch(prog: CellProgram, n, args):
+    """n evaluations of one unaggregated Cell program (compiler/codegen.batch_cells), args the n
+    operand lists concatenated; returns the tuple of results.  On the MI355X one launch of a
+    generated batched kernel covers all of them when they agree in operand kinds and dtypes;
+    otherwise each runs on its own."""
+    k = prog.n_in
+    sets = [list(args[i * k:(i + 1) * k]) for i in range(n)]
+    if backend.use_kernels:
+        r = _batch_kernel(prog, sets)
+        if r is not None:
+            stats["batched"] = stats.get("batched", 0) + n
+            return r
+    return tuple(evaluate(prog, a) for a in sets)
+
+
+def _batch_kernel(prog, sets):
+    from ..runtime.scalars import DevScalar
+    first = sets[0]
+    modes, dts, shapes = [], [], []
+    dev = None
+    f64 = False
+    for x in first:
+        if type(x) is _Tensor:
+            if not x.is_cuda or x.layout is not torch.strided or x.dtype not in _DT:
+                return None
+            dev = x.device
+            modes.append(FULL if x.numel() > 1 or x.dim() == 2 and x.shape != (1, 1) else DSCALAR)
+            dts.append(_DT[x.dtype])
+            f64 |= x.dtype == torch.float64
+        elif type(x) is DevScalar:
+            modes.append(DSCALAR)
+            dts.append(_DT[torch.float64])
+        elif isinstance(x, (int, float, bool)):
+            modes.append(HSCALAR)
+            dts.append(0)
+        else:
+            return None
+    if dev is None:
+        return None
+    T = torch.float64 if (f64 or backend.dtype == torch.float64) else torch.float32
+    n = len(sets)
+    tabs = (_HTab * n)()
+    outs = []
+    keep = []
+    b0 = 0
+    for i, a in enumerate(sets):
+        e = tabs[i]
+        shape = None
+        for q, x in enumerate(a):
+            tx = type(x)
+            if modes[q] == FULL:
+                if tx is not _Tensor or x.dtype not in _DT or _DT[x.dtype] != dts[q] or x.device != dev \
+                        or x.layout is not torch.strided:
+                    return None
+                if shape is None:
+                    shape = tuple(x.shape)
+                elif tuple(x.shape) != shape:
+                    return None
+                if not x.is_contiguous():
+                    x = x.contiguous()
+                keep.append(x)
+                e.inp[q] = x.data_ptr()
+            elif modes[q] == DSCALAR:
+                t = x.t.reshape(1) if tx is DevScalar else \
+                    (x.reshape(1) if tx is _Tensor and x.numel() == 1 else None)
+                if t is None or not t.is_cuda or t.dtype not in _DT or _DT[t.dtype] != dts[q]:
+                    return None
+                keep.append(t)
+                e.inp[q] = t.data_ptr()
+            else:
+                if not isinstance(x, (int, float, bool)):
+                    return None
+                e.s[q] = float(x)
+        if shape is None:
+            return None
+        if 0 < backend.act_bf16_min_cells <= shape[0] * shape[1]:
+            return None                         # the single-operand plan would store this one bf16
+        y = torch.empty(shape, dtype=T, device=dev)
+        outs.append(y)
+        e.out = y.data_ptr()
+        e.total = y.numel()
+        e.b0 = b0
+        b0 += (y.numel() + BATCH_CELLS - 1) // BATCH_CELLS
+    if b0 == 0 or b0 >= 2 ** 31:
+        return None
+    key = ("hcell", prog.key(), T, tuple(modes), tuple(dts), str(dev))
+    f = _rtc_funcs.get(key, False)
+    if f is False:
+        try:
+            src, name = generate_batch(prog, T, tuple(modes), tuple(dts))
+            code = compile_source(src, gpu_arch(dev))
+            fn = ctypes.c_void_p()
+            cbuf = ctypes.create_string_buffer(code, len(code))
+            rc = _rtc_lib().sysml_rtc_load(cbuf, name.encode(), ctypes.byref(fn))
+            if rc != 0:
+                raise RuntimeError(f"hipModuleLoadData failed ({rc})")
+            f = (fn, cbuf)
+        except RuntimeError as ex:
+            import warnings
+            warnings.warn(f"batched cell kernel not compiled, the updates run one by one: {ex}")
+            f = None
+        _rtc_funcs[key] = f
+    if f is None:
+        return None
+    nb = ctypes.sizeof(tabs)
+    host = torch.empty((nb,), dtype=torch.uint8, pin_memory=True)
+    ctypes.memmove(host.data_ptr(), ctypes.addressof(tabs), nb)
+    dtab = host.to(dev, non_blocking=True)
+    _hpinned.append(host)                       # alive until the copy has run (a short ring)
+    if len(_hpinned) > 64:
+        del _hpinned[:32]
+    A = _HArgs()
+    A.tab = dtab.data_ptr()
+    A.nt = n
+    st = torch.cuda.current_stream(dev).cuda_stream
+    rc = _rtc_lib().sysml_rtc_launch(f[0], b0, 1, 256, ctypes.byref(A), ctypes.sizeof(A), st)
+    if rc != 0:
+        raise RuntimeError(f"batched cell kernel launch failed: {rc}")
+    stats["rtc_launches"] += 1
+    from . import kernels
+    kernels._count("hcell")
+    del keep
+    return tuple(outs)
+
+
 # ----------------------------------------------------------------------------- multi-aggregate
 MAGG_COL_CW = 64           # column groups (of 4 columns) per workgroup of the column MAgg kernel
 

@@ -20,7 +20,7 @@ from .scalars import DevScalar
 
 
 _SPARSE_OK_OPS = {"lit", "tread", "fout", "fcall", "mm", "tsmm", "mmchain", "t", "agg", "b", "tak", "wquat", "cell",
-                  "magg", "row", "outer", "vprog"}
+                  "magg", "row", "outer", "vprog", "hcell"}
 # builtins with their own CSR paths (the sparse-safe fused operators of compiler/rewrites.py)
 _SPARSE_OK_BI = {"_nnz", "_minus_nz", "_log_nz"}
 # operators computing directly on cbind(X, const) views (ops/augmented.ConstCol)
@@ -30,10 +30,10 @@ _SPARSE_OK_UNARY = {"nrow", "ncol", "length", "cast_matrix", "abs", "sqrt", "rou
 # operators that accept HBM-resident scalars (runtime/scalars.DevScalar) as operands; all others
 # receive materialised Python values (one device sync)
 _LAZY_OK_OPS = {"lit", "tread", "b", "u", "fcall", "fout", "mm", "tsmm", "mmchain", "smgrad", "smobj", "t", "tak",
-                 "cell", "magg", "row", "outer", "vprog", "lix"}
+                 "cell", "magg", "row", "outer", "vprog", "lix", "hcell"}
 # operators that compute on matrix operands (placement applies); the rest move values around
 _COMPUTE_OPS = {"b", "u", "agg", "mm", "tsmm", "mmchain", "smgrad", "smobj", "wquat", "tak", "t", "rix", "lix", "bi",
-                 "cell", "magg", "row", "outer"}
+                 "cell", "magg", "row", "outer", "hcell"}
 transfer_stats = {"h2d": 0, "d2h": 0, "h2d_bytes": 0, "d2h_bytes": 0}   # -stats (utils/stats.gpu_report)
 _NO_PLACE_BI = {"print", "write", "stop", "assert", "printf", "list", "eval", "exists", "time", "toString",
                 "read"}
@@ -239,6 +239,11 @@ def _make_impl(h):
         from ..ops import cell as CELL
         prog = p["prog"]
         return (lambda ctx, a: CELL.evaluate(prog, a)), "spoofCell"
+    if op == "hcell":
+        # horizontal Cell batch (compiler/codegen.batch_cells): n same-program updates, one launch
+        from ..ops import cell as CELL
+        bprog, bn = p["prog"], p["n"]
+        return (lambda ctx, a: CELL.evaluate_batch(bprog, bn, a)), "spoofCellBatch"
     if op == "outer":
         # Outer-product template (compiler/codegen.fuse_outer): sampled at a sparse driver's
         # non-zeros (ops/outer.py)
