@@ -24,12 +24,13 @@ from ..runtime import scalars as S
 
 
 class ConstCol:
-    __slots__ = ("X", "c", "_pad")
+    __slots__ = ("X", "c", "_pad", "_uses")
 
     def __init__(self, X, c):
         self.X = X
         self.c = float(c)
         self._pad = None
+        self._uses = 0          # matrix products taken so far (the padded copy pays from the second)
 
     @property
     def shape(self):
@@ -131,6 +132,13 @@ def padded(a):
 _PADS = {}   # (id(X), version, c) -> (weakref to X, padded copy)
 
 
+def _PADS_HIT(a):
+    """a padded copy of this view's matrix is cached already (an earlier run of the script)"""
+    X = a.X
+    e = _PADS.get((id(X), getattr(X, "_version", -1), float(a.c)))
+    return e is not None and e[0]() is X
+
+
 def padv(v, Dp):
     """(D+1) x K operand zero-extended to the padded row length."""
     C = _C()
@@ -150,7 +158,11 @@ def mm(a, b, transA=False):
     if is_cc(b):
         b = b.materialize()
         return C.mm(a, b, transA)
-    Xp = padded(a)
+    # the padded copy (one more pass over X) pays off when the view is multiplied again and
+    # again (the solvers' X); a view used once -- (X ^ 2) %*% v in MultiLogReg's icpt=2 set-up --
+    # takes the split product on X and the constant column
+    a._uses += 1
+    Xp = padded(a) if (a._uses > 1 or a._pad is not None or _PADS_HIT(a)) else None
     if Xp is not None and isinstance(b, torch.Tensor):
         D1 = a.X.shape[1] + 1
         if transA:
@@ -228,12 +240,35 @@ def unary(op, a):
     return ConstCol(fx, float(S.as_double(C.unary(op, a.c))))
 
 
+_CELL1 = {}
+
+
+def _cell1(op, x, s, left):
+    """x op s (left) or s op x on a large device matrix as ONE generated Cell pass (a bf16 X is
+    read as stored; the generic path would widen it to fp32 first and then apply the op)."""
+    from .backend import backend
+    from . import cell as CELL
+    if not (backend.use_kernels and isinstance(x, torch.Tensor) and x.is_cuda and x.layout == torch.strided
+            and x.dim() == 2 and x.numel() >= (1 << 20) and op in CELL.BIN_CODES
+            and isinstance(s, (int, float)) and not isinstance(s, bool)):
+        return None
+    prog = _CELL1.get((op, left))
+    if prog is None:
+        prog = CELL.CellProgram([("b", op, 2, 0, 1) if left else ("b", op, 2, 1, 0)], 2, 2)
+        _CELL1[(op, left)] = prog
+    return CELL.evaluate(prog, [x, float(s)])
+
+
 def binary(op, a, b):
     C = _C()
     if is_cc(a) and not isinstance(b, (torch.Tensor, ConstCol)) and not C.is_dist(b):
-        return ConstCol(C.binary(op, a.X, b), float(S.as_double(S.binary(op, a.c, S.as_double(b)))))
+        r = _cell1(op, a.X, S.as_double(b) if type(b) is not float else b, True)
+        return ConstCol(C.binary(op, a.X, b) if r is None else r,
+                        float(S.as_double(S.binary(op, a.c, S.as_double(b)))))
     if is_cc(b) and not isinstance(a, (torch.Tensor, ConstCol)) and not C.is_dist(a):
-        return ConstCol(C.binary(op, a, b.X), float(S.as_double(S.binary(op, S.as_double(a), b.c))))
+        r = _cell1(op, b.X, S.as_double(a) if type(a) is not float else a, False)
+        return ConstCol(C.binary(op, a, b.X) if r is None else r,
+                        float(S.as_double(S.binary(op, S.as_double(a), b.c))))
     a = a.materialize() if is_cc(a) else a
     b = b.materialize() if is_cc(b) else b
     return C.binary(op, a, b)
