@@ -115,3 +115,32 @@ def test_resnet_step_runs_no_library_gemm_or_library_conv():
     tot = sum(kern.values())
     aten = sum(v for n, v in kern.items() if "at::native" in n)
     assert aten < 0.05 * tot, sorted(((v, n) for n, v in kern.items() if "at::native" in n), reverse=True)[:10]
+
+
+def test_optimizer_updates_batched():
+    """The ~220 per-parameter SGD-momentum updates of a step (v = mu v - lr (dW + wd W), W = W + v)
+    are horizontal Cell batches (codegen.batch_cells): a few launches instead of one per weight."""
+    from systemml_amd.compiler.blocks import BasicBlock
+    cs, _, _ = _compile()
+    assert cs.cp.rewrite_stats.get("cell-batched", 0) >= 200, cs.cp.rewrite_stats
+    seen, batches = set(), []
+
+    def rec(bl):
+        for b in bl:
+            if isinstance(b, BasicBlock):
+                st = list(b.roots) + list(b.env_out.values())
+                while st:
+                    h = st.pop()
+                    if h.id in seen:
+                        continue
+                    seen.add(h.id)
+                    if h.op == "hcell":
+                        batches.append(h.p["n"])
+                    st.extend(h.inputs)
+            else:
+                for a in ("body", "then_blocks", "else_blocks"):
+                    s = getattr(b, a, None)
+                    if isinstance(s, list):
+                        rec(s)
+    rec(cs.cp.blocks)
+    assert len(batches) <= 6 and max(batches) >= 100, batches
