@@ -113,8 +113,12 @@ def test_resnet_step_runs_no_library_gemm_or_library_conv():
     lib = [n for n in kern if any(s in n for s in _LIB_GEMM)]
     assert not lib, lib[:10]
     tot = sum(kern.values())
-    aten = sum(v for n, v in kern.items() if "at::native" in n)
-    assert aten < 0.05 * tot, sorted(((v, n) for n, v in kern.items() if "at::native" in n), reverse=True)[:10]
+    # the script's one-time weight initialisation (DML rand -> torch's generator kernels) is not
+    # part of a training step; everything else from ATen counts against the bound
+    aten_k = {n: v for n, v in kern.items() if "at::native" in n and "distribution_" not in n}
+    aten = sum(aten_k.values())
+    assert aten < 0.05 * tot, [(round(v), n[:90]) for v, n in sorted(((v, n) for n, v in aten_k.items()),
+                                                                       reverse=True)[:10]]
 
 
 def test_optimizer_updates_batched():
