@@ -851,9 +851,9 @@ CONV_BF16_FP32 = False     # fp32 convolutions on bf16 MFMA (fp32 accumulate) in
 # SYSML_CONV1X1_GEMM=0: the implicit-GEMM kernel of dnn.hip)
 CONV1X1_GEMM = os.environ.get("SYSML_CONV1X1_GEMM", "1") != "0"
 CONV3_DIRECT = os.environ.get("SYSML_CONV3_DIRECT", "1") != "0"   # 3x3 stride-1 layers on conv3.hip
-# 3x3 stride-1 filter gradient on wgrad.hip's patch kernel: off by default -- measured slower than
-# the implicit GEMM (tools/bench_conv_rn50.py, profiles/conv_rn50_b256_r5_wgrad3.txt: 122-239 TF, slower on 56x56;
-# its staging is not overlapped with the MFMAs)
+# 3x3 stride-1 filter gradient on wgrad.hip's patch kernel: off by default -- not faster than the
+# implicit GEMM overall (tools/bench_conv_rn50.py, profiles/conv_rn50_b256_r5_wgrad3.txt: 122-239 TF;
+# the 56x56 shapes, one output row per chunk, restage 3 input rows per 2 K steps)
 WGRAD3 = os.environ.get("SYSML_WGRAD3", "0") == "1"
 IM2COL_MAX_HW = int(os.environ.get("SYSML_IM2COL_MAX_HW", "196"))   # forward k x k convolutions via im2col + GEMM up to this Ho*Wo
 COL2IM_MAX_HW = int(os.environ.get("SYSML_COL2IM_MAX_HW", "196"))   # stride-1 backward data via GEMM + col2im up to this H*W (measured: faster at 14 x 14 and 7 x 7, slower at 28 x 28 and 56 x 56)
