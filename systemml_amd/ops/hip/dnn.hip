@@ -43,6 +43,7 @@ struct Conv {
   int ksplit, kper;  // BWD_FILTER split-K (kper: K elements per split, multiple of BK)
   int relu;          // FWD epilogue: max(0, .)
   int avec;          // FWD: filter rows 16-B aligned (vector loads of W)
+  void* slab;        // split-K partials (ksplit x M x Ncol, the output type) instead of atomics, or null
 };
 
 // bijective XCD-aware remap (dispatch is round-robin over the 8 XCDs)
@@ -354,7 +355,10 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
           CT v = (CT)acc[i][j][r];
           if constexpr (!OBF) {
             if (atomic) {
-              atomicAdd(out + out_index<MODE>(c, mo, no), v);
+              if (c.slab != nullptr)             // deterministic split-K: this split's slice
+                ((TO*)c.slab)[(int64_t)split * c.M * c.Ncol + (int64_t)mo * c.Ncol + no] = (TO)v;
+              else
+                atomicAdd(out + out_index<MODE>(c, mo, no), v);
               continue;
             }
           }
@@ -363,6 +367,16 @@ __global__ void __launch_bounds__(NT) conv_kernel(Conv c) {
           out[out_index<MODE>(c, mo, no)] = (TO)v;
         }
       }
+}
+
+// split-K slab of the backward filter: out[i] = sum_s slab[s, i] (fixed order, no atomics)
+template <typename T>
+__global__ void __launch_bounds__(256) slab_reduce(const T* __restrict__ slab, T* __restrict__ out, int64_t n, int S) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    T a = slab[i];
+    for (int q = 1; q < S; ++q) a += slab[(int64_t)q * n + i];
+    out[i] = a;
+  }
 }
 
 // ---- backward data for few input channels -------------------------------------------------
@@ -994,7 +1008,8 @@ int sysml_conv2d_tile_mode(int dtype, int mode, int64_t M, int64_t Nc) {
 // dtype: 0 bf16 in (fp32 out), 1 fp32 exact, 2 fp64 exact, 3 fp32 in / bf16 MFMA / fp32 out,
 // 4 bf16 in / bf16 out (forward and backward data, no split-K; fp32 bias).
 // mode: 0 forward, 1 backward data, 2 backward filter.  ksplit > 1 splits the GEMM depth over
-// blocks that accumulate atomically (ws unused).
+// blocks; the backward filter writes per-split slices into ws (ksplit x M x Ncol of the output
+// type, summed by one deterministic pass) when ws is given, else every split accumulates atomically.
 // Returns 0, -1 (unsupported) or a hipError_t.
 int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* D, const void* bias, void* out,
                  void* ws, int ksplit, int N, int C, int H, int Wd, int F, int KH, int KW, int sh, int sw, int ph,
@@ -1047,7 +1062,10 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
       return -1;
     return (int)hipGetLastError();
   }
-  if (ksplit > 1) {
+  // BWD_FILTER split-K: with a slab (ws, ksplit x M x Ncol of the output type) every split writes
+  // its own slice and one pass sums them in a fixed order; without one, atomics into zeroed out
+  c.slab = (mode == BWD_FILTER && ksplit > 1) ? ws : nullptr;
+  if (ksplit > 1 && c.slab == nullptr) {
     const int64_t n = M * Nc;
     if (hipMemsetAsync(out, 0, n * (dtype == 2 ? 8 : 4), s) != hipSuccess) return (int)hipGetLastError();
   }
@@ -1082,6 +1100,12 @@ int sysml_conv2d(int dtype, int mode, const void* X, const void* W, const void* 
     return -1;
   }
 #undef LAUNCH
+  if (c.slab != nullptr) {
+    const int64_t n = M * Nc;
+    const dim3 rg((unsigned)(n / 256 + 1 < 4096 ? n / 256 + 1 : 4096));
+    if (dtype == 2) hipLaunchKernelGGL(slab_reduce<double>, rg, dim3(256), 0, s, (const double*)ws, (double*)out, n, ksplit);
+    else hipLaunchKernelGGL(slab_reduce<float>, rg, dim3(256), 0, s, (const float*)ws, (float*)out, n, ksplit);
+  }
   if (ksplit > 1 && mode == FWD && (bias || relu)) {
     const int64_t n = M * Nc;
     const dim3 bg = bias_grid(n / P, (int)P);

@@ -855,6 +855,7 @@ CONV3_DIRECT = os.environ.get("SYSML_CONV3_DIRECT", "1") != "0"   # 3x3 stride-1
 # implicit GEMM overall (tools/bench_conv_rn50.py, profiles/conv_rn50_b256_r5_wgrad3.txt: 122-239 TF;
 # the 56x56 shapes, one output row per chunk, restage 3 input rows per 2 K steps)
 WGRAD3 = os.environ.get("SYSML_WGRAD3", "0") == "1"
+CONV_SLAB = os.environ.get("SYSML_CONV_SLAB", "1") != "0"   # backward-filter split-K into a slab, not atomics
 IM2COL_MAX_HW = int(os.environ.get("SYSML_IM2COL_MAX_HW", "196"))   # forward k x k convolutions via im2col + GEMM up to this Ho*Wo
 COL2IM_MAX_HW = int(os.environ.get("SYSML_COL2IM_MAX_HW", "196"))   # stride-1 backward data via GEMM + col2im up to this H*W (measured: faster at 14 x 14 and 7 x 7, slower at 28 x 28 and 56 x 56)
 CONV_SPLIT_BLOCKS = int(os.environ.get("SYSML_CONV_SPLIT_BLOCKS", "2048"))   # split K until ~this many blocks
@@ -1131,6 +1132,9 @@ def conv2d(mode, X, W, D, N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, bias=None, rel
         code, odt = 4, torch.bfloat16              # bf16 activations: the output is stored bf16
     out = torch.empty(shape, dtype=odt, device=dev)
     ws = None
+    if mode == 2 and ksplit > 1 and CONV_SLAB and ksplit * M * Nc * out.element_size() <= (256 << 20):
+        # deterministic split-K: per-split slices summed in a fixed order (no fp32 atomics)
+        ws = torch.empty((ksplit * M * Nc,), dtype=odt, device=dev)
     b = None if bias is None else bias.to(device=dev, dtype=bdt).contiguous().reshape(-1)
     rc = L.sysml_conv2d(code, mode, _ptr(X), _ptr(W), _ptr(D), _ptr(b), out.data_ptr(), _ptr(ws), ksplit,
                         N, C, H, Wd, F, KH, KW, sh, sw, ph, pw, int(bool(relu)), _stream())
