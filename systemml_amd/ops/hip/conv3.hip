@@ -11,7 +11,7 @@
 // Unlike the implicit GEMM of dnn.hip, which gathers every (pixel, tap, channel) operand element
 // from HBM with a bounds check (9 gathers per input element), a block here stages the input
 // PATCH its 128 output pixels need -- the padded rows they touch, all columns, 32 channels --
-// into LDS once per channel chunk, transposed to [position][channel] (80-B position pitch:
+// into LDS once per channel chunk, transposed to [position][channel] (96-B position pitch:
 // the 16 positions one MFMA fragment reads fall in distinct bank groups).  The nine taps are
 // then address offsets into that patch: each tap is one K=32 step whose B fragments are single
 // 16-B LDS reads, with no index math and no bounds checks in the MFMA loop.  The filter tile of
@@ -33,7 +33,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int NT = 256;      // 4 waves, 2 x 2 over the output tile
 constexpr int TN = 128;      // output pixels per tile
 constexpr int CB = 32;       // channels per chunk (one MFMA K step per tap)
-constexpr int CBP = 40;      // LDS pitch of a position / filter row, bf16 (80 B)
+constexpr int CBP = 48;      // LDS pitch of a position / filter row, bf16 (96 B: conflict-free for ds_read_b128's lane groups)
 constexpr int MAXIT = 8;     // patch items (position x 8 channels) per thread
 constexpr int MAXPOS = NT * MAXIT / (CB / 8);
 

@@ -17,7 +17,7 @@ namespace sysml_wg {
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int NT = 256, BK = 32, LDK = 40;   // LDS row pitch 80 B: conflict-free fragment reads
+constexpr int NT = 256, BK = 32, LDK = 48;   // LDS row pitch 96 B: conflict-free for ds_read_b128's lane groups
 
 struct WG {
   const uint16_t* A;
