@@ -110,6 +110,10 @@ def _pure(bb):
     for h in H.walk(list(bb.roots) + list(bb.env_out.values())):
         if h.op in ("sink", "fcall") or (h.op == "bi" and h.p.get("name") in (H.SIDE_EFFECT | H.NONDETERMINISTIC)):
             return False
+        # an update-in-place left index changes its target buffer before a later error would
+        # send execution to the original blocks, which then see the changed data
+        if h.op == "lix" and h.p.get("inplace"):
+            return False
     return True
 
 

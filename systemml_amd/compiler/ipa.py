@@ -299,6 +299,40 @@ def _is_ones(h):
     return d.op == "lit" and isinstance(d.value, (int, float)) and not isinstance(d.value, bool) and d.value == 1
 
 
+def _ones_shape(h):
+    """(rows, cols) hops of a matrix(1, rows=.., cols=..) datagen."""
+    named = dict(zip(h.named, h.inputs[len(h.inputs) - len(h.named):]))
+    return named.get("rows"), named.get("cols")
+
+
+def _broadcasts_into(ones, x):
+    """True if `x * ones` has x's shape: ones is x's shape, an x-length column or an x-width row
+    -- never an outer-vector product (n x 1 times 1 x k) or a ones matrix larger than x
+    (reference IPAPassRemoveConstantBinaryOps.java:139-143 skips isOuterVectorOperator).  Shapes
+    are matched structurally (rows=nrow(X) / cols=ncol(X) of the same variable, or 1), else by
+    known dimensions."""
+    r, c, xr, xc = ones.dim1, ones.dim2, x.dim1, x.dim2
+    if min(r, c, xr, xc) > 0:
+        return (r, c) in ((xr, xc), (xr, 1), (1, xc))
+    if x.op != "tread":
+        return False
+    rh, ch = _ones_shape(ones)
+
+    def fits(d, which):
+        if d is None:
+            return False
+        if d.op == "lit" and d.value == 1:
+            return True
+        return d.op == "u" and d.p.get("o") == which and d.inputs and d.inputs[0].op == "tread" \
+            and d.inputs[0].p.get("name") == x.p.get("name")
+    return fits(rh, "nrow") and fits(ch, "ncol")
+
+
+def _shape_vars(ones):
+    """Variables the ones matrix's shape expressions read (reassigning one invalidates it)."""
+    return {h.p["name"] for h in H.walk([i for i in _ones_shape(ones) if i is not None]) if h.op == "tread"}
+
+
 def remove_constant_binary_ops(cp, stats):
     """IPAPassRemoveConstantBinaryOps (reference hops/ipa/IPAPassRemoveConstantBinaryOps.java):
     a main-program variable assigned matrix(1, ...) in a basic block and not reassigned later
@@ -312,24 +346,27 @@ def remove_constant_binary_ops(cp, stats):
         for owner, roots in _block_dags(blocks):
             for h in H.walk(roots):
                 if h.op == "b" and h.p.get("o") == "*" and len(h.inputs) == 2:
-                    a, b = h.inputs
-                    for i, (x, y) in enumerate(((a, b), (b, a))):
-                        if y.op == "tread" and y.p.get("name") in ones and x.dt == "M":
-                            ins = list(h.inputs)
-                            ins[1 - i] = lit(1)
-                            h.inputs = ins
-                            n[0] += 1
-                            break
+                    # like the reference, only the RIGHT operand is replaced, and only when the
+                    # product keeps the left operand's shape: the ones matrix must broadcast INTO
+                    # X (same shape, X's column or X's row) -- never an outer-vector product
+                    # (n x 1 times 1 x k) or a ones matrix larger than X
+                    x, y = h.inputs
+                    if y.op == "tread" and y.p.get("name") in ones and x.dt == "M" \
+                            and _broadcasts_into(ones[y.p["name"]], x):
+                        h.inputs = [x, lit(1)]
+                        n[0] += 1
 
     for b in cp.blocks:
         upd = b.writes if isinstance(b, BasicBlock) else assigned_in([b])
         for v in upd:
             ones.pop(v, None)
+            for k in [k for k, o in ones.items() if v in _shape_vars(o)]:
+                ones.pop(k)
         if ones:
             rewrite([b])
         if isinstance(b, BasicBlock):
             for v, h in b.env_out.items():
-                if _is_ones(h):
+                if _is_ones(h) and not (_shape_vars(h) & set(b.writes)):
                     ones[v] = h
     if n[0]:
         stats["constant-binary-ops"] = n[0]

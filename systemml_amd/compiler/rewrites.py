@@ -919,8 +919,10 @@ class Rewriter:
         if not transA:
             # simplifyScalarMatrixMult (Dynamic.java:922): y %*% X -> as.scalar(y) * X and
             # X %*% y -> X * as.scalar(y) for a 1 x 1 y
-            for y, X in ((a, b), (b, a)):
-                if _one_by_one(y) and X.dt == "M":
+            # -- only when X's inner dimension is statically 1, so a mismatched product still
+            # raises instead of silently becoming a scaling
+            for y, X, inner in ((a, b, b.dim1), (b, a, a.dim2)):
+                if _one_by_one(y) and X.dt == "M" and inner == 1:
                     sc = Hop("u", [y], {"o": "cast_scalar"}, dt="S", dim1=0, dim2=0, pos=h.pos)
                     return self._hit("scalar-matrix-mult", Hop("b", [X, sc], {"o": "*"}, dt="M", dim1=X.dim1,
                                                                dim2=X.dim2, pos=h.pos))

@@ -27,3 +27,30 @@ def test_train_variants_match():
     res, _ = execute(cs, ins, out=lambda s: None)
     for a, b in zip(outs[::2], outs[1::2]):
         np.testing.assert_allclose(np.asarray(res[a]), np.asarray(res[b]), rtol=1e-12, atol=1e-12, err_msg=a)
+
+
+def test_train_constant_large_mean_channel_no_nan():
+    """A constant channel with a large mean and ema_mean = 0 (the first step): the shifted
+    moments cancel, and the variance is clamped at zero instead of going negative (NaN from
+    1/sqrt(v + eps))."""
+    import os
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.api.executor import compile_script, execute
+    src = """
+source("nn/layers/batch_norm2d.dml") as bn
+[o, em1, ev1, cm, cv, cn] = bn::forward(X, g, b, 2, 4, 4, "train", em, ev, 0.9, 1e-5)
+"""
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((8, 32))
+    X[:, :16] = 3.0e4 + 1e-3 * np.sin(np.arange(16))     # channel 0: nearly constant, mean 3e4
+    ins = {"X": X, "g": np.ones((2, 1)), "b": np.zeros((2, 1)), "em": np.zeros((2, 1)),
+           "ev": np.ones((2, 1))}
+    for prec in ("single", "double"):
+        cs = compile_script(src, {}, inputs=ins, outputs=["o", "cv", "ev1"],
+                            config=DMLConfig(gpu=False, precision=prec),
+                            filename=os.path.join(SCRIPTS_DIR, "bn_const_test.dml"))
+        res, _ = execute(cs, ins, out=lambda s: None)
+        cv = np.asarray(res["cv"], dtype=np.float64)
+        assert (cv >= 0).all(), (prec, cv)
+        assert np.isfinite(np.asarray(res["o"], dtype=np.float64)).all(), prec
+        assert np.isfinite(np.asarray(res["ev1"], dtype=np.float64)).all(), prec

@@ -61,6 +61,14 @@ def test_scalar_matrix_mult():
     _check("s = matrix(2, rows=1, cols=1)\nQ = s %*% C\nR = t(C) %*% s", {"C": C}, ["Q", "R"], "scalar-matrix-mult")
 
 
+def test_scalar_matrix_mult_keeps_dimension_check():
+    """A 1 x 1 times a matrix with more than one row is a dimension mismatch, not a scaling."""
+    from systemml_amd.parser.errors import DMLRuntimeError
+    with pytest.raises(Exception) as ei:
+        _run("s = matrix(2, rows=1, cols=1)\nQ = s %*% A\nprint(sum(Q))", {"A": A}, ["Q"])
+    assert "dim" in str(ei.value).lower() or isinstance(ei.value, DMLRuntimeError), ei.value
+
+
 def test_nnz():
     X = RNG.random((6, 5)) * (RNG.random((6, 5)) > 0.5)
     _check("n = sum(X != 0)\nprint(n)", {"X": X}, ["n"], "nnz")
@@ -232,6 +240,24 @@ def test_ipa_constant_binary_ops():
     assert cs.cp.ipa_stats.get("constant-binary-ops", 0) == 1, cs.cp.ipa_stats
     r, _ = EX.execute(cs, {"X": X}, out=lambda s: None)
     np.testing.assert_allclose(r["Z"].numpy(), X)
+
+
+@pytest.mark.parametrize("src,shape", [
+    # outer-vector product: n x 1 times a ones row is n x k, never v * 1
+    ("o = matrix(1, rows=1, cols=5)\nif (ncol(v) > 2) { print(\"x\") }\nZ = v * o\n", (6, 5)),
+    # ones on the left, larger than the vector: n x k, not n x 1
+    ("o = matrix(1, rows=nrow(v), cols=5)\nif (ncol(v) > 2) { print(\"x\") }\nZ = o * v\n", (6, 5)),
+    # a column vector times a larger ones matrix on the right
+    ("o = matrix(1, rows=nrow(v), cols=3)\nif (ncol(v) > 2) { print(\"x\") }\nZ = v * o\n", (6, 3)),
+])
+def test_ipa_constant_binary_ops_keeps_broadcast_shape(src, shape):
+    v = RNG.random((6, 1))
+    cs = EX.compile_script(src, {}, inputs={"v": v}, outputs=["Z"], config=DMLConfig(gpu=False))
+    assert cs.cp.ipa_stats.get("constant-binary-ops", 0) == 0, cs.cp.ipa_stats
+    r, _ = EX.execute(cs, {"v": v}, out=lambda s: None)
+    z = r["Z"].numpy()
+    assert z.shape == shape
+    np.testing.assert_allclose(z, np.broadcast_to(v, shape))
 
 
 def test_ipa_function_call_sizes():
