@@ -121,11 +121,51 @@ class MLResults:
     def getBoolean(self, name):
         return bool(self._values[name])
 
+    def getFrame(self, name):
+        """The output frame as a Frame (MLResults.java:486)."""
+        v = self._values[name]
+        if not isinstance(v, FrameBlock):
+            raise TypeError(f"output '{name}' is not a frame")
+        return Frame(v)
+
+    def getFrameAs2DStringArray(self, name):
+        from .jmlc import frame_to_strings
+        return frame_to_strings(self.getFrame(name).toFrameBlock())
+
+    def getMatrixAs2DDoubleArray(self, name):
+        return self.get(name).toNumPy()
+
+    def getDataFrame(self, name):
+        """The output matrix (or frame) as a pandas DataFrame (MLResults.java:287)."""
+        return self.get(name).toDF()
+
+    def getTuple(self, *names):
+        """The named outputs as one tuple, each converted like get() -- matrices as Matrix,
+        frames as Frame, scalars as Python values (MLResults.java:607-1990, Tuple1..Tuple22)."""
+        if not 1 <= len(names) <= 22:
+            raise ValueError("getTuple takes 1 to 22 output names")
+        return tuple(self._get1(n) for n in names)
+
+    def _get1(self, name):
+        if name not in self._values:
+            raise KeyError(f"Variable '{name}' not present")
+        v = self._values[name]
+        from ..runtime import scalars as S
+        if type(v) is S.DevScalar:
+            v = v.value()
+        return _wrap(v)
+
+    def getScript(self):
+        return getattr(self, "script", None)
+
     def keys(self):
         return list(self._values.keys())
 
     def __getitem__(self, name):
         return self.get(name)
+
+    def __repr__(self):
+        return "MLResults: " + ", ".join(f"{k} ({type(_wrap(v)).__name__})" for k, v in self._values.items())
 
 
 class Script:
@@ -301,9 +341,66 @@ class MLContext:
         self.last_stats = stats
         return MLResults(values, stats)
 
+    def setStatisticsMaxHeavyHitters(self, n):
+        """Number of heavy hitters in the statistics report (MLContext.java:622)."""
+        self.config.stats_count = int(n)
+        return self
+
+    def getStatisticsMaxHeavyHitters(self):
+        return self.config.stats_count
+
+    def isStatistics(self):
+        return self._stats
+
+    def isExplain(self):
+        return bool(self._explain)
+
+    def getExplainLevel(self):
+        return self._explain or None
+
+    def isGPU(self):
+        return bool(self.config.gpu)
+
+    def isForceGPU(self):
+        return bool(self.config.gpu)
+
+    def resetConfig(self):
+        """Back to the default configuration (MLContext.java:283)."""
+        self.config = get_default_config().copy()
+        return self
+
+    def info(self):
+        """Project information (MLContext.java:660 ProjectInfo): version, build and the
+        native libraries / device this context runs on."""
+        import torch as _t
+        from ..ops import kernels
+        d = {"Version": self.version(), "Main-Class": "systemml_amd", "Torch": _t.__version__,
+             "HIP": getattr(_t.version, "hip", None), "GPU": _t.cuda.is_available(),
+             "Native kernels": os.path.exists(kernels.LIB_PATH)}
+        if _t.cuda.is_available():
+            d["Device"] = _t.cuda.get_device_name(0)
+        return MLContextInfo(d)
+
+    def buildTime(self):
+        from ..ops import kernels
+        import time as _time
+        p = kernels.LIB_PATH
+        return _time.strftime("%Y-%m-%d %H:%M:%S", _time.localtime(os.path.getmtime(p))) if os.path.exists(p) \
+            else None
+
     def close(self):
         pass
 
     def version(self):
         from .. import __version__
         return __version__
+
+
+class MLContextInfo(dict):
+    """ProjectInfo of MLContext.info(): a dict with the reference's `property()` accessor."""
+
+    def property(self, key):
+        return self.get(key)
+
+    def __str__(self):
+        return "\n".join(f"{k}: {v}" for k, v in self.items())

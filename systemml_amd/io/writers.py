@@ -21,6 +21,8 @@ def _np(x):
         x = C._dist().gather(x)
     if isinstance(x, torch.Tensor):
         return x.detach().to("cpu").double().numpy()
+    if isinstance(x, np.ndarray) and x.ndim == 2:
+        return x.astype(np.float64, copy=False)
     raise DMLRuntimeError("write: expected a matrix")
 
 

@@ -198,3 +198,32 @@ def test_native_text_writers_match_java_formatting(tmp_path):
     i, j = np.nonzero(a)
     want = [f"{ii + 1} {jj + 1} {java_double_str(float(a[ii, jj]))}" for ii, jj in zip(i, j)]
     assert (tmp_path / "a.txt").read_text().splitlines() == want
+
+
+def test_mlresults_frame_tuple_and_context_accessors():
+    from systemml_amd.api.mlcontext import MLContext, Frame, Matrix, dml
+    ml = MLContext(config=CFG)
+    src = """
+    X = matrix("1 2 3 4", rows=2, cols=2)
+    F = as.frame(X)
+    s = sum(X)
+    name = "x"
+    """
+    r = ml.execute(dml(src).output("X", "F", "s", "name"))
+    f = r.getFrame("F")
+    assert isinstance(f, Frame) and f.shape == (2, 2)
+    assert r.getFrameAs2DStringArray("F") == [["1.0", "2.0"], ["3.0", "4.0"]]
+    X, F, s, name = r.getTuple("X", "F", "s", "name")
+    assert isinstance(X, Matrix) and isinstance(F, Frame) and s == 10.0 and name == "x"
+    np.testing.assert_array_equal(r.getMatrixAs2DDoubleArray("X"), [[1, 2], [3, 4]])
+    (only,) = r.getTuple("s")
+    assert only == 10.0
+    with pytest.raises(TypeError):
+        r.getFrame("X")
+    ml.setStatisticsMaxHeavyHitters(7)
+    assert ml.getStatisticsMaxHeavyHitters() == 7
+    ml.resetConfig()
+    assert ml.getStatisticsMaxHeavyHitters() == MLContext().getStatisticsMaxHeavyHitters()
+    info = ml.info()
+    assert info.property("Version") == ml.version()
+    assert not ml.isStatistics() and not ml.isExplain()
