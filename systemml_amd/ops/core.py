@@ -44,10 +44,29 @@ def cvt_sp(x):
 
 
 def cvt(x: Tensor) -> Tensor:
-    """bf16 storage → compute dtype (materialises; kernels avoid this)."""
+    """bf16 storage → compute dtype (materialises; kernels avoid this).  Device matrices widen
+    in one pass of reorg.hip's copy2d (any row pitch), not an ATen cast."""
     if x.dtype == torch.bfloat16:
+        if x.is_cuda and backend.use_kernels and x.dim() == 2:
+            from . import kernels
+            r = kernels.copy2d(x, backend.dtype)
+            if r is not None:
+                return r
         return x.to(backend.dtype)
     return x
+
+
+def dense_copy(x: Tensor) -> Tensor:
+    """A dense row-major copy of a device view (slice windows, strided rows) on reorg.hip; the
+    tensor itself when it is already contiguous."""
+    if x.is_contiguous():
+        return x
+    if x.is_cuda and backend.use_kernels and x.dim() == 2:
+        from . import kernels
+        r = kernels.copy2d(x)
+        if r is not None:
+            return r
+    return x.contiguous()
 
 
 def _num(v):
@@ -838,6 +857,12 @@ def transpose(x):
     x = _need_mat(x, "t")
     if SP.is_sparse(x):
         return SP.transpose(x)
+    if x.is_cuda and backend.use_kernels:
+        # LDS-tiled transpose of the stored cells (bf16 stays bf16: the consumers widen it)
+        from . import kernels
+        r = kernels.transpose(x)
+        if r is not None:
+            return r
     return cvt(x).t().contiguous()
 
 
@@ -877,6 +902,19 @@ def rix(x, rl, ru, cl, cu, list_mode=False):
     r0, r1 = _bound(rl, 1), _bound(ru, nr)
     c0, c1 = _bound(cl, 1), _bound(cu, nc)
     _check_range(r0, r1, c0, c1, nr, nc)
+    if x.is_cuda and backend.use_kernels:
+        from . import kernels
+        if SP.is_sparse(x) and x.layout == torch.sparse_csr:
+            # slice_sparse_dense_row (SystemML.cu:301): the window of a CSR matrix as dense cells
+            r = kernels.slice_csr(x, r0 - 1, r1, c0 - 1, c1)
+            if r is not None:
+                return r
+        elif x.layout is _STRIDED and (c1 - c0 + 1 != nc or (r0, r1) == (1, nr)):
+            # a column window (or the whole matrix) is one dense copy on reorg.hip; a full-width
+            # row range stays a zero-copy view of contiguous rows
+            r = kernels.copy2d(x[r0 - 1:r1, c0 - 1:c1])
+            if r is not None:
+                return r
     out = x[r0 - 1:r1, c0 - 1:c1]
     return out.clone() if out.data_ptr() == x.data_ptr() and out.shape == x.shape else out
 

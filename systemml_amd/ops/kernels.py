@@ -193,6 +193,25 @@ def load(required=False):
     L.sysml_cumagg.restype = ctypes.c_int
     L.sysml_cumagg.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+    I64, VP, CI = ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
+    L.sysml_copy2d.restype = CI
+    L.sysml_copy2d.argtypes = [CI, CI, VP, I64, VP, I64, I64, I64, VP]
+    L.sysml_transpose.restype = CI
+    L.sysml_transpose.argtypes = [CI, VP, I64, VP, I64, I64, VP]
+    L.sysml_tri.restype = CI
+    L.sysml_tri.argtypes = [CI, VP, VP, I64, I64, CI, CI, CI, VP]
+    L.sysml_gather_rows.restype = CI
+    L.sysml_gather_rows.argtypes = [CI, CI, VP, I64, VP, VP, I64, I64, VP]
+    L.sysml_slice_csr.restype = CI
+    L.sysml_slice_csr.argtypes = [CI, CI, VP, VP, VP, VP, I64, I64, I64, I64, VP]
+    L.sysml_sort_keys_prep.restype = CI
+    L.sysml_sort_keys_prep.argtypes = [CI, VP, I64, I64, VP, VP, VP, I64, VP]
+    L.sysml_sort_pairs_scratch.restype = I64
+    L.sysml_sort_pairs_scratch.argtypes = [I64]
+    L.sysml_sort_pairs.restype = CI
+    L.sysml_sort_pairs.argtypes = [VP, VP, VP, VP, I64, CI, VP, I64, VP]
+    L.sysml_perm_compose.restype = CI
+    L.sysml_perm_compose.argtypes = [VP, VP, VP, VP, CI, I64, VP]
     _lib = L
     return L
 
@@ -1609,3 +1628,207 @@ def spmm(A, B, transA=False):
         raise RuntimeError(f"sysml_spmm failed: {rc}")
     _count("spmm_t" if transA else "spmm")
     return C
+
+
+# ----------------------------------------------------------------------------
+# right indexing / transpose / tri / row gathers / sort (ops/hip/reorg.hip, ops/hip/sort.hip)
+# ----------------------------------------------------------------------------
+_TCODE = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2}
+
+
+def _rowpitch(x):
+    """Row pitch of a 2-D view whose rows are unit-stride (a slice of a row-major matrix), else
+    None."""
+    if x.dim() != 2 or x.layout != torch.strided:
+        return None
+    r, c = x.shape
+    if c == 1 or x.stride(1) == 1:
+        ld = x.stride(0) if r > 1 else c
+        return ld if ld >= c else None
+    return None
+
+
+def copy2d(x, dtype=None):
+    """Dense row-major copy of a 2-D device view x (a right-indexing window, any row pitch),
+    converted to `dtype` in the same pass; None when not covered (not a row-major view)."""
+    dtype = dtype or x.dtype
+    if not x.is_cuda or x.dtype not in _TCODE or dtype not in _TCODE:
+        return None
+    ld = _rowpitch(x)
+    if ld is None:
+        return None
+    L = load(required=True)
+    nr, nc = x.shape
+    out = torch.empty((nr, nc), dtype=dtype, device=x.device)
+    if out.numel() == 0:
+        return out
+    rc = L.sysml_copy2d(_TCODE[x.dtype], _TCODE[dtype], x.data_ptr(), ld, out.data_ptr(), nc, nr, nc, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_copy2d failed: {rc}")
+    _count("slice" if dtype == x.dtype else "cast")
+    return out
+
+
+def transpose(x):
+    """t(x) of a 2-D device matrix (row-major, any row pitch) as a dense matrix (LDS-tiled);
+    None when not covered."""
+    if not x.is_cuda or x.dtype not in _ESIZE:
+        return None
+    ld = _rowpitch(x)
+    if ld is None:
+        return None
+    L = load(required=True)
+    N, D = x.shape
+    out = torch.empty((D, N), dtype=x.dtype, device=x.device)
+    if out.numel() == 0:
+        return out
+    rc = L.sysml_transpose(_ESIZE[x.dtype], x.data_ptr(), ld, out.data_ptr(), N, D, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_transpose failed: {rc}")
+    _count("transpose")
+    return out
+
+
+def tri(x, lower, diag, values):
+    """lower.tri / upper.tri of a dense device matrix in one pass; None when not covered."""
+    if not x.is_cuda or x.dtype not in _ESIZE or x.dim() != 2 or x.layout != torch.strided:
+        return None
+    L = load(required=True)
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    if x.numel():
+        rc = L.sysml_tri(_ESIZE[x.dtype], x.data_ptr(), out.data_ptr(), x.shape[0], x.shape[1], int(bool(lower)),
+                         int(bool(diag)), int(bool(values)), _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_tri failed: {rc}")
+    _count("tri")
+    return out
+
+
+def gather_rows(x, idx):
+    """x[idx, ] for a 0-based int32 / int64 device index vector; None when not covered."""
+    if not x.is_cuda or x.dtype not in _ESIZE or idx.dtype not in (torch.int32, torch.int64) or not idx.is_cuda:
+        return None
+    ld = _rowpitch(x)
+    if ld is None:
+        return None
+    L = load(required=True)
+    idx = idx.reshape(-1).contiguous()
+    n, D = idx.numel(), x.shape[1]
+    out = torch.empty((n, D), dtype=x.dtype, device=x.device)
+    if out.numel():
+        rc = L.sysml_gather_rows(_ESIZE[x.dtype], int(idx.dtype == torch.int64), x.data_ptr(), ld, idx.data_ptr(),
+                                 out.data_ptr(), n, D, _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_gather_rows failed: {rc}")
+    _count("gather_rows")
+    return out
+
+
+def slice_csr(x, r0, r1, c0, c1):
+    """Dense window x[r0:r1, c0:c1] (0-based, half-open) of a device CSR matrix; None when not
+    covered."""
+    if not x.is_cuda or x.layout != torch.sparse_csr or x.dtype not in (torch.float32, torch.float64):
+        return None
+    L = load(required=True)
+    crow, col, val = x.crow_indices(), x.col_indices(), x.values()
+    if crow.dtype != col.dtype or crow.dtype not in (torch.int32, torch.int64):
+        return None
+    out = torch.zeros((r1 - r0, c1 - c0), dtype=x.dtype, device=x.device)
+    if out.numel() and val.numel():
+        rc = L.sysml_slice_csr(_TCODE[x.dtype], int(crow.dtype == torch.int64), crow.data_ptr(), col.data_ptr(),
+                               val.contiguous().data_ptr(), out.data_ptr(), r0, r1, c0, c1, _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_slice_csr failed: {rc}")
+    _count("slice_csr")
+    return out
+
+
+_sort_scratch = {}
+
+
+def _scratch(n, dev):
+    key = (dev, n)
+    b = _sort_scratch.get(key)
+    if b is None:
+        L = load(required=True)
+        nb = L.sysml_sort_pairs_scratch(n)
+        if nb < 0:
+            raise RuntimeError("sysml_sort_pairs_scratch failed")
+        b = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
+        if len(_sort_scratch) > 8:
+            _sort_scratch.clear()
+        _sort_scratch[key] = b
+    return b
+
+
+def order_perm(x, cols, decreasing):
+    """0-based int32 row permutation that sorts the rows of device matrix x by the 1-based key
+    columns `cols` (first most significant), stable, on the device: one radix pair sort per key
+    from the last to the first.  None when not covered."""
+    if not x.is_cuda or x.dtype not in _TCODE or x.shape[0] >= (1 << 31):
+        return None
+    ld = _rowpitch(x)
+    if ld is None:
+        return None
+    L = load(required=True)
+    n = x.shape[0]
+    dev = x.device
+    keys = torch.empty((n,), dtype=torch.float64, device=dev)
+    kout = torch.empty_like(keys)
+    perm = None
+    tmp = torch.empty((n,), dtype=torch.int32, device=dev)
+    vout = torch.empty((n,), dtype=torch.int32, device=dev)
+    scr = _scratch(n, dev)
+    for k in reversed(list(cols)):
+        # keys of the current order and positions 0..n-1 in it (remapped through perm after the sort)
+        rc = L.sysml_sort_keys_prep(_TCODE[x.dtype], x.data_ptr(), ld, int(k) - 1,
+                                    perm.data_ptr() if perm is not None else None, keys.data_ptr(),
+                                    tmp.data_ptr(), n, _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_sort_keys_prep failed: {rc}")
+        rc = L.sysml_sort_pairs(keys.data_ptr(), kout.data_ptr(), tmp.data_ptr(), vout.data_ptr(), n,
+                                int(bool(decreasing)), scr.data_ptr(), scr.numel(), _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_sort_pairs failed: {rc}")
+        if perm is None:
+            perm, vout = vout, torch.empty((n,), dtype=torch.int32, device=dev)
+        else:
+            newp = torch.empty((n,), dtype=torch.int32, device=dev)
+            rc = L.sysml_perm_compose(vout.data_ptr(), perm.data_ptr(), newp.data_ptr(), None, 0, n, _stream())
+            if rc != 0:
+                raise RuntimeError(f"sysml_perm_compose failed: {rc}")
+            perm = newp
+    _count("order")
+    return perm
+
+
+def perm_index(perm, dtype):
+    """(perm + 1) as an n x 1 matrix of `dtype` (order(..., index.return=TRUE))."""
+    L = load(required=True)
+    n = perm.numel()
+    out = torch.empty((n, 1), dtype=dtype, device=perm.device)
+    if n:
+        rc = L.sysml_perm_compose(perm.data_ptr(), None, None, out.data_ptr(), _TCODE[dtype], n, _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_perm_compose failed: {rc}")
+    return out
+
+
+def sort_values(v):
+    """Ascending sort of a device vector's values (quantile / median): (sorted fp64 values,
+    0-based int32 permutation)."""
+    x = v.reshape(-1, 1)
+    if not x.is_contiguous():
+        x = x.contiguous()
+    perm = order_perm(x, [1], False)
+    if perm is None:
+        return None
+    L = load(required=True)
+    n = x.shape[0]
+    vals = torch.empty((n,), dtype=torch.float64, device=x.device)
+    rc = L.sysml_sort_keys_prep(_TCODE[x.dtype], x.data_ptr(), 1, 0, perm.data_ptr(), vals.data_ptr(), None, n,
+                                _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_sort_keys_prep failed: {rc}")
+    return vals, perm

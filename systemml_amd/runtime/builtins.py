@@ -487,9 +487,20 @@ def b_diag(ctx, x):
     raise DMLRuntimeError("diag requires a square matrix or a column vector")
 
 
+def _tri_kernel(m, lower, diag, values):
+    """lower.tri / upper.tri of a device matrix in one pass (reorg.hip; SystemML.cu:425-429)."""
+    if isinstance(m, Tensor) and m.is_cuda and backend.use_kernels and m.layout == torch.strided:
+        from ..ops import kernels
+        return kernels.tri(m, lower, diag, values)
+    return None
+
+
 @builtin("lower.tri")
 def b_lower_tri(ctx, target=None, diag=False, values=False):
     m = _mat(target)
+    r = _tri_kernel(m, True, _bool(diag), _bool(values))
+    if r is not None:
+        return r
     k = 0 if _bool(diag) else -1
     out = torch.tril(m, diagonal=k)
     if not _bool(values):
@@ -500,6 +511,9 @@ def b_lower_tri(ctx, target=None, diag=False, values=False):
 @builtin("upper.tri")
 def b_upper_tri(ctx, target=None, diag=False, values=False):
     m = _mat(target)
+    r = _tri_kernel(m, False, _bool(diag), _bool(values))
+    if r is not None:
+        return r
     k = 0 if _bool(diag) else 1
     out = torch.triu(m, diagonal=k)
     if not _bool(values):
@@ -512,6 +526,20 @@ def b_order(ctx, target=None, by=1, decreasing=False, **kw):
     m = _mat(target)
     idx_ret = _bool(kw.get("index.return", False))
     dec = _bool(decreasing)
+    keys = [int(v) for v in by.reshape(-1).tolist()] if isinstance(by, Tensor) else [_int(by)]
+    for k in keys:
+        if k < 1 or k > m.shape[1]:
+            raise DMLRuntimeError(f"order: by column {k} out of range [1, {m.shape[1]}]")
+    if isinstance(m, Tensor) and m.is_cuda and backend.use_kernels and m.layout == torch.strided:
+        # device radix sort (sort.hip): stable key passes, then one row gather / index output
+        from ..ops import kernels
+        perm = kernels.order_perm(m, keys, dec)
+        if perm is not None:
+            if idx_ret:
+                return kernels.perm_index(perm, m.dtype if m.dtype != torch.bfloat16 else backend.dtype)
+            r = kernels.gather_rows(m, perm)
+            if r is not None:
+                return r
     if isinstance(by, Tensor) and by.numel() > 1:
         # several key columns (a column vector of indices): lexicographic, first column major --
         # stable sorts from the last key to the first
@@ -833,7 +861,19 @@ def b_cov(ctx, x, y, w=None):
 
 
 def _sorted_weighted(x, w):
-    v = _mat(x).reshape(-1)
+    m = _mat(x)
+    if isinstance(m, Tensor) and m.is_cuda and backend.use_kernels and m.layout == torch.strided:
+        from ..ops import kernels
+        r = kernels.sort_values(m)
+        if r is not None:
+            vals, perm = r
+            if w is None:
+                return vals, None
+            wm = _mat(w).reshape(-1, 1)
+            wg = kernels.gather_rows(wm.contiguous(), perm) if wm.is_cuda else None
+            if wg is not None:
+                return vals, C.cvt(wg).reshape(-1).to(vals.dtype)
+    v = m.reshape(-1)
     if w is None:
         return torch.sort(v).values, None
     wv = _mat(w).reshape(-1).to(v.dtype)
