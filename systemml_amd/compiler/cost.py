@@ -223,6 +223,8 @@ def _infer_bi(h, ins, dims=None):
         return (_int_or(_lv(h.inputs[1])), _int_or(_lv(h.inputs[2])))
     if name == "outer":
         return (ins[0][0], ins[1][1])
+    if name == "_seq_expand":
+        return (ins[0][0], _int_or(_lv(h.inputs[1])))
     return UNK
 
 

@@ -102,6 +102,65 @@ def _vec_kind(h):
     return None
 
 
+def _equal_size(A, B):
+    """dims(A) == dims(B): the same hop, or both sizes known and equal (HopRewriteUtils
+    .isEqualSize)."""
+    if A is B:
+        return True
+    return min(A.dim1, A.dim2, B.dim1, B.dim2) > 0 and (A.dim1, A.dim2) == (B.dim1, B.dim2)
+
+
+def _smaller(h, x):
+    """Known sizes with cells(h) < cells(x) (HopRewriteUtils.compareSize < 0)."""
+    return min(h.dim1, h.dim2, x.dim1, x.dim2) > 0 and h.dim1 * h.dim2 < x.dim1 * x.dim2
+
+
+def _seq_args(h):
+    if h.op != "bi" or h.p.get("name") != "seq" or h.named:
+        return None
+    a = h.inputs[:h.p.get("npos", len(h.inputs))]
+    return a if len(a) in (2, 3) else None
+
+
+def _basic_1n_seq(h):
+    """n when h is seq(1, n[, 1]) (HopRewriteUtils.isBasic1NSequence), else None."""
+    a = _seq_args(h)
+    if a is None or not _is_lit(a[0], 1) or (len(a) == 3 and not _is_lit(a[2], 1)):
+        return None
+    return a[1]
+
+
+def _basic_n1_seq(h):
+    """n when h is seq(n, 1, -1) (isBasicN1Sequence), else None."""
+    a = _seq_args(h)
+    if a is None or len(a) != 3 or not _is_lit(a[1], 1) or not _is_lit(a[2], -1):
+        return None
+    return a[0]
+
+
+def _same_hop_value(a, b):
+    """a and b denote the same scalar: one hop, equal literals, or nrow/ncol of one hop."""
+    if a is b:
+        return True
+    if _num_lit(a) and _num_lit(b):
+        return a.value == b.value
+    return a.op == "u" and b.op == "u" and a.p.get("o") == b.p.get("o") and a.p.get("o") in ("nrow", "ncol") \
+        and a.inputs[0] is b.inputs[0]
+
+
+def _const_datagen_value(h):
+    """The scalar of a constant datagen matrix(c, rows, cols) / rand(min=c, max=c), else None
+    (HopRewriteUtils.isDataGenOpWithConstantValue)."""
+    if h.op != "bi":
+        return None
+    if h.p.get("name") == "matrix":
+        args = _bi_args(h)
+        d = args.get("data")
+        if d is not None and d.dt == "S" and d.op == "lit" and _num_lit(d):
+            return d
+    return None
+
+
 def _one_by_one(h):
     """h is a 1 x 1 matrix by construction: matrix(x, rows=1, cols=1) or as.matrix(scalar).
     (Propagated hop dimensions are not trusted for rewrites that change the operator: a
@@ -257,6 +316,9 @@ class Rewriter:
         if m is not h:
             return m
         m = self._rw_more(h)
+        if m is not h:
+            return m
+        m = self._rw_extra(h)
         if m is not h:
             return m
         op = h.op
@@ -620,6 +682,112 @@ class Rewriter:
             return h
         return h
 
+    def _rw_extra(self, h):
+        """The remaining algebraic rules of RewriteAlgebraicSimplification{Static,Dynamic}.java
+        (line numbers in each comment)."""
+        op = h.op
+        sole = not any(c.id in self.multi for c in h.inputs if c.op not in ("lit", "tread"))
+        if op == "agg" and len(h.inputs) == 1 and h.p["o"] == "sum" and h.p["dir"] == "all":
+            x = h.inputs[0]
+            # pushdownSumOnAdditiveBinary (Dynamic:1151): sum(A+B) -> sum(A)+sum(B), sum(A-B) ->
+            # sum(A)-sum(B) for equal-size matrices (lets sum(X^2) / tak+* rules see each term)
+            if sole and x.op == "b" and x.p["o"] in ("+", "-") and x.dt == "M":
+                A, B = x.inputs
+                if A.dt == "M" and B.dt == "M" and _equal_size(A, B):
+                    s1 = Hop("agg", [A], {"o": "sum", "dir": "all"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                    s2 = Hop("agg", [B], {"o": "sum", "dir": "all"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                    return self._hit("pushdown-sum-additive",
+                                     Hop("b", [s1, s2], {"o": x.p["o"]}, dt="S", dim1=0, dim2=0, pos=h.pos))
+        if op == "mm" and not h.p.get("transA") and len(h.inputs) == 2:
+            a, b = h.inputs
+            # reorderMinusMatrixMult (Dynamic:2313): (0-A) %*% B -> 0-(A %*% B) (and the right
+            # form) when the product is smaller than A -- the negation runs on the product
+            for i, m in enumerate((a, b)):
+                if m.op == "b" and m.p.get("o") == "-" and _is_lit(m.inputs[0], 0) and m.inputs[1].dt == "M" \
+                        and sole and _smaller(h, m.inputs[1]):
+                    ins = [a, b]
+                    ins[i] = m.inputs[1]
+                    prod = Hop("mm", ins, dict(h.p), dt="M", dim1=h.dim1, dim2=h.dim2, pos=h.pos)
+                    return self._hit("reorder-minus-mm", Hop("b", [lit(0), prod], {"o": "-"}, dt="M", dim1=h.dim1,
+                                                            dim2=h.dim2, pos=h.pos))
+            # simplifyReverseOperation (Static:700): table(seq(1,n), seq(n,1,-1)) %*% X -> rev(X)
+            if a.op == "bi" and a.p.get("name") in ("table", "ctable") and not a.named and len(a.inputs) == 2:
+                n1 = _basic_1n_seq(a.inputs[0])
+                n2 = _basic_n1_seq(a.inputs[1])
+                if n1 is not None and n2 is not None and _same_hop_value(n1, n2):
+                    return self._hit("reverse-operation", Hop("bi", [b], {"name": "rev", "npos": 1}, dt="M",
+                                                             dim1=b.dim1, dim2=b.dim2, pos=h.pos))
+            # (the same table after the seq-ctable rewrite: the one-hot of seq(n, 1, -1), n x n)
+            if a.op == "bi" and a.p.get("name") == "_onehot" and _is_lit(a.inputs[1], -1) \
+                    and _is_lit(a.inputs[2], -1) and _basic_n1_seq(a.inputs[0]) is not None:
+                return self._hit("reverse-operation", Hop("bi", [b], {"name": "rev", "npos": 1}, dt="M",
+                                                         dim1=b.dim1, dim2=b.dim2, pos=h.pos))
+        if op == "b" and len(h.inputs) == 2 and h.dt == "M":
+            l, r = h.inputs
+            o = h.p["o"]
+            # canonicalizeMatrixMultScalarAdd (Static:640): eps + U%*%V -> U%*%V + eps and
+            # U%*%V - eps -> U%*%V + (-eps) (one form for the wdivmm / wcemm epsilon matchers)
+            if o == "+" and l.dt == "S" and r.op in ("mm", "tsmm"):
+                return self._hit("canonical-mm-scalar-add", Hop("b", [r, l], {"o": "+"}, dt="M", dim1=h.dim1,
+                                                               dim2=h.dim2, pos=h.pos))
+            if o == "-" and r.dt == "S" and l.op in ("mm", "tsmm"):
+                neg = lit(-r.value) if _num_lit(r) else Hop("u", [r], {"o": "neg"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                return self._hit("canonical-mm-scalar-add", Hop("b", [l, neg], {"o": "+"}, dt="M", dim1=h.dim1,
+                                                               dim2=h.dim2, pos=h.pos))
+        if op == "bi":
+            name = h.p.get("name")
+            # removeUnnecessaryIfElseOperation (Dynamic:444)
+            if name == "ifelse" and len(h.inputs) == 3 and not h.named:
+                e, A, B = h.inputs
+                if e.op == "lit" and isinstance(e.value, (bool, int, float)) and A.dt == B.dt:
+                    pick = A if bool(e.value) else B
+                    if A.dt == "S" or (A.dt == "M" and _equal_size(A, B)):
+                        return self._hit("ifelse-removal", pick)
+                if A is B and e.dt == "S" and A.dt == "M":
+                    return self._hit("ifelse-removal", A)
+            # simplifyCTableWithConstMatrixInputs (Static:672): table(X, matrix(1,..), matrix(7,..))
+            # -> table(X, 1, 7) (no constant vectors materialised)
+            if name in ("table", "ctable") and not h.named and len(h.inputs) in (2, 3, 4, 5):
+                ins = list(h.inputs)
+                changed = False
+                for i in range(1, min(3, len(ins))):
+                    c = _const_datagen_value(ins[i])
+                    if c is not None:
+                        ins[i] = c
+                        changed = True
+                if changed and ins[0].dt == "M":
+                    return self._hit("ctable-const-inputs", Hop("bi", ins, dict(h.p), [], dt="M", pos=h.pos))
+                # simplifyTableSeqExpand pattern b (Dynamic:2531): table(v, seq(1,nrow(v)), m, nrow(v))
+                # -> t(one-hot of v) (pattern a is the seq-ctable rewrite)
+                if len(ins) == 4 and h.inputs[0].dt == "M":
+                    n = _basic_1n_seq(h.inputs[1])
+                    if n is not None and _same_hop_value(n, h.inputs[3]):
+                        oh = Hop("bi", [h.inputs[0], lit(-1), h.inputs[2]], {"name": "_onehot", "npos": 3}, dt="M",
+                                 pos=h.pos)
+                        return self._hit("table-seq-expand", Hop("t", [oh], {}, dt="M", pos=h.pos))
+            # simplifyGroupedAggregate (Static:1641): aggregate(target=v, groups=g, fn="count")
+            # counts group members: target := groups (v is never read)
+            if name == "aggregate" and h.named:
+                args = dict(zip(h.named, h.inputs[len(h.inputs) - len(h.named):]))
+                fn = args.get("fn")
+                tgt, grp = args.get("target"), args.get("groups")
+                if fn is not None and fn.op == "lit" and fn.value == "count" and tgt is not None \
+                        and grp is not None and tgt is not grp and (_vec_kind(tgt) == "col" or tgt.dim2 == 1):
+                    ins = list(h.inputs)
+                    ins[len(h.inputs) - len(h.named) + h.named.index("target")] = args["groups"]
+                    return self._hit("grouped-aggregate-count", Hop("bi", ins, dict(h.p), list(h.named), dt="M",
+                                                                   pos=h.pos))
+            # simplifyOuterSeqExpand (Static:1766): outer(v, t(seq(1,m)), "==") -> the exact-match
+            # expansion of v into m indicator columns (no outer operator over a sequence)
+            if name == "outer" and len(h.inputs) == 3 and h.inputs[2].op == "lit" and h.inputs[2].value == "==":
+                v, w = h.inputs[0], h.inputs[1]
+                if w.op == "t":
+                    m = _basic_1n_seq(w.inputs[0])
+                    if m is not None and v.dt == "M":
+                        return self._hit("outer-seq-expand", Hop("bi", [v, m], {"name": "_seq_expand", "npos": 2},
+                                                                dt="M", pos=h.pos))
+        return h
+
     def _rw_order(self, h):
         """simplifyConstantSort (Static:1383): order of a constant matrix is the matrix (its
         index is 1..n); simplifyOrderedSort (Static:1421): order of an ascending seq is the seq
@@ -901,6 +1069,10 @@ class Rewriter:
                 return q
         if o == "sum":
             if x.op == "b" and x.p["o"] == "^" and _is_lit(x.inputs[1], 2) and x.inputs[0].dt != "S":
+                if d == "all" and (_col_vector(x.inputs[0]) or x.inputs[0].dim2 == 1):
+                    # simplifyDotProductSum (Dynamic:2075): sum(v^2) is the dot product v'v -- here
+                    # the fused sum of squares, which reads v once and needs no transpose
+                    self._count("dot-product-sum")
                 self._count("sumsq")
                 return Hop("agg", [x.inputs[0]], {"o": "sumsq", "dir": d}, dt=h.dt, pos=h.pos)
             if d == "all" and x.op == "b" and x.p["o"] == "*" and x.inputs[0].dt == "M" and x.inputs[1].dt == "M":
@@ -926,6 +1098,16 @@ class Rewriter:
                     sc = Hop("u", [y], {"o": "cast_scalar"}, dt="S", dim1=0, dim2=0, pos=h.pos)
                     return self._hit("scalar-matrix-mult", Hop("b", [X, sc], {"o": "*"}, dt="M", dim1=X.dim1,
                                                                dim2=X.dim2, pos=h.pos))
+            # (X ^ 2) %*% v -> rowSums(X ^ 2 * t(v)) for a column vector v (the rowSums_X_sq
+            # idiom of MultiLogReg / GLM with icpt=2): a row aggregate the Cell template fuses
+            # with the square, so X ^ 2 is never materialised (a 10M x 1K fp32 X ^ 2 costs more
+            # than the two fused passes over X together)
+            if a.op == "b" and a.p.get("o") == "^" and _is_lit(a.inputs[1], 2) and a.inputs[0].dt == "M" \
+                    and b.dt == "M" and (_col_vector(b) or (b.dim2 == 1 and b.dim1 > 1)):
+                tv = Hop("t", [b], {}, dt="M", dim1=1, dim2=b.dim1, pos=h.pos)
+                prod = Hop("b", [a, tv], {"o": "*"}, dt="M", dim1=a.dim1, dim2=a.dim2, pos=h.pos)
+                return self._hit("square-matrix-mult", Hop("agg", [prod], {"o": "sum", "dir": "row"}, dt="M",
+                                                          dim1=a.dim1, dim2=1, pos=h.pos))
             # simplifyMatrixMultDiag (Dynamic.java:960): diag(v) %*% Y -> v * Y for a column
             # vector v (a row scaling instead of an n x n diagonal matrix and a product)
             if _is_diag(a) and _col_vector(a.inputs[0]) and b.dt == "M":

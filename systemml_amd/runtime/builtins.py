@@ -775,6 +775,17 @@ def b_table(ctx, A=None, B=None, W=None, odim1=None, odim2=None, *rest, **kw):
     return _ctable(a, b, wv, dims)
 
 
+@builtin("_seq_expand")
+def b_seq_expand(ctx, v, m):
+    """outer(v, t(seq(1, m)), "==") without the sequence (rewrites.py simplifyOuterSeqExpand,
+    reference rexpand with ignore=TRUE, cast=FALSE): cell (i, j) is 1 where v[i] == j exactly;
+    values outside 1..m or not integral give a zero row."""
+    yv = _mat(v).reshape(-1)
+    k = _int(m)
+    cols = torch.arange(1, k + 1, dtype=yv.dtype, device=yv.device)
+    return (yv.reshape(-1, 1) == cols.reshape(1, -1)).to(_dt())
+
+
 @builtin("_onehot")
 def b_onehot(ctx, y, n=None, k=None):
     """table(seq(1, N), y [, N, K]) without materialising seq (rewrites.py _match_onehot):

@@ -69,6 +69,33 @@ def test_scalar_matrix_mult_keeps_dimension_check():
     assert "dim" in str(ei.value).lower() or isinstance(ei.value, DMLRuntimeError), ei.value
 
 
+def test_square_matrix_mult():
+    _check("v = t(colSums(A ^ 2))\nv[1, 1] = 2\nr = (A ^ 2) %*% (v ^ 2) + A %*% v\n", {"A": A}, ["r"],
+           "square-matrix-mult")
+
+
+V = np.floor(RNG.random((12, 1)) * 5) + 1
+M2 = RNG.random((12, 3))
+
+
+@pytest.mark.parametrize("src,outs,rule", [
+    ("s = sum(A + A * 2)\nt = sum(A - B[, 1:4])\n", ["s", "t"], "pushdown-sum-additive"),
+    ("R = (0 - A) %*% matrix(1, rows=4, cols=1)\n", ["R"], "reorder-minus-mm"),
+    ("R = table(seq(1, nrow(A)), seq(nrow(A), 1, -1)) %*% A\n", ["R"], "reverse-operation"),
+    ("R = 3 + A %*% t(A)\nQ = A %*% t(A) - 2\n", ["R", "Q"], "canonical-mm-scalar-add"),
+    ("R = ifelse(TRUE, A, A * 2)\nQ = ifelse(FALSE, A, A * 2)\nS = ifelse(sum(A) > 1, A, A)\n",
+     ["R", "Q", "S"], "ifelse-removal"),
+    ("T = table(V, matrix(1, rows=nrow(V), cols=1), matrix(2, rows=nrow(V), cols=1))\n", ["T"],
+     "ctable-const-inputs"),
+    ("T = table(V, seq(1, nrow(V)), 5, nrow(V))\n", ["T"], "table-seq-expand"),
+    ("G = aggregate(target=M2[, 1], groups=V, fn=\"count\")\n", ["G"], "grouped-aggregate-count"),
+    ("O = outer(V, t(seq(1, 4)), \"==\")\n", ["O"], "outer-seq-expand"),
+    ("s = sum(V ^ 2)\n", ["s"], "dot-product-sum"),
+])
+def test_remaining_algebraic_rules(src, outs, rule):
+    _check(src, {"A": A, "B": B, "V": V, "M2": M2}, outs, rule)
+
+
 def test_nnz():
     X = RNG.random((6, 5)) * (RNG.random((6, 5)) > 0.5)
     _check("n = sum(X != 0)\nprint(n)", {"X": X}, ["n"], "nnz")
