@@ -136,7 +136,8 @@ def main():
     from systemml_amd.utils.stats import Statistics
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    ctx = D.init() if world > 1 else None
+    # SYSML_DIST_FORCE=1 runs the SPMD plan as one RCCL rank on one GPU (DIST overhead check)
+    ctx = D.init() if world > 1 or os.environ.get("SYSML_DIST_FORCE") == "1" else None
     rank = ctx.rank if ctx else 0
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")

@@ -238,6 +238,10 @@ def mem_estimate(d, bytes_per_cell=8):
     return d[0] * d[1] * bytes_per_cell
 
 
+# SYSML_DIST_FORCE=1 (parallel/dist.py init): one-rank SPMD runs plan DIST like N > 1 ranks
+_FORCE_DIST = __import__("os").environ.get("SYSML_DIST_FORCE") == "1"
+
+
 def _world(config):
     w = getattr(config, "_world", None) if config is not None else None
     if w is None:
@@ -260,7 +264,7 @@ def exec_type(h, d, in_dims, config):
         return None
     gpu = config is not None and getattr(config, "gpu", False)
     world = _world(config) if config is not None else 1
-    if config is not None and world > 1:
+    if config is not None and (world > 1 or _FORCE_DIST):
         if getattr(config, "dist_min_rows", 0) and d[0] >= config.dist_min_rows:
             return "DIST"
         budget = getattr(config, "gpu_mem_budget", 0)

@@ -820,9 +820,25 @@ static int route_m(int var, int mode, int J, bool occ, const void* X, int64_t N,
 #undef C4M_CASE
 }
 
+// live flag of the iteration after a queued one in a k-deep run-ahead loop: live only when
+// the queued iteration was live AND its predicate continues the loop.  A dead iteration skips
+// its kernels and leaves its predicate unwritten, so its successor must not read that value.
+__global__ void __launch_bounds__(64) live_and_kernel(const double* prev, const double* q, double* out) {
+  if (threadIdx.x == 0) out[threadIdx.x] = (!sysml_dead(prev) && !sysml_dead(q)) ? 1.0 : 0.0;
+}
+
 }  // namespace sysml_c4
 
 extern "C" {
+
+// out (fp64) = 1.0 when neither encoded live flag (address | inverted-sense bit, 0 = none) is
+// dead, else 0.0
+int sysml_live_and(const void* prev, const void* q, void* out, void* stream) {
+  if (out == nullptr) return -1;
+  hipLaunchKernelGGL(sysml_c4::live_and_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const double*)prev,
+                     (const double*)q, (double*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 // Matrix-core chain (bf16 X, K = 4): blocks per CU, and the launch (arguments as sysml_chain4).
 int sysml_chain4m_occupancy(int mode, int D) {

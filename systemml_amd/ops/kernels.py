@@ -210,6 +210,8 @@ def load(required=False):
     L.sysml_sort_pairs_scratch.argtypes = [I64]
     L.sysml_sort_pairs.restype = CI
     L.sysml_sort_pairs.argtypes = [VP, VP, VP, VP, I64, CI, VP, I64, VP]
+    L.sysml_live_and.restype = CI
+    L.sysml_live_and.argtypes = [VP, VP, VP, VP]
     L.sysml_perm_compose.restype = CI
     L.sysml_perm_compose.argtypes = [VP, VP, VP, VP, CI, I64, VP]
     _lib = L
@@ -1832,3 +1834,14 @@ def sort_values(v):
     if rc != 0:
         raise RuntimeError(f"sysml_sort_keys_prep failed: {rc}")
     return vals, perm
+
+
+def live_and(prev_enc, q_enc):
+    """Device fp64 flag: 1.0 when neither encoded run-ahead live flag (address | inverted bit;
+    0 = none) is dead (chain4.hip live_and_kernel)."""
+    L = load(required=True)
+    out = torch.empty((), dtype=torch.float64, device="cuda")
+    rc = L.sysml_live_and(prev_enc or None, q_enc or None, out.data_ptr(), _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_live_and failed: {rc}")
+    return out

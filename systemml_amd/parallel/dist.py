@@ -120,10 +120,26 @@ def init(backend=None, device=None):
     """Initialise SPMD execution from torchrun-style env vars (RANK/WORLD_SIZE/MASTER_*)."""
     global _CTX
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world <= 1:
+    force = os.environ.get("SYSML_DIST_FORCE") == "1"
+    if world <= 1 and not force:
         _CTX = None
         return None
     rank = int(os.environ.get("RANK", "0"))
+    if world <= 1:
+        # SYSML_DIST_FORCE=1: a one-rank process group, so the SPMD code path (row-partitioned
+        # operands, packed / device-scalar all-reduces, run-ahead under RCCL) runs on one GPU
+        # and can be compared with the single-process plan
+        world, rank = 1, 0
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            sk.close()
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("LOCAL_RANK", "0")
     # SYSML_DIST_BACKEND=gloo with SYSML_DIST_DEVICE=cuda rehearses the GPU SPMD path with
     # several ranks on ONE GPU (RCCL refuses two ranks per device): same partitioning,
     # kernels and collectives, host-staged transport

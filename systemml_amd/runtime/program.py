@@ -9,6 +9,7 @@ a driver/worker split.
 """
 from __future__ import annotations
 
+import collections
 import sys
 import threading
 import time
@@ -494,6 +495,36 @@ def _pred_var(b):
     return r
 
 
+# Iterations queued past an unresolved predicate: with depth k the host reads iteration i's
+# predicate only after queueing iteration i + k, so host and device overlap even when their
+# per-iteration times are equal (depth 1 stalls the device whenever the host jitters).
+# Deeper iterations may run on the (skipped, garbage) outputs of a dead one; bodies with
+# operators that index memory by data values (table / one-hot / gathers / order / grouped
+# aggregates) therefore stay at depth 1, where a dead iteration still reads live data.
+RUNAHEAD_DEPTH = max(1, int(__import__("os").environ.get("SYSML_RUNAHEAD_DEPTH", "3")))
+_RA_INDEXING_BI = frozenset({"table", "ctable", "_onehot", "_gather_rows", "removeEmpty", "order", "aggregate",
+                             "rexpand", "_seq_expand", "replace", "transformapply", "transformdecode"})
+
+
+def _runahead_depth(b):
+    d = getattr(b, "_ra_depth", None)
+    if d is None:
+        from ..compiler import hops as H
+        roots = [b.pred.root]
+        stack = list(b.body)
+        while stack:
+            x = stack.pop()
+            if isinstance(x, BasicBlock):
+                roots.extend(list(x.roots) + list(x.env_out.values()))
+            elif isinstance(x, IfBlock):
+                roots.append(x.pred.root)
+                stack.extend(x.then_blocks)
+                stack.extend(x.else_blocks)
+        deep = not any(h.op == "bi" and h.p.get("name") in _RA_INDEXING_BI for h in H.walk(roots))
+        d = b._ra_depth = RUNAHEAD_DEPTH if deep else 1
+    return d
+
+
 def _exec_while_runahead(ctx, b):
     from ..ops.backend import backend
     if not _to_bool(eval_pred(ctx, b.pred)):
@@ -501,14 +532,41 @@ def _exec_while_runahead(ctx, b):
     runahead_stats["loops"] += 1
     vars_ = ctx.vars
     pv = _pred_var(b)
-    pend = None          # device predicate guarding the iteration being queued (None: known live)
-    pinv = False         # pend is the negation of the loop predicate
+    depth = _runahead_depth(b)
+    # queued iterations whose predicates are unread: (predicate after the iteration, inverted,
+    # variable map after the iteration)
+    pending = collections.deque()
+
+    def drain(keep, unqueued=0):
+        """Read predicates oldest first until `keep` remain; True when one ends the loop (the
+        variable map is then the one after that last live iteration).  `unqueued`: iterations
+        run but not in `pending` (dead too when an earlier predicate ends the loop)."""
+        while len(pending) > keep:
+            q, inv, after = pending.popleft()
+            if bool(q.value()) == inv:
+                runahead_stats["dead"] += len(pending) + unqueued
+                vars_.clear()
+                vars_.update(after)
+                pending.clear()
+                return True
+        return False
+
+    flag = None        # depth > 1: device flag "every queued iteration so far is live"
     try:
         while True:
-            snap = vars_.copy()
             live = 0
-            if pend is not None and pend.t.is_cuda and pend.t.dtype == torch.float64:
-                live = pend.t.data_ptr() | (1 if pinv else 0)
+            if pending:
+                q0, inv0 = pending[-1][0], pending[-1][1]
+                if q0.t.is_cuda and q0.t.dtype == torch.float64:
+                    live = q0.t.data_ptr() | (1 if inv0 else 0)
+                    if depth > 1:
+                        # chain the flags: a dead iteration's predicate is never written, so the
+                        # next one is live only if all earlier ones were (one 1-thread kernel)
+                        from ..ops import kernels as _K
+                        flag = _K.live_and(flag.data_ptr() if flag is not None else 0, live)
+                        live = flag.data_ptr()
+            else:
+                flag = None            # nothing unresolved: this iteration is known live
             backend.set_runahead(True, live)
             err = None
             q = None
@@ -527,21 +585,19 @@ def _exec_while_runahead(ctx, b):
             except Exception as e:      # noqa: BLE001 - re-raised below unless the iteration was dead
                 err = e
             runahead_stats["iterations"] += 1
-            if pend is not None and bool(pend.value()) == pinv:
-                # the iteration just queued lies past the loop's end: undo it
-                runahead_stats["dead"] += 1
-                vars_.clear()
-                vars_.update(snap)
-                return
             if err is not None:
+                # an error in an iteration past the loop's end is not an error
+                if drain(0, 1):
+                    return
                 raise err
             if type(q) is S.DevScalar:
-                pend, pinv = q, qinv
+                pending.append((q, qinv, vars_.copy()))
+                if drain(depth):
+                    return
             else:
                 runahead_stats["host_pred"] += 1
-                if not _to_bool(q):
+                if drain(0, 1) or not _to_bool(q):
                     return
-                pend, pinv = None, False
     finally:
         backend.set_runahead(False, 0)
 

@@ -63,3 +63,64 @@ def test_softmax_objective_one_packed_allreduce(ctx):
     torch.testing.assert_close(g1.double().cpu(), g0.double().cpu(), rtol=1e-6, atol=1e-6)
     assert s11 == pytest.approx(float(s10), rel=1e-6) and s21 == pytest.approx(float(s20), rel=1e-6)
     np.testing.assert_allclose(p1.local.double().cpu().numpy(), p0.double().cpu().numpy(), rtol=1e-6)
+
+
+def test_headline_scripts_spmd_rccl_with_runahead(ctx, monkeypatch):
+    """The headline's DIST plan end to end on a one-rank RCCL group: LinregCG + MultiLogReg on a
+    row-partitioned bf16 X (as bench.py with SYSML_DIST_FORCE=1 / every rank of an N-GPU run)
+    give the single-process results, with run-ahead CG loops under the NCCL context, device-
+    scalar all-reduces and no fallback gather of a row-partitioned operand."""
+    import os
+    from systemml_amd.api import executor as EX
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.compiler import cost
+    from systemml_amd.conf import DMLConfig
+    from systemml_amd.parallel import dist as D
+    from systemml_amd.runtime import program as PR
+    from systemml_amd.runtime.scalars import DevScalar
+    g = torch.Generator(device="cuda").manual_seed(11)
+    n, d = 60000, 128
+    X = (torch.rand(n, d, generator=g, device="cuda") * 2 - 1).to(torch.bfloat16)
+    w = torch.rand(d, 1, generator=g, device="cuda") - 0.5
+    y = X.float() @ w + 0.01 * torch.randn(n, 1, generator=g, device="cuda")
+    lab = (torch.argmax(X[:, :4].float() + 0.2 * torch.rand(n, 4, generator=g, device="cuda"), 1) + 1)
+    lab = lab.float().reshape(-1, 1)
+    srcs = {k: open(os.path.join(SCRIPTS_DIR, "algorithms", f)).read()
+            for k, f in (("lr", "LinearRegCG.dml"), ("mlr", "MultiLogReg.dml"))}
+    args = {"lr": dict(X="X", Y="y", B="B", icpt=0, maxi=20, tol=1e-9, reg=0.01, fmt="csv"),
+            "mlr": dict(X="X", Y="Y", B="B", icpt=0, reg=0.01, tol=1e-9, moi=4, mii=5)}
+
+    def run(spmd):
+        out = {}
+        for k in ("lr", "mlr"):
+            ins = {"X": X, "y": y} if k == "lr" else {"X": X, "Y_vec": lab}
+            if spmd:
+                ins = {a: D.from_local(ctx, t, n) for a, t in ins.items()}
+            cfg = DMLConfig(precision="single", dist_min_rows=10000)
+            cs = EX.compile_script(srcs[k], args[k], inputs=ins, outputs=["B_out"], config=cfg)
+            r, _ = EX.execute(cs, ins, out=lambda s: None, dist=ctx if spmd else None)
+            b = r["B_out"]
+            out[k] = (D.gather(b) if D._is_d(b) else b).double().cpu().numpy()
+        return out
+
+    ref = run(False)
+    monkeypatch.setattr(cost, "_FORCE_DIST", True)
+    monkeypatch.setattr(D, "_CTX", ctx)
+    D.reset_stats()
+    st = dict(PR.runahead_stats)
+    calls = []
+    orig = D.DistContext.allreduce_dev
+
+    def spy(self, v, op="sum"):
+        r = orig(self, v, op)
+        calls.append(type(r))
+        return r
+    monkeypatch.setattr(D.DistContext, "allreduce_dev", spy)
+    got = run(True)
+    for k in ("lr", "mlr"):
+        np.testing.assert_allclose(got[k], ref[k], rtol=2e-3, atol=2e-4, err_msg=k)
+    assert D.stats["fallback_gathers"] == 0, D.fallback_sites
+    assert D.stats["allreduce"] > 0
+    assert calls and all(c is DevScalar for c in calls), calls[:5]
+    assert PR.runahead_stats["loops"] > st["loops"], PR.runahead_stats
+    assert PR.runahead_stats["dead"] > st["dead"], PR.runahead_stats

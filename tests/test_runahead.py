@@ -92,9 +92,11 @@ def _mlr(X, y, icpt, runahead, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("icpt", [0, 2])
-def test_multilogreg_same_with_and_without_runahead(monkeypatch, icpt):
+@pytest.mark.parametrize("depth", [1, 3])
+def test_multilogreg_same_with_and_without_runahead(monkeypatch, icpt, depth):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setattr(PR, "RUNAHEAD_DEPTH", depth)
     g = torch.Generator().manual_seed(5)
     X = torch.rand(20000, 64, generator=g).to(torch.bfloat16).cuda()
     y = (torch.argmax(X[:, :4].float().cpu() + 0.3 * torch.rand(20000, 4, generator=g), 1) + 1).double()
@@ -105,18 +107,22 @@ def test_multilogreg_same_with_and_without_runahead(monkeypatch, icpt):
     loops = PR.runahead_stats["loops"] - st["loops"]
     dead = PR.runahead_stats["dead"] - st["dead"]
     assert loops >= 3, PR.runahead_stats
-    # each loop is left by undoing the one iteration queued past its end
-    assert dead == loops, PR.runahead_stats
+    # each loop is left by undoing the iterations queued past its end (1 .. depth of them)
+    assert loops <= dead <= depth * loops, PR.runahead_stats
+    if depth == 1:
+        assert dead == loops, PR.runahead_stats
     np.testing.assert_allclose(b1, b0, rtol=1e-6, atol=1e-7)
     assert out1 == out0
 
 
 @pytest.mark.gpu
-def test_dead_iteration_errors_are_dropped():
+@pytest.mark.parametrize("depth", [1, 3])
+def test_dead_iteration_errors_are_dropped(monkeypatch, depth):
     """The iteration queued past the end reads v[k + 1, 1] out of bounds; only a live
     iteration may raise."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setattr(PR, "RUNAHEAD_DEPTH", depth)
     src = """
     A = A0
     v = matrix(1, rows=3, cols=1)
@@ -136,3 +142,21 @@ def test_dead_iteration_errors_are_dropped():
            out=out.append)
     assert out == ["3"]
     assert PR.runahead_stats["loops"] - st["loops"] == 1, PR.runahead_stats
+
+
+def test_runahead_depth_is_one_for_data_indexing_bodies():
+    src = """
+    s = 10
+    y = Y0
+    while (s > 1) {
+      T = table(y, y, round(s) + 1, round(s) + 1)
+      s = s / 2 + sum(T) / 1000
+    }
+    w = 10
+    while (w > 1) {
+      w = w / 2
+    }
+    """
+    cs = EX.compile_script(src, {}, inputs={"Y0": np.ones((4, 1))}, outputs=[], config=DMLConfig())
+    loops = _loops(cs.cp.blocks)
+    assert [PR._runahead_depth(b) for b in loops] == [1, PR.RUNAHEAD_DEPTH]
