@@ -501,7 +501,10 @@ def _pred_var(b):
 # Deeper iterations may run on the (skipped, garbage) outputs of a dead one; bodies with
 # operators that index memory by data values (table / one-hot / gathers / order / grouped
 # aggregates) therefore stay at depth 1, where a dead iteration still reads live data.
-RUNAHEAD_DEPTH = max(1, int(__import__("os").environ.get("SYSML_RUNAHEAD_DEPTH", "3")))
+# Default 1: on the headline the host's per-iteration time exceeds the device's at the 8-GPU
+# per-rank size (1.25M rows: depth 3 70.9 vs depth 1 71.1 ms/step) and the chained flags cost
+# a launch per iteration at 10M (388 vs 382 ms; profiles/headline_check_r6a.txt).
+RUNAHEAD_DEPTH = max(1, int(__import__("os").environ.get("SYSML_RUNAHEAD_DEPTH", "1")))
 _RA_INDEXING_BI = frozenset({"table", "ctable", "_onehot", "_gather_rows", "removeEmpty", "order", "aggregate",
                              "rexpand", "_seq_expand", "replace", "transformapply", "transformdecode"})
 
