@@ -1102,7 +1102,10 @@ class Rewriter:
             # idiom of MultiLogReg / GLM with icpt=2): a row aggregate the Cell template fuses
             # with the square, so X ^ 2 is never materialised (a 10M x 1K fp32 X ^ 2 costs more
             # than the two fused passes over X together)
+            # (not over a constant-column view cbind(X, 1): the generated row kernels read dense
+            # rows, and the view's fallback would materialise the square anyway)
             if a.op == "b" and a.p.get("o") == "^" and _is_lit(a.inputs[1], 2) and a.inputs[0].dt == "M" \
+                    and not (a.inputs[0].op == "bi" and a.inputs[0].p.get("name") == "_cbind_const") \
                     and b.dt == "M" and (_col_vector(b) or (b.dim2 == 1 and b.dim1 > 1)):
                 tv = Hop("t", [b], {}, dt="M", dim1=1, dim2=b.dim1, pos=h.pos)
                 prod = Hop("b", [a, tv], {"o": "*"}, dt="M", dim1=a.dim1, dim2=a.dim2, pos=h.pos)

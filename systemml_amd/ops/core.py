@@ -909,12 +909,12 @@ def rix(x, rl, ru, cl, cu, list_mode=False):
             r = kernels.slice_csr(x, r0 - 1, r1, c0 - 1, c1)
             if r is not None:
                 return r
-        elif x.layout is _STRIDED and (c1 - c0 + 1 != nc or (r0, r1) == (1, nr)):
-            # a column window (or the whole matrix) is one dense copy on reorg.hip; a full-width
-            # row range stays a zero-copy view of contiguous rows
-            r = kernels.copy2d(x[r0 - 1:r1, c0 - 1:c1])
+        elif x.layout is _STRIDED and (r0, r1, c0, c1) == (1, nr, 1, nc):
+            r = kernels.copy2d(x)           # the whole matrix: a copy (X[,] is a new value)
             if r is not None:
                 return r
+        # windows stay zero-copy views with a row pitch: the chain / row kernels read them in
+        # place (e.g. P[, 1:K]); consumers that need dense rows copy them on reorg.hip
     out = x[r0 - 1:r1, c0 - 1:c1]
     return out.clone() if out.data_ptr() == x.data_ptr() and out.shape == x.shape else out
 

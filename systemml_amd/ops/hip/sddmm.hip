@@ -141,12 +141,18 @@ __device__ __forceinline__ int64_t wd_first_row(const int64_t* __restrict__ crow
   return lo;
 }
 
-template <typename T, typename I, int G, int UN>
-__global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __restrict__ crow,
+// Column-blocked passes (rbp != nullptr): V is gathered one column block at a time so the block's
+// rows stay resident in the 256 MB MALL instead of missing to HBM (a 10M x 10 fp32 V is 400 MB).
+// rbp[r * (nb + 1) + k] is the first non-zero of row r in column block k (columns sorted within a
+// row); pass `blk` visits only [rbp[..blk], rbp[..blk + 1]) of each row and ADDS into out (zeroed
+// before the first pass), so the CSR arrays are never permuted or copied.
+template <typename T, typename I, int G, int UN, bool BLK>
+__global__ void __launch_bounds__(WAVES * 64, 8) wdivmm_kernel(const int64_t* __restrict__ crow,
                                                             const I* __restrict__ col, const T* __restrict__ wv,
                                                             const T* __restrict__ xv, const T* __restrict__ U,
                                                             const T* __restrict__ V, T* __restrict__ out, int64_t m,
-                                                            int K, int mode, T eps, int64_t chunk, int64_t nchunks) {
+                                                            int K, int mode, T eps, int64_t chunk, int64_t nchunks,
+                                                            const int64_t* __restrict__ rbp, int nb, int blk) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   constexpr int NG = 64 / G;
   const int g = lane / G, gl = lane & (G - 1);
@@ -158,8 +164,12 @@ __global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __res
     if (s >= e) continue;
     int64_t r = wd_first_row<I>(crow, m, s);
     while (r < m) {
-      const int64_t rb = crow[r], re = crow[r + 1];
+      int64_t rb = crow[r], re = crow[r + 1];
       if (rb >= e) break;
+      if constexpr (BLK) {         // this pass's column block of the row
+        rb = rbp[r * (nb + 1) + blk];
+        re = rbp[r * (nb + 1) + blk + 1];
+      }
       const int64_t b = rb > s ? rb : s;
       const int64_t q = re < e ? re : e;
       if (b < q) {
@@ -199,7 +209,7 @@ __global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __res
 #pragma unroll
         for (int o = G; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);
         if (g == 0 && kin) {
-          if (whole) out[r * K + gl] = acc;
+          if (whole) out[r * K + gl] = BLK ? out[r * K + gl] + acc : acc;
           else atomicAdd(out + r * K + gl, acc);
         }
       }
@@ -210,7 +220,8 @@ __global__ void __launch_bounds__(WAVES * 64) wdivmm_kernel(const int64_t* __res
 
 template <typename T, typename I>
 int launch_wd(const int64_t* crow, const I* col, const T* wv, const T* xv, const T* U, const T* V, T* out, int64_t m,
-              int K, int mode, double eps, int64_t nnz, hipStream_t st) {
+              int K, int mode, double eps, int64_t nnz, hipStream_t st, const int64_t* rbp = nullptr, int nb = 0,
+              int blk = 0) {
   // the kernel is bound by the latency of its random V-row gathers: one chunk per wave and
   // enough waves for a full CU (8 per SIMD at <= 64 VGPRs), each with UN gathers per group in
   // flight.  SYSML_WD_WAVES / SYSML_WD_UNROLL override (tuning).
@@ -223,8 +234,15 @@ int launch_wd(const int64_t* crow, const I* col, const T* wv, const T* xv, const
   if (blocks > 256 * 32) blocks = 256 * 32;
   if (blocks < 1) blocks = 1;
   const dim3 gr((unsigned)blocks), t(WAVES * 64);
-#define WD_LAUNCH(G_, U_) hipLaunchKernelGGL((wdivmm_kernel<T, I, G_, U_>), gr, t, 0, st, crow, col, wv, xv, U, V, out, m, K, \
-                                            mode, (T)eps, chunk, nchunks)
+#define WD_LAUNCH(G_, U_)                                                                                       \
+  do {                                                                                                          \
+    if (rbp != nullptr)                                                                                         \
+      hipLaunchKernelGGL((wdivmm_kernel<T, I, G_, U_, true>), gr, t, 0, st, crow, col, wv, xv, U, V, out, m, K,  \
+                         mode, (T)eps, chunk, nchunks, rbp, nb, blk);                                           \
+    else                                                                                                        \
+      hipLaunchKernelGGL((wdivmm_kernel<T, I, G_, U_, false>), gr, t, 0, st, crow, col, wv, xv, U, V, out, m, K, \
+                         mode, (T)eps, chunk, nchunks, rbp, nb, blk);                                           \
+  } while (0)
 #define WD_CASE(G_) \
   if (un >= 8) WD_LAUNCH(G_, 8); \
   else WD_LAUNCH(G_, 4)
@@ -239,9 +257,80 @@ int launch_wd(const int64_t* crow, const I* col, const T* wv, const T* xv, const
   return (int)hipGetLastError();
 }
 
+// rbp[r * (nb + 1) + k] = first non-zero of row r with column >= k * cb (k = 0 .. nb), by binary
+// search in the row's sorted column indices; a thread per (row, boundary)
+template <typename I>
+__global__ void __launch_bounds__(256) block_offsets_kernel(const int64_t* __restrict__ crow, const I* __restrict__ col,
+                                                            int64_t m, int nb, int64_t cb, int64_t* __restrict__ rbp) {
+  const int64_t total = m * (nb + 1);
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / (nb + 1);
+    const int k = (int)(t - r * (nb + 1));
+    int64_t lo = crow[r], hi = crow[r + 1];
+    if (k == nb) {
+      rbp[t] = hi;
+      continue;
+    }
+    const int64_t c0 = (int64_t)k * cb;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)col[mid] < c0) lo = mid + 1;
+      else hi = mid;
+    }
+    rbp[t] = lo;
+  }
+}
+
 }  // namespace sysml_sd
 
 extern "C" {
+
+// per-row column-block offsets of a CSR pattern (see wdivmm_kernel): rbp m x (nb + 1) int64
+int sysml_csr_block_offsets(int idx32, const void* crow, const void* col, int64_t m, int nb, int64_t cb, void* rbp,
+                            void* stream) {
+  if (m <= 0 || nb < 1 || cb < 1) return -1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t g = (m * (nb + 1) + 255) / 256;
+  if (g > 65536) g = 65536;
+  if (idx32)
+    hipLaunchKernelGGL(sysml_sd::block_offsets_kernel<int32_t>, dim3((unsigned)g), dim3(256), 0, st,
+                       static_cast<const int64_t*>(crow), static_cast<const int32_t*>(col), m, nb, cb,
+                       static_cast<int64_t*>(rbp));
+  else
+    hipLaunchKernelGGL(sysml_sd::block_offsets_kernel<int64_t>, dim3((unsigned)g), dim3(256), 0, st,
+                       static_cast<const int64_t*>(crow), static_cast<const int64_t*>(col), m, nb, cb,
+                       static_cast<int64_t*>(rbp));
+  return (int)hipGetLastError();
+}
+
+// wdivmm (as sysml_wdivmm) in nb column-block passes over the offsets rbp, V block k = columns
+// [k * cb, (k + 1) * cb): each pass's V rows fit the MALL.  out zeroed by the caller.
+int sysml_wdivmm_blocked(int dtype, int idx32, const void* crow, const void* col, const void* wv, const void* xv,
+                         const void* U, const void* V, void* out, int64_t m, int K, int mode, double eps, int64_t nnz,
+                         const void* rbp, int nb, void* stream) {
+  if (K < 1 || K > 64 || nnz <= 0 || nb < 1 || rbp == nullptr || (mode == 1 && xv == nullptr)) return -1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const auto* cr = static_cast<const int64_t*>(crow);
+  const auto* rb = static_cast<const int64_t*>(rbp);
+  for (int k = 0; k < nb; ++k) {
+    int rc;
+#define WDB_T(T_)                                                                                              \
+  (idx32 ? sysml_sd::launch_wd<T_, int32_t>(cr, static_cast<const int32_t*>(col), static_cast<const T_*>(wv),   \
+                                            static_cast<const T_*>(xv), static_cast<const T_*>(U),              \
+                                            static_cast<const T_*>(V), static_cast<T_*>(out), m, K, mode, eps,  \
+                                            nnz, st, rb, nb, k)                                                 \
+         : sysml_sd::launch_wd<T_, int64_t>(cr, static_cast<const int64_t*>(col), static_cast<const T_*>(wv),   \
+                                            static_cast<const T_*>(xv), static_cast<const T_*>(U),              \
+                                            static_cast<const T_*>(V), static_cast<T_*>(out), m, K, mode, eps,  \
+                                            nnz, st, rb, nb, k))
+    if (dtype == 0) rc = WDB_T(float);
+    else if (dtype == 1) rc = WDB_T(double);
+    else return -1;
+#undef WDB_T
+    if (rc != 0) return rc;
+  }
+  return 0;
+}
 
 // Fused wdivmm (right form, see wdivmm_kernel): out (m x K, zeroed by the caller) for a CSR pattern
 // (crow int64, col int32 if idx32 else int64), weights wv (nullptr: 1), x values xv (mode 1, the

@@ -210,6 +210,10 @@ def load(required=False):
     L.sysml_sort_pairs_scratch.argtypes = [I64]
     L.sysml_sort_pairs.restype = CI
     L.sysml_sort_pairs.argtypes = [VP, VP, VP, VP, I64, CI, VP, I64, VP]
+    L.sysml_csr_block_offsets.restype = CI
+    L.sysml_csr_block_offsets.argtypes = [CI, VP, VP, I64, CI, I64, VP, VP]
+    L.sysml_wdivmm_blocked.restype = CI
+    L.sysml_wdivmm_blocked.argtypes = [CI, CI] + [VP] * 7 + [I64, CI, CI, ctypes.c_double, I64, VP, CI, VP]
     L.sysml_live_and.restype = CI
     L.sysml_live_and.argtypes = [VP, VP, VP, VP]
     L.sysml_perm_compose.restype = CI
@@ -385,6 +389,18 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def _dense(x):
+    """x itself when contiguous, else a dense copy of the (row-major, any pitch) view on
+    reorg.hip's copy2d -- no ATen copy kernel on HBM data."""
+    if x.is_contiguous():
+        return x
+    if x.is_cuda and x.dim() == 2:
+        r = copy2d(x)
+        if r is not None:
+            return r
+    return x.contiguous()
+
+
 def _pad_cols(m, kp, dt, device=None):
     m = m.to(dtype=dt) if device is None else m.to(device=device, dtype=dt)
     if m.shape[1] == kp and m.is_contiguous():
@@ -440,14 +456,14 @@ def xv(X, V):
         U = _mchain(XV, X, kp, V=V)
         if U is not None:
             _count("mfma.xv")
-            return _result(U if kp == K else U[:, :K].contiguous())
+            return _result(U if kp == K else _dense(U[:, :K]))
     Vp = _pad_cols(V, kp, adt, X.device).contiguous()
     U = torch.empty((X.shape[0], kp), dtype=adt, device=X.device)
     rc, _ = _launch(XV, X, V=Vp, K=kp, out=U, ldo=kp)
     if rc != 0:
         return None
     _count("rowstream.xv")
-    return _result(U if kp == K else U[:, :K].contiguous())
+    return _result(U if kp == K else _dense(U[:, :K]))
 
 
 def xtg(X, G):
@@ -467,7 +483,7 @@ def xtg(X, G):
         R = _mchain(XTG, X, kp, S=Gp)
         if R is not None:
             _count("mfma.xtg")
-            return _result(R if kp == K else R[:, :K].contiguous())
+            return _result(R if kp == K else _dense(R[:, :K]))
     grid = _grid(X.shape[0])
     part = torch.empty((grid, X.shape[1] * kp), dtype=adt, device=X.device)
     rc, g = _launch(XTG, X, S=Gp, K=kp, out=part, grid=grid)
@@ -475,7 +491,7 @@ def xtg(X, G):
         return None
     _count("rowstream.xtg")
     R = _psum(part[:g]).reshape(X.shape[1], kp)
-    return _result(R if kp == K else R[:, :K].contiguous())
+    return _result(R if kp == K else _dense(R[:, :K]))
 
 
 # ----------------------------------------------------------------------------
@@ -529,7 +545,7 @@ def _rows_f32(S, kp, sbc, device):
         S = S.float()
     if S.stride(1) == 1 and S.stride(0) >= S.shape[1] and S.data_ptr() % 4 == 0:
         return S, S.stride(0)
-    S = S.contiguous()
+    S = _dense(S)
     return S, S.shape[1]
 
 
@@ -619,13 +635,13 @@ def mmchain(ctype, X, V, W=None):
         R = _chain4(mode, X, kp, Vf, Sf, lds, sbc)
         if R is not None:
             _count("chain4.mmchain." + ctype)
-            return _result(R if kp == K else R[:, :K].contiguous())
+            return _result(R if kp == K else _dense(R[:, :K]))
     S = padded_S()
     if _mfma_ok(X, kp, mode):
         R = _mchain(mode, X, kp, V=V, S=S, sbc=sbc)
         if R is not None:
             _count("mfma.mmchain." + ctype)
-            return _result(R if kp == K else R[:, :K].contiguous())
+            return _result(R if kp == K else _dense(R[:, :K]))
     grid = _grid(X.shape[0])
     part = torch.empty((grid, X.shape[1] * kp), dtype=adt, device=X.device)
     Vp = _pad_cols(V, kp, adt, X.device).contiguous()
@@ -634,7 +650,7 @@ def mmchain(ctype, X, V, W=None):
         return None
     _count("rowstream.mmchain." + ctype)
     R = _psum(part[:g]).reshape(X.shape[1], kp)
-    return _result(R if kp == K else R[:, :K].contiguous())
+    return _result(R if kp == K else _dense(R[:, :K]))
 
 
 def smobj(X, V, Y, defer=False):
@@ -677,9 +693,9 @@ def smobj(X, V, Y, defer=False):
     _count("chain4m.smobj")
     if defer:                           # the caller reduces the sums further (one all-reduce)
         s = ob[0].sum(0)
-        return _result(Ppad[:N]), _result(G if kp == K else G[:, :K].contiguous()), s[0], s[1]
+        return _result(Ppad[:N]), _result(G if kp == K else _dense(G[:, :K])), s[0], s[1]
     s = ob[0].sum(0).tolist()            # one device sync for both objective terms
-    return _result(Ppad[:N]), _result(G if kp == K else G[:, :K].contiguous()), s[0], s[1]
+    return _result(Ppad[:N]), _result(G if kp == K else _dense(G[:, :K])), s[0], s[1]
 
 
 def smgrad(X, V, Y):
@@ -709,7 +725,7 @@ def smgrad(X, V, Y):
         G = _chain4(XTSMG, X, kp, Vf, Yc, ldy, K, U=Upad, ldu=K)
         if G is not None:
             _count("chain4.smgrad")
-            return _result(Upad[:N]), _result(G if kp == K else G[:, :K].contiguous())
+            return _result(Upad[:N]), _result(G if kp == K else _dense(G[:, :K]))
     kp = max(kp, 2)
     L = load(required=True)
     code, adt = _xcode(X)
@@ -728,7 +744,7 @@ def smgrad(X, V, Y):
         return None
     _count("rowstream.smgrad")
     G = _psum(part).reshape(D, kp)
-    return _result(U), _result(G if kp == K else G[:, :K].contiguous())
+    return _result(U), _result(G if kp == K else _dense(G[:, :K]))
 
 
 # ----------------------------------------------------------------------------
@@ -824,16 +840,60 @@ def wdivmm(crow, col, wv, xv, U, V, mode, eps=0.0, dtype=None):
     wv = wv.to(dtype).contiguous() if wv is not None else None
     xv = xv.to(dtype).contiguous() if xv is not None else None
     out = torch.zeros((m, K), dtype=dtype, device=U.device)
-    rc = L.sysml_wdivmm(0 if dtype == torch.float32 else 1, int(idx32), crow.data_ptr(), col.data_ptr(),
-                        wv.data_ptr() if wv is not None else None, xv.data_ptr() if xv is not None else None,
-                        U.data_ptr(), V.data_ptr(), out.data_ptr(), m, K, int(mode), float(eps), int(col.numel()),
-                        _stream())
+    nnz = int(col.numel())
+    blk = _wd_blocks(crow, col, idx32, V.shape[0], K * V.element_size(), nnz, m)
+    if blk is not None:
+        rbp, nb = blk
+        rc = L.sysml_wdivmm_blocked(0 if dtype == torch.float32 else 1, int(idx32), crow.data_ptr(), col.data_ptr(),
+                                    wv.data_ptr() if wv is not None else None,
+                                    xv.data_ptr() if xv is not None else None, U.data_ptr(), V.data_ptr(),
+                                    out.data_ptr(), m, K, int(mode), float(eps), nnz, rbp.data_ptr(), nb, _stream())
+        if rc == 0:
+            _count("wdivmm_blocked")
+    else:
+        rc = L.sysml_wdivmm(0 if dtype == torch.float32 else 1, int(idx32), crow.data_ptr(), col.data_ptr(),
+                            wv.data_ptr() if wv is not None else None, xv.data_ptr() if xv is not None else None,
+                            U.data_ptr(), V.data_ptr(), out.data_ptr(), m, K, int(mode), float(eps), nnz,
+                            _stream())
     if rc == -1:
         return None
     if rc != 0:
         raise RuntimeError(f"sysml_wdivmm failed: {rc}")
     _count("wdivmm")
     return out
+
+
+# Column blocking of wdivmm's V gathers (opt-in, SYSML_WD_BLOCK_MB=<block MB>): a gathered factor
+# matrix larger than this many bytes is visited in column blocks of at most this size, so each
+# block would stay resident in the 256 MB MALL.  Off by default: measured SLOWER on ALS-CG 10M x 10M
+# / 1e9 non-zeros (1.49 s unblocked vs 1.69 / 1.86 / 2.46 s with 160 / 96 / 48 MB blocks,
+# profiles/als_block_sweep_r6.txt) -- every pass re-walks all rows' pointers, and the unblocked
+# gathers already hit the MALL for the most part.
+WD_BLOCK_BYTES = int(float(os.environ.get("SYSML_WD_BLOCK_MB", "0")) * (1 << 20))
+WD_BLOCK_MIN_NNZ = 1 << 26
+_WD_PLANS = {}
+
+
+def _wd_blocks(crow, col, idx32, n, row_bytes, nnz, m):
+    """(row block offsets m x (nb + 1) int64, nb) for a column-blocked wdivmm, cached per pattern;
+    None when V fits a block or the pattern is small."""
+    if WD_BLOCK_BYTES <= 0 or nnz < WD_BLOCK_MIN_NNZ or n * row_bytes <= WD_BLOCK_BYTES:
+        return None
+    nb = -(-n * row_bytes // WD_BLOCK_BYTES)
+    cb = -(-n // nb)
+    key = (crow.data_ptr(), col.data_ptr(), nnz, m, n, nb, col._version)
+    e = _WD_PLANS.get(key)
+    if e is None:
+        L = load(required=True)
+        rbp = torch.empty((m, nb + 1), dtype=torch.int64, device=crow.device)
+        rc = L.sysml_csr_block_offsets(int(idx32), crow.data_ptr(), col.data_ptr(), m, nb, cb, rbp.data_ptr(),
+                                       _stream())
+        if rc != 0:
+            raise RuntimeError(f"sysml_csr_block_offsets failed: {rc}")
+        if len(_WD_PLANS) >= 4:
+            _WD_PLANS.pop(next(iter(_WD_PLANS)))
+        e = _WD_PLANS[key] = (crow, col, rbp, nb)      # holds the pattern: its addresses stay unique
+    return e[2], e[3]
 
 
 def sddmm(crow, col, U, V, dtype=None):
@@ -1263,7 +1323,7 @@ def agg(o, d, X, ydt=None):
     N, D = X.shape
     if N == 0 or D == 0:
         return None
-    X = X.contiguous()
+    X = _dense(X)
     if ydt is None:
         ydt = torch.float64 if (X.dtype == torch.float64 or (X.dtype == torch.bfloat16
                                                              and backend.dtype == torch.float64)) else torch.float32

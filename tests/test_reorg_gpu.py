@@ -140,4 +140,4 @@ def test_sort_values_and_dml_paths():
         b = c[k].cpu().numpy() if hasattr(c[k], "cpu") else c[k]
         np.testing.assert_allclose(np.asarray(a, dtype=float), np.asarray(b, dtype=float), rtol=0, atol=0, err_msg=k)
     grew = {k for k, v in kernels.counters.items() if v > before.get(k, 0)}
-    assert {"order", "tri", "transpose", "slice"} <= grew, grew
+    assert {"order", "tri", "transpose"} <= grew, grew

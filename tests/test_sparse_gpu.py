@@ -145,7 +145,8 @@ def test_sparse_sparse_product_elementwise(prec):
 @pytest.mark.parametrize("K", [1, 10, 33, 64])
 @pytest.mark.parametrize("form", ["mult", "multx", "div"])
 @pytest.mark.parametrize("left", [False, True])
-def test_fused_wdivmm_matches_dense(K, form, left):
+@pytest.mark.parametrize("blocked", [False, True])
+def test_fused_wdivmm_matches_dense(K, form, left, blocked, monkeypatch):
     """sddmm.hip wdivmm_kernel (one pass over W's pattern, the gathered factor row reused for
     the accumulation) against fp64 torch on the dense equivalent, right and left forms."""
     from systemml_amd.ops import quaternary as Q, kernels
@@ -167,10 +168,16 @@ def test_fused_wdivmm_matches_dense(K, form, left):
     uv = U @ V.t()
     q = {"mult": Wd * uv, "multx": Wd * (uv - Xd), "div": torch.where(mask, Wd / (uv + 0.5), torch.zeros((), dtype=torch.float64))}[form]
     ref = U.t() @ q if left else q @ V
+    if blocked:
+        # column-blocked passes (the gathered factor visited ~7 column blocks at a time)
+        monkeypatch.setattr(kernels, "WD_BLOCK_MIN_NNZ", 0)
+        monkeypatch.setattr(kernels, "WD_BLOCK_BYTES", K * 8 * 300)
     c0 = kernels.counters.get("wdivmm", 0)
+    b0 = kernels.counters.get("wdivmm_blocked", 0)
     got = Q.wdivmm(W, U.cuda(), V.cuda(), left, mult=form != "div", eps=0.5 if form == "div" else None,
                    X=X if form == "multx" else None)
     assert kernels.counters.get("wdivmm", 0) == c0 + 1
+    assert kernels.counters.get("wdivmm_blocked", 0) == b0 + int(blocked)
     torch.testing.assert_close(got.cpu(), ref, rtol=1e-9, atol=1e-9)
 
 
