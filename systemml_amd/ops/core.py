@@ -233,6 +233,15 @@ def _dev_bool(x):
 
 
 def _dev_binary(op, a, b):
+    # a device scalar whose value the host already read (a branch, a print) is a host value from
+    # then on: its further scalar algebra runs on the host, not as tiny device launches between
+    # host syncs (the solvers' outer-loop bookkeeping)
+    if type(a) is DevScalar and a._v is not None:
+        a = a._v
+    if type(b) is DevScalar and b._v is not None:
+        b = b._v
+    if type(a) is not DevScalar and type(b) is not DevScalar:
+        return binary(op, a, b)
     da, db = type(a) is DevScalar, type(b) is DevScalar
     other = b if da else a
     if isinstance(other, Tensor) and not (da and db):
@@ -290,6 +299,8 @@ _DEV_UN = {"neg": torch.neg, "abs": torch.abs, "exp": torch.exp, "log": torch.lo
 
 
 def _dev_unary(op, x):
+    if x._v is not None:                 # already read back: host arithmetic (see _dev_binary)
+        return unary(op, x._v)
     f = _DEV_UN.get(op)
     if f is not None and x.vt != "b":
         return DevScalar(f(x.t), "i" if (x.vt == "i" and op in ("neg", "abs", "sign", "floor", "ceil", "round"))
