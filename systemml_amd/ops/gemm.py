@@ -47,6 +47,8 @@ def _L():
         L.sysml_gemm_ktile.argtypes = [ctypes.c_int]
         L.sysml_gemm_set_bk.restype = None
         L.sysml_gemm_set_bk.argtypes = [ctypes.c_int]
+        L.sysml_gemm_set_pf.restype = None
+        L.sysml_gemm_set_pf.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
 
@@ -54,6 +56,12 @@ def _L():
 def set_bk(bk):
     """bf16 K-tile override for A/B runs: 32 (4 LDS stages, counted vmcnt), 64 (2 stages), 0 = auto."""
     _L().sysml_gemm_set_bk(int(bk))
+
+
+def set_pf(on):
+    """bf16 main-loop variant for A/B runs (gemm.hip): False the 8-wave kernel of the DNN
+    paths, True the register-pipelined one (gemm_bf16_pf, default for plain GEMMs)."""
+    _L().sysml_gemm_set_pf(int(bool(on)))
 
 
 def _count(k):

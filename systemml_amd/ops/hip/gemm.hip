@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
+#include <cstdlib>
 
 namespace sysml_gk {
 
@@ -130,10 +131,10 @@ __device__ __forceinline__ void glds16(const uint16_t* sbase, uint32_t voff, uin
 }
 #pragma clang diagnostic pop
 
-template <bool KMAJ, int BKT, int ROWS = 256>
+template <bool KMAJ, int BKT, int ROWS = 256, int NW = 8>   // NW: waves sharing the DMAs
 struct Stager {
   static_assert(KMAJ || ROWS == 256, "MN-major images are 256 columns wide");
-  static constexpr int NJ = ROWS * BKT * 2 / 8192; // DMA instructions per wave per K-tile
+  static constexpr int NJ = ROWS * BKT * 2 / (1024 * NW); // DMA instructions per wave per K-tile (NW waves)
   static constexpr int RPI = 1024 / (BKT * 2);   // K-major rows per 1-KiB instruction
   static constexpr int CPR = BKT / 8;            // 16-B chunks per K-major row
   int off[NJ];
@@ -430,6 +431,106 @@ gemm_bf16_kernel(Args a) {
         if (a.vec && nv == 4) *(f4*)p = f4{v[0], v[1], v[2], v[3]};
         else
           for (int r = 0; r < nv; ++r) p[r] = v[r];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// bf16 kernel, register-pipelined (plain C / split-K slabs only; K a multiple of 64): the same
+// 256x256x64 block tile, LDS images and 2-stage LDS-DMA as gemm_bf16_kernel, but the MFMA
+// fragments are software-pipelined one 32-deep step ahead ACROSS the K-tile boundary:
+//   step kk=1 of tile t is read from LDS while the 32 MFMAs of step kk=0 issue; after the
+//   barrier that publishes tile t+1, step kk=0 of tile t+1 is read while kk=1's MFMAs issue,
+//   and the DMA of tile t+2 goes into tile t's buffer right there (its fragments already sit
+//   in registers) -- so every ds_read has a full step of MFMAs (512 cycles per wave) to land,
+//   and every DMA about a whole tile.  Two fragment sets: 2 x 48 VGPRs + 128 accumulators.
+// ---------------------------------------------------------------------------------------
+template <bool TA, bool TB>
+__global__ void __launch_bounds__(NTHR, 1)
+gemm_bf16_pf(Args a) {
+  constexpr bool AK = !TA, BKM = TB;
+  constexpr int BKT = 64, WM = 128, MI = 8, OPA = BM * BKT * 2, STG = 2 * OPA;
+  extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % a.ntiles, split = wg / a.ntiles;
+  int bm, bn;
+  tile_coords(a, tile, bm, bn);
+  const int ktiles = a.K / BKT;
+  const int kt0 = split * a.ktps;
+  const int kt1 = (kt0 + a.ktps < ktiles) ? kt0 + a.ktps : ktiles;
+  Stager<AK, BKT> sa;
+  Stager<BKM, BKT> sb;
+  sa.init((const uint16_t*)a.A, wave, lane, bm * BM, a.M, a.lda);
+  sb.init((const uint16_t*)a.B, wave, lane, bn * BN, a.N, a.ldb);
+  f4 acc[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  s8 fa0[MI], fb0[4], fa1[MI], fb1[4];
+  auto issue = [&](int kt) {
+    lds_char* st = smem + (kt & 1) * STG;
+    sa.issue(kt * BKT, a.K, false, st, wave, lane);
+    sb.issue(kt * BKT, a.K, false, st + OPA, wave, lane);
+  };
+  auto load = [&](int kt, int kk, s8 (&fa)[MI], s8 (&fb)[4]) {
+    const lds_char* st = smem + (kt & 1) * STG;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = frag<BKM, BKT>(st + OPA, wc * 64 + j * 16, kk, lane);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = frag<AK, BKT>(st, wr * WM + i * 16, kk, lane);
+  };
+  auto mma = [&](const s8 (&fa)[MI], const s8 (&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf8)fb[j], (bf8)fa[i], acc[i][j], 0, 0, 0);
+  };
+  if (kt0 < kt1) {
+    issue(kt0);
+    wait_vm<0>();
+    __syncthreads();
+    load(kt0, 0, fa0, fb0);
+    if (kt0 + 1 < kt1) issue(kt0 + 1);
+    for (int kt = kt0; kt < kt1; ++kt) {
+      load(kt, 1, fa1, fb1);
+      mma(fa0, fb0);
+      if (kt + 1 < kt1) {
+        wait_vm<0>();          // this wave's DMA of tile kt+1 landed
+        bar_keep_dma();        // ... every wave's; and every read of tile kt's buffer retired
+        load(kt + 1, 0, fa0, fb0);
+        if (kt + 2 < kt1) issue(kt + 2);    // into tile kt's buffer: its fragments are in registers
+      }
+      mma(fa1, fb1);
+    }
+  }
+  const int64_t ldc = a.ldc;
+  const int rbase = bm * BM + wr * WM + (lane & 15);
+  const int cbase = bn * BN + wc * 64 + (lane >> 4) * 4;
+  float* dst = (float*)a.C + (a.slab ? (int64_t)split * a.slab : 0);
+  const bool acc_in = a.beta && !a.slab;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int row = rbase + i * 16;
+    if (row >= a.M) continue;
+    float* prow = dst + (int64_t)row * ldc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = cbase + j * 16;
+      if (a.vec && col + 3 < a.N) {
+        f4 v = acc[i][j];
+        if (acc_in) v += *(const f4*)(prow + col);
+        *(f4*)(prow + col) = v;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (col + r < a.N) prow[col + r] = acc_in ? prow[col + r] + acc[i][j][r] : acc[i][j][r];
       }
     }
   }
@@ -761,8 +862,26 @@ static int launch_bf16_t(const Args& a, hipStream_t st) {
   return launch_kernel(gemm_bf16_kernel<TA, TB, BKT, BMT>, a, NTHR, LDS_BYTES, st);
 }
 
+// register-pipelined bf16 kernel (gemm_bf16_pf): 1 = on for plain GEMMs with K % 64 == 0 and a
+// 64-deep K tile, 0 = off (SYSML_GEMM_PF / sysml_gemm_set_pf)
+static int g_pf = [] { const char* e = getenv("SYSML_GEMM_PF"); return e ? atoi(e) : 1; }();
+
+template <bool TA, bool TB>
+static int launch_bf16_pf(const Args& a, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)gemm_bf16_pf<TA, TB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            LDS_BYTES) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  return launch_kernel(gemm_bf16_pf<TA, TB>, a, NTHR, LDS_BYTES, st);
+}
+
 template <bool TA, bool TB>
 static int launch_bf16(const Args& a, int bk, hipStream_t st) {
+  if (g_pf && bk == 64 && a.K % 64 == 0 && a.hwb == 0 && !a.obf16 && !a.relu && a.bias == nullptr)
+    return launch_bf16_pf<TA, TB>(a, st);
   return bk == 64 ? launch_bf16_t<TA, TB, 64>(a, st) : launch_bf16_t<TA, TB, 32>(a, st);
 }
 
@@ -799,6 +918,10 @@ extern "C" {
 int sysml_gemm_tile(int dtype) { return dtype == 2 ? BM : FBM; }
 int sysml_gemm_ktile(int dtype) { return dtype == 2 ? 64 : FBK; }
 void sysml_gemm_set_bk(int bk) { g_bk = (bk == 64 || bk == 32) ? bk : 0; }
+// 0: the 8-wave kernel, 1: register-pipelined (gemm_bf16_pf).  A 4-wave 128 x 128-per-wave
+// variant was measured slower (993 vs 1,181 TF nn 8192^3: 256 VGPRs + 256 AGPRs spill at one wave
+// per SIMD) and dropped.
+void sysml_gemm_set_pf(int on) { g_pf = on ? 1 : 0; }
 
 // C[M][N] (+)= op(A) op(B), op(A) = A (ta=0, A stored [M][lda]) or A^T (ta=1, A stored [K][lda]);
 // op(B) = B (tb=0, B stored [K][ldb]) or B^T (tb=1, B stored [N][ldb]).

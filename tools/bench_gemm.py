@@ -57,14 +57,21 @@ def main():
         flop = 2.0 * M * N * K
         it = max(1, int(2e12 / flop * (1 if dt == torch.bfloat16 else 0.1)))
         res = {}
-        for bk in ((0, 32, 64) if dt == torch.bfloat16 else (0,)):
-            gemm.set_bk(bk)
+        ref0 = (P.float() @ Q.float())
+        for bk in ((0, 32, 64, "64nopf") if dt == torch.bfloat16 else (0,)):
+            gemm.set_bk(64 if bk == "64nopf" else bk)
+            gemm.set_pf(bk != "64nopf")
+            out = gemm.matmul(P, Q)
+            err = float((out.float() - ref0).abs().max()) / max(1.0, float(ref0.abs().max()))
+            assert err < 1e-2, (bk, err)
             res[bk] = timeit(lambda: gemm.matmul(P, Q), it)
         gemm.set_bk(0)
+        gemm.set_pf(True)
+        del ref0
         ref = timeit(lambda: P @ Q, it)
         rows.append({"case": f"{dts} {lay} M={M} N={N} K={K}", "ours_ms": res[0][0], "torch_ms": ref[0],
                      "ours_tflops": flop / res[0][0] / 1e9, "torch_tflops": flop / ref[0] / 1e9})
-        for bk in (32, 64):
+        for bk in (32, 64, "64nopf"):
             if bk in res:
                 rows[-1][f"bk{bk}_tflops"] = flop / res[bk][0] / 1e9
         print(json.dumps(rows[-1]), flush=True)
