@@ -934,9 +934,11 @@ int sysml_gemm(int dtype, const void* A, int64_t lda, int ta, const void* B, int
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || ksplit < 1 || (tri && M != N)) return -1;
   const int tile = dtype == 2 ? BM : FBM;
-  // bf16 K-tile by measurement (profiles/gemm_kbench_r2.json): the 2-stage BK=64 kernel wins on
-  // square shapes, the 4-stage BK=32 one on split-K tall reductions
-  const int bk = g_bk ? g_bk : (ksplit > 1 ? 32 : 64);
+  // bf16 K-tile by measurement: the 2-stage BK=64 kernel wins on square shapes, the 4-stage BK=32
+  // one on split-K tall reductions (profiles/gemm_kbench_r2.json) -- unless the register-pipelined
+  // BK=64 kernel applies (K % 64 == 0), which wins there too (tn 1000 x 1000 x 1M: 1,103 vs 1,076
+  // TF, profiles/gemm_kbench_r6b.json)
+  const int bk = g_bk ? g_bk : ((ksplit > 1 && !(g_pf && K % 64 == 0)) ? 32 : 64);
   const int kt = dtype == 2 ? bk : FBK;
   Args a;
   a.veca = a.vecb = 0;

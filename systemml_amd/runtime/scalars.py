@@ -9,6 +9,7 @@ ScalarObjectFactory (INT op INT stays INT except for '/' and '^').
 from __future__ import annotations
 
 import math
+import weakref
 from decimal import Decimal
 
 from ..parser.errors import DMLRuntimeError
@@ -27,7 +28,7 @@ class DevScalar:
     the CP ScalarObject (runtime/instructions/cp/DoubleObject.java), which is always on the
     JVM heap — on the GPU backend that costs a device round trip per scalar.
     """
-    __slots__ = ("t", "vt", "_v", "_hb", "_ev")
+    __slots__ = ("t", "vt", "_v", "_hb", "_ev", "_seq", "__weakref__")
     is_dev_scalar = True
 
     def __init__(self, t, vt="d"):
@@ -36,6 +37,36 @@ class DevScalar:
         self._v = None
         self._hb = None     # pinned host copy in flight (start_read)
         self._ev = None
+        self._seq = next(_dev_seq)
+        _pending.append(weakref.ref(self))
+        if len(_pending) > _PENDING_MAX:
+            del _pending[:len(_pending) - _PENDING_MAX]
+
+    def _convert(self, x):
+        return (x != 0.0) if self.vt == "b" else (int(x) if self.vt == "i" else x)
+
+    def _read_older(self):
+        """One device read for this value and every unread device scalar queued before it (the
+        same stream: they are complete when this one is), so the host's later branches and
+        scalar algebra on them need no further synchronisation (the solvers' outer-loop
+        bookkeeping: objective, ratios, trust-region tests).  Not in run-ahead loops, which
+        read their predicate late on purpose."""
+        import torch
+        dev = self.t.device
+        older = []
+        for r in _pending:
+            d = r()
+            if d is not None and d._v is None and d._hb is None and d._seq < self._seq and d.t.device == dev \
+                    and d.t.numel() == 1:
+                older.append(d)
+        if not older:
+            return False
+        older.append(self)
+        vals = torch.stack([d.t.reshape(()).to(torch.float64) for d in older]).cpu().tolist()
+        for d, x in zip(older, vals):
+            d._v = d._convert(x)
+        _pending[:] = [r for r in _pending if r() is not None and r()._v is None]
+        return True
 
     def start_read(self):
         """Queue the device-to-host copy of the value behind the work that produces it and
@@ -59,8 +90,10 @@ class DevScalar:
                 x = float(self._hb[0])
                 self._hb = self._ev = None
             else:
+                if BATCH_READS and self.t.is_cuda and not _in_runahead() and self._read_older():
+                    return self._v
                 x = float(self.t.item())
-            self._v = (x != 0.0) if self.vt == "b" else (int(x) if self.vt == "i" else x)
+            self._v = self._convert(x)
         return self._v
 
     def __float__(self):
@@ -83,6 +116,18 @@ class DevScalar:
 
     def __repr__(self):
         return f"DevScalar({self.t!r}, {self.vt})"
+
+
+_dev_seq = __import__("itertools").count()
+_pending = []            # weak references to device scalars, creation order (DevScalar._read_older)
+_PENDING_MAX = 256
+# SYSML_BATCH_SCALAR_READS=0: read every device scalar on its own
+BATCH_READS = __import__("os").environ.get("SYSML_BATCH_SCALAR_READS", "1") != "0"
+
+
+def _in_runahead():
+    from ..ops.backend import backend
+    return backend.defer
 
 
 def materialize(v):
