@@ -27,7 +27,10 @@ class DMLConfig:
     lazy_scalars: bool = False          # GPU backend: aggregates return HBM-resident scalars (runtime/scalars.DevScalar);
                                         # implies every matrix lives in HBM (gpu_min_cells ignored)
     parallelism: int = 8                # parfor local workers
-    parfor_gpu_streams: int = 4         # parfor on the GPU backend: concurrent worker streams (HW queues)
+    parfor_gpu_streams: int = 1         # parfor on the GPU backend without par=: worker streams per device
+                                        # (1 = one worker per GPU, as the reference's rule-based optimizer;
+                                        # 4 streams on one MI355X measured 0.26-0.86x of the serial loop,
+                                        # profiles/parfor_gpu_r5*.txt)
     parfor_gpus: int = 1                # parfor on the GPU backend: devices used by one process's workers
     # compiler
     rewrites: bool = True

@@ -294,8 +294,10 @@ def optimize(ctx, b, n_iters, as_int=True):
                  rank runs the iterations of the rows it owns, no collective in the body);
                  LOCAL_GPU (worker streams / devices) on a GPU backend; LOCAL_CPU threads
                  otherwise;
-      k          the script's par=, else the exec type's parallelism (GPU: hardware queues
-                 = config.parfor_gpu_streams, times the devices used), capped by the
+      k          the script's par=, else the exec type's parallelism (GPU: one worker per
+                 device used, times config.parfor_gpu_streams -- default 1, so a one-GPU
+                 run without par= executes sequentially: worker streams sharing one GPU lost
+                 to the serial loop, profiles/parfor_gpu_r5*.txt), capped by the
                  iterations and by the memory budget (rewriteSetDegreeOfParallelism,
                  :1178: free device / host memory over one worker's estimate);
       tasks      the script's taskpartitioner=, else STATIC for bodies of uniform cost (no
@@ -329,7 +331,7 @@ def optimize(ctx, b, n_iters, as_int=True):
         pl.exec_type = "LOCAL_GPU"
         ndev = max(1, min(int(getattr(cfg, "parfor_gpus", 1) or 1), torch.cuda.device_count()))
         pl.devices = ndev
-        k = max(1, int(getattr(cfg, "parfor_gpu_streams", 4) or 1)) * ndev
+        k = max(1, int(getattr(cfg, "parfor_gpu_streams", 1) or 1)) * ndev
     else:
         pl.exec_type = "LOCAL_CPU"
         k = cfg.parallelism
