@@ -61,6 +61,7 @@ class DevScalar:
                 older.append(d)
         if not older:
             return False
+        older = older[-_BATCH_MAX:]           # the most recent: the values the next branches use
         older.append(self)
         vals = torch.stack([d.t.reshape(()).to(torch.float64) for d in older]).cpu().tolist()
         for d, x in zip(older, vals):
@@ -121,6 +122,7 @@ class DevScalar:
 _dev_seq = __import__("itertools").count()
 _pending = []            # weak references to device scalars, creation order (DevScalar._read_older)
 _PENDING_MAX = 256
+_BATCH_MAX = 16
 # SYSML_BATCH_SCALAR_READS=0: read every device scalar on its own
 BATCH_READS = __import__("os").environ.get("SYSML_BATCH_SCALAR_READS", "1") != "0"
 
