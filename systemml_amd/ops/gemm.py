@@ -59,9 +59,10 @@ def set_bk(bk):
 
 
 def set_pf(on):
-    """bf16 main-loop variant for A/B runs (gemm.hip): False the 8-wave kernel of the DNN
-    paths, True the register-pipelined one (gemm_bf16_pf, default for plain GEMMs)."""
-    _L().sysml_gemm_set_pf(int(bool(on)))
+    """bf16 main-loop variant for A/B runs (gemm.hip): 0/False the 8-wave kernel everywhere,
+    1/True the register-pipelined one (gemm_bf16_pf) for plain GEMMs (the default), 2 also for
+    the image-blocked DNN GEMMs (opt-in: measured no faster on ResNet-50)."""
+    _L().sysml_gemm_set_pf(int(on))
 
 
 def _count(k):

@@ -424,20 +424,24 @@ gemm_bf16_kernel(Args a) {
         if (a.vec && nv == 4) {
           *(uint2*)p = uint2{(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
         } else {
-          for (int r = 0; r < nv; ++r) p[r] = h[r];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (r < nv) p[r] = h[r];
         }
       } else {
         float* p = (float*)a.C + o;
         if (a.vec && nv == 4) *(f4*)p = f4{v[0], v[1], v[2], v[3]};
         else
-          for (int r = 0; r < nv; ++r) p[r] = v[r];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (r < nv) p[r] = v[r];
       }
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// bf16 kernel, register-pipelined (plain C / split-K slabs only; K a multiple of 64): the same
+// bf16 kernel, register-pipelined (K a multiple of 64; plain, split-K slab and DNN epilogues): the same
 // 256x256x64 block tile, LDS images and 2-stage LDS-DMA as gemm_bf16_kernel, but the MFMA
 // fragments are software-pipelined one 32-deep step ahead ACROSS the K-tile boundary:
 //   step kk=1 of tile t is read from LDS while the 32 MFMAs of step kk=0 issue; after the
@@ -446,7 +450,7 @@ gemm_bf16_kernel(Args a) {
 //   in registers) -- so every ds_read has a full step of MFMAs (512 cycles per wave) to land,
 //   and every DMA about a whole tile.  Two fragment sets: 2 x 48 VGPRs + 128 accumulators.
 // ---------------------------------------------------------------------------------------
-template <bool TA, bool TB>
+template <bool TA, bool TB, bool DNN>
 __global__ void __launch_bounds__(NTHR, 1)
 gemm_bf16_pf(Args a) {
   constexpr bool AK = !TA, BKM = TB;
@@ -466,7 +470,7 @@ gemm_bf16_pf(Args a) {
   Stager<AK, BKT> sa;
   Stager<BKM, BKT> sb;
   sa.init((const uint16_t*)a.A, wave, lane, bm * BM, a.M, a.lda);
-  sb.init((const uint16_t*)a.B, wave, lane, bn * BN, a.N, a.ldb);
+  sb.init((const uint16_t*)a.B, wave, lane, bn * BN, a.N, a.ldb, DNN ? a.hwb : 0, DNN ? a.simgB : 0);
   f4 acc[MI][4];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -513,24 +517,78 @@ gemm_bf16_pf(Args a) {
   const int64_t ldc = a.ldc;
   const int rbase = bm * BM + wr * WM + (lane & 15);
   const int cbase = bn * BN + wc * 64 + (lane >> 4) * 4;
-  float* dst = (float*)a.C + (a.slab ? (int64_t)split * a.slab : 0);
-  const bool acc_in = a.beta && !a.slab;
+  if (!DNN || a.slab) {   // plain fp32 C, or split-K slabs (the reduction pass applies the DNN epilogue)
+    float* dst = (float*)a.C + (a.slab ? (int64_t)split * a.slab : 0);
+    const bool acc_in = a.beta && !a.slab;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = rbase + i * 16;
+      if (row >= a.M) continue;
+      float* prow = dst + (int64_t)row * ldc;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = cbase + j * 16;
+        if (a.vec && col + 3 < a.N) {
+          f4 v = acc[i][j];
+          if (acc_in) v += *(const f4*)(prow + col);
+          *(f4*)(prow + col) = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (col + r < a.N) prow[col + r] = acc_in ? prow[col + r] + acc[i][j][r] : acc[i][j][r];
+        }
+      }
+    }
+    return;
+  }
+  // DNN epilogue (as gemm_bf16_kernel): image-blocked columns, per-row bias, relu, bf16 / fp32 C
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int row = rbase + i * 16;
     if (row >= a.M) continue;
-    float* prow = dst + (int64_t)row * ldc;
+    const float bv = a.bias != nullptr ? a.bias[row] : 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = cbase + j * 16;
-      if (a.vec && col + 3 < a.N) {
-        f4 v = acc[i][j];
-        if (acc_in) v += *(const f4*)(prow + col);
-        *(f4*)(prow + col) = v;
-      } else {
+      if (col >= a.N) continue;
+      int64_t cofs = col;
+      int nv = a.N - col < 4 ? a.N - col : 4;
+      if (a.hwb > 0) {
+        const int img = col / a.hwb, px = col - img * a.hwb;
+        nv = a.hwr - px < nv ? a.hwr - px : nv;
+        cofs = (int64_t)img * a.simgC + px;
+      }
+      if (nv <= 0) continue;
+      float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (col + r < a.N) prow[col + r] = acc_in ? prow[col + r] + acc[i][j][r] : acc[i][j][r];
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[i][j][r] + bv;
+        if (a.relu) v[r] = v[r] > 0.f ? v[r] : 0.f;
+      }
+      const int64_t o = (int64_t)row * ldc + cofs;
+      if (a.obf16) {
+        uint16_t h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          uint32_t u = __float_as_uint(v[r]);
+          u += 0x7fffu + ((u >> 16) & 1u);
+          h[r] = (uint16_t)(u >> 16);
+        }
+        uint16_t* p = (uint16_t*)a.C + o;
+        if (a.vec && nv == 4) {
+          *(uint2*)p = uint2{(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (r < nv) p[r] = h[r];
+        }
+      } else {
+        float* p = (float*)a.C + o;
+        if (a.vec && nv == 4) *(f4*)p = f4{v[0], v[1], v[2], v[3]};
+        else
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (r < nv) p[r] = v[r];
       }
     }
   }
@@ -863,19 +921,21 @@ static int launch_bf16_t(const Args& a, hipStream_t st) {
 }
 
 // register-pipelined bf16 kernel (gemm_bf16_pf): 1 = on for plain GEMMs with K % 64 == 0 and a
-// 64-deep K tile, 0 = off (SYSML_GEMM_PF / sysml_gemm_set_pf)
+// 64-deep K tile, 0 = off, 2 = also the image-blocked DNN GEMMs (SYSML_GEMM_PF / sysml_gemm_set_pf).
+// The DNN route is opt-in: ResNet-50 b256 measured 51.6 ms/step with it vs 51.2 without
+// (profiles/gemm_pf_dnn_r6.txt) -- its 1x1 GEMMs are HBM-bound, not issue-bound
 static int g_pf = [] { const char* e = getenv("SYSML_GEMM_PF"); return e ? atoi(e) : 1; }();
 
-template <bool TA, bool TB>
+template <bool TA, bool TB, bool DNN = false>
 static int launch_bf16_pf(const Args& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_pf<TA, TB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)gemm_bf16_pf<TA, TB, DNN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             LDS_BYTES) != hipSuccess)
       return -3;
     attr = true;
   }
-  return launch_kernel(gemm_bf16_pf<TA, TB>, a, NTHR, LDS_BYTES, st);
+  return launch_kernel(gemm_bf16_pf<TA, TB, DNN>, a, NTHR, LDS_BYTES, st);
 }
 
 template <bool TA, bool TB>
@@ -921,7 +981,7 @@ void sysml_gemm_set_bk(int bk) { g_bk = (bk == 64 || bk == 32) ? bk : 0; }
 // 0: the 8-wave kernel, 1: register-pipelined (gemm_bf16_pf).  A 4-wave 128 x 128-per-wave
 // variant was measured slower (993 vs 1,181 TF nn 8192^3: 256 VGPRs + 256 AGPRs spill at one wave
 // per SIMD) and dropped.
-void sysml_gemm_set_pf(int on) { g_pf = on ? 1 : 0; }
+void sysml_gemm_set_pf(int on) { g_pf = on < 0 ? 0 : (on > 2 ? 2 : on); }
 
 // C[M][N] (+)= op(A) op(B), op(A) = A (ta=0, A stored [M][lda]) or A^T (ta=1, A stored [K][lda]);
 // op(B) = B (tb=0, B stored [K][ldb]) or B^T (tb=1, B stored [N][ldb]).
@@ -1047,6 +1107,7 @@ int sysml_gemm_dnn(const void* A, int64_t lda, const void* B, int64_t ldb, int64
                    : ((ldc % 4 == 0) && (simgC % 4 == 0) && (((uintptr_t)C & (obf16 ? 7 : 15)) == 0));
   int rc;
   if (small) rc = rowtile == 64 ? launch_bf16_t<false, false, 64, 64>(a, st) : launch_bf16_t<false, false, 64, 128>(a, st);
+  else if (g_pf > 1 && bk == 64 && K % 64 == 0) rc = launch_bf16_pf<false, false, true>(a, st);
   else rc = bk == 64 ? launch_bf16_t<false, false, 64>(a, st) : launch_bf16_t<false, false, 32>(a, st);
   if (rc || !use_slab) return rc;
   const int64_t total = (int64_t)M * N;

@@ -113,8 +113,10 @@ def test_gemm_nonfinite_tail(G):
     (512, 2048, 32, 49, True, False),    # 7 x 7 images (padded to 56), split-K
     (128, 1152, 12, 196, False, True),   # 14 x 14 (padded to 200), 64-row tile, split-K
     (1000, 72, 3, 100, True, True),      # ragged M, padded pixels
+    (512, 1024, 16, 196, True, True),    # 256-row tile, K % 64 == 0, one K split
 ])
-def test_gemm_img_matches_fp32(M, K, nimg, hw, bias, relu):
+@pytest.mark.parametrize("pf", [1, 2])
+def test_gemm_img_matches_fp32(M, K, nimg, hw, bias, relu, pf):
     """sysml_gemm_dnn: out[n] = relu(A . B[n] + bias) for all images in one launch, bf16 out,
     against an fp32 torch evaluation on the same bf16 operands."""
     if not torch.cuda.is_available():
@@ -127,7 +129,13 @@ def test_gemm_img_matches_fp32(M, K, nimg, hw, bias, relu):
     b = torch.randn(M, device="cuda", generator=g) if bias else None
     out = torch.empty(nimg, M, hw, dtype=torch.bfloat16, device="cuda")
     before = Kn.counters.get("gemm_dnn", 0)
-    Kn._gemm_img(A, B, out, M, K, nimg, hw, bias=b, relu=relu)
+    from systemml_amd.ops import gemm as G
+    G.set_pf(pf)      # 2: the register-pipelined kernel on the image-blocked DNN path too
+    try:
+        Kn._gemm_img(A, B, out, M, K, nimg, hw, bias=b, relu=relu)
+        torch.cuda.synchronize()
+    finally:
+        G.set_pf(1)
     ref = torch.matmul(A.float(), B.float())
     if bias:
         ref = ref + b.reshape(1, -1, 1)
