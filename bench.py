@@ -305,7 +305,9 @@ def main():
         if st is not None:
             print(st.report(25), file=sys.stderr)
         if a.verbose:
+            from systemml_amd.runtime import program as _PR, graphloop as _GL
             print(f"datagen {t_gen:.2f}s, kernels {kernels.counters}, dist {D.stats}", file=sys.stderr)
+            print(f"run-ahead {_PR.runahead_stats}, graph replay {_GL.stats}", file=sys.stderr)
         res = {
             "metric": METRIC, "value": round(sec, 4), "unit": "s", "n_gpus": n_phys, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(sec * 1000, 2), "higher_is_better": False,

@@ -867,7 +867,12 @@ def _live_block(b, live_after):
             if new_end == end:
                 break
             end = new_end
+        # read before written in one iteration (runtime/graphloop.py); computed before the
+        # final pass below, which leaves the body blocks' live_out as they must be
+        reads = _live_list(b.body, set())
         lin = _live_list(b.body, end)
+        b.iter_live = set(end)          # live after every iteration
+        b.body_live_in = set(reads)
         if isinstance(b, ForBlock):
             b.result_vars = sorted(set(live_after) & _all_writes(b.body))
             lin = lin - {b.var}

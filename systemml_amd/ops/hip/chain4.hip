@@ -827,9 +827,59 @@ __global__ void __launch_bounds__(64) live_and_kernel(const double* prev, const 
   if (threadIdx.x == 0) out[threadIdx.x] = (!sysml_dead(prev) && !sysml_dead(q)) ? 1.0 : 0.0;
 }
 
+// commit of a graph-replayed run-ahead iteration (runtime/program.py _GraphLoop): copy each
+// (src -> dst) pair of the iteration's loop state into the loop's static buffers, only when
+// the iteration is live -- a dead (speculative) replay leaves the last live state in place.
+constexpr int COMMIT_MAX = 16;
+struct CommitTab {
+  const void* src[COMMIT_MAX];
+  void* dst[COMMIT_MAX];
+  long long nbytes[COMMIT_MAX];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) commit_live_kernel(const CommitTab T, const double* live) {
+  if (sysml_dead(live)) return;
+  const long long tid = (long long)blockIdx.x * 256 + threadIdx.x, step = (long long)gridDim.x * 256;
+  for (int p = 0; p < T.n; ++p) {
+    const long long nb = T.nbytes[p];
+    const bool words = ((nb | (long long)(uintptr_t)T.src[p] | (long long)(uintptr_t)T.dst[p]) & 3) == 0;
+    if (words) {
+      const uint32_t* s = (const uint32_t*)T.src[p];
+      uint32_t* d = (uint32_t*)T.dst[p];
+      for (long long i = tid; i < (nb >> 2); i += step) d[i] = s[i];
+    } else {
+      const uint8_t* s = (const uint8_t*)T.src[p];
+      uint8_t* d = (uint8_t*)T.dst[p];
+      for (long long i = tid; i < nb; i += step) d[i] = s[i];
+    }
+  }
+}
+
 }  // namespace sysml_c4
 
 extern "C" {
+
+// n <= COMMIT_MAX pairs; live: encoded run-ahead flag (address | inverted-sense bit)
+int sysml_commit_live(int n, const void* const* src, void* const* dst, const long long* nbytes, const void* live,
+                      void* stream) {
+  using namespace sysml_c4;
+  if (n < 0 || n > COMMIT_MAX || live == nullptr) return -1;
+  CommitTab T;
+  long long mx = 0;
+  for (int p = 0; p < n; ++p) {
+    if (nbytes[p] < 0 || (nbytes[p] > 0 && (src[p] == nullptr || dst[p] == nullptr))) return -1;
+    T.src[p] = src[p];
+    T.dst[p] = dst[p];
+    T.nbytes[p] = nbytes[p];
+    mx = nbytes[p] > mx ? nbytes[p] : mx;
+  }
+  T.n = n;
+  long long g = (mx / 4 + 255) / 256;
+  g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
+  hipLaunchKernelGGL(commit_live_kernel, dim3((int)g), dim3(256), 0, (hipStream_t)stream, T, (const double*)live);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 // out (fp64) = 1.0 when neither encoded live flag (address | inverted-sense bit, 0 = none) is
 // dead, else 0.0

@@ -216,6 +216,8 @@ def load(required=False):
     L.sysml_wdivmm_blocked.argtypes = [CI, CI] + [VP] * 7 + [I64, CI, CI, ctypes.c_double, I64, VP, CI, VP]
     L.sysml_live_and.restype = CI
     L.sysml_live_and.argtypes = [VP, VP, VP, VP]
+    L.sysml_commit_live.restype = CI
+    L.sysml_commit_live.argtypes = [CI, VP, VP, VP, VP, VP]
     L.sysml_perm_compose.restype = CI
     L.sysml_perm_compose.argtypes = [VP, VP, VP, VP, CI, I64, VP]
     _lib = L
@@ -1894,6 +1896,28 @@ def sort_values(v):
     if rc != 0:
         raise RuntimeError(f"sysml_sort_keys_prep failed: {rc}")
     return vals, perm
+
+
+COMMIT_MAX = 16
+
+
+def commit_live(pairs, live_enc):
+    """Copy each (src, dst) tensor pair (same byte size) when the encoded run-ahead live flag
+    (address | inverted bit) is live -- one launch (chain4.hip commit_live_kernel)."""
+    L = load(required=True)
+    n = len(pairs)
+    if n > COMMIT_MAX or not live_enc:
+        raise ValueError("commit_live: at most 16 pairs and a live flag")
+    src = (ctypes.c_void_p * COMMIT_MAX)(*[s.data_ptr() for s, _ in pairs])
+    dst = (ctypes.c_void_p * COMMIT_MAX)(*[d.data_ptr() for _, d in pairs])
+    nb = (ctypes.c_longlong * COMMIT_MAX)(*[s.numel() * s.element_size() for s, _ in pairs])
+    for s, d in pairs:
+        if s.numel() * s.element_size() != d.numel() * d.element_size() or not (s.is_contiguous() and d.is_contiguous()):
+            raise ValueError("commit_live: pairs must be contiguous and of one byte size")
+    rc = L.sysml_commit_live(n, src, dst, nb, live_enc, _stream())
+    if rc != 0:
+        raise RuntimeError(f"sysml_commit_live failed: {rc}")
+    _count("commit_live")
 
 
 def live_and(prev_enc, q_enc):

@@ -70,6 +70,13 @@ class DistContext:
 
     # -- collectives --------------------------------------------------------
     def allreduce_(self, t, op="sum"):
+        from ..runtime import graphloop as _GL
+        seg = _GL.capturing()
+        if seg is not None:
+            # a run-ahead loop iteration being captured (runtime/graphloop.py): the graph is cut
+            # here and the replay issues this all-reduce on the same buffer between segments
+            seg.collective(self, t, op)
+            return t
         stats["allreduce"] += 1
         rop = {"sum": tdist.ReduceOp.SUM, "max": tdist.ReduceOp.MAX, "min": tdist.ReduceOp.MIN,
                "prod": tdist.ReduceOp.PRODUCT}[op]

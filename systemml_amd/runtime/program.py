@@ -533,9 +533,13 @@ def _exec_while_runahead(ctx, b):
     if not _to_bool(eval_pred(ctx, b.pred)):
         return
     runahead_stats["loops"] += 1
+    from . import graphloop as _GL
+    if _GL.try_entry(ctx, b, runahead_stats):      # replay of a graph captured at an earlier entry
+        return
     vars_ = ctx.vars
     pv = _pred_var(b)
     depth = _runahead_depth(b)
+    n_queued = 0
     # queued iterations whose predicates are unread: (predicate after the iteration, inverted,
     # variable map after the iteration)
     pending = collections.deque()
@@ -597,6 +601,15 @@ def _exec_while_runahead(ctx, b):
                 pending.append((q, qinv, vars_.copy()))
                 if drain(depth):
                     return
+                n_queued += 1
+                if _GL.want_capture(ctx, b, n_queued):
+                    # the rest of the loop as HIP-graph replays (runtime/graphloop.py): settle
+                    # the queued iterations first, so the captured state is a live one
+                    if drain(0):
+                        return
+                    flag = None
+                    if _GL.capture_and_run(ctx, b, pv, exec_blocks, eval_pred, runahead_stats):
+                        return
             else:
                 runahead_stats["host_pred"] += 1
                 if drain(0, 1) or not _to_bool(q):

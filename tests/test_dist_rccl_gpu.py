@@ -124,3 +124,47 @@ def test_headline_scripts_spmd_rccl_with_runahead(ctx, monkeypatch):
     assert calls and all(c is DevScalar for c in calls), calls[:5]
     assert PR.runahead_stats["loops"] > st["loops"], PR.runahead_stats
     assert PR.runahead_stats["dead"] > st["dead"], PR.runahead_stats
+
+
+def test_headline_mlr_spmd_graph_replay_with_collectives(ctx, monkeypatch):
+    """runtime/graphloop.py under the one-rank RCCL group: the inner CG iteration is captured
+    in segments cut at its all-reduce, replayed with the all-reduce issued between them, and
+    gives the op-by-op SPMD result; the collectives per replayed iteration are the op-by-op
+    ones (same count with and without graphs, plus the ranks' one agreement on the capture)."""
+    import os
+    from systemml_amd.api import executor as EX
+    from systemml_amd.api.mlcontext import SCRIPTS_DIR
+    from systemml_amd.compiler import cost
+    from systemml_amd.conf import DMLConfig
+    from systemml_amd.parallel import dist as D
+    from systemml_amd.runtime import graphloop as GL
+    g = torch.Generator(device="cuda").manual_seed(13)
+    n, d = 60000, 128
+    X = (torch.rand(n, d, generator=g, device="cuda") * 2 - 1).to(torch.bfloat16)
+    lab = (torch.argmax(X[:, :4].float() + 0.2 * torch.rand(n, 4, generator=g, device="cuda"), 1) + 1)
+    lab = lab.float().reshape(-1, 1)
+    src = open(os.path.join(SCRIPTS_DIR, "algorithms", "MultiLogReg.dml")).read()
+    args = dict(X="X", Y="Y", B="B", icpt=0, reg=0.01, tol=1e-9, moi=4, mii=5)
+    monkeypatch.setattr(cost, "_FORCE_DIST", True)
+    monkeypatch.setattr(D, "_CTX", ctx)
+
+    def run():
+        ins = {a: D.from_local(ctx, t, n) for a, t in {"X": X, "Y_vec": lab}.items()}
+        cs = EX.compile_script(src, args, inputs=ins, outputs=["B_out"],
+                               config=DMLConfig(precision="single", dist_min_rows=10000))
+        D.reset_stats()
+        r, _ = EX.execute(cs, ins, out=lambda s: None, dist=ctx)
+        b = r["B_out"]
+        return (D.gather(b) if D._is_d(b) else b).double().cpu().numpy(), D.stats["allreduce"]
+
+    monkeypatch.setattr(GL, "ENABLED", False)
+    ref, n_ref = run()
+    monkeypatch.setattr(GL, "ENABLED", True)
+    monkeypatch.setattr(GL, "DIST", True)
+    st = dict(GL.stats)
+    got, n_got = run()
+    dd = {k: GL.stats[k] - st[k] for k in st if k != "why"}
+    assert dd["captures"] >= 1 and dd["failed"] == 0 and dd["replays"] > 0, (dd, GL.stats["why"])
+    assert dd["segments"] >= 2, dd              # cut at the Hessian-vector product's all-reduce
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-7)
+    assert n_got == n_ref + dd["captures"], (n_got, n_ref, dd)   # + one success agreement per capture

@@ -160,3 +160,101 @@ def test_runahead_depth_is_one_for_data_indexing_bodies():
     cs = EX.compile_script(src, {}, inputs={"Y0": np.ones((4, 1))}, outputs=[], config=DMLConfig())
     loops = _loops(cs.cp.blocks)
     assert [PR._runahead_depth(b) for b in loops] == [1, PR.RUNAHEAD_DEPTH]
+
+
+# ----------------------------------------------------------------------------- graph replay (GPU)
+def _graph_on(monkeypatch, on, depth=2):
+    from systemml_amd.runtime import graphloop as GL
+    monkeypatch.setattr(GL, "ENABLED", on)
+    monkeypatch.setattr(GL, "DEPTH", depth)
+    return GL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("icpt", [0, 2])
+@pytest.mark.parametrize("gdepth", [1, 2])
+def test_multilogreg_graph_replay_matches_op_by_op(monkeypatch, icpt, gdepth):
+    """runtime/graphloop.py: the inner CG loop captured once and replayed for every later
+    iteration and outer-loop entry gives the op-by-op run-ahead result."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator().manual_seed(7)
+    X = torch.rand(20000, 64, generator=g).to(torch.bfloat16).cuda()
+    y = (torch.argmax(X[:, :4].float().cpu() + 0.3 * torch.rand(20000, 4, generator=g), 1) + 1).double()
+    y = y.reshape(-1, 1).cuda().float()
+    _graph_on(monkeypatch, False)
+    b0, out0 = _mlr(X, y, icpt, True, monkeypatch)
+    GL = _graph_on(monkeypatch, True, gdepth)
+    st = dict(GL.stats)
+    b1, out1 = _mlr(X, y, icpt, True, monkeypatch)
+    d = {k: GL.stats[k] - st[k] for k in st if k != "why"}
+    if icpt == 0:
+        assert d["captures"] >= 1 and d["failed"] == 0 and d["replays"] > 0, d
+        assert d["entries"] >= 3, d            # later outer iterations re-enter the captured loop
+    np.testing.assert_allclose(b1, b0, rtol=1e-6, atol=1e-7)
+    assert out1 == out0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gdepth", [1, 3])
+def test_graph_replay_counters_and_reentry(monkeypatch, gdepth):
+    """Host counters become device state in the graph; every entry of the inner loop (new
+    start matrix, reset counter) replays the one capture; dead replays change nothing."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    src = """
+    for (j in 1:4) {
+      A = A0 * j
+      s = 100
+      k = 0
+      while (s > 0.5) {
+        A = A * 0.9
+        s = sum(A)
+        k = k + 1
+      }
+      print(j + " " + k + " " + s)
+    }
+    """
+    cfg = lambda: DMLConfig(gpu=True, precision="double")
+    _graph_on(monkeypatch, False)
+    ref = []
+    EX.run(src, inputs={"A0": np.full((300, 200), 0.01)}, config=cfg(), out=ref.append)
+    GL = _graph_on(monkeypatch, True, gdepth)
+    st = dict(GL.stats)
+    got = []
+    EX.run(src, inputs={"A0": np.full((300, 200), 0.01)}, config=cfg(), out=got.append)
+    d = {k: GL.stats[k] - st[k] for k in st if k != "why"}
+    assert got == ref
+    assert d["captures"] == 1 and d["failed"] == 0 and d["entries"] == 4, d
+    assert d["dead"] <= 4 * gdepth, d
+
+
+@pytest.mark.gpu
+def test_graph_capture_failure_falls_back(monkeypatch):
+    """A body that needs the host (a device-scalar row index) cannot be captured: the loop
+    continues op by op with the same result, and no capture is tried again."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    src = """
+    A = A0
+    v = seq(1, 50)
+    s = 100
+    k = 1
+    while (s > 0.5) {
+      A = A * 0.5
+      s = sum(A) + as.scalar(v[k, 1]) * 0
+      k = k + 1
+    }
+    print(k + " " + s)
+    """
+    _graph_on(monkeypatch, False)
+    ref = []
+    EX.run(src, inputs={"A0": np.full((200, 100), 0.01)}, config=DMLConfig(gpu=True, precision="double"),
+           out=ref.append)
+    GL = _graph_on(monkeypatch, True)
+    st = dict(GL.stats)
+    got = []
+    EX.run(src, inputs={"A0": np.full((200, 100), 0.01)}, config=DMLConfig(gpu=True, precision="double"),
+           out=got.append)
+    assert got == ref
+    assert GL.stats["captures"] == st["captures"]
