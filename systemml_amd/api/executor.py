@@ -103,7 +103,43 @@ def _compile_script(source, args, inputs, outputs, config, pydml, filename, base
     cs.source = source
     cs.compile_args = dict(args=args, inputs=inputs, outputs=outputs, pydml=pydml, filename=filename,
                            base_dir=base_dir)
+    _tag_loops(cp, source, args, inputs, outputs, config, pydml)
     return cs
+
+
+def _tag_loops(cp, source, args, inputs, outputs, config, pydml):
+    """Key every while loop by what determines its compiled body -- script text, arguments,
+    input metadata, configuration and the loop's ordinal: a recompilation of the same script
+    (the bench compiles every step) finds the HIP graph its loop was captured into
+    (runtime/graphloop.py) instead of capturing again."""
+    import hashlib
+    from ..compiler.blocks import BasicBlock, WhileBlock
+    meta = []
+    if isinstance(inputs, dict):
+        for k in sorted(inputs):
+            v = inputs[k]
+            meta.append((k, type(v).__name__, tuple(getattr(v, "shape", ())), str(getattr(v, "dtype", ""))))
+    h = hashlib.sha1(repr((source, sorted((args or {}).items(), key=lambda kv: kv[0]), meta, list(outputs),
+                           repr(config), pydml)).encode()).hexdigest()
+    n = [0]
+
+    def walk(blocks):
+        for b in blocks or ():
+            if isinstance(b, BasicBlock):
+                continue
+            if isinstance(b, WhileBlock):
+                # + the body's variable names: compiler temporaries (_licm*) are numbered per
+                # compilation, and the graph binds them by name
+                from ..compiler.translator import _all_writes
+                names = (tuple(sorted(getattr(b, "body_live_in", ()) or ())), tuple(sorted(_all_writes(b.body))),
+                         tuple(sorted(b.pred.reads)))
+                b._gkey = (h, n[0], names)
+                n[0] += 1
+            for attr in ("body", "then_blocks", "else_blocks"):
+                walk(getattr(b, attr, None))
+    walk(cp.blocks)
+    for k in sorted(cp.functions, key=repr):
+        walk(getattr(cp.functions[k], "body", None))
 
 
 def value_dt(v):

@@ -166,6 +166,10 @@ def hoist_loop_invariants(blocks, stats=None):
 
 
 def hoist_program(cp):
+    # temporaries numbered per program: a recompilation of the same script names them alike
+    # (runtime/graphloop.py finds a loop's captured graph by the names its body reads)
+    global _names
+    _names = itertools.count(1)
     stats = hoist_loop_invariants(cp.blocks)
     for fb in cp.functions.values():
         if fb.body is not None:

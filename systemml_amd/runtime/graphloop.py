@@ -40,6 +40,7 @@ import collections
 import gc
 import os
 import threading
+import time
 import weakref
 
 import torch
@@ -54,6 +55,7 @@ COPY_MAX_BYTES = 1 << 30       # invariant matrices up to this size are staged i
 MAX_COMMIT = 15                # state variables (+ the predicate) of the one commit launch
 
 stats = {"captures": 0, "failed": 0, "entries": 0, "replays": 0, "dead": 0, "rebind_fail": 0, "segments": 0,
+         "host_uploads": 0, "t_bind": 0.0, "t_replay": 0.0, "t_wait": 0.0, "t_exit": 0.0, "t_capture": 0.0,
          "why": ""}
 
 _SEG = [None]                  # the segmented capture in progress (DistContext.allreduce_ hook)
@@ -63,6 +65,9 @@ _SEG = [None]                  # the segmented capture in progress (DistContext.
 # alive past its loop block; _sweep frees those whose block is gone.
 _LOCK = threading.Lock()
 _ALL = []
+_BYKEY = {}                          # loop key (api/executor._tag_loops) -> GraphLoop of a recompiled loop
+_BYKEY_MAX = 32
+_RETIRED = []
 
 
 def _sweep():
@@ -172,7 +177,7 @@ class GraphLoop:
         self.fl = torch.empty((), dtype=torch.float64, device="cuda")
         self.one = torch.ones((), dtype=torch.float64, device="cuda")     # always-live flag (staging)
         self.hstage = None
-        self.fails = 0
+        self.busy = False     # replaying (a loop of another thread's plan must not share the buffers)
 
     # ------------------------------------------------------------------ classification
     def _static_for(self, v, x):
@@ -266,6 +271,7 @@ class GraphLoop:
         (a baked value or an address-bound matrix changed, or a shape did).  Floating-point
         state and staged matrices are converted to the captured dtype (a fresh host-placed
         zero matrix entering a loop whose graph was captured on its fp32 device state)."""
+        t0 = time.perf_counter()
         for v, k in self.kind.items():
             x = vars_.get(v)
             if not self._fits(v, k, x):
@@ -291,6 +297,7 @@ class GraphLoop:
                 t = _local(x)
                 if not t.is_cuda:
                     st.copy_(t)
+                    stats["host_uploads"] += 1
                     continue
                 if t.dtype != st.dtype:
                     t = t.to(st.dtype)
@@ -308,6 +315,7 @@ class GraphLoop:
         self.hstage[:n].copy_(torch.tensor(hv, dtype=torch.float64).pin_memory(), non_blocking=True)
         pairs.extend((self.hstage[i], d) for i, d in enumerate(hd))
         self._copy(pairs)
+        stats["t_bind"] += time.perf_counter() - t0
         return True
 
     def _copy(self, pairs):
@@ -425,24 +433,30 @@ class GraphLoop:
         pending = collections.deque()
         seg = self.seg
         while True:
+            t0 = time.perf_counter()
             seg.replay()
             stats["replays"] += 1
             runahead_stats["iterations"] += 1
             pending.append(S.DevScalar(self.st_q, "b").start_read())
+            t1 = time.perf_counter()
+            stats["t_replay"] += t1 - t0
             ended = False
             while len(pending) > depth:
                 if bool(pending.popleft().value()) == self.inv:
                     ended = True
                     break
+            stats["t_wait"] += time.perf_counter() - t1
             if ended:
                 stats["dead"] += len(pending)
                 runahead_stats["dead"] += len(pending)
                 break
         # the state leaves the static buffers (the next entry overwrites them): one copy launch
+        t0 = time.perf_counter()
         pairs = [(self.st[v], torch.empty_like(self.st[v])) for v in self.commit]
         self._copy(pairs)
         for v, (_, t) in zip(self.commit, pairs):
             vars_[v] = self._wrap(v, t) if self.kind[v] == "T" else S.DevScalar(t, self.vt[v])
+        stats["t_exit"] += time.perf_counter() - t0
 
 
 class _NoGraph(Exception):
@@ -470,15 +484,27 @@ def try_entry(ctx, b, runahead_stats):
     """At loop entry (predicate true): replay a graph captured in an earlier entry. True when
     the loop ran to its end here."""
     gl = getattr(b, "_graph", None)
-    if not isinstance(gl, GraphLoop) or not _usable(ctx):
+    if gl is None and not getattr(b, "_gnocache", False):
+        key = getattr(b, "_gkey", None)
+        gl = _BYKEY.get(key) if key is not None else None
+        if gl is not None and _usable(ctx):
+            b._graph = gl              # the same loop of an earlier compilation of this script
+    if not isinstance(gl, GraphLoop) or not _usable(ctx) or gl.busy:
         return False
     if not gl.bind(ctx.vars):
+        # another address-bound input / shape than at the capture: this loop may capture anew
+        # (replacing the cached graph); twice in a row and it stays op by op
         stats["rebind_fail"] += 1
-        gl.fails += 1
-        if gl.fails >= 2:
-            b._graph = False
+        n = getattr(b, "_gfails", 0) + 1
+        b._gfails = n
+        b._graph = False if n >= 2 else None
+        b._gnocache = True
         return False
-    gl.run(ctx.vars, runahead_stats, _depth(ctx, b))
+    gl.busy = True
+    try:
+        gl.run(ctx.vars, runahead_stats, _depth(ctx, b))
+    finally:
+        gl.busy = False
     return True
 
 
@@ -491,7 +517,11 @@ def capture_and_run(ctx, b, pv, exec_blocks, eval_pred, runahead_stats):
     rest of the loop. True when the loop ran to its end here; False leaves it op by op."""
     with _LOCK:
         _sweep()
-        return _capture_and_run(ctx, b, pv, exec_blocks, eval_pred, runahead_stats)
+        t0 = time.perf_counter()
+        try:
+            return _capture_and_run(ctx, b, pv, exec_blocks, eval_pred, runahead_stats)
+        finally:
+            stats["t_capture"] += time.perf_counter() - t0
 
 
 def _capture_and_run(ctx, b, pv, exec_blocks, eval_pred, runahead_stats):
@@ -510,6 +540,16 @@ def _capture_and_run(ctx, b, pv, exec_blocks, eval_pred, runahead_stats):
         b._graph = False
         return False
     b._graph = gl
-    _ALL.append((weakref.ref(b), gl))
-    gl.run(ctx.vars, runahead_stats, _depth(ctx, b))
+    key = getattr(b, "_gkey", None)
+    if key is not None and (key in _BYKEY or len(_BYKEY) < _BYKEY_MAX):
+        if key in _BYKEY:
+            _RETIRED.append(_BYKEY[key])        # blocks may still hold it: never freed mid-capture
+        _BYKEY[key] = gl                        # kept for the process
+    else:
+        _ALL.append((weakref.ref(b), gl))
+    gl.busy = True
+    try:
+        gl.run(ctx.vars, runahead_stats, _depth(ctx, b))
+    finally:
+        gl.busy = False
     return True

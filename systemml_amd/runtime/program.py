@@ -379,7 +379,11 @@ def _exec_control(ctx, b):
                 ctx.owned.discard(x)
     if isinstance(b, WhileBlock):
         if RUNAHEAD and _runahead_ok(ctx, b):
-            return _exec_while_runahead(ctx, b)
+            t0 = time.perf_counter()
+            try:
+                return _exec_while_runahead(ctx, b)
+            finally:
+                runahead_stats["t"] += time.perf_counter() - t0
         while _to_bool(eval_pred(ctx, b.pred)):
             exec_blocks(ctx, b.body)
         return
@@ -476,7 +480,7 @@ def _runahead_ok(ctx, b):
     return ok
 
 
-runahead_stats = {"loops": 0, "iterations": 0, "dead": 0, "host_pred": 0}
+runahead_stats = {"loops": 0, "iterations": 0, "dead": 0, "host_pred": 0, "t": 0.0}
 
 
 def _pred_var(b):
