@@ -739,6 +739,11 @@ def _form_row_region(root, consumers, outs, pos, memo, costed, RowProgram, RMAXI
                 leaf(c)
     if len(leaves) > RMAXIN or len(body) > RMAXOPS:
         return 0
+    # a constant-column view cbind(X, c) (ops/augmented.ConstCol) is no dense row operand: the
+    # generated kernel cannot read it, and a region over it would run operator by operator
+    # (materialising its squares); its products stay the view's own passes
+    if any(x.op == "bi" and x.p.get("name") == "_cbind_const" for x in leaves):
+        return 0
     # a few very long rows (e.g. N x (C*H*W) activations of a small batch): one row per lane
     # group leaves the chip idle -- the unfused operators parallelise within rows instead
     for x in leaves:

@@ -1102,8 +1102,26 @@ class Rewriter:
             # idiom of MultiLogReg / GLM with icpt=2): a row aggregate the Cell template fuses
             # with the square, so X ^ 2 is never materialised (a 10M x 1K fp32 X ^ 2 costs more
             # than the two fused passes over X together)
-            # (not over a constant-column view cbind(X, 1): the generated row kernels read dense
-            # rows, and the view's fallback would materialise the square anyway)
+            # Over a constant-column view cbind(X, c) (MultiLogReg's icpt = 2 scaling) the square
+            # is split off the view first: (X ^ 2) %*% v[1:D, ] + c ^ 2 * v[D + 1, 1], so it stays
+            # over X as a fused row aggregate (the generated row kernels read dense rows only)
+            if a.op == "b" and a.p.get("o") == "^" and _is_lit(a.inputs[1], 2) and a.inputs[0].op == "bi" \
+                    and a.inputs[0].p.get("name") == "_cbind_const" and b.dt == "M" \
+                    and (_col_vector(b) or (b.dim2 == 1 and b.dim1 > 1)):
+                X, c, _n = a.inputs[0].inputs
+                none = Hop("lit", p={"v": None, "vt": "STRING"}, dt="S", pos=h.pos)
+                nr = Hop("u", [b], {"o": "nrow"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                top = Hop("b", [nr, H.lit(1, h.pos)], {"o": "-"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                d1 = b.dim1 - 1 if b.dim1 and b.dim1 > 0 else -1
+                vtop = Hop("rix", [b, H.lit(1, h.pos), top, none, none], {}, dt="M", dim1=d1, dim2=1, pos=h.pos)
+                vlast = Hop("rix", [b, nr, nr, none, none], {}, dt="M", dim1=1, dim2=1, pos=h.pos)
+                xsq = Hop("b", [X, H.lit(2, h.pos)], {"o": "^"}, dt="M", dim1=X.dim1, dim2=X.dim2, pos=h.pos)
+                prod = self._rw_mm(Hop("mm", [xsq, vtop], dict(h.p), dt="M", dim1=X.dim1, dim2=1, pos=h.pos))
+                c2 = Hop("b", [c, c], {"o": "*"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                sv = Hop("u", [vlast], {"o": "cast_scalar"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                corr = Hop("b", [sv, c2], {"o": "*"}, dt="S", dim1=0, dim2=0, pos=h.pos)
+                return self._hit("square-matrix-mult-cbind", Hop("b", [prod, corr], {"o": "+"}, dt="M",
+                                                                 dim1=X.dim1, dim2=1, pos=h.pos))
             if a.op == "b" and a.p.get("o") == "^" and _is_lit(a.inputs[1], 2) and a.inputs[0].dt == "M" \
                     and not (a.inputs[0].op == "bi" and a.inputs[0].p.get("name") == "_cbind_const") \
                     and b.dt == "M" and (_col_vector(b) or (b.dim2 == 1 and b.dim1 > 1)):

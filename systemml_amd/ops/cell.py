@@ -29,6 +29,7 @@ import time
 import torch
 
 from . import core as C
+from .augmented import ConstCol as _ConstCol
 from .backend import backend
 
 BIN_CODES = {"+": 1, "-": 2, "*": 3, "/": 4, "^": 5, "%%": 6, "%/%": 7, "==": 8, "!=": 9, "<": 10,
@@ -122,6 +123,11 @@ def evaluate(prog: CellProgram, args):
     if r is not None:
         stats["kernel"] += 1
         return r
+    if backend.use_kernels and any(type(x) is _ConstCol for x in args):
+        r = _split_cc(prog, args)
+        if r is not None:
+            stats["kernel"] += 1
+            return r
     stats["sequential"] += 1
     if TRACE and backend.use_kernels:
         # SYSML_CELL_TRACE=1: which programs miss the generated kernels, on which operands
@@ -150,6 +156,60 @@ def _axpy_form(prog):
                 f = (b2, a1, b1, 1.0)
     prog._code["axpy"] = f
     return f
+
+
+def _split_cc(prog, args):
+    """The program over constant-column-augmented operands (cbind(X, c), ops/augmented.py) --
+    e.g. MultiLogReg's icpt=2 `rowSums(X ^ 2 * t(sc ^ 2))` on cbind(X, 1): the generated kernel
+    runs over X itself (bf16 as stored, the aggregation fused) and the constant column's value
+    follows on the host, instead of materialising f(cbind(X, c)) (a full-size pass and a
+    full-size write).  Matrix operands: augmented ones over one shape, and row vectors over all
+    D + 1 columns (split into their first D entries and the last); scalars must be host
+    values.  None when that or the aggregation does not fit (or for a bare aggregate, which
+    ops/augmented.agg serves)."""
+    from . import augmented as AUG
+    if not prog.ops:
+        return None
+    shape = None
+    for x in args:
+        if AUG.is_cc(x):
+            if shape is None:
+                shape = tuple(x.X.shape)
+            elif tuple(x.X.shape) != shape:
+                return None
+    xs, cs = [], []
+    for x in args:
+        if AUG.is_cc(x):
+            xs.append(x.X)
+            cs.append(torch.full((1, 1), x.c, dtype=torch.float64))
+        elif type(x) in (float, int, bool):
+            xs.append(x)
+            cs.append(x)
+        elif type(x) is _Tensor and x.dim() == 2 and x.shape[0] == 1 and x.shape[1] == shape[1] + 1 \
+                and x.layout is torch.strided:
+            xs.append(x[:, :shape[1]])
+            cs.append(x[:, shape[1]:].detach().to("cpu", torch.float64))
+        else:
+            return None
+    agg = prog.agg
+    if agg is not None and agg[0] not in ("sum", "min", "max"):
+        return None
+    r = _kernel(prog, xs)
+    if r is None:
+        return None
+    elem = CellProgram(prog.ops, prog.n_in, prog.out)
+    fc = float(sequential(elem, cs).reshape(-1)[0])        # the constant column's value, on the host
+    n = shape[0]
+    if agg is None:
+        return AUG.ConstCol(r, fc)
+    o, d = agg
+    if d == "col":
+        rc = C.cvt(r)
+        v = n * fc if o == "sum" else fc
+        return torch.cat([rc, torch.full((1, 1), v, dtype=rc.dtype, device=rc.device)], 1)
+    if d == "row":
+        return C.binary("+" if o == "sum" else o, r, fc)
+    return C.binary("+", r, n * fc) if o == "sum" else C.binary(o, r, fc)
 
 
 def sequential(prog: CellProgram, args):

@@ -60,3 +60,37 @@ def test_linreg_cg_intercept_on_padded_copy(monkeypatch):
         res[gpu] = r["B_out"].double().cpu().numpy()
     assert AUG.stats["padded"] > before
     np.testing.assert_allclose(res[True], res[False], rtol=2e-3, atol=1e-2)   # fp32 vs fp64 solves
+
+
+@pytest.mark.parametrize("agg", [None, ("sum", "col"), ("sum", "row"), ("sum", "all"), ("max", "col"),
+                                 ("min", "row")])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_cell_program_over_const_column_operand(agg, dt):
+    """ops/cell._split_cc: a Cell program (here (x - 0.5)^2 * 3, or (x - 0.5)^2 * t(v) with a row
+    vector over all D + 1 columns) over cbind(X, c) runs its kernel over X and appends the
+    constant column's value, against torch on the materialised matrix."""
+    from systemml_amd.ops import augmented as AUG
+    from systemml_amd.ops import cell as CELL
+    from systemml_amd.ops.backend import backend
+    backend.configure(DMLConfig(gpu=True, precision="single"))
+    g = torch.Generator(device="cuda").manual_seed(3)
+    X = torch.rand(4096, 64, device="cuda", generator=g).to(dt)
+    cc = AUG.ConstCol(X, 1.0)
+    prog = CELL.CellProgram([("b", "-", 3, 0, 1), ("u", "sq", 4, 3, 0), ("b", "*", 5, 4, 2)], 3, 5, agg)
+    before = CELL.stats["sequential"]
+    r = CELL.evaluate(prog, [cc, 0.5, 3.0])
+    assert CELL.stats["sequential"] == before           # no operator-by-operator fallback
+    M = torch.cat([X.double(), torch.ones(4096, 1, dtype=torch.float64, device="cuda")], 1)
+    E = (M - 0.5) ** 2 * 3.0
+    if agg is None:
+        assert AUG.is_cc(r)
+        got = r.materialize().double()
+        ref = E
+    else:
+        o, d = agg
+        f = {"sum": torch.sum, "max": torch.amax, "min": torch.amin}[o]
+        ref = f(E) if d == "all" else f(E, dim=0 if d == "col" else 1, keepdim=True)
+        got = r.double() if isinstance(r, torch.Tensor) else torch.tensor(float(r), dtype=torch.float64)
+        got = got.to(ref.device)
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(got.reshape(ref.shape), ref, rtol=tol, atol=tol * max(1.0, float(ref.abs().max())))

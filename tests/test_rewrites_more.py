@@ -74,6 +74,12 @@ def test_square_matrix_mult():
            "square-matrix-mult")
 
 
+def test_square_matrix_mult_over_intercept_column():
+    """(cbind(A, 1) ^ 2) %*% v -> (A ^ 2) %*% v[1:D, ] + 1 ^ 2 * v[D + 1, 1] (MultiLogReg icpt=2)."""
+    _check("X = cbind(A, matrix(1, rows=nrow(A), cols=1))\nv = t(colSums(X))\nv[1, 1] = 2\n"
+           "r = (X ^ 2) %*% (v ^ 2) + 3\n", {"A": A}, ["r"], "square-matrix-mult-cbind")
+
+
 V = np.floor(RNG.random((12, 1)) * 5) + 1
 M2 = RNG.random((12, 3))
 
