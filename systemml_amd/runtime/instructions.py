@@ -78,6 +78,10 @@ def make_impl(h):
     return wrapped, code
 
 
+# SYSML_RUNAHEAD_DEVICE=0: run-ahead iterations keep the host placement of small operators
+_RA_DEVICE = __import__("os").environ.get("SYSML_RUNAHEAD_DEVICE", "1") != "0"
+
+
 def _placed(fn, h):
     """CP / GPU execution of one operator by its compiler-chosen exec type (reference:
     hops/Hop.java#findExecTypeByMemEstimate with the GPU operator threshold, re-selected by
@@ -97,6 +101,14 @@ def _placed(fn, h):
     def run(ctx, a):
         small = backend.small_cells
         if small <= 0 or not backend.on_gpu:
+            return fn(ctx, a)
+        if backend.defer and _RA_DEVICE:
+            # a run-ahead loop iteration (runtime/program.py) is queued on the device behind
+            # unread predicates: a host placement would synchronise in the middle of it (the
+            # intercept scripts' D x K bookkeeping: 8 reads per CG iteration at icpt = 2), so
+            # every operator runs in HBM, host operands (loop invariants) uploaded once
+            a = [_upload(x) if (type(x) is Tensor and not x.is_cuda and x.layout == torch.strided) else x
+                 for x in a]
             return fn(ctx, a)
         et = h.exec_type
         if keep_dev:
@@ -135,6 +147,11 @@ def _placed(fn, h):
         ts["h2d"] += 1
         ts["h2d_bytes"] += x.numel() * x.element_size()
         return x.to(backend.device, non_blocking=True)
+
+    def _upload(x):
+        from ..ops.vprog import _uploads
+        ts["h2d"] += 1
+        return _uploads.get(x, backend.device)
 
     def d2h(x):
         ts["d2h"] += 1
