@@ -252,6 +252,8 @@ def _dev_binary(op, a, b):
             return BIN[op](s, m) if da else BIN[op](m, s)
         return binary(op, S.materialize(a), S.materialize(b))
     if isinstance(other, (str,)) or not (da and db or isinstance(other, (int, float, bool))):
+        if op == "+" and type(other) is str and backend.defer:
+            return S.lazy_concat(a, b)       # a run-ahead iteration: read the value when it is live
         return binary(op, S.materialize(a), S.materialize(b))
     x = a.t if da else float(S._num(a))
     y = b.t if db else float(S._num(b))
@@ -325,6 +327,10 @@ _CC = AUG.ConstCol
 def binary(op, a, b):
     if type(a) is _CC or type(b) is _CC:
         return AUG.binary(op, a, b)
+    if type(a) is S.LazyStr or type(b) is S.LazyStr:
+        if op == "+":
+            return S.lazy_concat(a, b)
+        a, b = S.materialize(a), S.materialize(b)
     # fast paths: two Python scalars; dense same-device same-dtype tensors (or tensor-scalar)
     ta_, tb_ = type(a), type(b)
     if ta_ in _PYNUM and tb_ in _PYNUM:

@@ -93,6 +93,12 @@ def _bool(v):
 # ============================================================================
 @builtin("print")
 def b_print(ctx, x="", *rest, **kw):
+    buf = getattr(ctx, "_ra_prints", None)
+    if buf is not None and not rest:
+        # a run-ahead loop iteration (runtime/program.py): printed once the iteration is
+        # known to be live, in order; a deferred string is resolved then
+        buf.append(x if type(x) is S.LazyStr else to_display_string(x))
+        return None
     if rest:
         # printf-style print("fmt %d", a, b)
         s = _format(x, rest)
@@ -413,8 +419,13 @@ def _one_device(ms):
 def b_cbind(ctx, *args, **kw):
     if any(C.is_dist(a) for a in args):
         return C._dist().cbind(args)
-    if isinstance(args[0], str):
+    if isinstance(args[0], (str, S.LazyStr)):
         # string append (reference: StringObject append joins with a newline)
+        if any(type(a) is S.LazyStr or type(a) is S.DevScalar for a in args) and backend.defer:
+            r = args[0]
+            for a in args[1:]:
+                r = S.lazy_concat(r, a, "\n")
+            return r
         return "\n".join(S.to_str(a) for a in args)
     if isinstance(args[0], ListObject):
         out = ListObject(args[0].data, args[0].names)

@@ -84,6 +84,22 @@ def _all_writes(blocks):
     return aw(blocks)
 
 
+def _has_print(blocks):
+    from ..compiler import hops as H
+    from ..compiler.blocks import BasicBlock, IfBlock
+    roots = []
+    stack = list(blocks)
+    while stack:
+        x = stack.pop()
+        if isinstance(x, BasicBlock):
+            roots.extend(list(x.roots) + list(x.env_out.values()))
+        elif isinstance(x, IfBlock):
+            roots.append(x.pred.root)
+            stack.extend(x.then_blocks)
+            stack.extend(x.else_blocks)
+    return any(h.op == "sink" for h in H.walk(roots))
+
+
 def _is_dm(x):
     from ..parallel.dist import DistMatrix
     return type(x) is DistMatrix
@@ -191,6 +207,9 @@ class GraphLoop:
         live = getattr(b, "iter_live", None)
         lin = getattr(b, "body_live_in", None)
         if live is None or lin is None:
+            return False
+        if _has_print(b.body):
+            stats["why"] = "prints"            # buffered per live iteration: op by op only
             return False
         writes = _all_writes(b.body)
         self.commit = sorted(writes & live)

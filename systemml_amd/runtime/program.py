@@ -438,12 +438,19 @@ RUNAHEAD = __import__("os").environ.get("SYSML_RUNAHEAD", "1") != "0"
 _RA_BAD_BI = frozenset({"print", "write", "stop", "assert", "printf", "rand", "sample", "time", "read", "eval",
                         "list", "exists", "toString", "setwd"})
 _RA_BAD_OPS = frozenset({"fcall", "sink"})
+# SYSML_RUNAHEAD_PRINTS=0: a loop that prints is not run ahead
+_RA_PRINTS = __import__("os").environ.get("SYSML_RUNAHEAD_PRINTS", "1") != "0"
 
 
 def _pure_hops(roots):
     from ..compiler import hops as H
     for h in H.walk(roots):
         if h.op in _RA_BAD_OPS:
+            # print(x): a run-ahead iteration buffers its lines and the loop prints them once
+            # the iteration is known to be live (builtins.b_print, _exec_while_runahead)
+            if _RA_PRINTS and h.op == "sink" and h.p.get("name") == "print" and len(h.inputs) == 1 \
+                    and not h.named:
+                continue
             return False
         if h.op == "bi" and h.p.get("name") in _RA_BAD_BI:
             return False
@@ -477,7 +484,29 @@ def _runahead_ok(ctx, b):
     if ok is None:
         ok = b._runahead = (not getattr(b, "inplace_vars", None) and not b.pred.is_const
                             and _pure_hops([b.pred.root]) and _pure_blocks(b.body))
+        if ok:
+            from .graphloop import _has_print
+            b._ra_has_print = _has_print(b.body)
+    if ok and b._ra_has_print:
+        # a printing loop's deferred strings and device-side scalar algebra cost the host more
+        # per iteration than its synchronous prints: worth it only when the device work of an
+        # iteration is large (10M x 1K: 400.6 vs 407.8 ms; 1.25M x 1K: 77.8 vs 72.7 ms)
+        return _streams_big(ctx, b)
     return ok
+
+
+RA_PRINT_MIN_CELLS = 1 << 32
+
+
+def _streams_big(ctx, b):
+    from ..ops import augmented as AUG
+    for v in getattr(b, "body_live_in", ()) or ():
+        x = ctx.vars.get(v)
+        x = getattr(x, "local", x)                  # a row-partitioned matrix: this rank's block
+        x = x.X if AUG.is_cc(x) else x
+        if isinstance(x, torch.Tensor) and x.numel() >= RA_PRINT_MIN_CELLS:
+            return True
+    return False
 
 
 runahead_stats = {"loops": 0, "iterations": 0, "dead": 0, "host_pred": 0, "t": 0.0}
@@ -548,12 +577,19 @@ def _exec_while_runahead(ctx, b):
     # variable map after the iteration)
     pending = collections.deque()
 
+    def emit(buf):
+        for x in buf:
+            ctx.print(x if type(x) is str else str(x))
+
     def drain(keep, unqueued=0):
         """Read predicates oldest first until `keep` remain; True when one ends the loop (the
         variable map is then the one after that last live iteration).  `unqueued`: iterations
-        run but not in `pending` (dead too when an earlier predicate ends the loop)."""
+        run but not in `pending` (dead too when an earlier predicate ends the loop).  An
+        iteration reached here is live (every earlier predicate continued the loop): its
+        buffered prints go out, before its own predicate is tested."""
         while len(pending) > keep:
-            q, inv, after = pending.popleft()
+            q, inv, after, buf = pending.popleft()
+            emit(buf)
             if bool(q.value()) == inv:
                 runahead_stats["dead"] += len(pending) + unqueued
                 vars_.clear()
@@ -582,6 +618,7 @@ def _exec_while_runahead(ctx, b):
             err = None
             q = None
             qinv = False
+            buf = ctx._ra_prints = []
             try:
                 exec_blocks(ctx, b.body)
                 v = vars_.get(pv[0]) if pv is not None else None
@@ -595,14 +632,16 @@ def _exec_while_runahead(ctx, b):
                 raise
             except Exception as e:      # noqa: BLE001 - re-raised below unless the iteration was dead
                 err = e
+            ctx._ra_prints = None
             runahead_stats["iterations"] += 1
             if err is not None:
                 # an error in an iteration past the loop's end is not an error
                 if drain(0, 1):
                     return
+                emit(buf)
                 raise err
             if type(q) is S.DevScalar:
-                pending.append((q, qinv, vars_.copy()))
+                pending.append((q, qinv, vars_.copy(), buf))
                 if drain(depth):
                     return
                 n_queued += 1
@@ -616,10 +655,19 @@ def _exec_while_runahead(ctx, b):
                         return
             else:
                 runahead_stats["host_pred"] += 1
-                if drain(0, 1) or not _to_bool(q):
+                if drain(0, 1):
+                    return
+                emit(buf)
+                if not _to_bool(q):
                     return
     finally:
+        ctx._ra_prints = None
         backend.set_runahead(False, 0)
+        # strings built from unread device scalars leave the loop resolved (their reads were
+        # queued with them; the variable map is a live iteration's)
+        for k, v in list(vars_.items()):
+            if type(v) is S.LazyStr:
+                vars_[k] = str(v)
 
 
 # ----------------------------------------------------------------------------

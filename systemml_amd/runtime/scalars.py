@@ -133,8 +133,45 @@ def _in_runahead():
 
 
 def materialize(v):
-    """Python value of a possibly device-resident scalar."""
-    return v.value() if type(v) is DevScalar else v
+    """Python value of a possibly device-resident scalar (or deferred string)."""
+    t = type(v)
+    if t is DevScalar:
+        return v.value()
+    if t is LazyStr:
+        return str(v)
+    return v
+
+
+class LazyStr:
+    """A string built inside a run-ahead loop iteration (runtime/program.py) from device
+    scalars whose values are not read yet -- LinearRegCG's per-iteration
+    `print("Iteration " + it + ": ... " + sqrt(rr / rr0))` and its log appends.  The parts'
+    device-to-host copies are queued at once (DevScalar.start_read), so resolving the string
+    once the iteration is known to be live waits for those copies only.  The run-ahead loop
+    prints a live iteration's strings in order and resolves every deferred string left in the
+    variable map when it ends."""
+    __slots__ = ("parts",)
+
+    def __init__(self, parts):
+        self.parts = parts
+
+    def __str__(self):
+        return "".join(p if type(p) is str else to_str(p) for p in self.parts)
+
+
+def lazy_concat(a, b, sep=""):
+    """a + sep + b as a LazyStr (parts flattened; device scalars' reads started)."""
+    parts = []
+    for x in (a, b):
+        if type(x) is LazyStr:
+            parts.extend(x.parts)
+        elif type(x) is DevScalar:
+            parts.append(x.start_read())
+        else:
+            parts.append(to_str(x))
+        if sep and x is a:
+            parts.append(sep)
+    return LazyStr(parts)
 
 
 def java_double_str(d: float) -> str:
@@ -168,6 +205,8 @@ def java_double_str(d: float) -> str:
 def to_str(v) -> str:
     if type(v) is DevScalar:
         v = v.value()
+    elif type(v) is LazyStr:
+        return str(v)
     if isinstance(v, bool):
         return "TRUE" if v else "FALSE"
     if isinstance(v, int):

@@ -57,6 +57,7 @@ def test_headline_step_kernel_counts():
     out = []
     cs = EX.compile_script(_src("LinearRegCG.dml"), LR_ARGS, inputs={"X": X1, "y": y1}, outputs=["B_out"], config=cfg)
     EX.execute(cs, {"X": X1, "y": y1}, out=out.append)
+    dead0 = PR.runahead_stats["dead"]        # LinearRegCG's loop runs ahead too (its prints buffered)
     cs = EX.compile_script(_src("MultiLogReg.dml"), MLR_ARGS, inputs={"X": X2, "Y_vec": lab}, outputs=["B_out"],
                            config=cfg)
     r, _ = EX.execute(cs, {"X": X2, "Y_vec": lab}, out=out.append)

@@ -55,7 +55,8 @@ def test_pure_loops_qualify_and_side_effects_do_not():
     cs = EX.compile_script(src, {}, inputs={"A0": np.ones((4, 4))}, outputs=["A"], config=DMLConfig())
     loops = _loops(cs.cp.blocks)
     assert len(loops) == 3
-    assert [_qualifies(b) for b in loops] == [True, False, False]
+    # print(x) is buffered per iteration and printed once the iteration is live (the k loop)
+    assert [_qualifies(b) for b in loops] == [True, True, False]
 
 
 def test_multilogreg_inner_cg_loop_qualifies():
@@ -263,3 +264,48 @@ def test_graph_capture_failure_falls_back(monkeypatch):
            out=got.append)
     assert got == ref
     assert GL.stats["captures"] == st["captures"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [1, 3])
+def test_runahead_prints_only_live_iterations(monkeypatch, depth):
+    """A loop that prints device scalars runs ahead: each iteration's lines are buffered
+    (strings of unread device scalars stay deferred) and printed once the iteration is known
+    to be live, in order; the speculative iterations past the end print nothing, and a
+    string variable built in the loop leaves it resolved (LinearRegCG's per-iteration print
+    and log appends)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from systemml_amd.runtime import scalars as S
+    monkeypatch.setattr(PR, "RUNAHEAD_DEPTH", depth)
+    monkeypatch.setattr(PR, "RA_PRINT_MIN_CELLS", 0)      # printing loops run ahead at any size
+    src = """
+    A = A0
+    s = 100
+    log = "start"
+    k = 0
+    while (s > 0.5) {
+      A = A * 0.5
+      s = sum(A)
+      k = k + 1
+      print("it " + k + " s=" + s)
+      log = append(log, "s " + s)
+    }
+    print("after " + k)
+    print(log)
+    """
+    outs = {}
+    for ra in (False, True):
+        monkeypatch.setattr(PR, "RUNAHEAD", ra)
+        st = dict(PR.runahead_stats)
+        out = []
+        r, _ = EX.execute(EX.compile_script(src, {}, inputs={"A0": np.full((200, 100), 0.01)}, outputs=["log"],
+                                            config=DMLConfig(gpu=True, precision="double")),
+                          {"A0": np.full((200, 100), 0.01)}, out=out.append)
+        outs[ra] = out
+        assert type(r["log"]) is str
+        if ra:
+            assert PR.runahead_stats["loops"] - st["loops"] == 1, PR.runahead_stats
+    assert outs[True] == outs[False]
+    assert outs[True][0].startswith("it 1 s=") and outs[True][-2] == "after 9"
+    assert not any(type(x) is S.LazyStr for x in outs[True])
