@@ -438,8 +438,10 @@ RUNAHEAD = __import__("os").environ.get("SYSML_RUNAHEAD", "1") != "0"
 _RA_BAD_BI = frozenset({"print", "write", "stop", "assert", "printf", "rand", "sample", "time", "read", "eval",
                         "list", "exists", "toString", "setwd"})
 _RA_BAD_OPS = frozenset({"fcall", "sink"})
-# SYSML_RUNAHEAD_PRINTS=0: a loop that prints is not run ahead
-_RA_PRINTS = __import__("os").environ.get("SYSML_RUNAHEAD_PRINTS", "1") != "0"
+# SYSML_RUNAHEAD_PRINTS=1: a loop that prints runs ahead too (its lines buffered per iteration).
+# Off by default: on the headline's LinearRegCG loop it measured within box noise (10M rows
+# 400.6 vs 407.8 ms on one box, 397.7 vs 394.6 on another; profiles/runahead_prints_r6.txt)
+_RA_PRINTS = __import__("os").environ.get("SYSML_RUNAHEAD_PRINTS", "0") == "1"
 
 
 def _pure_hops(roots):
@@ -502,7 +504,12 @@ def _streams_big(ctx, b):
     from ..ops import augmented as AUG
     for v in getattr(b, "body_live_in", ()) or ():
         x = ctx.vars.get(v)
-        x = getattr(x, "local", x)                  # a row-partitioned matrix: this rank's block
+        if hasattr(x, "local") and hasattr(x, "nrows"):
+            # a row-partitioned matrix: the global size over the ranks -- every rank must take
+            # the same decision (a speculative iteration issues collectives)
+            if x.nrows * x.ncols // max(1, x.ctx.world) >= RA_PRINT_MIN_CELLS:
+                return True
+            continue
         x = x.X if AUG.is_cc(x) else x
         if isinstance(x, torch.Tensor) and x.numel() >= RA_PRINT_MIN_CELLS:
             return True

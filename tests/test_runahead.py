@@ -55,8 +55,9 @@ def test_pure_loops_qualify_and_side_effects_do_not():
     cs = EX.compile_script(src, {}, inputs={"A0": np.ones((4, 4))}, outputs=["A"], config=DMLConfig())
     loops = _loops(cs.cp.blocks)
     assert len(loops) == 3
-    # print(x) is buffered per iteration and printed once the iteration is live (the k loop)
-    assert [_qualifies(b) for b in loops] == [True, True, False]
+    # print(x) is buffered per iteration and printed once the iteration is live (the k loop,
+    # SYSML_RUNAHEAD_PRINTS=1)
+    assert [_qualifies(b) for b in loops] == [True, PR._RA_PRINTS, False]
 
 
 def test_multilogreg_inner_cg_loop_qualifies():
@@ -279,6 +280,7 @@ def test_runahead_prints_only_live_iterations(monkeypatch, depth):
     from systemml_amd.runtime import scalars as S
     monkeypatch.setattr(PR, "RUNAHEAD_DEPTH", depth)
     monkeypatch.setattr(PR, "RA_PRINT_MIN_CELLS", 0)      # printing loops run ahead at any size
+    monkeypatch.setattr(PR, "_RA_PRINTS", True)
     src = """
     A = A0
     s = 100
