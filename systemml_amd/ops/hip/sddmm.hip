@@ -152,7 +152,8 @@ __global__ void __launch_bounds__(WAVES * 64, 8) wdivmm_kernel(const int64_t* __
                                                             const T* __restrict__ xv, const T* __restrict__ U,
                                                             const T* __restrict__ V, T* __restrict__ out, int64_t m,
                                                             int K, int mode, T eps, int64_t chunk, int64_t nchunks,
-                                                            const int64_t* __restrict__ rbp, int nb, int blk) {
+                                                            const int64_t* __restrict__ rbp, int nb, int blk,
+                                                            int64_t ldv) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   constexpr int NG = 64 / G;
   const int g = lane / G, gl = lane & (G - 1);
@@ -189,7 +190,7 @@ __global__ void __launch_bounds__(WAVES * 64, 8) wdivmm_kernel(const int64_t* __
             xt[t] = (in && mode == 1) ? xv[p] : T(0);
           }
 #pragma unroll
-          for (int t = 0; t < UN; ++t) bv[t] = kin ? V[cj[t] * K + gl] : T(0);
+          for (int t = 0; t < UN; ++t) bv[t] = kin ? V[cj[t] * ldv + gl] : T(0);
 #pragma unroll
           for (int t = 0; t < UN; ++t) dt[t] = u * bv[t];
 #pragma unroll
@@ -221,7 +222,8 @@ __global__ void __launch_bounds__(WAVES * 64, 8) wdivmm_kernel(const int64_t* __
 template <typename T, typename I>
 int launch_wd(const int64_t* crow, const I* col, const T* wv, const T* xv, const T* U, const T* V, T* out, int64_t m,
               int K, int mode, double eps, int64_t nnz, hipStream_t st, const int64_t* rbp = nullptr, int nb = 0,
-              int blk = 0) {
+              int blk = 0, int64_t ldv = 0) {
+  if (ldv < K) ldv = K;
   // the kernel is bound by the latency of its random V-row gathers: one chunk per wave and
   // enough waves for a full CU (8 per SIMD at <= 64 VGPRs), each with UN gathers per group in
   // flight.  SYSML_WD_WAVES / SYSML_WD_UNROLL override (tuning).
@@ -238,10 +240,10 @@ int launch_wd(const int64_t* crow, const I* col, const T* wv, const T* xv, const
   do {                                                                                                          \
     if (rbp != nullptr)                                                                                         \
       hipLaunchKernelGGL((wdivmm_kernel<T, I, G_, U_, true>), gr, t, 0, st, crow, col, wv, xv, U, V, out, m, K,  \
-                         mode, (T)eps, chunk, nchunks, rbp, nb, blk);                                           \
+                         mode, (T)eps, chunk, nchunks, rbp, nb, blk, ldv);                                      \
     else                                                                                                        \
       hipLaunchKernelGGL((wdivmm_kernel<T, I, G_, U_, false>), gr, t, 0, st, crow, col, wv, xv, U, V, out, m, K, \
-                         mode, (T)eps, chunk, nchunks, rbp, nb, blk);                                           \
+                         mode, (T)eps, chunk, nchunks, rbp, nb, blk, ldv);                                      \
   } while (0)
 #define WD_CASE(G_) \
   if (un >= 8) WD_LAUNCH(G_, 8); \
@@ -307,7 +309,7 @@ int sysml_csr_block_offsets(int idx32, const void* crow, const void* col, int64_
 // [k * cb, (k + 1) * cb): each pass's V rows fit the MALL.  out zeroed by the caller.
 int sysml_wdivmm_blocked(int dtype, int idx32, const void* crow, const void* col, const void* wv, const void* xv,
                          const void* U, const void* V, void* out, int64_t m, int K, int mode, double eps, int64_t nnz,
-                         const void* rbp, int nb, void* stream) {
+                         const void* rbp, int nb, int64_t ldv, void* stream) {
   if (K < 1 || K > 64 || nnz <= 0 || nb < 1 || rbp == nullptr || (mode == 1 && xv == nullptr)) return -1;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const auto* cr = static_cast<const int64_t*>(crow);
@@ -318,11 +320,11 @@ int sysml_wdivmm_blocked(int dtype, int idx32, const void* crow, const void* col
   (idx32 ? sysml_sd::launch_wd<T_, int32_t>(cr, static_cast<const int32_t*>(col), static_cast<const T_*>(wv),   \
                                             static_cast<const T_*>(xv), static_cast<const T_*>(U),              \
                                             static_cast<const T_*>(V), static_cast<T_*>(out), m, K, mode, eps,  \
-                                            nnz, st, rb, nb, k)                                                 \
+                                            nnz, st, rb, nb, k, ldv)                                            \
          : sysml_sd::launch_wd<T_, int64_t>(cr, static_cast<const int64_t*>(col), static_cast<const T_*>(wv),   \
                                             static_cast<const T_*>(xv), static_cast<const T_*>(U),              \
                                             static_cast<const T_*>(V), static_cast<T_*>(out), m, K, mode, eps,  \
-                                            nnz, st, rb, nb, k))
+                                            nnz, st, rb, nb, k, ldv))
     if (dtype == 0) rc = WDB_T(float);
     else if (dtype == 1) rc = WDB_T(double);
     else return -1;
@@ -335,19 +337,21 @@ int sysml_wdivmm_blocked(int dtype, int idx32, const void* crow, const void* col
 // Fused wdivmm (right form, see wdivmm_kernel): out (m x K, zeroed by the caller) for a CSR pattern
 // (crow int64, col int32 if idx32 else int64), weights wv (nullptr: 1), x values xv (mode 1, the
 // pattern's order), factors U (m x K), V (n x K).  dtype 0 fp32, 1 fp64.  -1: unsupported.
+// ldv: row pitch of V in elements (>= K; a padded copy keeps every gathered row in one 64-B
+// segment -- K = 10 fp32 rows of 40 B straddle two segments 60 % of the time)
 int sysml_wdivmm(int dtype, int idx32, const void* crow, const void* col, const void* wv, const void* xv,
                  const void* U, const void* V, void* out, int64_t m, int K, int mode, double eps, int64_t nnz,
-                 void* stream) {
+                 int64_t ldv, void* stream) {
   if (K < 1 || K > 64 || nnz <= 0 || (mode == 1 && xv == nullptr)) return -1;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const auto* cr = static_cast<const int64_t*>(crow);
 #define WD_T(T_)                                                                                             \
   (idx32 ? sysml_sd::launch_wd<T_, int32_t>(cr, static_cast<const int32_t*>(col), static_cast<const T_*>(wv),           \
                                   static_cast<const T_*>(xv), static_cast<const T_*>(U), static_cast<const T_*>(V), \
-                                  static_cast<T_*>(out), m, K, mode, eps, nnz, st)                           \
+                                  static_cast<T_*>(out), m, K, mode, eps, nnz, st, nullptr, 0, 0, ldv)       \
          : sysml_sd::launch_wd<T_, int64_t>(cr, static_cast<const int64_t*>(col), static_cast<const T_*>(wv),           \
                                   static_cast<const T_*>(xv), static_cast<const T_*>(U), static_cast<const T_*>(V), \
-                                  static_cast<T_*>(out), m, K, mode, eps, nnz, st))
+                                  static_cast<T_*>(out), m, K, mode, eps, nnz, st, nullptr, 0, 0, ldv))
   if (dtype == 0) return WD_T(float);
   if (dtype == 1) return WD_T(double);
 #undef WD_T

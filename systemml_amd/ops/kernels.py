@@ -162,7 +162,7 @@ def load(required=False):
         [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
     L.sysml_wdivmm.restype = ctypes.c_int
     L.sysml_wdivmm.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 7 + \
-        [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int64, ctypes.c_void_p]
+        [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
     L.sysml_pad_pixels.restype = ctypes.c_int
     L.sysml_pad_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
@@ -213,7 +213,7 @@ def load(required=False):
     L.sysml_csr_block_offsets.restype = CI
     L.sysml_csr_block_offsets.argtypes = [CI, VP, VP, I64, CI, I64, VP, VP]
     L.sysml_wdivmm_blocked.restype = CI
-    L.sysml_wdivmm_blocked.argtypes = [CI, CI] + [VP] * 7 + [I64, CI, CI, ctypes.c_double, I64, VP, CI, VP]
+    L.sysml_wdivmm_blocked.argtypes = [CI, CI] + [VP] * 7 + [I64, CI, CI, ctypes.c_double, I64, VP, CI, I64, VP]
     L.sysml_live_and.restype = CI
     L.sysml_live_and.argtypes = [VP, VP, VP, VP]
     L.sysml_commit_live.restype = CI
@@ -843,19 +843,21 @@ def wdivmm(crow, col, wv, xv, U, V, mode, eps=0.0, dtype=None):
     xv = xv.to(dtype).contiguous() if xv is not None else None
     out = torch.zeros((m, K), dtype=dtype, device=U.device)
     nnz = int(col.numel())
+    Vg, ldv = _wd_padded(V, nnz)
     blk = _wd_blocks(crow, col, idx32, V.shape[0], K * V.element_size(), nnz, m)
     if blk is not None:
         rbp, nb = blk
         rc = L.sysml_wdivmm_blocked(0 if dtype == torch.float32 else 1, int(idx32), crow.data_ptr(), col.data_ptr(),
                                     wv.data_ptr() if wv is not None else None,
-                                    xv.data_ptr() if xv is not None else None, U.data_ptr(), V.data_ptr(),
-                                    out.data_ptr(), m, K, int(mode), float(eps), nnz, rbp.data_ptr(), nb, _stream())
+                                    xv.data_ptr() if xv is not None else None, U.data_ptr(), Vg.data_ptr(),
+                                    out.data_ptr(), m, K, int(mode), float(eps), nnz, rbp.data_ptr(), nb, ldv,
+                                    _stream())
         if rc == 0:
             _count("wdivmm_blocked")
     else:
         rc = L.sysml_wdivmm(0 if dtype == torch.float32 else 1, int(idx32), crow.data_ptr(), col.data_ptr(),
                             wv.data_ptr() if wv is not None else None, xv.data_ptr() if xv is not None else None,
-                            U.data_ptr(), V.data_ptr(), out.data_ptr(), m, K, int(mode), float(eps), nnz,
+                            U.data_ptr(), Vg.data_ptr(), out.data_ptr(), m, K, int(mode), float(eps), nnz, ldv,
                             _stream())
     if rc == -1:
         return None
@@ -863,6 +865,41 @@ def wdivmm(crow, col, wv, xv, U, V, mode, eps=0.0, dtype=None):
         raise RuntimeError(f"sysml_wdivmm failed: {rc}")
     _count("wdivmm")
     return out
+
+
+# Row padding of wdivmm's gathered factor (opt-in, SYSML_WD_PAD=1): a K-wide row whose byte
+# length is not a power of two (rank 10 fp32: 40 B) straddles two 64-B segments for most column
+# indices; a copy with the row pitch rounded up to a power of two keeps every gathered row in one
+# segment.  Made once per factor version (the CG iterations of one ALS half-step reuse it).
+# Off: ALS-CG 10M x 10M / 1e9 non-zeros measured 1.498 s padded vs 1.469 s (profiles/
+# als_pad_r6.txt) -- the gathers are latency-bound, not segment-bound.
+WD_PAD = os.environ.get("SYSML_WD_PAD", "0") == "1"
+WD_PAD_MIN_NNZ = 1 << 22
+_WD_PADDED = {}
+
+
+def _wd_padded(V, nnz):
+    import torch
+    n, K = V.shape
+    ld = 1
+    while ld < K:
+        ld *= 2
+    if not WD_PAD or ld == K or nnz < WD_PAD_MIN_NNZ or ld * V.element_size() > 256:
+        return V, K
+    key = (V.data_ptr(), V._version, n, K, V.dtype)
+    e = _WD_PADDED.get(key)
+    if e is not None and e[0]() is V:
+        return e[1], ld
+    Vp = torch.zeros((n, ld), dtype=V.dtype, device=V.device)
+    Vp[:, :K].copy_(V)
+    import weakref
+    for k in [k for k, v in _WD_PADDED.items() if v[0]() is None]:
+        _WD_PADDED.pop(k, None)
+    if len(_WD_PADDED) >= 2:
+        _WD_PADDED.pop(next(iter(_WD_PADDED)))
+    _WD_PADDED[key] = (weakref.ref(V), Vp)
+    _count("wdivmm_padV")
+    return Vp, ld
 
 
 # Column blocking of wdivmm's V gathers (opt-in, SYSML_WD_BLOCK_MB=<block MB>): a gathered factor

@@ -146,7 +146,8 @@ def test_sparse_sparse_product_elementwise(prec):
 @pytest.mark.parametrize("form", ["mult", "multx", "div"])
 @pytest.mark.parametrize("left", [False, True])
 @pytest.mark.parametrize("blocked", [False, True])
-def test_fused_wdivmm_matches_dense(K, form, left, blocked, monkeypatch):
+@pytest.mark.parametrize("pad", [False, True])
+def test_fused_wdivmm_matches_dense(K, form, left, blocked, pad, monkeypatch):
     """sddmm.hip wdivmm_kernel (one pass over W's pattern, the gathered factor row reused for
     the accumulation) against fp64 torch on the dense equivalent, right and left forms."""
     from systemml_amd.ops import quaternary as Q, kernels
@@ -172,12 +173,18 @@ def test_fused_wdivmm_matches_dense(K, form, left, blocked, monkeypatch):
         # column-blocked passes (the gathered factor visited ~7 column blocks at a time)
         monkeypatch.setattr(kernels, "WD_BLOCK_MIN_NNZ", 0)
         monkeypatch.setattr(kernels, "WD_BLOCK_BYTES", K * 8 * 300)
+    # pad: the gathered factor as a copy with power-of-two row pitch (K = 10 / 33: 16 / 64)
+    monkeypatch.setattr(kernels, "WD_PAD", pad)
+    monkeypatch.setattr(kernels, "WD_PAD_MIN_NNZ", 0)
+    p0 = kernels.counters.get("wdivmm_padV", 0)
     c0 = kernels.counters.get("wdivmm", 0)
     b0 = kernels.counters.get("wdivmm_blocked", 0)
     got = Q.wdivmm(W, U.cuda(), V.cuda(), left, mult=form != "div", eps=0.5 if form == "div" else None,
                    X=X if form == "multx" else None)
     assert kernels.counters.get("wdivmm", 0) == c0 + 1
     assert kernels.counters.get("wdivmm_blocked", 0) == b0 + int(blocked)
+    if pad and K == 10:
+        assert kernels.counters.get("wdivmm_padV", 0) >= p0 + (0 if left else 1)
     torch.testing.assert_close(got.cpu(), ref, rtol=1e-9, atol=1e-9)
 
 
