@@ -25,6 +25,13 @@
 // store per group (lane-selected address, never skipped) and enters the vmcnt count.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+// cache policy of the streamed X rows' LDS-DMA (aux of global_load_lds): 2 = non-temporal -- each
+// X row is read once per pass and X is far larger than the 256 MB MALL, so the default policy
+// only evicts the small operands (MI355X_MICROARCH.md: LDS-DMA streams 6.4 -> 6.5-6.8 TB/s nt)
+#ifndef SYSML_X_AUX
+#define SYSML_X_AUX 2
+#endif
 #include <unordered_set>
 
 // Run-ahead loops (runtime/program.py _exec_while_runahead): the device address of the fp64
@@ -268,7 +275,7 @@ chain4_kernel(const T* __restrict__ X, int64_t N, int D, const float* __restrict
       for (int h = 0; h < P; ++h)
         __builtin_amdgcn_global_load_lds((const void*)(row + coff[j] + h * (8 / P)),
                                          (void __attribute__((address_space(3)))*)(sb + (j * P + h) * 1024), 16, 0,
-                                         0);
+                                         SYSML_X_AUX);
     __builtin_amdgcn_global_load_lds((const void*)(S + rr * (int64_t)lds + scol),
                                      (void __attribute__((address_space(3)))*)(sb + XB), 4, 0, 0);
   };
@@ -531,7 +538,7 @@ chain4m_kernel(const uint16_t* __restrict__ X, int64_t N, int D, const float* __
 #pragma unroll
     for (int j = 0; j < J; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(row + coff[j]),
-                                       (void __attribute__((address_space(3)))*)(sb + j * 1024), 16, 0, 0);
+                                       (void __attribute__((address_space(3)))*)(sb + j * 1024), 16, 0, SYSML_X_AUX);
     __builtin_amdgcn_global_load_lds((const void*)(S + rr * (int64_t)lds + scol),
                                      (void __attribute__((address_space(3)))*)(sb + XB), 4, 0, 0);
   };

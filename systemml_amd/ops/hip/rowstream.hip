@@ -34,6 +34,13 @@
 #include <unordered_set>
 #include <stdint.h>
 
+// cache policy of the streamed X rows' LDS-DMA (aux of global_load_lds): 2 = non-temporal -- each
+// X row is read once per pass and X is far larger than the 256 MB MALL, so the default policy
+// only evicts the small operands (MI355X_MICROARCH.md: LDS-DMA streams 6.4 -> 6.5-6.8 TB/s nt)
+#ifndef SYSML_X_AUX
+#define SYSML_X_AUX 2
+#endif
+
 namespace sysml {
 
 enum Mode { XV = 0, XTG = 1, XTXV = 2, XTWXV = 3, XTXVY = 4, XTPSXV = 5,
@@ -709,7 +716,7 @@ rowstream_dma_kernel(const T* __restrict__ X, int64_t N, int D,
       for (int h = 0; h < PIECES; ++h)
         __builtin_amdgcn_global_load_lds((const void*)(row + coff[j] + h * (8 / PIECES)),
                                          (void __attribute__((address_space(3)))*)(sb + (j * PIECES + h) * 1024),
-                                         16, 0, 0);
+                                         16, 0, SYSML_X_AUX);
     if constexpr (OPS::NEEDS)
       __builtin_amdgcn_global_load_lds((const void*)(S + rr * (int64_t)lds + scol),
                                        (void __attribute__((address_space(3)))*)(sb + XB), 4, 0, 0);

@@ -22,7 +22,7 @@ from .backend import backend
 from . import sparse as SP
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsysml_hip.so")
+LIB_PATH = os.environ.get("SYSML_HIP_LIB") or os.path.join(_HERE, "lib", "libsysml_hip.so")   # env: A/B builds
 _lib = None
 
 # modes (must match ops/hip/rowstream.hip)
