@@ -42,6 +42,9 @@ AGG_CODES = {"sum": 0, "sumsq": 1, "mean": 0, "min": 2, "max": 3}
 AGG_DIRS = {"all": 1, "row": 2, "col": 3}
 MAXIN, MAXOPS, NR = 12, 40, 16
 COL4 = 1000           # column-aggregate variant offset: 4 adjacent columns per lane (sysml_cell_col4)
+# row aggregates over 4-cell groups with vector loads (sysml_cell_row4); SYSML_CELL_ROW4=0: one cell
+# per lane (sysml_cell_row)
+ROW4 = os.environ.get("SYSML_CELL_ROW4", "1") != "0"
 FULL, ROWV, COLV, HSCALAR, DSCALAR, CHAN = range(6)
 # per-channel broadcast operators (bias_add / bias_multiply: a C x 1 vector over the H*W columns
 # of each channel of an N x (C*H*W) operand); generated kernels only (mode CHAN)
@@ -361,7 +364,8 @@ def generate(prog: CellProgram, T, modes, dts, vecs, mode, variant, idx32=False,
     elif mode == 1:
         call = "sysml_cell_flat<Spec, 1>(A);"
     elif mode == 2:
-        call = f"sysml_cell_row<Spec, {variant}>(A);"
+        call = (f"sysml_cell_row4<Spec, {variant - COL4}>(A);" if variant >= COL4
+                else f"sysml_cell_row<Spec, {variant}>(A);")
     elif variant >= COL4:
         call = f"sysml_cell_col4<Spec, {variant - COL4}>(A);"
     else:
@@ -650,6 +654,9 @@ def _make_plan(prog, args):
         vecs = tuple(P.inp[k].vec for k in range(prog.n_in))
         if mode == 2:
             variant = 1 if Cc <= 8 else (4 if Cc <= 32 else (16 if Cc <= 128 else 64))
+            if ROW4 and Cc % 4 == 0 and Cc >= 64:
+                g4 = Cc // 4
+                variant = COL4 + (64 if g4 >= 64 else (16 if g4 >= 16 else 4))   # 4 cells per lane
         elif mode == 3:
             variant = 8 if Cc <= 8 else 64
             if Cc % 4 == 0 and Cc >= 1024:
