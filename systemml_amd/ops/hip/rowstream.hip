@@ -70,11 +70,23 @@ template <> struct Raw8<double>   { double2 v[4]; };
 template <typename T>
 __device__ __forceinline__ void load_raw(Raw8<T>& r, const T* __restrict__ row, int c0, int D, bool vec);
 
+typedef unsigned int sysml_u4v __attribute__((ext_vector_type(4)));
+
+// a bf16 X row piece, non-temporal (X streams once per pass, SYSML_X_AUX above)
+__device__ __forceinline__ uint4 ld_x16(const uint16_t* p) {
+#if SYSML_X_AUX
+  const sysml_u4v t = __builtin_nontemporal_load(reinterpret_cast<const sysml_u4v*>(p));
+  return make_uint4(t.x, t.y, t.z, t.w);
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+
 template <>
 __device__ __forceinline__ void load_raw<uint16_t>(Raw8<uint16_t>& r, const uint16_t* __restrict__ row,
                                                    int c0, int D, bool vec) {
   if (vec && c0 + 8 <= D) {
-    r.v = *reinterpret_cast<const uint4*>(row + c0);
+    r.v = ld_x16(row + c0);
   } else {
     uint32_t e[8];
 #pragma unroll
@@ -119,7 +131,7 @@ template <typename T>
 __device__ __forceinline__ void load_vec(Raw8<T>& r, const T* __restrict__ p);
 template <>
 __device__ __forceinline__ void load_vec<uint16_t>(Raw8<uint16_t>& r, const uint16_t* __restrict__ p) {
-  r.v = *reinterpret_cast<const uint4*>(p);
+  r.v = ld_x16(p);
 }
 template <>
 __device__ __forceinline__ void load_vec<float>(Raw8<float>& r, const float* __restrict__ p) {
