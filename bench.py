@@ -90,8 +90,8 @@ def gen_data(ctx, rows, cols, classes, dtype, sparsity=0.9, seed=7):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--cols", type=int, default=1000)
     ap.add_argument("--classes", type=int, default=5)
